@@ -1,0 +1,560 @@
+// gr_engine.hip — libgpuraft.so: the HIP step kernel for gfx950 and the
+// C-ABI declared in include/gpuraft.h.
+//
+// One lane per Raft group (peer). Work is integer compares, min/max, a
+// sorting network and gathers over structure-of-arrays state: HBM-bandwidth
+// bound, no MFMA. 256-lane workgroups, one lane per slot,
+// consecutive lanes on consecutive slots so every SoA field access of a wave
+// is one contiguous 512-byte (u64) or 64-byte (u8) segment.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "gr_host.h"
+#include "gr_lane.h"
+
+namespace gr {
+
+constexpr int kBlock = 256;
+
+template <int S>
+__global__ __launch_bounds__(kBlock) void gr_step_kernel(StepParams kp) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t lc = 0, fc = 0, es = 0, mi = 0, mo = 0;
+  if (i < kp.n_lanes) {
+    const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+    Lane<S> L(kp, i, p);
+    L.step(&lc, &fc, &es, &mi, &mo);
+  }
+  if (!kp.stats) return;
+  // per-workgroup partial counters (no atomics on global memory)
+  __shared__ uint32_t red[5];
+  if (threadIdx.x < 5) red[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t bl = __ballot(lc != 0), bf = __ballot(fc != 0), be = __ballot(es != 0);
+  for (int off = 32; off > 0; off >>= 1) {
+    mi += __shfl_xor(mi, off);
+    mo += __shfl_xor(mo, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&red[0], (uint32_t)__popcll(bl));
+    atomicAdd(&red[1], (uint32_t)__popcll(bf));
+    atomicAdd(&red[2], (uint32_t)__popcll(be));
+    atomicAdd(&red[3], mi);
+    atomicAdd(&red[4], mo);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t* row = kp.stats + (uint64_t)blockIdx.x * NSTAT;
+    row[ST_LEADER_COMMITS] += red[0];
+    row[ST_FOLLOWER_COMMITS] += red[1];
+    row[ST_ESCALATIONS] += red[2];
+    row[ST_MSGS_IN] += red[3];
+    row[ST_MSGS_OUT] += red[4];
+  }
+}
+
+template <int S>
+static hipError_t launch(const StepParams& kp, hipStream_t s) {
+  if (kp.n_lanes == 0) return hipSuccess;
+  const uint32_t blocks = (kp.n_lanes + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(gr_step_kernel<S>, dim3(blocks), dim3(kBlock), 0, s, kp);
+  return hipGetLastError();
+}
+
+static hipError_t launch_slots(uint32_t S, const StepParams& kp, hipStream_t s) {
+  switch (S) {
+    case 1: return launch<1>(kp, s);
+    case 3: return launch<3>(kp, s);
+    case 5: return launch<5>(kp, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+static uint32_t instantiated_slots(uint32_t want) {
+  if (want <= 1) return 1;
+  if (want <= 3) return 3;
+  if (want <= 5) return 5;
+  return 0;
+}
+
+}  // namespace gr
+
+using namespace gr;
+using namespace gr::host;
+
+struct gr_engine {
+  gr_config cfg{};
+  uint32_t S = 0;
+  uint32_t cap = 0;  // padded slot capacity (row stride)
+  hipStream_t stream = nullptr;
+
+  StateBase st{};
+  LaneBase ln{};
+  uint64_t* stats = nullptr;
+  uint32_t stats_rows = 0;
+  bool routes_bound = false;
+  bool locals_set = false;
+  uint64_t passes = 0;
+
+  // host-path staging
+  void* d_in = nullptr;
+  void* d_out = nullptr;
+  size_t d_in_bytes = 0, d_out_bytes = 0;
+  uint8_t* h_in = nullptr;
+  uint8_t* h_out = nullptr;
+  size_t h_in_bytes = 0, h_out_bytes = 0;
+  std::vector<gr_message> out_msgs;
+  std::vector<gr_peer_result> out_results;
+  std::mutex mu;  // one host-path pass at a time per engine
+};
+
+namespace {
+
+#define HIPCHK(x)                              \
+  do {                                         \
+    hipError_t _e = (x);                       \
+    if (_e != hipSuccess) return GR_EDEVICE;   \
+  } while (0)
+
+constexpr uint32_t kStageChunk = 1u << 16;
+
+int transfer_state(gr_engine* e, uint32_t first, size_t n, gr_peer* host, bool to_device) {
+  if (!e || (n && !host)) return GR_EINVAL;
+  if ((uint64_t)first + n > e->cfg.max_peers) return GR_ERANGE;
+  const uint32_t S = e->S, n64 = rows_u64(S), n8 = rows_u8(S);
+  std::vector<uint64_t> b64;
+  std::vector<uint8_t> b8;
+  for (size_t base = 0; base < n; base += kStageChunk) {
+    const uint32_t m = (uint32_t)std::min<size_t>(kStageChunk, n - base);
+    b64.assign((size_t)n64 * m, 0);
+    b8.assign((size_t)n8 * m, 0);
+    if (to_device) {
+      for (uint32_t k = 0; k < m; ++k) {
+        const gr_peer& g = host[base + k];
+        if (g.n_runs > GR_K || g.read_index_count > GR_Q) return GR_EINVAL;
+        if (g.self_slot != GR_SLOT_NONE && g.self_slot >= S) return GR_EINVAL;
+        for (uint32_t r = 0; r < n64; ++r) b64[(size_t)r * m + k] = get_u64_row(g, r, S);
+        for (uint32_t r = 0; r < n8; ++r) b8[(size_t)r * m + k] = get_u8_row(g, r, S);
+      }
+      for (uint32_t r = 0; r < n64; ++r)
+        HIPCHK(hipMemcpy(e->st.u64(r) + first + base, b64.data() + (size_t)r * m, (size_t)m * 8,
+                         hipMemcpyHostToDevice));
+      for (uint32_t r = 0; r < n8; ++r)
+        HIPCHK(hipMemcpy(e->st.u8(r) + first + base, b8.data() + (size_t)r * m, (size_t)m,
+                         hipMemcpyHostToDevice));
+    } else {
+      for (uint32_t r = 0; r < n64; ++r)
+        HIPCHK(hipMemcpy(b64.data() + (size_t)r * m, e->st.u64(r) + first + base, (size_t)m * 8,
+                         hipMemcpyDeviceToHost));
+      for (uint32_t r = 0; r < n8; ++r)
+        HIPCHK(hipMemcpy(b8.data() + (size_t)r * m, e->st.u8(r) + first + base, (size_t)m,
+                         hipMemcpyDeviceToHost));
+      for (uint32_t k = 0; k < m; ++k) {
+        gr_peer& g = host[base + k];
+        memset(&g, 0, sizeof(g));
+        for (uint32_t r = 0; r < n64; ++r) set_u64_row(g, r, S, b64[(size_t)r * m + k]);
+        for (uint32_t r = 0; r < n8; ++r) set_u8_row(g, r, S, b8[(size_t)r * m + k]);
+      }
+    }
+  }
+  return GR_OK;
+}
+
+StepParams base_params(gr_engine* e) {
+  StepParams kp;
+  memset(&kp, 0, sizeof(kp));
+  kp.st = e->st;
+  kp.ln = e->ln;
+  kp.stats = e->stats;
+  kp.max_entry_size = e->cfg.max_entry_size;
+  return kp;
+}
+
+int grow_device(void** p, size_t* have, size_t want) {
+  if (*have >= want) return GR_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  HIPCHK(hipMalloc(p, want));
+  *have = want;
+  return GR_OK;
+}
+int grow_pinned(uint8_t** p, size_t* have, size_t want) {
+  if (*have >= want) return GR_OK;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *have = 0;
+  HIPCHK(hipHostMalloc((void**)p, want, hipHostMallocDefault));
+  *have = want;
+  return GR_OK;
+}
+
+// Upload per-lane local inputs for lanes [0, n) in lane order.
+int upload_locals(gr_engine* e, const std::vector<gr_local_input>& byLane, uint32_t n, hipStream_t s) {
+  std::vector<uint32_t> lt(n, 0), lq(n, 0), lp(n, 0);
+  std::vector<uint8_t> lf(n, 0);
+  std::vector<uint64_t> llo(n, 0), lhi(n, 0), lr(n, 0);
+  for (uint32_t l = 0; l < n; ++l) {
+    const gr_local_input& x = byLane[l];
+    lt[l] = x.ticks;
+    lq[l] = x.quiesced_ticks;
+    lp[l] = x.propose_entries;
+    lf[l] = (uint8_t)((x.read_index ? LF_READ_INDEX : 0) | (x.propose_has_config_change ? LF_PROPOSE_CC : 0));
+    llo[l] = x.read_ctx_low;
+    lhi[l] = x.read_ctx_high;
+    lr[l] = x.rand;
+  }
+  const LaneBase& L = e->ln;
+  HIPCHK(hipMemcpyAsync(L.u32(LR_TICKS), lt.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(L.u32(LR_QTICKS), lq.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(L.u32(LR_PROPOSE), lp.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(L.u8(LR_LFLAGS), lf.data(), (size_t)n, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(L.u64(LR_RI_LO), llo.data(), (size_t)n * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(L.u64(LR_RI_HI), lhi.data(), (size_t)n * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(L.u64(LR_RAND), lr.data(), (size_t)n * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));  // the host vectors go out of scope
+  return GR_OK;
+}
+
+// Download per-lane results for lanes [first, first+n).
+int download_results(gr_engine* e, uint32_t first, uint32_t n, std::vector<gr_peer_result>* out,
+                     const uint32_t* peer_of_lane) {
+  const LaneBase& L = e->ln;
+  std::vector<uint8_t> rflags(n), esc(n), pres(n), rtrc(n);
+  std::vector<uint32_t> escitem(n);
+  std::vector<uint64_t> afrom(n), pfirst(n), rti((size_t)GR_Q * n), rtl((size_t)GR_Q * n),
+      rth((size_t)GR_Q * n);
+  HIPCHK(hipMemcpy(rflags.data(), L.u8(LR_RFLAGS) + first, n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(esc.data(), L.u8(LR_ESC_REASON) + first, n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(pres.data(), L.u8(LR_PROP_RESULT) + first, n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(rtrc.data(), L.u8(LR_RTR_COUNT) + first, n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(escitem.data(), L.u32(LR_ESC_ITEM) + first, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(afrom.data(), L.u64(LR_APPEND_FROM) + first, (size_t)n * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(pfirst.data(), L.u64(LR_PROPOSE_FIRST) + first, (size_t)n * 8, hipMemcpyDeviceToHost));
+  for (int q = 0; q < GR_Q; ++q) {
+    HIPCHK(hipMemcpy(rti.data() + (size_t)q * n, L.u64(LR_RTR_INDEX + q) + first, (size_t)n * 8,
+                     hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(rtl.data() + (size_t)q * n, L.u64(LR_RTR_LO + q) + first, (size_t)n * 8,
+                     hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(rth.data() + (size_t)q * n, L.u64(LR_RTR_HI + q) + first, (size_t)n * 8,
+                     hipMemcpyDeviceToHost));
+  }
+  out->resize(n);
+  for (uint32_t l = 0; l < n; ++l) {
+    gr_peer_result& pr = (*out)[l];
+    memset(&pr, 0, sizeof(pr));
+    pr.peer = peer_of_lane ? peer_of_lane[l] : first + l;
+    const uint8_t rf = rflags[l];
+    if (rf & RF_ESCALATED) {
+      pr.escalation = esc[l];
+      pr.esc_item = escitem[l];
+    }
+    if (rf & RF_PROPOSE) {
+      pr.propose_result = pres[l];
+      pr.propose_first = pfirst[l];
+    }
+    if (rf & RF_APPEND) pr.append_from = afrom[l];
+    if (rf & RF_READY) {
+      pr.n_ready = rtrc[l];
+      for (int q = 0; q < pr.n_ready && q < GR_Q; ++q) {
+        pr.ready[q].index = rti[(size_t)q * n + l];
+        pr.ready[q].ctx_low = rtl[(size_t)q * n + l];
+        pr.ready[q].ctx_high = rth[(size_t)q * n + l];
+      }
+    }
+  }
+  return GR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gr_strerror(int err) {
+  switch (err) {
+    case GR_OK: return "ok";
+    case GR_EINVAL: return "invalid argument";
+    case GR_ENOMEM: return "out of memory";
+    case GR_EDEVICE: return "HIP device error";
+    case GR_ERANGE: return "slot range out of bounds";
+    case GR_ECAPACITY: return "mailbox capacity exceeded";
+    case GR_ESTATE: return "engine state error";
+  }
+  return "unknown error";
+}
+
+const char* gr_escalation_name(int esc) {
+  static const char* names[] = {"none", "term_window", "random", "unsupported", "election", "panic",
+                                "capacity", "snapshot", "entry_size", "msg_runs", "nonmember",
+                                "config_change"};
+  if (esc < 0 || esc > GR_ESC_CONFIG_CHANGE) return "unknown";
+  return names[esc];
+}
+
+int gr_create(const gr_config* cfg, gr_engine** out) {
+  if (!cfg || !out) return GR_EINVAL;
+  *out = nullptr;
+  if (cfg->window_runs != GR_K || cfg->read_index_depth != GR_Q || cfg->mailbox_depth != GR_C)
+    return GR_EINVAL;
+  if (cfg->max_peers == 0 || cfg->slots == 0 || cfg->slots > GR_SMAX) return GR_EINVAL;
+  const uint32_t S = instantiated_slots(cfg->slots);
+  if (!S) return GR_EINVAL;
+  if (hipSetDevice((int)cfg->device) != hipSuccess) return GR_EDEVICE;
+  gr_engine* e = new (std::nothrow) gr_engine();
+  if (!e) return GR_ENOMEM;
+  e->cfg = *cfg;
+  e->S = S;
+  e->cap = pad_cap(cfg->max_peers);
+  e->st.cap = e->cap;
+  e->st.S = S;
+  e->ln.lcap = e->cap;
+  e->ln.S = S;
+  const size_t sb = state_bytes(S, e->cap), lb = lane_bytes(S, e->cap);
+  e->stats_rows = (e->cap + kBlock - 1) / kBlock;
+  void *ds = nullptr, *dl = nullptr;
+  if (hipMalloc(&ds, sb) != hipSuccess || hipMalloc(&dl, lb) != hipSuccess ||
+      hipMalloc((void**)&e->stats, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess) {
+    if (ds) (void)hipFree(ds);
+    if (dl) (void)hipFree(dl);
+    e->st.base = nullptr;
+    e->ln.base = nullptr;
+    gr_destroy(e);
+    return GR_ENOMEM;
+  }
+  e->st.base = (uint8_t*)ds;
+  e->ln.base = (uint8_t*)dl;
+  if (hipMemset(ds, 0, sb) != hipSuccess || hipMemset(dl, 0, lb) != hipSuccess ||
+      hipMemset(e->stats, 0, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    gr_destroy(e);
+    return GR_EDEVICE;
+  }
+  *out = e;
+  return GR_OK;
+}
+
+void gr_destroy(gr_engine* e) {
+  if (!e) return;
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->st.base) (void)hipFree(e->st.base);
+  if (e->ln.base) (void)hipFree(e->ln.base);
+  if (e->stats) (void)hipFree(e->stats);
+  if (e->d_in) (void)hipFree(e->d_in);
+  if (e->d_out) (void)hipFree(e->d_out);
+  if (e->h_in) (void)hipHostFree(e->h_in);
+  if (e->h_out) (void)hipHostFree(e->h_out);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int gr_load_groups(gr_engine* e, uint32_t first, const gr_peer* peers, size_t n) {
+  if (e) HIPCHK(hipDeviceSynchronize());
+  return transfer_state(e, first, n, const_cast<gr_peer*>(peers), true);
+}
+
+int gr_sync_groups_to_host(gr_engine* e, uint32_t first, gr_peer* out, size_t n) {
+  if (e) HIPCHK(hipDeviceSynchronize());
+  return transfer_state(e, first, n, out, false);
+}
+
+uint64_t gr_space_chunk_bytes(uint32_t positions) { return space_chunk_bytes_pc(space_pad_positions(positions)); }
+uint64_t gr_space_bytes(uint32_t n_chunks, uint32_t positions) {
+  return (uint64_t)n_chunks * gr_space_chunk_bytes(positions);
+}
+
+int gr_space_encode(void* space_host, uint32_t n_chunks, uint32_t positions, const gr_message* msgs,
+                    size_t n, const uint32_t* pos_of_msg) {
+  if (!space_host || (n && (!msgs || !pos_of_msg))) return GR_EINVAL;
+  const SpaceView v = make_view(space_host, n_chunks, positions);
+  for (size_t k = 0; k < n; ++k) {
+    const uint32_t g = pos_of_msg[k];
+    if (g / v.pc >= n_chunks || g % v.pc >= positions) return GR_ERANGE;
+    const Mailbox mb = v.at(g);
+    const uint8_t c = mb.cnt();
+    if (c >= GR_C) return GR_ECAPACITY;
+    encode_msg(mb, c, msgs[k]);
+    mb.cnt() = (uint8_t)(c + 1);
+  }
+  return GR_OK;
+}
+
+int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t positions, gr_message* out,
+                    size_t cap, size_t* n_out) {
+  if (!space_host || !n_out) return GR_EINVAL;
+  const SpaceView v = make_view(space_host, n_chunks, positions);
+  size_t n = 0;
+  for (uint32_t c = 0; c < n_chunks; ++c) {
+    for (uint32_t l = 0; l < positions; ++l) {
+      const uint32_t g = c * v.pc + l;
+      const Mailbox mb = v.at(g);
+      const uint32_t cnt = std::min<uint32_t>(mb.cnt(), GR_C);
+      for (uint32_t k = 0; k < cnt; ++k) {
+        if (out && n < cap) {
+          out[n] = decode_msg(mb, k);
+          out[n].peer = g;
+          out[n].slot = (uint8_t)k;
+        }
+        n++;
+      }
+    }
+  }
+  *n_out = n;
+  return n <= cap || !out ? GR_OK : GR_ECAPACITY;
+}
+
+int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
+  if (!e || !in || !out) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  const uint32_t S = e->S;
+  out->msgs = nullptr;
+  out->n_msgs = 0;
+  out->results = nullptr;
+  out->n_results = 0;
+  e->out_msgs.clear();
+  e->out_results.clear();
+  PackedInbox pk;
+  int r = pack_inbox(in, S, e->cfg.max_peers, &pk);
+  if (r) return r;
+  const uint32_t nl = (uint32_t)pk.peers.size();
+  if (nl == 0) return GR_OK;
+  const size_t in_bytes = gr_space_bytes(1, pk.in_positions);
+  const size_t out_bytes = gr_space_bytes(1, pk.out_positions);
+  if ((r = grow_pinned(&e->h_in, &e->h_in_bytes, in_bytes))) return r;
+  if ((r = grow_pinned(&e->h_out, &e->h_out_bytes, out_bytes))) return r;
+  if ((r = grow_device(&e->d_in, &e->d_in_bytes, in_bytes))) return r;
+  if ((r = grow_device(&e->d_out, &e->d_out_bytes, out_bytes))) return r;
+  memset(e->h_in, 0, in_bytes);
+  encode_inbox(in, pk, e->h_in);
+  const hipStream_t s = e->stream;
+  if ((r = upload_locals(e, pk.locals, nl, s))) return r;
+  HIPCHK(hipMemcpyAsync(e->d_in, e->h_in, in_bytes, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(e->ln.u32(LR_LANE_PEER), pk.peers.data(), (size_t)nl * 4, hipMemcpyHostToDevice, s));
+  for (uint32_t j = 0; j < S; ++j) {
+    HIPCHK(hipMemcpyAsync(e->ln.in_pos() + (size_t)j * e->cap, pk.in_pos.data() + (size_t)j * nl,
+                          (size_t)nl * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(e->ln.out_pos() + (size_t)j * e->cap, pk.out_pos.data() + (size_t)j * nl,
+                          (size_t)nl * 4, hipMemcpyHostToDevice, s));
+  }
+  StepParams kp = base_params(e);
+  kp.has_locals = 1;
+  kp.has_lane_peer = 1;
+  kp.has_routes = 1;
+  kp.in = make_view(e->d_in, 1, pk.in_positions);
+  kp.out = make_view(e->d_out, 1, pk.out_positions);
+  kp.n_lanes = nl;
+  HIPCHK(launch_slots(S, kp, s));
+  e->passes++;
+  e->locals_set = false;    // the lane rows now hold this pass's compact locals
+  e->routes_bound = false;  // and its compact routes
+  HIPCHK(hipMemcpyAsync(e->h_out, e->d_out, out_bytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if ((r = download_results(e, 0, nl, &e->out_results, pk.peers.data()))) return r;
+  decode_outbox(e->h_out, pk, S, &e->out_msgs);
+  out->msgs = e->out_msgs.data();
+  out->n_msgs = e->out_msgs.size();
+  out->results = e->out_results.data();
+  out->n_results = e->out_results.size();
+  return GR_OK;
+}
+
+int gr_release_outbox(gr_engine* e, gr_outbox* out) {
+  if (!e || !out) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  e->out_msgs.clear();
+  e->out_msgs.shrink_to_fit();
+  e->out_results.clear();
+  e->out_results.shrink_to_fit();
+  out->msgs = nullptr;
+  out->n_msgs = 0;
+  out->results = nullptr;
+  out->n_results = 0;
+  return GR_OK;
+}
+
+int gr_stats_get(gr_engine* e, gr_stats* out) {
+  if (!e || !out) return GR_EINVAL;
+  HIPCHK(hipDeviceSynchronize());
+  std::vector<uint64_t> rows((size_t)e->stats_rows * NSTAT);
+  HIPCHK(hipMemcpy(rows.data(), e->stats, rows.size() * 8, hipMemcpyDeviceToHost));
+  memset(out, 0, sizeof(*out));
+  out->passes = e->passes;
+  for (uint32_t b = 0; b < e->stats_rows; ++b) {
+    const uint64_t* row = rows.data() + (size_t)b * NSTAT;
+    out->leader_commits += row[ST_LEADER_COMMITS];
+    out->follower_commits += row[ST_FOLLOWER_COMMITS];
+    out->escalations += row[ST_ESCALATIONS];
+    out->msgs_in += row[ST_MSGS_IN];
+    out->msgs_out += row[ST_MSGS_OUT];
+  }
+  return GR_OK;
+}
+
+int gr_stats_reset(gr_engine* e) {
+  if (!e) return GR_EINVAL;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemset(e->stats, 0, (size_t)e->stats_rows * NSTAT * 8));
+  e->passes = 0;
+  return GR_OK;
+}
+
+int gr_bind_routes(gr_engine* e, const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n_peers) {
+  if (!e || !in_pos || !out_pos || n_peers > e->cfg.max_peers) return GR_EINVAL;
+  HIPCHK(hipDeviceSynchronize());
+  for (uint32_t j = 0; j < e->S; ++j) {
+    HIPCHK(hipMemcpy(e->ln.in_pos() + (size_t)j * e->cap, in_pos + (size_t)j * n_peers, (size_t)n_peers * 4,
+                     hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->ln.out_pos() + (size_t)j * e->cap, out_pos + (size_t)j * n_peers,
+                     (size_t)n_peers * 4, hipMemcpyHostToDevice));
+  }
+  e->routes_bound = true;
+  return GR_OK;
+}
+
+int gr_set_locals(gr_engine* e, const gr_local_input* locals, size_t n) {
+  if (!e || (n && !locals)) return GR_EINVAL;
+  HIPCHK(hipDeviceSynchronize());
+  std::vector<gr_local_input> byPeer(e->cfg.max_peers);
+  memset(byPeer.data(), 0, byPeer.size() * sizeof(gr_local_input));
+  for (size_t k = 0; k < n; ++k) {
+    if (locals[k].peer >= e->cfg.max_peers) return GR_EINVAL;
+    byPeer[locals[k].peer] = locals[k];
+  }
+  const int r = upload_locals(e, byPeer, e->cfg.max_peers, e->stream);
+  if (r) return r;
+  e->locals_set = n > 0;
+  return GR_OK;
+}
+
+int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t in_chunks,
+                   uint32_t in_positions, uint32_t out_chunks, uint32_t out_positions, uint32_t n_peers,
+                   void* stream) {
+  if (!e || !in_space || !out_space || n_peers > e->cfg.max_peers) return GR_EINVAL;
+  StepParams kp = base_params(e);
+  kp.has_locals = e->locals_set ? 1 : 0;
+  kp.has_lane_peer = 0;
+  kp.has_routes = e->routes_bound ? 1 : 0;
+  kp.in = make_view(in_space, in_chunks, in_positions);
+  kp.out = make_view(out_space, out_chunks, out_positions);
+  kp.n_lanes = n_peers;
+  HIPCHK(launch_slots(e->S, kp, (hipStream_t)stream));
+  e->passes++;
+  return GR_OK;
+}
+
+int gr_collect_results(gr_engine* e, uint32_t first, gr_peer_result* out, size_t n) {
+  if (!e || (n && !out) || (uint64_t)first + n > e->cfg.max_peers) return GR_EINVAL;
+  HIPCHK(hipDeviceSynchronize());
+  std::vector<gr_peer_result> tmp;
+  const int r = download_results(e, first, (uint32_t)n, &tmp, nullptr);
+  if (r) return r;
+  memcpy(out, tmp.data(), n * sizeof(gr_peer_result));
+  return GR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,290 @@
+// gr_host.h — host-side helpers shared by libgpuraft.so and the test-only
+// CPU harness: gr_peer <-> SoA row conversion and the message codec of the
+// mailbox spaces (gr_layout.h). No HIP runtime calls.
+#pragma once
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "gr_layout.h"
+
+namespace gr {
+namespace host {
+
+// Row accessors between gr_peer and the SoA state rows (host side).
+inline uint64_t get_u64_row(const gr_peer& g, uint32_t row, uint32_t S) {
+  if (row < SR_RUN_START) {
+    const uint64_t v[] = {g.term, g.vote, g.committed, g.applied, g.last_index, g.first_index_m1,
+                          g.leader_id, g.leader_transfer_target, g.node_id, g.election_tick,
+                          g.heartbeat_tick, g.randomized_election_timeout, g.election_timeout,
+                          g.heartbeat_timeout, g.entry_size_ub};
+    return v[row];
+  }
+  if (row < SR_RUN_TERM) return g.run_start[row - SR_RUN_START];
+  if (row < SR_REMOTE) return g.run_term[row - SR_RUN_TERM];
+  uint32_t r = row - SR_REMOTE;
+  if (r < S) return g.remotes[r].match;
+  r -= S;
+  if (r < S) return g.remotes[r].next;
+  r -= S;
+  if (r < S) return g.remotes[r].snapshot_index;
+  r -= S;
+  if (r < S) return g.remote_id[r];
+  r -= S;
+  if (r < GR_Q) return g.read_index[r].index;
+  r -= GR_Q;
+  if (r < GR_Q) return g.read_index[r].ctx_low;
+  r -= GR_Q;
+  return g.read_index[r].ctx_high;
+}
+inline void set_u64_row(gr_peer& g, uint32_t row, uint32_t S, uint64_t v) {
+  if (row < SR_RUN_START) {
+    uint64_t* f[] = {&g.term, &g.vote, &g.committed, &g.applied, &g.last_index, &g.first_index_m1,
+                     &g.leader_id, &g.leader_transfer_target, &g.node_id, &g.election_tick,
+                     &g.heartbeat_tick, &g.randomized_election_timeout, &g.election_timeout,
+                     &g.heartbeat_timeout, &g.entry_size_ub};
+    *f[row] = v;
+    return;
+  }
+  if (row < SR_RUN_TERM) { g.run_start[row - SR_RUN_START] = v; return; }
+  if (row < SR_REMOTE) { g.run_term[row - SR_RUN_TERM] = v; return; }
+  uint32_t r = row - SR_REMOTE;
+  if (r < S) { g.remotes[r].match = v; return; }
+  r -= S;
+  if (r < S) { g.remotes[r].next = v; return; }
+  r -= S;
+  if (r < S) { g.remotes[r].snapshot_index = v; return; }
+  r -= S;
+  if (r < S) { g.remote_id[r] = v; return; }
+  r -= S;
+  if (r < GR_Q) { g.read_index[r].index = v; return; }
+  r -= GR_Q;
+  if (r < GR_Q) { g.read_index[r].ctx_low = v; return; }
+  r -= GR_Q;
+  g.read_index[r].ctx_high = v;
+}
+// u8 rows: state flags self n_runs ri_count, rstate[S], ractive[S], rkind[S], rifrom[Q], riack[Q]
+inline uint8_t get_u8_row(const gr_peer& g, uint32_t row, uint32_t S) {
+  switch (row) {
+    case 0: return g.state;
+    case 1: return g.flags;
+    case 2: return g.self_slot;
+    case 3: return g.n_runs;
+    case 4: return g.read_index_count;
+  }
+  uint32_t r = row - 5;
+  if (r < S) return g.remotes[r].state;
+  r -= S;
+  if (r < S) return g.remotes[r].active;
+  r -= S;
+  if (r < S) return g.remotes[r].kind;
+  r -= S;
+  if (r < GR_Q) return g.read_index[r].from_slot;
+  r -= GR_Q;
+  return g.read_index[r].ack_bits;
+}
+inline void set_u8_row(gr_peer& g, uint32_t row, uint32_t S, uint8_t v) {
+  switch (row) {
+    case 0: g.state = v; return;
+    case 1: g.flags = v; return;
+    case 2: g.self_slot = v; return;
+    case 3: g.n_runs = v; return;
+    case 4: g.read_index_count = v; return;
+  }
+  uint32_t r = row - 5;
+  if (r < S) { g.remotes[r].state = v; return; }
+  r -= S;
+  if (r < S) { g.remotes[r].active = v; return; }
+  r -= S;
+  if (r < S) { g.remotes[r].kind = v; return; }
+  r -= S;
+  if (r < GR_Q) { g.read_index[r].from_slot = v; return; }
+  r -= GR_Q;
+  g.read_index[r].ack_bits = v;
+}
+
+inline int validate_msg(const gr_message& m, uint32_t S, uint32_t cap) {
+  if (m.peer >= cap || m.slot >= S) return GR_EINVAL;
+  if (m.type > GR_TIMEOUT_NOW) return GR_EINVAL;
+  if (m.n_runs > 2) return GR_EINVAL;
+  if (m.n_entries == 0 && m.n_runs != 0) return GR_EINVAL;
+  if (m.n_entries != 0 && m.n_runs == 0) return GR_EINVAL;
+  if (m.n_runs == 2 && (m.run2_offset == 0 || m.run2_offset >= m.n_entries)) return GR_EINVAL;
+  return GR_OK;
+}
+
+inline void encode_msg(const Mailbox& mb, uint32_t k, const gr_message& m) {
+  mb.type(k) = m.type;
+  mb.flags(k) = (uint8_t)((m.reject ? MFL_REJECT : 0) | (m.n_runs << MFL_RUNS_SHIFT));
+  mb.n(k) = m.n_entries;
+  mb.run2(k) = m.run2_offset;
+  mb.u64(k, MF_TERM) = m.term;
+  mb.u64(k, MF_LOG_INDEX) = m.log_index;
+  mb.u64(k, MF_LOG_TERM) = m.log_term;
+  mb.u64(k, MF_COMMIT) = m.commit;
+  mb.u64(k, MF_HINT) = m.hint;
+  mb.u64(k, MF_HINT_HIGH) = m.hint_high;
+  mb.u64(k, MF_RT0) = m.run_term[0];
+  mb.u64(k, MF_RT1) = m.run_term[1];
+}
+
+// Decode one message; fields a type does not carry on the device are zero.
+inline gr_message decode_msg(const Mailbox& mb, uint32_t k) {
+  gr_message m;
+  memset(&m, 0, sizeof(m));
+  m.type = mb.type(k);
+  const uint8_t fl = mb.flags(k);
+  m.reject = (fl & MFL_REJECT) ? 1 : 0;
+  m.n_runs = (fl >> MFL_RUNS_SHIFT) & 3u;
+  m.term = mb.u64(k, MF_TERM);
+  switch (m.type) {
+    case GR_REPLICATE:
+      m.n_entries = mb.n(k);
+      m.log_index = mb.u64(k, MF_LOG_INDEX);
+      m.log_term = mb.u64(k, MF_LOG_TERM);
+      m.commit = mb.u64(k, MF_COMMIT);
+      if (m.n_entries) m.run_term[0] = mb.u64(k, MF_RT0);
+      if (m.n_runs == 2) {
+        m.run2_offset = mb.run2(k);
+        m.run_term[1] = mb.u64(k, MF_RT1);
+      }
+      break;
+    case GR_REPLICATE_RESP:
+      m.log_index = mb.u64(k, MF_LOG_INDEX);
+      m.hint = mb.u64(k, MF_HINT);
+      break;
+    case GR_HEARTBEAT:
+      m.commit = mb.u64(k, MF_COMMIT);
+      m.hint = mb.u64(k, MF_HINT);
+      m.hint_high = mb.u64(k, MF_HINT_HIGH);
+      break;
+    case GR_HEARTBEAT_RESP:
+      m.hint = mb.u64(k, MF_HINT);
+      m.hint_high = mb.u64(k, MF_HINT_HIGH);
+      break;
+    default:
+      m.n_entries = mb.n(k);
+      m.run2_offset = mb.run2(k);
+      m.log_index = mb.u64(k, MF_LOG_INDEX);
+      m.log_term = mb.u64(k, MF_LOG_TERM);
+      m.commit = mb.u64(k, MF_COMMIT);
+      m.hint = mb.u64(k, MF_HINT);
+      m.hint_high = mb.u64(k, MF_HINT_HIGH);
+      m.run_term[0] = mb.u64(k, MF_RT0);
+      m.run_term[1] = mb.u64(k, MF_RT1);
+      break;
+  }
+  return m;
+}
+
+
+
+// Pack a gr_step inbox: lanes = sorted unique peers with input; in-space
+// mailboxes only for (lane, slot) pairs that carry messages, filled in
+// arrival order; out-space identity lane*S + slot. Returns GR_* status.
+struct PackedInbox {
+  std::vector<uint32_t> peers;    // lane -> peer
+  std::vector<uint32_t> in_pos;   // [S][nl]
+  std::vector<uint32_t> out_pos;  // [S][nl]
+  std::vector<gr_local_input> locals;  // by lane
+  uint32_t in_positions = 1, out_positions = 0;
+  std::vector<std::pair<uint32_t, uint32_t>> msg_pos;  // message k -> (position, k-th in mailbox)
+  uint32_t lane(uint32_t pp) const {
+    return (uint32_t)(std::lower_bound(peers.begin(), peers.end(), pp) - peers.begin());
+  }
+};
+
+inline int pack_inbox(const gr_inbox* in, uint32_t S, uint32_t max_peers, PackedInbox* pk) {
+  pk->peers.clear();
+  for (size_t k = 0; k < in->n_msgs; ++k) {
+    const int r = validate_msg(in->msgs[k], S, max_peers);
+    if (r) return r;
+    pk->peers.push_back(in->msgs[k].peer);
+  }
+  for (size_t k = 0; k < in->n_locals; ++k) {
+    if (in->locals[k].peer >= max_peers) return GR_EINVAL;
+    pk->peers.push_back(in->locals[k].peer);
+  }
+  std::sort(pk->peers.begin(), pk->peers.end());
+  pk->peers.erase(std::unique(pk->peers.begin(), pk->peers.end()), pk->peers.end());
+  const uint32_t nl = (uint32_t)pk->peers.size();
+  std::vector<uint32_t> mcount((size_t)nl * S, 0);
+  for (size_t k = 0; k < in->n_msgs; ++k) {
+    uint32_t& c = mcount[(size_t)pk->lane(in->msgs[k].peer) * S + in->msgs[k].slot];
+    if (++c > GR_C) return GR_ECAPACITY;
+  }
+  pk->in_pos.assign((size_t)S * nl, NOPOS);
+  uint32_t npos = 0;
+  for (uint32_t l = 0; l < nl; ++l)
+    for (uint32_t j = 0; j < S; ++j)
+      if (mcount[(size_t)l * S + j]) pk->in_pos[(size_t)j * nl + l] = npos++;
+  pk->in_positions = std::max<uint32_t>(npos, 1);
+  pk->out_positions = std::max<uint32_t>(nl * S, 1);
+  pk->out_pos.resize((size_t)S * nl);
+  for (uint32_t j = 0; j < S; ++j)
+    for (uint32_t l = 0; l < nl; ++l) pk->out_pos[(size_t)j * nl + l] = l * S + j;
+  std::vector<uint32_t> fill((size_t)nl * S, 0);
+  pk->msg_pos.resize(in->n_msgs);
+  for (size_t k = 0; k < in->n_msgs; ++k) {
+    const gr_message& m = in->msgs[k];
+    const uint32_t l = pk->lane(m.peer);
+    pk->msg_pos[k] = {pk->in_pos[(size_t)m.slot * nl + l], fill[(size_t)l * S + m.slot]++};
+  }
+  pk->locals.assign(nl, gr_local_input{});
+  for (size_t k = 0; k < in->n_locals; ++k) pk->locals[pk->lane(in->locals[k].peer)] = in->locals[k];
+  return GR_OK;
+}
+
+inline uint64_t space_total_bytes(uint32_t n_chunks, uint32_t positions) {
+  return (uint64_t)n_chunks * space_chunk_bytes_pc(space_pad_positions(positions));
+}
+
+inline SpaceView make_view(const void* base, uint32_t n_chunks, uint32_t positions) {
+  SpaceView v;
+  v.base = (uint8_t*)base;
+  v.n_chunks = n_chunks;
+  v.pc = space_pad_positions(positions);
+  v.chunk_bytes = space_chunk_bytes_pc(v.pc);
+  return v;
+}
+
+inline void encode_inbox(const gr_inbox* in, const PackedInbox& pk, void* space) {
+  const SpaceView v = make_view(space, 1, pk.in_positions);
+  for (size_t k = 0; k < in->n_msgs; ++k) {
+    const Mailbox mb = v.at(pk.msg_pos[k].first);
+    encode_msg(mb, pk.msg_pos[k].second, in->msgs[k]);
+    mb.cnt() = (uint8_t)(pk.msg_pos[k].second + 1);
+  }
+}
+
+inline void decode_outbox(const void* space, const PackedInbox& pk, uint32_t S, std::vector<gr_message>* out) {
+  const SpaceView v = make_view(space, 1, pk.out_positions);
+  const uint32_t nl = (uint32_t)pk.peers.size();
+  for (uint32_t l = 0; l < nl; ++l) {
+    for (uint32_t j = 0; j < S; ++j) {
+      const Mailbox mb = v.at(l * S + j);
+      const uint32_t c = std::min<uint32_t>(mb.cnt(), GR_C);
+      for (uint32_t k = 0; k < c; ++k) {
+        gr_message m = decode_msg(mb, k);
+        m.peer = pk.peers[l];
+        m.slot = (uint8_t)j;
+        out->push_back(m);
+      }
+    }
+  }
+}
+
+// Local-input rows of a lane block (host copies).
+inline void locals_to_rows(const gr_local_input& x, uint32_t* ticks, uint32_t* qticks, uint32_t* prop,
+                           uint8_t* lflags, uint64_t* rlo, uint64_t* rhi, uint64_t* rnd) {
+  *ticks = x.ticks;
+  *qticks = x.quiesced_ticks;
+  *prop = x.propose_entries;
+  *lflags = (uint8_t)((x.read_index ? LF_READ_INDEX : 0) | (x.propose_has_config_change ? LF_PROPOSE_CC : 0));
+  *rlo = x.read_ctx_low;
+  *rhi = x.read_ctx_high;
+  *rnd = x.rand;
+}
+
+}  // namespace host
+}  // namespace gr

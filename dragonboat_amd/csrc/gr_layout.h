@@ -1,0 +1,191 @@
+// gr_layout.h — device data layout of the gpuraft engine.
+//
+// Group state is structure-of-arrays in HBM, all in ONE allocation: row r of
+// the u64 region is the array of one field over all engine slots, so a field
+// address is base + r*8*cap + 8*p, with r a compile-time constant. The kernel
+// therefore takes one base pointer and one row stride instead of ~70 array
+// pointers (keeps the kernel argument small and in SGPRs).
+//   u64 rows: scalar fields, term-run window [GR_K] x2, remotes [S] x4,
+//             ReadIndex FIFO [GR_Q] x3
+//   u8 rows:  scalar fields, remotes [S] x3, ReadIndex FIFO [GR_Q] x2
+// Per-remote fields are [slot j][peer p], so a wave reading "match of slot j"
+// for 64 consecutive peers reads 512 contiguous bytes.
+//
+// Messages live in "spaces" of mailboxes. A mailbox holds up to GR_C messages
+// sent by one remote to one peer in one pass; message fields are SoA inside a
+// chunk so a wave of lanes reading "message k of its mailbox" is coalesced.
+// Chunk layout (pc = positions per chunk, a multiple of 64):
+//   [cnt u8 x pc] then for k < GR_C: [type u8 x pc][flags u8 x pc]
+//   [n u32 x pc][run2 u32 x pc][8 x (u64 x pc)] — u64 fields below.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gpuraft.h"
+
+namespace gr {
+
+constexpr uint32_t NOPOS = 0xFFFFFFFFu;
+
+// ---------------------------------------------------------------- state rows
+enum U64Row : uint32_t {
+  SR_TERM = 0, SR_VOTE, SR_COMMITTED, SR_APPLIED, SR_LAST_INDEX, SR_LO, SR_LEADER_ID, SR_LTT,
+  SR_NODE_ID, SR_ETICK, SR_HTICK, SR_RETIMEOUT, SR_ETIMEOUT, SR_HTIMEOUT, SR_ENTRY_UB,
+  SR_RUN_START,                    // + r, r < GR_K
+  SR_RUN_TERM = SR_RUN_START + GR_K,  // + r
+  SR_REMOTE = SR_RUN_TERM + GR_K,     // remote rows start; see below
+};
+template <int S>
+struct Rows {
+  static constexpr uint32_t MATCH = SR_REMOTE;        // + j
+  static constexpr uint32_t NEXT = MATCH + S;         // + j
+  static constexpr uint32_t SNAP = NEXT + S;          // + j
+  static constexpr uint32_t RID = SNAP + S;           // + j
+  static constexpr uint32_t RI_INDEX = RID + S;       // + q
+  static constexpr uint32_t RI_LO = RI_INDEX + GR_Q;  // + q
+  static constexpr uint32_t RI_HI = RI_LO + GR_Q;     // + q
+  static constexpr uint32_t NU64 = RI_HI + GR_Q;
+  // u8 rows (after the u64 region)
+  static constexpr uint32_t B_STATE = 0, B_FLAGS = 1, B_SELF = 2, B_NRUNS = 3, B_RIC = 4;
+  static constexpr uint32_t B_RSTATE = 5;             // + j
+  static constexpr uint32_t B_RACTIVE = B_RSTATE + S; // + j
+  static constexpr uint32_t B_RKIND = B_RACTIVE + S;  // + j
+  static constexpr uint32_t B_RIFROM = B_RKIND + S;   // + q
+  static constexpr uint32_t B_RIACK = B_RIFROM + GR_Q;// + q
+  static constexpr uint32_t NU8 = B_RIACK + GR_Q;
+};
+__host__ __device__ inline uint32_t pad_cap(uint32_t n) { return (n + 63u) & ~63u; }
+__host__ __device__ inline uint32_t rows_u64(uint32_t S) { return SR_REMOTE + 4 * S + 3 * GR_Q; }
+__host__ __device__ inline uint32_t rows_u8(uint32_t S) { return 5 + 3 * S + 2 * GR_Q; }
+__host__ __device__ inline uint64_t state_bytes(uint32_t S, uint32_t cap) {
+  return (uint64_t)cap * (8ull * rows_u64(S) + rows_u8(S));
+}
+
+struct StateBase {
+  uint8_t* base;
+  uint32_t cap;  // padded, multiple of 64
+  uint32_t S;
+  __host__ __device__ inline uint64_t* u64(uint32_t row) const {
+    return reinterpret_cast<uint64_t*>(base) + (uint64_t)row * cap;
+  }
+  __host__ __device__ inline uint8_t* u8(uint32_t row) const {
+    return base + 8ull * cap * rows_u64(S) + (uint64_t)row * cap;
+  }
+};
+
+// ---------------------------------------------------------------- lane rows
+// Per-pass arrays indexed by lane: local inputs and results.
+enum LaneU64Row : uint32_t {
+  LR_RI_LO = 0, LR_RI_HI, LR_RAND, LR_APPEND_FROM, LR_PROPOSE_FIRST,
+  LR_RTR_INDEX,                         // + q
+  LR_RTR_LO = LR_RTR_INDEX + GR_Q,      // + q
+  LR_RTR_HI = LR_RTR_LO + GR_Q,         // + q
+  LR_NU64 = LR_RTR_HI + GR_Q,
+};
+enum LaneU32Row : uint32_t { LR_TICKS = 0, LR_QTICKS, LR_PROPOSE, LR_ESC_ITEM, LR_LANE_PEER, LR_NU32 };
+enum LaneU8Row : uint32_t { LR_LFLAGS = 0, LR_RFLAGS, LR_ESC_REASON, LR_PROP_RESULT, LR_RTR_COUNT, LR_NU8 };
+__host__ __device__ inline uint64_t lane_bytes(uint32_t S, uint32_t lcap) {
+  // + in_pos / out_pos route tables [S][lcap] u32 each
+  return (uint64_t)lcap * (8ull * LR_NU64 + 4ull * LR_NU32 + LR_NU8 + 8ull * S);
+}
+struct LaneBase {
+  uint8_t* base;
+  uint32_t lcap;
+  uint32_t S;
+  __host__ __device__ inline uint64_t* u64(uint32_t row) const {
+    return reinterpret_cast<uint64_t*>(base) + (uint64_t)row * lcap;
+  }
+  __host__ __device__ inline uint32_t* u32(uint32_t row) const {
+    return reinterpret_cast<uint32_t*>(base + 8ull * LR_NU64 * lcap) + (uint64_t)row * lcap;
+  }
+  __host__ __device__ inline uint8_t* u8(uint32_t row) const {
+    return base + (8ull * LR_NU64 + 4ull * LR_NU32) * lcap + (uint64_t)row * lcap;
+  }
+  __host__ __device__ inline uint32_t* in_pos() const {
+    return reinterpret_cast<uint32_t*>(base + (8ull * LR_NU64 + 4ull * LR_NU32 + LR_NU8) * lcap);
+  }
+  __host__ __device__ inline uint32_t* out_pos() const { return in_pos() + (uint64_t)S * lcap; }
+};
+constexpr uint8_t LF_READ_INDEX = 0x01;
+constexpr uint8_t LF_PROPOSE_CC = 0x02;
+constexpr uint8_t RF_ESCALATED = 0x01;
+constexpr uint8_t RF_PROPOSE = 0x02;
+constexpr uint8_t RF_READY = 0x04;
+constexpr uint8_t RF_APPEND = 0x08;
+
+// ---------------------------------------------------------------- message spaces
+enum U64Field : uint32_t {
+  MF_TERM = 0, MF_LOG_INDEX = 1, MF_LOG_TERM = 2, MF_COMMIT = 3,
+  MF_HINT = 4, MF_HINT_HIGH = 5, MF_RT0 = 6, MF_RT1 = 7, MF_NUM_U64 = 8
+};
+constexpr uint8_t MFL_REJECT = 0x01;
+constexpr uint8_t MFL_RUNS_SHIFT = 1;  // bits 1..2: n_runs
+
+__host__ __device__ inline uint32_t space_pad_positions(uint32_t positions) {
+  return (positions + 63u) & ~63u;
+}
+__host__ __device__ inline uint64_t space_k_bytes(uint32_t pc) { return (uint64_t)pc * (2 + 8 + 8 * MF_NUM_U64); }
+__host__ __device__ inline uint64_t space_chunk_bytes_pc(uint32_t pc) {
+  uint64_t b = (uint64_t)pc + GR_C * space_k_bytes(pc);
+  return (b + 255u) & ~(uint64_t)255u;
+}
+
+struct Mailbox {
+  uint8_t* chunk;
+  uint32_t local;
+  uint32_t pc;
+  __host__ __device__ inline uint8_t* kblock(uint32_t k) const {
+    return chunk + pc + (uint64_t)k * space_k_bytes(pc);
+  }
+  __host__ __device__ inline uint8_t& cnt() const { return chunk[local]; }
+  __host__ __device__ inline uint8_t& type(uint32_t k) const { return kblock(k)[local]; }
+  __host__ __device__ inline uint8_t& flags(uint32_t k) const { return kblock(k)[pc + local]; }
+  __host__ __device__ inline uint32_t& n(uint32_t k) const {
+    return reinterpret_cast<uint32_t*>(kblock(k) + 2ull * pc)[local];
+  }
+  __host__ __device__ inline uint32_t& run2(uint32_t k) const {
+    return reinterpret_cast<uint32_t*>(kblock(k) + 6ull * pc)[local];
+  }
+  __host__ __device__ inline uint64_t& u64(uint32_t k, uint32_t f) const {
+    return reinterpret_cast<uint64_t*>(kblock(k) + 10ull * pc + (uint64_t)f * 8ull * pc)[local];
+  }
+};
+
+struct SpaceView {
+  uint8_t* base;
+  uint32_t n_chunks;
+  uint32_t pc;
+  uint64_t chunk_bytes;
+  __host__ __device__ inline Mailbox at(uint32_t gpos) const {
+    uint32_t c = gpos / pc;
+    Mailbox m;
+    m.chunk = base + (uint64_t)c * chunk_bytes;
+    m.local = gpos - c * pc;
+    m.pc = pc;
+    return m;
+  }
+};
+
+// Stats partials: one row of NSTAT u64 per workgroup, owned by that workgroup.
+enum StatField : uint32_t {
+  ST_PASSES = 0, ST_LEADER_COMMITS = 1, ST_FOLLOWER_COMMITS = 2, ST_ESCALATIONS = 3,
+  ST_MSGS_IN = 4, ST_MSGS_OUT = 5, NSTAT = 8
+};
+
+// Kernel argument (small, passed by value, lives in SGPRs).
+// Lane i steps peer lane_peer[i] (identity when has_lane_peer == 0). Route
+// tables live in the lane block; has_routes == 0 => identity i*S + j.
+struct StepParams {
+  StateBase st;
+  LaneBase ln;
+  SpaceView in, out;
+  uint64_t* stats;     // [gridDim.x][NSTAT] or nullptr
+  uint64_t max_entry_size;
+  uint32_t n_lanes;
+  uint8_t has_locals;
+  uint8_t has_lane_peer;
+  uint8_t has_routes;
+  uint8_t pad;
+};
+
+}  // namespace gr

@@ -1,0 +1,172 @@
+"""Python binding of libgpuraft.so (the product C-ABI, include/gpuraft.h).
+
+This is the host-side mirror a Go ``internal/gpuraft`` package would be
+(INTEGRATION.md): load groups, step them with messages and local inputs, read
+back messages, results and state. The library is loaded from the in-tree
+build (``dragonboat_amd/_build``); there is no fallback: if the HIP library
+is missing or no GPU is usable, construction raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libgpuraft.so")
+_lib = None
+
+
+class GpuRaftError(RuntimeError):
+    pass
+
+
+def load_library(path=LIB_PATH):
+    """Load the HIP engine library (import torch first so one HIP runtime is shared)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise GpuRaftError(f"libgpuraft.so not built at {path}; run __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
+    c = ctypes
+    lib.gr_create.argtypes = [c.POINTER(abi.Config), c.POINTER(c.c_void_p)]
+    lib.gr_destroy.argtypes = [c.c_void_p]
+    lib.gr_destroy.restype = None
+    lib.gr_strerror.restype = c.c_char_p
+    lib.gr_strerror.argtypes = [c.c_int]
+    lib.gr_escalation_name.restype = c.c_char_p
+    lib.gr_escalation_name.argtypes = [c.c_int]
+    lib.gr_load_groups.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p, c.c_size_t]
+    lib.gr_sync_groups_to_host.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p, c.c_size_t]
+    lib.gr_step.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.POINTER(abi.Outbox)]
+    lib.gr_release_outbox.argtypes = [c.c_void_p, c.POINTER(abi.Outbox)]
+    lib.gr_stats_get.argtypes = [c.c_void_p, c.POINTER(abi.Stats)]
+    lib.gr_stats_reset.argtypes = [c.c_void_p]
+    lib.gr_space_bytes.restype = c.c_uint64
+    lib.gr_space_bytes.argtypes = [c.c_uint32, c.c_uint32]
+    lib.gr_space_chunk_bytes.restype = c.c_uint64
+    lib.gr_space_chunk_bytes.argtypes = [c.c_uint32]
+    lib.gr_bind_routes.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32]
+    lib.gr_set_locals.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
+    lib.gr_step_device.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32,
+                                   c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p]
+    lib.gr_collect_results.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p, c.c_size_t]
+    lib.gr_space_decode.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_void_p, c.c_size_t,
+                                    c.POINTER(c.c_size_t)]
+    lib.gr_space_encode.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_void_p, c.c_size_t,
+                                    c.c_void_p]
+    _lib = lib
+    return lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise GpuRaftError(f"{what}: {load_library().gr_strerror(rc).decode()} ({rc})")
+
+
+class Engine:
+    """One engine = one device's slab of group slots (engine slots 0..max_peers-1)."""
+
+    def __init__(self, max_peers, slots=3, device=0, max_entry_size=abi.MAX_ENTRY_SIZE):
+        lib = load_library()
+        cfg = abi.Config(max_peers=max_peers, slots=slots, window_runs=abi.GR_K,
+                         read_index_depth=abi.GR_Q, mailbox_depth=abi.GR_C, device=device,
+                         max_entry_size=max_entry_size)
+        h = ctypes.c_void_p()
+        _check(lib.gr_create(ctypes.byref(cfg), ctypes.byref(h)), "gr_create")
+        self._h = h
+        self.max_peers = max_peers
+        self.slots = slots
+        self.lib = lib
+
+    def close(self):
+        if self._h:
+            self.lib.gr_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load(self, peers, first=0):
+        peers = np.ascontiguousarray(peers, dtype=abi.PEER)
+        _check(self.lib.gr_load_groups(self._h, first, peers.ctypes.data, len(peers)), "gr_load_groups")
+
+    def sync(self, n=None, first=0):
+        n = self.max_peers - first if n is None else n
+        out = np.zeros(n, dtype=abi.PEER)
+        _check(self.lib.gr_sync_groups_to_host(self._h, first, out.ctypes.data, n), "gr_sync")
+        return out
+
+    def step(self, msgs=None, locals_=None):
+        """One synchronous pass (gr_step). Returns (messages, results) record arrays."""
+        msgs = np.zeros(0, abi.MESSAGE) if msgs is None else np.ascontiguousarray(msgs, abi.MESSAGE)
+        locals_ = np.zeros(0, abi.LOCAL) if locals_ is None else np.ascontiguousarray(locals_, abi.LOCAL)
+        ib = abi.inbox_of(msgs, locals_)
+        ob = abi.Outbox()
+        _check(self.lib.gr_step(self._h, ctypes.byref(ib), ctypes.byref(ob)), "gr_step")
+        out = np.zeros(ob.n_msgs, abi.MESSAGE)
+        res = np.zeros(ob.n_results, abi.RESULT)
+        if ob.n_msgs:
+            ctypes.memmove(out.ctypes.data, ob.msgs, ob.n_msgs * abi.MESSAGE.itemsize)
+        if ob.n_results:
+            ctypes.memmove(res.ctypes.data, ob.results, ob.n_results * abi.RESULT.itemsize)
+        _check(self.lib.gr_release_outbox(self._h, ctypes.byref(ob)), "gr_release_outbox")
+        return out, res
+
+    def stats(self):
+        s = abi.Stats()
+        _check(self.lib.gr_stats_get(self._h, ctypes.byref(s)), "gr_stats_get")
+        return {k: getattr(s, k) for k, _ in abi.Stats._fields_}
+
+    def reset_stats(self):
+        _check(self.lib.gr_stats_reset(self._h), "gr_stats_reset")
+
+    # ---- device-resident path -------------------------------------------------
+    def space_bytes(self, n_chunks, positions):
+        return int(self.lib.gr_space_bytes(n_chunks, positions))
+
+    def chunk_bytes(self, positions):
+        return int(self.lib.gr_space_chunk_bytes(positions))
+
+    def bind_routes(self, in_pos, out_pos):
+        """in_pos/out_pos: uint32 arrays [slots][n_peers] (mailbox positions, 0xFFFFFFFF = none)."""
+        in_pos = np.ascontiguousarray(in_pos, np.uint32)
+        out_pos = np.ascontiguousarray(out_pos, np.uint32)
+        n = in_pos.shape[1]
+        _check(self.lib.gr_bind_routes(self._h, in_pos.ctypes.data, out_pos.ctypes.data, n), "gr_bind_routes")
+
+    def set_locals(self, locals_):
+        locals_ = np.ascontiguousarray(locals_, abi.LOCAL)
+        _check(self.lib.gr_set_locals(self._h, locals_.ctypes.data if len(locals_) else None,
+                                      len(locals_)), "gr_set_locals")
+
+    def step_device(self, in_ptr, out_ptr, in_chunks, in_positions, out_chunks, out_positions,
+                    n_peers, stream=0):
+        _check(self.lib.gr_step_device(self._h, in_ptr, out_ptr, in_chunks, in_positions, out_chunks,
+                                       out_positions, n_peers, stream), "gr_step_device")
+
+    def collect_results(self, n=None, first=0):
+        n = self.max_peers - first if n is None else n
+        out = np.zeros(n, abi.RESULT)
+        _check(self.lib.gr_collect_results(self._h, first, out.ctypes.data, n), "gr_collect_results")
+        return out
+
+
+def decode_space(buf, n_chunks, positions):
+    """Decode a host copy of a message space (bytes/uint8 array) into records.
+
+    peer = mailbox position, slot = index within the mailbox."""
+    lib = load_library()
+    buf = np.ascontiguousarray(buf, np.uint8)
+    n = ctypes.c_size_t()
+    _check(lib.gr_space_decode(buf.ctypes.data, n_chunks, positions, None, 0, ctypes.byref(n)), "decode")
+    out = np.zeros(n.value, abi.MESSAGE)
+    if n.value:
+        _check(lib.gr_space_decode(buf.ctypes.data, n_chunks, positions, out.ctypes.data, n.value,
+                                   ctypes.byref(n)), "decode")
+    return out

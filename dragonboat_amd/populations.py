@@ -1,0 +1,119 @@
+"""Synthetic Raft group populations and replica topologies (BASELINE.json configs).
+
+Peers are laid out replica-major: engine slot p = r * G + g holds replica r of
+group g, so the followers of 64 consecutive groups are 64 consecutive slots and
+every per-field access of a wave stays contiguous. Replica r of a group has
+node id r + 1 and remote slot r in every member's slot table; replica 0 is the
+leader unless a generator says otherwise.
+"""
+import numpy as np
+
+from . import abi
+
+NOPOS = 0xFFFFFFFF
+
+
+def make_groups(G, R=3, seed=2, term_lo=1, term_hi=5, base_index=2**32, spread=2**20,
+                election=10, heartbeat=1, check_quorum=False, payload=16, slots=None,
+                log_span=1024):
+    """Steady-state groups: leader at term T, followers caught up, all committed.
+
+    BASELINE config 2/4: T ~ U[term_lo, term_hi] and lastIndex = 2^32 + U[0, 2^20)
+    (exercises the upper 32 bits of every index)."""
+    S = slots or R
+    rng = np.random.default_rng(seed)
+    T = rng.integers(term_lo, term_hi + 1, G).astype(np.uint64)
+    hi = (np.uint64(base_index) + rng.integers(0, spread, G).astype(np.uint64))
+    lo = hi - np.uint64(log_span)
+    peers = np.zeros(R * G, abi.PEER)
+    for r in range(R):
+        v = peers[r * G:(r + 1) * G]
+        v["term"] = T
+        v["vote"] = 1
+        v["committed"] = hi
+        v["applied"] = hi
+        v["last_index"] = hi
+        v["first_index_m1"] = lo
+        v["leader_id"] = 1
+        v["node_id"] = r + 1
+        v["election_timeout"] = election
+        v["heartbeat_timeout"] = heartbeat
+        v["randomized_election_timeout"] = election + rng.integers(0, election, G)
+        v["election_tick"] = 0 if r == 0 else rng.integers(0, election, G)
+        v["entry_size_ub"] = 128 + payload
+        two = T > 1
+        v["n_runs"] = np.where(two, 2, 1)
+        v["run_start"][:, 0] = lo
+        v["run_term"][:, 0] = np.where(two, T - np.uint64(1), T)
+        v["run_start"][:, 1] = np.where(two, hi, 0)
+        v["run_term"][:, 1] = np.where(two, T, 0)
+        for j in range(R):
+            v["remote_id"][:, j] = j + 1
+            v["remotes"][:, j]["kind"] = abi.SLOT_VOTER
+            if r == 0:  # leader: followers in Replicate state, caught up
+                v["remotes"][:, j]["match"] = hi
+                v["remotes"][:, j]["next"] = hi + np.uint64(1)
+                v["remotes"][:, j]["state"] = abi.RETRY if j == 0 else abi.REPLICATE_ST
+                v["remotes"][:, j]["active"] = 0 if j == 0 else 1
+            else:  # follower: remotes as reset() leaves them
+                v["remotes"][:, j]["match"] = hi if j == r else 0
+                v["remotes"][:, j]["next"] = hi + np.uint64(1)
+                v["remotes"][:, j]["state"] = abi.RETRY
+        v["state"] = abi.LEADER if r == 0 else abi.FOLLOWER
+        v["self_slot"] = r
+        v["flags"] = abi.F_CHECK_QUORUM if check_quorum else 0
+    for j in range(R, S):
+        peers["remotes"][:, j]["kind"] = abi.SLOT_EMPTY
+    return peers
+
+
+class Topology:
+    """Replica-major topology: slot j of peer p talks to replica j of the same group."""
+
+    def __init__(self, G, R):
+        self.G, self.R = G, R
+        p = np.arange(R * G, dtype=np.int64)
+        self.group = p % G
+        self.replica = p // G
+
+    def dest(self, peer, slot):
+        """Engine slot of the remote in `slot` of `peer`, and the sender's slot at the receiver."""
+        peer = np.asarray(peer, np.int64)
+        slot = np.asarray(slot, np.int64)
+        return slot * self.G + peer % self.G, peer // self.G
+
+    def route_messages(self, out):
+        """Outbox records (peer = sender, slot = target) -> inbox records of the next pass."""
+        nxt = out.copy()
+        dp, ds = self.dest(out["peer"], out["slot"])
+        nxt["peer"] = dp.astype(np.uint32)
+        nxt["slot"] = ds.astype(np.uint8)
+        # stable order: by receiver, then sender slot, then arrival
+        order = np.lexsort((np.arange(len(nxt)), nxt["slot"], nxt["peer"]))
+        return nxt[order]
+
+    def loopback_routes(self, S):
+        """in_pos/out_pos tables [S][n] for a one-space loopback: mailbox p*S + j."""
+        n = self.R * self.G
+        p = np.arange(n, dtype=np.int64)
+        in_pos = np.full((S, n), NOPOS, np.uint32)
+        out_pos = np.full((S, n), NOPOS, np.uint32)
+        for j in range(self.R):
+            other = self.replica != j
+            in_pos[j, other] = (p[other] * S + j).astype(np.uint32)
+            dp = j * self.G + self.group
+            out_pos[j, other] = (dp[other] * S + self.replica[other]).astype(np.uint32)
+        return in_pos, out_pos
+
+
+def propose_locals(n_peers, leaders, entries=1, seed=0, pass_index=0, ticks=0, quiesced=None):
+    """Per-pass local inputs: `entries` proposals on each leader slot, random draws for all."""
+    loc = np.zeros(n_peers, abi.LOCAL)
+    loc["peer"] = np.arange(n_peers, dtype=np.uint32)
+    loc["propose_entries"][leaders] = entries
+    loc["ticks"] = ticks
+    if quiesced is not None:
+        loc["quiesced_ticks"] = quiesced
+    rng = np.random.default_rng([seed, pass_index])
+    loc["rand"] = rng.integers(0, 2**63, n_peers, dtype=np.uint64)
+    return loc

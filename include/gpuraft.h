@@ -1,0 +1,278 @@
+/*
+ * gpuraft.h — C-ABI of libgpuraft.so, the MI355X batched Raft state-advance
+ * engine (dragonboat_amd).
+ *
+ * Drop-in boundary for dragonboat's raft step path. In the reference, each
+ * step worker (execengine.go:432-523) walks its ready clusters and calls
+ * node.stepNode() (node.go:638-650), which drives raft.Peer one group at a
+ * time: Peer.Handle per inbound message (peer.go:199-209), Peer.ReadIndex
+ * (peer.go:262-269), Peer.Tick/QuiescedTick (peer.go:104-112) and
+ * Peer.ProposeEntries (peer.go:126-134), in the order of node.handleEvents
+ * (node.go:652-676) / handleReceivedMessages (node.go:746-780).
+ * This library replaces that per-group loop (execengine.go:453-465) with one
+ * device pass over every loaded group; a Go package internal/gpuraft binds it
+ * through cgo. Plain C types only: no torch, no HIP types.
+ *
+ * Conventions:
+ *  - int return: 0 = OK, negative = gr_error. Never aborts.
+ *  - Inputs are caller-owned and read only during the call. Outbox arrays are
+ *    engine-owned pinned memory, valid until gr_release_outbox() or the next
+ *    gr_step() (the LookupDBStateMachine/FreeLookupResult pairing of
+ *    internal/cpp/wrapper.go:242-258).
+ *  - A reference invariant panic (e.g. logentry.go:284-287, readindex.go:55-58)
+ *    never aborts here: the group escalates with GR_ESC_PANIC and the host
+ *    re-runs that item with the unchanged Go code, which panics identically.
+ *  - Peers are addressed by engine slot (0..max_peers-1). Remote nodes of a
+ *    peer are addressed by remote slot (0..slots-1); the host keeps the
+ *    slot <-> NodeID map (gr_peer.remote_id) and resolves m.From before
+ *    packing, dropping responses from non-members as Peer.Handle does.
+ */
+#ifndef GPURAFT_H_
+#define GPURAFT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Build-time capacities (a gr_config must match them). */
+#define GR_K 4    /* term runs per group window (entryLog.term window) */
+#define GR_Q 4    /* ReadIndex FIFO depth (readIndex.queue, readindex.go:31-34) */
+#define GR_C 4    /* messages per (peer, remote slot) mailbox per pass */
+#define GR_SMAX 8 /* remote slots per peer (voters + observers, incl. self) */
+#define GR_SLOT_NONE 0xFF
+
+/* raftpb/raft.pb.go:26-50 */
+enum gr_msg_type {
+  GR_LOCAL_TICK = 0, GR_ELECTION = 1, GR_LEADER_HEARTBEAT = 2, GR_CONFIG_CHANGE_EVENT = 3,
+  GR_NOOP = 4, GR_PING = 5, GR_PONG = 6, GR_PROPOSE = 7, GR_SNAPSHOT_STATUS = 8,
+  GR_UNREACHABLE = 9, GR_CHECK_QUORUM = 10, GR_BATCHED_READ_INDEX = 11, GR_REPLICATE = 12,
+  GR_REPLICATE_RESP = 13, GR_REQUEST_VOTE = 14, GR_REQUEST_VOTE_RESP = 15,
+  GR_INSTALL_SNAPSHOT = 16, GR_HEARTBEAT = 17, GR_HEARTBEAT_RESP = 18, GR_READ_INDEX = 19,
+  GR_READ_INDEX_RESP = 20, GR_QUIESCE = 21, GR_SNAPSHOT_RECEIVED = 22,
+  GR_LEADER_TRANSFER = 23, GR_TIMEOUT_NOW = 24
+};
+
+/* raft.go:58-66 */
+enum gr_raft_state { GR_FOLLOWER = 0, GR_CANDIDATE = 1, GR_LEADER = 2, GR_OBSERVER = 3 };
+/* remote.go:29-34 */
+enum gr_remote_state { GR_RETRY = 0, GR_WAIT = 1, GR_REPLICATE_ST = 2, GR_SNAPSHOT_ST = 3 };
+/* membership of a remote slot: raft.remotes (voter) / raft.observers */
+enum gr_slot_kind { GR_SLOT_EMPTY = 0, GR_SLOT_VOTER = 1, GR_SLOT_OBSERVER = 2 };
+
+/* gr_peer.flags */
+#define GR_F_CHECK_QUORUM 0x01              /* raft.checkQuorum */
+#define GR_F_IS_LEADER_TRANSFER_TARGET 0x02 /* raft.isLeaderTransferTarget */
+#define GR_F_PENDING_CONFIG_CHANGE 0x04     /* raft.pendingConfigChange */
+
+/* Why a group left the device fast path for the rest of a pass. */
+enum gr_escalation {
+  GR_ESC_NONE = 0,
+  GR_ESC_TERM_WINDOW = 1,    /* term lookup below the device term window (LogReader.Term path) */
+  GR_ESC_RANDOM = 2,         /* a second reset() in one pass needs another random draw */
+  GR_ESC_UNSUPPORTED = 3,    /* message/state pair handled by the host (votes, snapshots, candidate) */
+  GR_ESC_ELECTION = 4,       /* campaign() (raft.go:779-807) */
+  GR_ESC_PANIC = 5,          /* the reference would panic on this item */
+  GR_ESC_CAPACITY = 6,       /* mailbox / ReadIndex FIFO / ReadyToRead capacity */
+  GR_ESC_SNAPSHOT = 7,       /* Replicate needs entries below firstIndex: InstallSnapshot path */
+  GR_ESC_ENTRY_SIZE = 8,     /* settings.Soft.MaxEntrySize may bind (raft.go:513) */
+  GR_ESC_MSG_RUNS = 9,       /* Replicate entries span more than 2 term runs */
+  GR_ESC_NONMEMBER = 10,     /* target node id has no remote slot */
+  GR_ESC_CONFIG_CHANGE = 11  /* proposal carries a ConfigChangeEntry (raft.go:1134-1143) */
+};
+
+enum gr_error {
+  GR_OK = 0,
+  GR_EINVAL = -1,
+  GR_ENOMEM = -2,
+  GR_EDEVICE = -3,
+  GR_ERANGE = -4,
+  GR_ECAPACITY = -5,
+  GR_ESTATE = -6
+};
+
+typedef struct gr_config {
+  uint32_t max_peers;         /* engine slots */
+  uint32_t slots;             /* remote slots per peer, 1..GR_SMAX (3 for R=3, 5 for R=5) */
+  uint32_t window_runs;       /* must equal GR_K */
+  uint32_t read_index_depth;  /* must equal GR_Q */
+  uint32_t mailbox_depth;     /* must equal GR_C */
+  uint32_t device;            /* HIP device ordinal */
+  uint64_t max_entry_size;    /* settings.Soft.MaxEntrySize (soft.go:236) */
+} gr_config;
+
+/* remote.go:47-54 */
+typedef struct gr_remote {
+  uint64_t match, next, snapshot_index;
+  uint8_t state;  /* gr_remote_state */
+  uint8_t active; /* remote.active */
+  uint8_t kind;   /* gr_slot_kind */
+  uint8_t pad[5];
+} gr_remote;
+
+/* readindex.go:21-26; the confirmed map is a bitmap over remote slots */
+typedef struct gr_read_status {
+  uint64_t index, ctx_low, ctx_high;
+  uint8_t from_slot; /* GR_SLOT_NONE = NoNode (local Peer.ReadIndex) */
+  uint8_t ack_bits;  /* readStatus.confirmed */
+  uint8_t pad[6];
+} gr_read_status;
+
+/*
+ * Per-group state the device owns while the group is loaded: the fields of
+ * raft (raft.go:124-154), entryLog (logentry.go:79-84) and the remotes that
+ * the step path reads or writes. The log itself is represented by a term-run
+ * window: runs (run_start[i], run_term[i]), i < n_runs, strictly increasing
+ * starts, run i covering [run_start[i], run_start[i+1]) and the last run
+ * covering up to last_index. term(index) is 0 outside [first_index_m1,
+ * last_index] (logentry.go:141-145) and escalates below run_start[0].
+ */
+typedef struct gr_peer {
+  uint64_t term, vote;
+  uint64_t committed;      /* entryLog.committed */
+  uint64_t applied;        /* raft.applied (NotifyRaftLastApplied), read by hasConfigChangeToApply */
+  uint64_t last_index;     /* entryLog.lastIndex() */
+  uint64_t first_index_m1; /* entryLog.firstIndex() - 1 */
+  uint64_t leader_id, leader_transfer_target, node_id;
+  uint64_t election_tick, heartbeat_tick, randomized_election_timeout;
+  uint64_t election_timeout, heartbeat_timeout;
+  uint64_t entry_size_ub;  /* upper bound of Entry.SizeUpperLimit() in this log (host-maintained) */
+  uint64_t run_start[GR_K], run_term[GR_K];
+  uint64_t remote_id[GR_SMAX];
+  gr_remote remotes[GR_SMAX];
+  gr_read_status read_index[GR_Q];
+  uint8_t state;           /* gr_raft_state */
+  uint8_t n_runs;
+  uint8_t self_slot;       /* slot whose remote_id == node_id, GR_SLOT_NONE if self removed */
+  uint8_t flags;           /* GR_F_* */
+  uint8_t read_index_count;
+  uint8_t pad[3];
+} gr_peer;
+
+/*
+ * A step-path message (raftpb.Message, raft.pb.go:780-794, restricted to the
+ * fields the step reads). Entries travel as term runs: entries have indexes
+ * log_index+1 .. log_index+n_entries; entries [0, run2_offset) have term
+ * run_term[0], entries [run2_offset, n_entries) have run_term[1]
+ * (n_runs = 0 when n_entries = 0, 1 or 2 otherwise). Payloads stay host-side.
+ */
+typedef struct gr_message {
+  uint32_t peer;       /* inbox: receiving engine slot; outbox: sending engine slot */
+  uint8_t type;        /* gr_msg_type */
+  uint8_t slot;        /* inbox: sender's remote slot; outbox: target remote slot */
+  uint8_t reject;
+  uint8_t n_runs;
+  uint32_t n_entries;
+  uint32_t run2_offset;
+  uint64_t term, log_index, log_term, commit, hint, hint_high;
+  uint64_t run_term[2];
+} gr_message;
+
+/* Per-pass local inputs of one peer, processed after its messages in the
+ * order of node.handleReceivedMessages/handleEvents (node.go:652-780):
+ * batched ReadIndex, ticks (clamped by the host to ElectionRTT, node.go:728),
+ * quiesced ticks, then ProposeEntries. */
+typedef struct gr_local_input {
+  uint32_t peer;
+  uint32_t ticks;          /* Peer.Tick() calls */
+  uint32_t quiesced_ticks; /* Peer.QuiescedTick() calls after the normal ticks */
+  uint32_t propose_entries;/* ProposeEntries batch size, 0 = none */
+  uint8_t read_index;      /* Peer.ReadIndex(ctx) this pass */
+  uint8_t propose_has_config_change;
+  uint8_t pad[6];
+  uint64_t read_ctx_low, read_ctx_high;
+  uint64_t rand;           /* next random.LockGuardedRand.Uint64() draw for reset() */
+} gr_local_input;
+
+/* propose outcome */
+enum gr_propose_result { GR_PROP_NONE = 0, GR_PROP_APPENDED = 1, GR_PROP_DROPPED = 2, GR_PROP_FORWARDED = 3 };
+
+typedef struct gr_ready_to_read {
+  uint64_t index, ctx_low, ctx_high;
+} gr_ready_to_read;
+
+typedef struct gr_peer_result {
+  uint32_t peer;
+  uint8_t escalation;      /* gr_escalation */
+  uint8_t propose_result;  /* gr_propose_result */
+  uint8_t n_ready;
+  uint8_t pad;
+  uint32_t esc_item;       /* first item NOT applied on device (messages, read index, ticks, qticks, propose) */
+  uint32_t pad2;
+  uint64_t append_from;    /* lowest index appended by Replicate this pass (0 = none): persist [append_from, last] */
+  uint64_t propose_first;  /* index of the first proposed entry when appended */
+  gr_ready_to_read ready[GR_Q];
+} gr_peer_result;
+
+typedef struct gr_inbox {
+  const gr_message* msgs;
+  size_t n_msgs;
+  const gr_local_input* locals;
+  size_t n_locals;
+} gr_inbox;
+
+typedef struct gr_outbox {
+  gr_message* msgs;        /* engine-owned */
+  size_t n_msgs;
+  gr_peer_result* results; /* one per peer that had input or produced output */
+  size_t n_results;
+} gr_outbox;
+
+typedef struct gr_stats {
+  uint64_t passes;
+  uint64_t leader_commits;   /* leaders whose committed advanced, summed over passes */
+  uint64_t follower_commits;
+  uint64_t escalations;
+  uint64_t msgs_in, msgs_out;
+} gr_stats;
+
+typedef struct gr_engine gr_engine;
+
+/* Lifetime. */
+int gr_create(const gr_config* cfg, gr_engine** out);
+void gr_destroy(gr_engine* e);
+const char* gr_strerror(int err);
+const char* gr_escalation_name(int esc);
+
+/* Load groups into engine slots [first, first+n) / read them back (the
+ * loadBucketNodes hook, execengine.go:403-430, and the escalation hand-off). */
+int gr_load_groups(gr_engine* e, uint32_t first, const gr_peer* peers, size_t n);
+int gr_sync_groups_to_host(gr_engine* e, uint32_t first, gr_peer* out, size_t n);
+
+/* One synchronous pass over host buffers (what a cgo caller uses). */
+int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out);
+int gr_release_outbox(gr_engine* e, gr_outbox* out);
+int gr_stats_get(gr_engine* e, gr_stats* out);
+int gr_stats_reset(gr_engine* e);
+
+/*
+ * Device-resident path (benchmarks, multi-GPU exchange). Messages live in
+ * "spaces": n_chunks chunks of `positions` mailboxes, each mailbox holding up
+ * to GR_C messages in structure-of-arrays form. in_pos[j*max_peers+p] /
+ * out_pos[j*max_peers+p] give the mailbox that peer p reads from / writes to
+ * for remote slot j (0xFFFFFFFF = none). A chunk is one contiguous byte range,
+ * so chunked spaces can be exchanged with one all-to-all.
+ */
+uint64_t gr_space_bytes(uint32_t n_chunks, uint32_t positions);
+uint64_t gr_space_chunk_bytes(uint32_t positions);
+int gr_bind_routes(gr_engine* e, const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n_peers);
+int gr_set_locals(gr_engine* e, const gr_local_input* locals, size_t n);
+/* Launch one pass on `stream` (a hipStream_t, may be NULL) without syncing.
+ * in_space/out_space are device pointers laid out by gr_space_bytes(). */
+int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t in_chunks,
+                   uint32_t in_positions, uint32_t out_chunks, uint32_t out_positions,
+                   uint32_t n_peers, void* stream);
+/* Copy per-peer results of the last device pass for peers [first, first+n). */
+int gr_collect_results(gr_engine* e, uint32_t first, gr_peer_result* out, size_t n);
+/* Decode the messages of a device space into gr_message records (testing). */
+int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t positions,
+                    gr_message* out, size_t cap, size_t* n_out);
+int gr_space_encode(void* space_host, uint32_t n_chunks, uint32_t positions,
+                    const gr_message* msgs, size_t n, const uint32_t* pos_of_msg);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPURAFT_H_ */

@@ -1,0 +1,584 @@
+// batch.cpp — TEST INFRASTRUCTURE: the oracle as a population of faithful
+// raft objects (raft_oracle.hpp) driven through the gpuraft record formats
+// (include/gpuraft.h), so parity tests can feed identical inputs to the GPU
+// engine and to the CPU restatement and compare every output.
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load
+// this library (oracle/_build/liboracle.so). It is never part of the product.
+//
+// Per pass and per peer, inputs are applied in the engine's documented order,
+// which is one of the orders node.stepNode can produce (node.go:652-780):
+// messages grouped by sender slot (arrival order within a slot) through
+// Peer.Handle (peer.go:199-209), then Peer.ReadIndex, Peer.Tick x n,
+// Peer.QuiescedTick x n, Peer.ProposeEntries.
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <thread>
+#include <vector>
+
+#include "gpuraft.h"
+#include "raft_oracle.hpp"
+
+using namespace oracle;
+
+namespace {
+
+// A sparse ILogDB over term runs: the persisted log is [marker+1, last] with
+// terms given by runs; entries are materialised on demand with a fixed
+// payload size, so SizeUpperLimit() equals the host's entry_size_ub.
+// Semantics follow TestLogDB (logdb_test.go:99-150).
+struct RunLogDB : ILogDB {
+  u64 marker = 0, markerTerm = 0, last = 0;
+  std::vector<std::pair<u64, u64>> runs;  // (start, term), starts ascending, covering (marker, last]
+  size_t payload = 16;
+  State st;
+  Snapshot snap;
+
+  u64 termAt(u64 i) const {  // i in (marker, last]
+    u64 t = runs.empty() ? markerTerm : runs[0].second;
+    for (auto& r : runs)
+      if (r.first <= i) t = r.second;
+    return t;
+  }
+  std::pair<u64, u64> GetRange() override { return {marker + 1, last}; }
+  State NodeState(Membership* m) override {
+    if (m) *m = snap.membership;
+    return st;
+  }
+  void SetState(const State& s) override { st = s; }
+  Err CreateSnapshot(const Snapshot&) override { return Err::None; }
+  Err ApplySnapshot(const Snapshot&) override { return Err::None; }
+  Snapshot GetSnapshot() override { return snap; }
+  u64 Term(u64 index, Err* err) override {
+    *err = Err::None;
+    if (index == marker) return markerTerm;
+    auto e = Entries(index, index + 1, UINT64_MAX, err);
+    if (*err != Err::None) return 0;
+    if (e.empty()) return 0;
+    return e[0].Term;
+  }
+  std::vector<Entry> Entries(u64 low, u64 high, u64 maxSize, Err* err) override {
+    *err = Err::None;
+    if (low <= marker) { *err = Err::Compacted; return {}; }
+    if (high > last + 1) { *err = Err::Unavailable; return {}; }
+    if (last == marker) { *err = Err::Unavailable; return {}; }
+    std::vector<Entry> out;
+    u64 total = 0;
+    for (u64 i = low; i < high; i++) {
+      Entry e;
+      e.Index = i;
+      e.Term = termAt(i);
+      e.Cmd.assign(payload, 0);
+      total += (u64)e.SizeUpperLimit();
+      if (!out.empty() && total > maxSize) break;  // limitSize
+      out.push_back(std::move(e));
+    }
+    return out;
+  }
+  Err Compact(u64) override { return Err::None; }
+  Err Append(std::vector<Entry> es) override {
+    if (es.empty()) return Err::None;
+    u64 first = es[0].Index;
+    if (first <= marker) panicf("RunLogDB append below marker");
+    if (first > last + 1) panicf("RunLogDB hole");
+    while (!runs.empty() && runs.back().first >= first) runs.pop_back();
+    for (auto& e : es) {
+      u64 prevTerm = runs.empty() ? (e.Index - 1 == marker ? markerTerm : ~0ull) : runs.back().second;
+      if (runs.empty() || prevTerm != e.Term) runs.push_back({e.Index, e.Term});
+    }
+    last = es.back().Index;
+    return Err::None;
+  }
+};
+
+using u8 = uint8_t;
+
+struct OPeer {
+  std::unique_ptr<RunLogDB> db;
+  std::unique_ptr<raft> r;
+  std::vector<u64> ids;   // slot -> node id
+  std::vector<u8> kinds;  // slot -> gr_slot_kind
+  u64 entryUB = 0;
+  std::vector<u64> rand;  // draws for the current pass
+  size_t randNext = 0;
+  u64 appendFrom = 0;
+  uint32_t slotOf(u64 id) const {
+    for (size_t j = 0; j < ids.size(); ++j)
+      if (kinds[j] != GR_SLOT_EMPTY && ids[j] == id) return (uint32_t)j;
+    return GR_SLOT_NONE;
+  }
+};
+
+}  // namespace
+
+struct ob_pop {
+  uint32_t S = 0;
+  u64 maxEntrySize = MaxEntrySize;
+  std::vector<OPeer> peers;
+};
+
+namespace {
+
+void build_peer(const gr_peer& g, uint32_t S, u64 maxEntrySize, OPeer* op) {
+  op->db.reset(new RunLogDB());
+  RunLogDB& db = *op->db;
+  const u64 lo = g.first_index_m1, hi = g.last_index;
+  db.marker = lo;
+  db.last = hi;
+  db.payload = g.entry_size_ub >= 128 ? (size_t)(g.entry_size_ub - 128) : 0;
+  // term at lo: the first run if it starts at lo, else that run's term (the
+  // region below the device window is filled with the oldest known term).
+  db.markerTerm = g.n_runs ? g.run_term[0] : 0;
+  for (int k = 0; k < g.n_runs; ++k) {
+    u64 s = std::max(g.run_start[k], lo + 1);
+    if (s > hi) continue;
+    if (!db.runs.empty() && db.runs.back().first == s) db.runs.back().second = g.run_term[k];
+    else db.runs.push_back({s, g.run_term[k]});
+  }
+  Config c;
+  c.NodeID = g.node_id;
+  c.ElectionRTT = g.election_timeout;
+  c.HeartbeatRTT = g.heartbeat_timeout;
+  c.CheckQuorum = (g.flags & GR_F_CHECK_QUORUM) != 0;
+  c.IsObserver = g.state == GR_OBSERVER;
+  OPeer* self = op;
+  op->r.reset(new raft(c, &db, [self]() -> u64 {
+    u64 v;
+    if (self->randNext < self->rand.size()) v = self->rand[self->randNext];
+    else v = SplitMix64(self->rand.empty() ? 7 : self->rand.back() + self->randNext)();
+    self->randNext++;
+    return v;
+  }));
+  raft& r = *op->r;
+  r.maxEntrySize = maxEntrySize;
+  r.term = g.term;
+  r.vote = g.vote;
+  r.log->committed = g.committed;
+  r.log->applied = lo;
+  r.applied = g.applied;
+  r.state = (RaftState)g.state;
+  r.leaderID = g.leader_id;
+  r.leaderTransferTarget = g.leader_transfer_target;
+  r.isLeaderTransferTarget = (g.flags & GR_F_IS_LEADER_TRANSFER_TARGET) != 0;
+  r.pendingConfigChange = (g.flags & GR_F_PENDING_CONFIG_CHANGE) != 0;
+  r.checkQuorum = (g.flags & GR_F_CHECK_QUORUM) != 0;
+  r.electionTick = g.election_tick;
+  r.heartbeatTick = g.heartbeat_tick;
+  r.randomizedElectionTimeout = g.randomized_election_timeout;
+  r.electionTimeout = g.election_timeout;
+  r.heartbeatTimeout = g.heartbeat_timeout;
+  r.remotes.clear();
+  r.observers.clear();
+  op->ids.assign(S, 0);
+  op->kinds.assign(S, GR_SLOT_EMPTY);
+  for (uint32_t j = 0; j < S; ++j) {
+    op->ids[j] = g.remote_id[j];
+    op->kinds[j] = g.remotes[j].kind;
+    if (g.remotes[j].kind == GR_SLOT_EMPTY) continue;
+    remote rm;
+    rm.match = g.remotes[j].match;
+    rm.next = g.remotes[j].next;
+    rm.snapshotIndex = g.remotes[j].snapshot_index;
+    rm.state = (remoteStateType)g.remotes[j].state;
+    rm.active = g.remotes[j].active != 0;
+    if (g.remotes[j].kind == GR_SLOT_VOTER) r.remotes[g.remote_id[j]] = rm;
+    else r.observers[g.remote_id[j]] = rm;
+  }
+  r.resetMatchValueArray();
+  r.readIdx = readIndex{};
+  for (int q = 0; q < g.read_index_count; ++q) {
+    const gr_read_status& rs = g.read_index[q];
+    SystemCtx ctx{rs.ctx_low, rs.ctx_high};
+    auto s = std::make_shared<readStatus>();
+    s->index = rs.index;
+    s->from = rs.from_slot == GR_SLOT_NONE ? 0 : g.remote_id[rs.from_slot];
+    s->ctx = ctx;
+    for (uint32_t j = 0; j < S; ++j)
+      if (rs.ack_bits & (1u << j)) s->confirmed[g.remote_id[j]] = true;
+    r.readIdx.queue.push_back(ctx);
+    r.readIdx.pending[ctx] = s;
+  }
+  r.msgs.clear();
+  r.readyToRead.clear();
+  op->entryUB = g.entry_size_ub;
+  r.log->onTryAppend = [op](u64 ci) { op->appendFrom = op->appendFrom ? std::min(op->appendFrom, ci) : ci; };
+}
+
+// Term runs of the oracle log over [lo, hi] (lo = firstIndex-1): the logdb
+// part below the in-memory marker, then the in-memory entries.
+std::vector<std::pair<u64, u64>> log_runs(const OPeer& op) {
+  const entryLog& l = *op.r->log;
+  const u64 lo = l.firstIndex() - 1, hi = l.lastIndex();
+  std::vector<std::pair<u64, u64>> runs;
+  auto add = [&](u64 idx, u64 t) {
+    if (runs.empty() || runs.back().second != t) runs.push_back({idx, t});
+  };
+  Err e;
+  add(lo, l.term(lo, &e));
+  const u64 mark = l.inmem.markerIndex;
+  const RunLogDB& db = *op.db;
+  const u64 dbTop = std::min(hi, mark - 1);
+  for (auto& rr : db.runs) {
+    if (rr.first > dbTop) break;
+    u64 nextStart = dbTop + 1;
+    for (auto& r2 : db.runs)
+      if (r2.first > rr.first) { nextStart = r2.first; break; }
+    if (nextStart <= lo + 1) continue;
+    add(std::max(rr.first, lo + 1), rr.second);
+  }
+  for (auto& en : l.inmem.entries)
+    if (en.Index > lo && en.Index <= hi) add(en.Index, en.Term);
+  return runs;
+}
+
+void export_peer(const OPeer& op, uint32_t S, gr_peer* g) {
+  const raft& r = *op.r;
+  memset(g, 0, sizeof(*g));
+  g->term = r.term;
+  g->vote = r.vote;
+  g->committed = r.log->committed;
+  g->applied = r.applied;
+  g->last_index = r.log->lastIndex();
+  g->first_index_m1 = r.log->firstIndex() - 1;
+  g->leader_id = r.leaderID;
+  g->leader_transfer_target = r.leaderTransferTarget;
+  g->node_id = r.nodeID;
+  g->election_tick = r.electionTick;
+  g->heartbeat_tick = r.heartbeatTick;
+  g->randomized_election_timeout = r.randomizedElectionTimeout;
+  g->election_timeout = r.electionTimeout;
+  g->heartbeat_timeout = r.heartbeatTimeout;
+  g->entry_size_ub = op.entryUB;
+  auto runs = log_runs(op);
+  size_t first = runs.size() > GR_K ? runs.size() - GR_K : 0;
+  g->n_runs = (uint8_t)(runs.size() - first);
+  for (size_t k = first; k < runs.size(); ++k) {
+    g->run_start[k - first] = runs[k].first;
+    g->run_term[k - first] = runs[k].second;
+  }
+  g->state = (uint8_t)r.state;
+  g->flags = (uint8_t)((r.checkQuorum ? GR_F_CHECK_QUORUM : 0) |
+                       (r.isLeaderTransferTarget ? GR_F_IS_LEADER_TRANSFER_TARGET : 0) |
+                       (r.pendingConfigChange ? GR_F_PENDING_CONFIG_CHANGE : 0));
+  g->self_slot = GR_SLOT_NONE;
+  for (uint32_t j = 0; j < S; ++j) {
+    g->remote_id[j] = op.ids[j];
+    const remote* rm = nullptr;
+    auto it = r.remotes.find(op.ids[j]);
+    auto ot = r.observers.find(op.ids[j]);
+    uint8_t kind = GR_SLOT_EMPTY;
+    if (op.kinds[j] != GR_SLOT_EMPTY && it != r.remotes.end()) { rm = &it->second; kind = GR_SLOT_VOTER; }
+    else if (op.kinds[j] != GR_SLOT_EMPTY && ot != r.observers.end()) { rm = &ot->second; kind = GR_SLOT_OBSERVER; }
+    g->remotes[j].kind = kind;
+    if (rm) {
+      g->remotes[j].match = rm->match;
+      g->remotes[j].next = rm->next;
+      g->remotes[j].snapshot_index = rm->snapshotIndex;
+      g->remotes[j].state = (uint8_t)rm->state;
+      g->remotes[j].active = rm->active ? 1 : 0;
+      if (op.ids[j] == r.nodeID) g->self_slot = (uint8_t)j;
+    }
+  }
+  int q = 0;
+  for (auto& ctx : r.readIdx.queue) {
+    if (q >= GR_Q) break;
+    auto s = r.readIdx.pending.at(ctx);
+    gr_read_status& rs = g->read_index[q++];
+    rs.index = s->index;
+    rs.ctx_low = ctx.Low;
+    rs.ctx_high = ctx.High;
+    rs.from_slot = s->from == 0 ? GR_SLOT_NONE : (uint8_t)op.slotOf(s->from);
+    uint8_t ack = 0;
+    for (auto& kv : s->confirmed) {
+      uint32_t j = op.slotOf(kv.first);
+      if (j != GR_SLOT_NONE) ack |= (uint8_t)(1u << j);
+    }
+    rs.ack_bits = ack;
+  }
+  g->read_index_count = (uint8_t)q;
+}
+
+// raftpb.Message -> gr_message (target slot, entries as term runs).
+bool to_record(const OPeer& op, uint32_t peer, const Message& m, gr_message* o) {
+  memset(o, 0, sizeof(*o));
+  o->peer = peer;
+  o->type = (uint8_t)m.Type;
+  o->slot = (uint8_t)op.slotOf(m.To);
+  o->reject = m.Reject ? 1 : 0;
+  o->term = m.Term;
+  o->log_index = m.LogIndex;
+  o->log_term = m.LogTerm;
+  o->commit = m.Commit;
+  o->hint = m.Hint;
+  o->hint_high = m.HintHigh;
+  o->n_entries = (uint32_t)m.Entries.size();
+  bool ok = o->slot != GR_SLOT_NONE;
+  if (!m.Entries.empty()) {
+    o->n_runs = 1;
+    o->run_term[0] = m.Entries[0].Term;
+    for (size_t k = 1; k < m.Entries.size(); ++k) {
+      if (m.Entries[k].Term != m.Entries[k - 1].Term) {
+        if (o->n_runs == 2) { ok = false; break; }
+        o->n_runs = 2;
+        o->run2_offset = (uint32_t)k;
+        o->run_term[1] = m.Entries[k].Term;
+      }
+    }
+  }
+  return ok;
+}
+
+Message from_record(const OPeer& op, const gr_message& g) {
+  Message m;
+  m.Type = (MessageType)g.type;
+  m.From = op.ids[g.slot];
+  m.To = op.r->nodeID;
+  m.Term = g.term;
+  m.LogIndex = g.log_index;
+  m.LogTerm = g.log_term;
+  m.Commit = g.commit;
+  m.Reject = g.reject != 0;
+  m.Hint = g.hint;
+  m.HintHigh = g.hint_high;
+  const size_t payload = op.entryUB >= 128 ? (size_t)(op.entryUB - 128) : 0;
+  for (uint32_t k = 0; k < g.n_entries; ++k) {
+    Entry e;
+    e.Index = g.log_index + 1 + k;
+    e.Term = (g.n_runs == 2 && k >= g.run2_offset) ? g.run_term[1] : g.run_term[0];
+    e.Cmd.assign(payload, 0);
+    m.Entries.push_back(std::move(e));
+  }
+  return m;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ob_create(uint32_t slots, uint64_t max_entry_size, const gr_peer* peers, uint32_t n, ob_pop** out) {
+  if (!out || (n && !peers) || slots == 0 || slots > GR_SMAX) return GR_EINVAL;
+  ob_pop* p = new ob_pop();
+  p->S = slots;
+  p->maxEntrySize = max_entry_size;
+  p->peers.resize(n);
+  try {
+    for (uint32_t k = 0; k < n; ++k) build_peer(peers[k], slots, max_entry_size, &p->peers[k]);
+  } catch (const std::exception&) {
+    delete p;
+    return GR_ESTATE;
+  }
+  *out = p;
+  return GR_OK;
+}
+
+void ob_destroy(ob_pop* p) { delete p; }
+
+int ob_export(ob_pop* p, gr_peer* out, uint32_t n) {
+  if (!p || n > p->peers.size()) return GR_EINVAL;
+  for (uint32_t k = 0; k < n; ++k) export_peer(p->peers[k], p->S, &out[k]);
+  return GR_OK;
+}
+
+// Persist and apply everything after a pass (node.go processRaftUpdate /
+// Peer.Commit): entriesToSave -> LogDB, StableLogTo, AppliedTo = committed,
+// NotifyRaftLastApplied(committed). Keeps in-memory logs bounded in long runs.
+int ob_commit_all(ob_pop* p) {
+  if (!p) return GR_EINVAL;
+  for (auto& op : p->peers) {
+    raft& r = *op.r;
+    auto es = r.log->entriesToSave();
+    if (!es.empty()) {
+      op.db->Append(es);
+      UpdateCommit uc;
+      uc.StableLogTo = es.back().Index;
+      uc.StableLogTerm = es.back().Term;
+      r.log->commitUpdate(uc);
+    }
+    if (r.log->committed > r.log->applied) {
+      UpdateCommit ac;
+      ac.AppliedTo = r.log->committed;
+      r.log->commitUpdate(ac);
+    }
+    r.applied = r.log->committed;
+  }
+  return GR_OK;
+}
+
+// One pass over the population. For peer p, items are numbered as the engine
+// numbers them (messages, ReadIndex, ticks, one quiesced-tick item, propose).
+// If limits != NULL, mid[p] receives the state after items < limits[p] and
+// results/ready reflect only that prefix; messages carry the emitting item
+// index in out_item so callers can split device-prefix and host-suffix output.
+// n_threads > 1 steps disjoint peer ranges concurrently (clusterID % T, the
+// FixedPartitioner rule of internal/server/partition.go:34-36).
+int ob_step(ob_pop* p, const gr_inbox* in, const uint32_t* limits, gr_peer* mid, gr_message* out,
+            uint32_t* out_item, size_t cap, size_t* n_out, gr_peer_result* results, uint32_t n_threads,
+            char* err, size_t errcap) {
+  if (!p || !in || !n_out) return GR_EINVAL;
+  const uint32_t n = (uint32_t)p->peers.size(), S = p->S;
+  // bucket messages per peer, slot-major then arrival order
+  std::vector<std::vector<std::vector<const gr_message*>>> box(n, std::vector<std::vector<const gr_message*>>(S));
+  for (size_t k = 0; k < in->n_msgs; ++k) {
+    const gr_message& m = in->msgs[k];
+    if (m.peer >= n || m.slot >= S) return GR_EINVAL;
+    box[m.peer][m.slot].push_back(&m);
+  }
+  std::vector<const gr_local_input*> loc(n, nullptr);
+  for (size_t k = 0; k < in->n_locals; ++k) {
+    if (in->locals[k].peer >= n) return GR_EINVAL;
+    loc[in->locals[k].peer] = &in->locals[k];
+  }
+  struct Out {
+    uint32_t peer, item;
+    gr_message rec;
+    bool ok;
+  };
+  if (n_threads == 0) n_threads = 1;
+  std::vector<std::vector<Out>> outs(n_threads);
+  std::vector<std::string> errs(n_threads);
+  auto work = [&](uint32_t t) {
+    for (uint32_t pi = t; pi < n; pi += n_threads) {
+      OPeer& op = p->peers[pi];
+      raft& r = *op.r;
+      const uint32_t limit = limits ? limits[pi] : 0xFFFFFFFFu;
+      r.msgs.clear();
+      r.readyToRead.clear();
+      op.appendFrom = 0;
+      op.rand.clear();
+      op.randNext = 0;
+      if (loc[pi]) op.rand.push_back(loc[pi]->rand);
+      uint32_t item = 0;
+      gr_peer_result res;
+      memset(&res, 0, sizeof(res));
+      res.peer = pi;
+      bool midTaken = false;
+      auto take_mid = [&]() {
+        if (midTaken) return;
+        midTaken = true;
+        if (mid) export_peer(op, S, &mid[pi]);
+        res.n_ready = (uint8_t)std::min<size_t>(r.readyToRead.size(), 255);
+        for (size_t q = 0; q < r.readyToRead.size() && q < GR_Q; ++q) {
+          res.ready[q].index = r.readyToRead[q].Index;
+          res.ready[q].ctx_low = r.readyToRead[q].ctx.Low;
+          res.ready[q].ctx_high = r.readyToRead[q].ctx.High;
+        }
+        res.append_from = op.appendFrom;
+      };
+      auto flush = [&](uint32_t it) {
+        for (auto& m : r.msgs) {
+          Out o;
+          o.peer = pi;
+          o.item = it;
+          o.ok = to_record(op, pi, m, &o.rec);
+          outs[t].push_back(o);
+        }
+        r.msgs.clear();
+      };
+      try {
+        for (uint32_t j = 0; j < S; ++j) {
+          for (const gr_message* gm : box[pi][j]) {
+            if (item == limit) take_mid();
+            Message m = from_record(op, *gm);
+            // Peer.Handle (peer.go:199-209)
+            bool member = op.kinds[j] != GR_SLOT_EMPTY;
+            if (member || !isResponseMessageType(m.Type)) r.Handle(m);
+            flush(item);
+            item++;
+          }
+        }
+        const gr_local_input* L = loc[pi];
+        if (L) {
+          if (L->read_index) {
+            if (item == limit) take_mid();
+            SystemCtx ctx{L->read_ctx_low, L->read_ctx_high};
+            Message m;
+            m.Type = ReadIndex;
+            m.Hint = ctx.Low;
+            m.HintHigh = ctx.High;
+            r.Handle(m);  // Peer.ReadIndex (peer.go:262-269)
+            flush(item);
+            item++;
+          }
+          for (uint32_t k = 0; k < L->ticks; ++k) {
+            if (item == limit) take_mid();
+            r.tick();
+            flush(item);
+            item++;
+          }
+          if (L->quiesced_ticks) {
+            if (item == limit) take_mid();
+            for (uint32_t k = 0; k < L->quiesced_ticks; ++k) r.quiescedTick();
+            item++;
+          }
+          if (L->propose_entries) {
+            if (item == limit) take_mid();
+            const u64 before = r.log->lastIndex();
+            std::vector<Entry> es(L->propose_entries);
+            const size_t payload = op.entryUB >= 128 ? (size_t)(op.entryUB - 128) : 0;
+            for (auto& e : es) e.Cmd.assign(payload, 0);
+            if (L->propose_has_config_change) es[0].Type = ConfigChangeEntry;
+            Message m;
+            m.Type = Propose;
+            m.From = r.nodeID;
+            m.Entries = es;
+            const size_t outBefore = outs[t].size();
+            r.Handle(m);  // Peer.ProposeEntries (peer.go:126-134)
+            bool fwd = false;
+            for (auto& x : r.msgs) fwd = fwd || x.Type == Propose;
+            flush(item);
+            (void)outBefore;
+            if (!midTaken) {
+              if (r.log->lastIndex() > before) {
+                res.propose_result = GR_PROP_APPENDED;
+                res.propose_first = before + 1;
+              } else {
+                res.propose_result = fwd ? GR_PROP_FORWARDED : GR_PROP_DROPPED;
+              }
+            }
+            item++;
+          }
+        }
+        take_mid();
+      } catch (const std::exception& ex) {
+        if (errs[t].empty()) errs[t] = "peer " + std::to_string(pi) + " item " + std::to_string(item) + ": " + ex.what();
+        take_mid();
+        res.escalation = GR_ESC_PANIC;
+        res.esc_item = item;
+      }
+      if (results) results[pi] = res;
+    }
+  };
+  if (n_threads == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < n_threads; ++t) th.emplace_back(work, t);
+    for (auto& x : th) x.join();
+  }
+  size_t k = 0;
+  bool bad = false;
+  for (auto& v : outs) {
+    for (auto& o : v) {
+      if (out && k < cap) {
+        out[k] = o.rec;
+        if (out_item) out_item[k] = o.item;
+      }
+      if (!o.ok) bad = true;
+      k++;
+    }
+  }
+  *n_out = k;
+  std::string e;
+  for (auto& s : errs)
+    if (!s.empty()) { e = s; break; }
+  if (bad && e.empty()) e = "message not representable as a gr_message record";
+  if (err && errcap) {
+    strncpy(err, e.c_str(), errcap - 1);
+    err[errcap - 1] = 0;
+  }
+  if (k > cap && out) return GR_ECAPACITY;
+  return e.empty() ? GR_OK : GR_ESTATE;
+}
+
+}  // extern "C"

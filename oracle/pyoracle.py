@@ -1,0 +1,124 @@
+"""TEST INFRASTRUCTURE: ctypes bindings of the oracle (oracle/_build/liboracle.so)
+and of the test-only host-lane harness (tests/_build/libhostlane.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module. The product (dragonboat_amd) never does.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from dragonboat_amd import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+HOSTLANE_LIB = os.path.join(ROOT, "tests", "_build", "libhostlane.so")
+KAT_BIN = os.path.join(ROOT, "oracle", "_build", "kat_tests")
+
+_olib = None
+_hlib = None
+
+
+def oracle_lib():
+    global _olib
+    if _olib is None:
+        lib = ctypes.CDLL(ORACLE_LIB)
+        c = ctypes
+        lib.ob_create.argtypes = [c.c_uint32, c.c_uint64, c.c_void_p, c.c_uint32, c.POINTER(c.c_void_p)]
+        lib.ob_destroy.argtypes = [c.c_void_p]
+        lib.ob_destroy.restype = None
+        lib.ob_export.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32]
+        lib.ob_commit_all.argtypes = [c.c_void_p]
+        lib.ob_step.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.c_void_p, c.c_void_p, c.c_void_p,
+                                c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t), c.c_void_p, c.c_uint32,
+                                c.c_char_p, c.c_size_t]
+        _olib = lib
+    return _olib
+
+
+def hostlane_lib():
+    global _hlib
+    if _hlib is None:
+        lib = ctypes.CDLL(HOSTLANE_LIB)
+        c = ctypes
+        lib.hl_step.argtypes = [c.c_uint32, c.c_uint64, c.c_void_p, c.c_uint32, c.POINTER(abi.Inbox),
+                                c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t), c.c_void_p,
+                                c.POINTER(c.c_size_t)]
+        _hlib = lib
+    return _hlib
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+class OraclePopulation:
+    """Faithful per-group raft objects (the CPU restatement of internal/raft)."""
+
+    def __init__(self, peers, slots=3, max_entry_size=abi.MAX_ENTRY_SIZE):
+        self.lib = oracle_lib()
+        peers = np.ascontiguousarray(peers, abi.PEER)
+        h = ctypes.c_void_p()
+        rc = self.lib.ob_create(slots, max_entry_size, peers.ctypes.data, len(peers), ctypes.byref(h))
+        if rc:
+            raise OracleError(f"ob_create failed {rc}")
+        self._h = h
+        self.n = len(peers)
+        self.slots = slots
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self.lib.ob_destroy(self._h)
+            self._h = None
+
+    def export(self):
+        out = np.zeros(self.n, abi.PEER)
+        self.lib.ob_export(self._h, out.ctypes.data, self.n)
+        return out
+
+    def commit_all(self):
+        self.lib.ob_commit_all(self._h)
+
+    def step(self, msgs=None, locals_=None, limits=None, threads=1, allow_error=False):
+        """Returns dict(msgs, items, results, mid, error)."""
+        msgs = np.zeros(0, abi.MESSAGE) if msgs is None else np.ascontiguousarray(msgs, abi.MESSAGE)
+        locals_ = np.zeros(0, abi.LOCAL) if locals_ is None else np.ascontiguousarray(locals_, abi.LOCAL)
+        ib = abi.inbox_of(msgs, locals_)
+        lim = None
+        if limits is not None:
+            lim = np.ascontiguousarray(limits, np.uint32)
+        mid = np.zeros(self.n, abi.PEER)
+        res = np.zeros(self.n, abi.RESULT)
+        cap = max(16, 4 * len(msgs) + 8 * self.n * self.slots)
+        out = np.zeros(cap, abi.MESSAGE)
+        items = np.zeros(cap, np.uint32)
+        n_out = ctypes.c_size_t()
+        err = ctypes.create_string_buffer(512)
+        rc = self.lib.ob_step(self._h, ctypes.byref(ib), lim.ctypes.data if lim is not None else None,
+                              mid.ctypes.data, out.ctypes.data, items.ctypes.data, cap, ctypes.byref(n_out),
+                              res.ctypes.data, threads, err, 512)
+        if rc and not (allow_error and rc == -6):
+            raise OracleError(f"ob_step rc={rc}: {err.value.decode()}")
+        n = n_out.value
+        return {"msgs": out[:n], "items": items[:n], "results": res, "mid": mid,
+                "error": err.value.decode() if rc else ""}
+
+
+def hostlane_step(peers, msgs=None, locals_=None, slots=3, max_entry_size=abi.MAX_ENTRY_SIZE):
+    """Run the engine's lane code on the CPU (test-only). Returns (peers', msgs, results)."""
+    lib = hostlane_lib()
+    peers = np.array(peers, dtype=abi.PEER, copy=True)
+    msgs = np.zeros(0, abi.MESSAGE) if msgs is None else np.ascontiguousarray(msgs, abi.MESSAGE)
+    locals_ = np.zeros(0, abi.LOCAL) if locals_ is None else np.ascontiguousarray(locals_, abi.LOCAL)
+    ib = abi.inbox_of(msgs, locals_)
+    cap = max(16, 8 * len(peers) * slots)
+    out = np.zeros(cap, abi.MESSAGE)
+    n_out = ctypes.c_size_t()
+    res = np.zeros(len(peers), abi.RESULT)
+    n_res = ctypes.c_size_t()
+    rc = lib.hl_step(slots, max_entry_size, peers.ctypes.data, len(peers), ctypes.byref(ib), out.ctypes.data,
+                     cap, ctypes.byref(n_out), res.ctypes.data, ctypes.byref(n_res))
+    if rc:
+        raise OracleError(f"hl_step rc={rc}")
+    return peers, out[:n_out.value], res[:n_res.value]

@@ -399,6 +399,7 @@ struct entryLog {
   inMemory inmem;
   u64 committed = 0;
   u64 applied = 0;
+  std::function<void(u64)> onTryAppend;  // observation hook for the batch harness (no effect)
 
   // A struct literal &entryLog{logdb: db} as several reference tests build it
   // (e.g. raft_etcd_test.go:1916-1919): all other fields zero.
@@ -522,6 +523,7 @@ struct entryLog {
       if (conflictIndex <= committed)
         panicf("entry %llu conflicts with committed entry, committed %llu",
                (unsigned long long)conflictIndex, (unsigned long long)committed);
+      if (onTryAppend) onTryAppend(conflictIndex);
       append(slice(ents, conflictIndex - index - 1, ents.size()));
       return true;
     }

@@ -1,0 +1,122 @@
+// hostlane.hip — TEST ONLY. Runs the engine's per-lane step (gr_lane.h) on
+// the CPU over host memory, with exactly the packing gr_step uses
+// (gr_host.h), so lane logic can be checked against the oracle in the
+// no-GPU test tier. It never touches the HIP runtime and is never loaded by
+// the product; the GPU parity tests (-m gpu) run the real kernel.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "gr_host.h"
+#include "gr_lane.h"
+
+using namespace gr;
+using namespace gr::host;
+
+namespace {
+
+template <int S>
+void run_lanes(const StepParams& kp) {
+  for (uint32_t i = 0; i < kp.n_lanes; ++i) {
+    const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+    Lane<S> L(kp, i, p);
+    uint32_t a, b, c, d, e;
+    L.step(&a, &b, &c, &d, &e);
+  }
+}
+
+uint32_t inst(uint32_t want) { return want <= 1 ? 1 : want <= 3 ? 3 : want <= 5 ? 5 : 0; }
+
+}  // namespace
+
+extern "C" int hl_step(uint32_t slots, uint64_t max_entry_size, gr_peer* peers, uint32_t n_peers,
+                       const gr_inbox* in, gr_message* out_msgs, size_t out_cap, size_t* n_out,
+                       gr_peer_result* results, size_t* n_results) {
+  const uint32_t S = inst(slots);
+  if (!S || !in || !n_out || !n_results) return GR_EINVAL;
+  PackedInbox pk;
+  int r = pack_inbox(in, S, n_peers, &pk);
+  if (r) return r;
+  const uint32_t nl = (uint32_t)pk.peers.size();
+  // state rows on the host
+  StateBase st;
+  st.cap = pad_cap(std::max<uint32_t>(n_peers, 1));
+  st.S = S;
+  std::vector<uint64_t> sbuf((state_bytes(S, st.cap) + 7) / 8, 0);
+  st.base = (uint8_t*)sbuf.data();
+  for (uint32_t p = 0; p < n_peers; ++p) {
+    for (uint32_t row = 0; row < rows_u64(S); ++row) st.u64(row)[p] = get_u64_row(peers[p], row, S);
+    for (uint32_t row = 0; row < rows_u8(S); ++row) st.u8(row)[p] = get_u8_row(peers[p], row, S);
+  }
+  LaneBase ln;
+  ln.lcap = pad_cap(std::max<uint32_t>(nl, 1));
+  ln.S = S;
+  std::vector<uint64_t> lbuf((lane_bytes(S, ln.lcap) + 7) / 8, 0);
+  ln.base = (uint8_t*)lbuf.data();
+  for (uint32_t l = 0; l < nl; ++l) {
+    ln.u32(LR_LANE_PEER)[l] = pk.peers[l];
+    locals_to_rows(pk.locals[l], &ln.u32(LR_TICKS)[l], &ln.u32(LR_QTICKS)[l], &ln.u32(LR_PROPOSE)[l],
+                   &ln.u8(LR_LFLAGS)[l], &ln.u64(LR_RI_LO)[l], &ln.u64(LR_RI_HI)[l], &ln.u64(LR_RAND)[l]);
+    for (uint32_t j = 0; j < S; ++j) {
+      ln.in_pos()[(size_t)j * ln.lcap + l] = pk.in_pos[(size_t)j * nl + l];
+      ln.out_pos()[(size_t)j * ln.lcap + l] = pk.out_pos[(size_t)j * nl + l];
+    }
+  }
+  std::vector<uint64_t> ibuf((space_total_bytes(1, pk.in_positions) + 7) / 8, 0);
+  std::vector<uint64_t> obuf((space_total_bytes(1, pk.out_positions) + 7) / 8, 0);
+  encode_inbox(in, pk, ibuf.data());
+  StepParams kp;
+  memset(&kp, 0, sizeof(kp));
+  kp.st = st;
+  kp.ln = ln;
+  kp.in = make_view(ibuf.data(), 1, pk.in_positions);
+  kp.out = make_view(obuf.data(), 1, pk.out_positions);
+  kp.max_entry_size = max_entry_size;
+  kp.n_lanes = nl;
+  kp.has_locals = 1;
+  kp.has_lane_peer = 1;
+  kp.has_routes = 1;
+  if (S == 1) run_lanes<1>(kp);
+  else if (S == 3) run_lanes<3>(kp);
+  else run_lanes<5>(kp);
+  std::vector<gr_message> msgs;
+  decode_outbox(obuf.data(), pk, S, &msgs);
+  *n_out = msgs.size();
+  if (out_msgs) memcpy(out_msgs, msgs.data(), std::min(out_cap, msgs.size()) * sizeof(gr_message));
+  for (uint32_t p = 0; p < n_peers; ++p) {
+    gr_peer g;
+    memset(&g, 0, sizeof(g));
+    for (uint32_t row = 0; row < rows_u64(S); ++row) set_u64_row(g, row, S, st.u64(row)[p]);
+    for (uint32_t row = 0; row < rows_u8(S); ++row) set_u8_row(g, row, S, st.u8(row)[p]);
+    for (uint32_t j = S; j < GR_SMAX; ++j) g.remotes[j].kind = GR_SLOT_EMPTY;
+    peers[p] = g;
+  }
+  *n_results = nl;
+  if (results) {
+    for (uint32_t l = 0; l < nl; ++l) {
+      gr_peer_result& pr = results[l];
+      memset(&pr, 0, sizeof(pr));
+      pr.peer = pk.peers[l];
+      const uint8_t rf = ln.u8(LR_RFLAGS)[l];
+      if (rf & RF_ESCALATED) {
+        pr.escalation = ln.u8(LR_ESC_REASON)[l];
+        pr.esc_item = ln.u32(LR_ESC_ITEM)[l];
+      }
+      if (rf & RF_PROPOSE) {
+        pr.propose_result = ln.u8(LR_PROP_RESULT)[l];
+        pr.propose_first = ln.u64(LR_PROPOSE_FIRST)[l];
+      }
+      if (rf & RF_APPEND) pr.append_from = ln.u64(LR_APPEND_FROM)[l];
+      if (rf & RF_READY) {
+        pr.n_ready = ln.u8(LR_RTR_COUNT)[l];
+        for (int q = 0; q < pr.n_ready && q < GR_Q; ++q) {
+          pr.ready[q].index = ln.u64(LR_RTR_INDEX + q)[l];
+          pr.ready[q].ctx_low = ln.u64(LR_RTR_LO + q)[l];
+          pr.ready[q].ctx_high = ln.u64(LR_RTR_HI + q)[l];
+        }
+      }
+    }
+  }
+  return GR_OK;
+}

@@ -1,0 +1,153 @@
+"""Parity helpers: compare engine outputs (GPU kernel or the test-only host-lane
+build of the same code) with the oracle, field by field, bit-exact.
+
+States are compared on every field of gr_peer except the term-run window,
+which is checked semantically: every device run must describe the oracle's log
+exactly over [run_start[0], last_index] (the device may know fewer old runs
+than the oracle after dropping its oldest run, never a different term).
+Messages are compared per (sender, target slot) as ordered lists: the
+reference orders broadcasts by Go map iteration, so only per-target order is
+defined.
+"""
+import numpy as np
+
+from dragonboat_amd import abi
+
+SCALARS = ["term", "vote", "committed", "applied", "last_index", "first_index_m1", "leader_id",
+           "leader_transfer_target", "node_id", "election_tick", "heartbeat_tick",
+           "randomized_election_timeout", "election_timeout", "heartbeat_timeout", "entry_size_ub",
+           "state", "self_slot", "flags", "read_index_count"]
+MSG_FIELDS = ["type", "slot", "reject", "term", "log_index", "log_term", "commit", "hint", "hint_high",
+              "n_entries", "n_runs", "run2_offset"]
+
+
+def oracle_runs(o):
+    return [(int(o["run_start"][k]), int(o["run_term"][k])) for k in range(int(o["n_runs"]))]
+
+
+def term_at(runs, lo, hi, idx):
+    if idx < lo or idx > hi:
+        return 0
+    t = None
+    for s, tt in runs:
+        if s <= idx:
+            t = tt
+    return t
+
+
+def window_consistent(g, o):
+    """Device window g agrees with oracle export o wherever g claims knowledge."""
+    gr_ = oracle_runs(g)
+    orr = oracle_runs(o)
+    lo, hi = int(o["first_index_m1"]), int(o["last_index"])
+    if int(g["last_index"]) != hi:
+        return False, "last_index"
+    if not gr_:
+        return True, ""
+    if orr and gr_[0][0] < orr[0][0]:
+        return False, f"device window starts below oracle window {gr_[0][0]} < {orr[0][0]}"
+    for k, (s, t) in enumerate(gr_):
+        end = gr_[k + 1][0] - 1 if k + 1 < len(gr_) else hi
+        if s > end:
+            return False, f"empty run {k}"
+        if term_at(orr, lo, hi, s) != t or term_at(orr, lo, hi, end) != t:
+            return False, f"run {k} ({s},{t}) disagrees with oracle {orr}"
+        if k > 0 and term_at(orr, lo, hi, s - 1) == t:
+            return False, f"run boundary {s} is not a term change in {orr}"
+    return True, ""
+
+
+def compare_peer(g, o, S):
+    diffs = []
+    for f in SCALARS:
+        if g[f] != o[f]:
+            diffs.append(f"{f}: engine={g[f]} oracle={o[f]}")
+    for j in range(S):
+        for f in ["match", "next", "snapshot_index", "state", "active", "kind"]:
+            if g["remotes"][j][f] != o["remotes"][j][f]:
+                diffs.append(f"remotes[{j}].{f}: engine={g['remotes'][j][f]} oracle={o['remotes'][j][f]}")
+        if g["remote_id"][j] != o["remote_id"][j]:
+            diffs.append(f"remote_id[{j}]")
+    for q in range(int(o["read_index_count"])):
+        for f in ["index", "ctx_low", "ctx_high", "from_slot", "ack_bits"]:
+            if g["read_index"][q][f] != o["read_index"][q][f]:
+                diffs.append(f"read_index[{q}].{f}: engine={g['read_index'][q][f]} oracle={o['read_index'][q][f]}")
+    ok, why = window_consistent(g, o)
+    if not ok:
+        diffs.append("window: " + why)
+    return diffs
+
+
+def compare_states(eng, orc, S, peers=None, limit=20):
+    idx = range(len(eng)) if peers is None else peers
+    bad = []
+    for p in idx:
+        d = compare_peer(eng[p], orc[p], S)
+        if d:
+            bad.append((int(p), d))
+            if len(bad) >= limit:
+                break
+    return bad
+
+
+def _norm(m):
+    row = [int(m[f]) for f in MSG_FIELDS]
+    if m["type"] == abi.PROPOSE:  # forwarded proposals: payload and terms stay host-side
+        row[MSG_FIELDS.index("n_runs")] = 0
+        row[MSG_FIELDS.index("run2_offset")] = 0
+        return tuple(row) + (0, 0)
+    nr = int(m["n_runs"])
+    return tuple(row) + (int(m["run_term"][0]) if nr >= 1 else 0, int(m["run_term"][1]) if nr == 2 else 0)
+
+
+def group_msgs(msgs):
+    d = {}
+    for m in msgs:
+        d.setdefault((int(m["peer"]), int(m["slot"])), []).append(_norm(m))
+    return d
+
+
+def compare_msgs(eng_msgs, orc_msgs, limit=20):
+    a, b = group_msgs(eng_msgs), group_msgs(orc_msgs)
+    bad = []
+    for k in sorted(set(a) | set(b)):
+        if a.get(k, []) != b.get(k, []):
+            bad.append((k, a.get(k, []), b.get(k, [])))
+            if len(bad) >= limit:
+                break
+    return bad
+
+
+def compare_results(eng_res, orc_res, limit=20):
+    """eng_res: results per lane (peer field); orc_res: per peer (prefix results)."""
+    bad = []
+    for r in eng_res:
+        p = int(r["peer"])
+        o = orc_res[p]
+        fields = ["propose_result", "propose_first", "append_from", "n_ready"]
+        d = [f"{f}: engine={r[f]} oracle={o[f]}" for f in fields if r[f] != o[f]]
+        for q in range(min(int(r["n_ready"]), abi.GR_Q)):
+            if tuple(r["ready"][q]) != tuple(o["ready"][q]):
+                d.append(f"ready[{q}]: engine={r['ready'][q]} oracle={o['ready'][q]}")
+        if d:
+            bad.append((p, d))
+            if len(bad) >= limit:
+                break
+    return bad
+
+
+def limits_from(results, n):
+    lim = np.full(n, 0xFFFFFFFF, np.uint32)
+    for r in results:
+        if r["escalation"]:
+            lim[int(r["peer"])] = r["esc_item"]
+    return lim
+
+
+def prefix_msgs(orc, limits):
+    """Oracle messages emitted by items the engine applied (item < limit of their sender)."""
+    m, it = orc["msgs"], orc["items"]
+    if len(m) == 0:
+        return m
+    keep = it < limits[m["peer"].astype(np.int64)]
+    return m[keep]
