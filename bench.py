@@ -1,0 +1,199 @@
+"""Headline benchmark: commit-index updates/sec for 1M Raft groups x 3 replicas
+(BASELINE.json configs[3]), one device pass per step, inputs resident in HBM.
+
+A step = one pass of the batched raft step over every replica of every group:
+leaders ingest the previous pass's ReplicateResp batch, run the quorum commit
+and propose one 16-byte entry; followers log-match the previous pass's
+Replicate batch. Messages go device-to-device through mailbox spaces (no host
+round trip). In steady state every group's leader advances committed by one
+index per pass; `value` counts those advances (device stats) per second.
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
+per GPU, each owning its own 1M groups ("scaling": "weak"). Replicas of a group
+are placed on ranks g, g+1, g+2 (mod N) when --placement spread (default for
+N > 1) and Replicate/ReplicateResp mailboxes cross GPUs with one RCCL
+all_to_all_single per pass; --placement local keeps replicas on one rank.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# SURVEY.md §8d canonical algorithmic bytes of one group-round (reference field
+# widths): B_round(R) = (R-1)*(69 + 65 + 138) + 8R + 48 -> R=3: 616 B.
+def b_round(R):
+    return (R - 1) * (69 + 65 + 138) + 8 * R + 48
+
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--groups", type=int, default=1_000_000, help="groups per GPU")
+    ap.add_argument("--replicas", type=int, default=3)
+    ap.add_argument("--placement", choices=["local", "spread"], default=None)
+    ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
+    ap.add_argument("--cpu-groups", type=int, default=20000)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--check", action="store_true", help="verify the final state against a host replay")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, R):
+    """The oracle (C++ restatement of the reference Go step, faithful data
+    structures) on a bounded sample of the same workload, host cores only."""
+    import numpy as np
+    from dragonboat_amd import abi, populations as P
+    from oracle.pyoracle import OraclePopulation
+    G = args.cpu_groups
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    peers = P.make_groups(G, R, seed=2)
+    topo = P.Topology(G, R)
+    pop = OraclePopulation(peers, R)
+    msgs = np.zeros(0, abi.MESSAGE)
+    # warm to steady state (2 passes), then time
+    for k in range(2):
+        loc = P.propose_locals(R * G, np.arange(G), pass_index=k)
+        o = pop.step(msgs, loc, threads=threads)
+        msgs = topo.route_messages(o["msgs"])
+    passes, t_step, commits = 0, 0.0, 0
+    before = pop.export()["committed"][:G].copy()
+    t_end = time.time() + 10.0
+    k = 2
+    while time.time() < t_end or passes < 2:
+        loc = P.propose_locals(R * G, np.arange(G), pass_index=k)
+        t0 = time.perf_counter()
+        o = pop.step(msgs, loc, threads=threads)
+        t_step += time.perf_counter() - t0
+        msgs = topo.route_messages(o["msgs"])
+        pop.commit_all()
+        passes += 1
+        k += 1
+    after = pop.export()["committed"][:G]
+    commits = int(np.sum(after - before))
+    return {"value": commits / t_step, "unit": "commit-index updates/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{G} groups x {R} replicas, {passes} passes, oracle raft step timed "
+                      f"(message routing and persistence excluded), {threads} threads"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from dragonboat_amd import abi, populations as P
+    from dragonboat_amd.engine import Engine
+    from dragonboat_amd.exchange import build_exchange
+
+    R = args.replicas
+    S = R
+    G = args.groups
+    placement = args.placement or ("spread" if world > 1 else "local")
+    ex = build_exchange(G, R, S, world, rank, placement)
+    n = ex.n_peers
+    eng = Engine(n, S, device=local_rank)
+    eng.load(ex.peers)
+    eng.bind_routes(ex.in_pos, ex.out_pos)
+    loc = P.propose_locals(n, ex.leader_slots, pass_index=0)
+    eng.set_locals(loc)
+    spaces = ex.allocate(eng, dev)
+    stream = torch.cuda.current_stream()
+
+    def one_pass(k):
+        ex.step(eng, spaces, k, stream)
+
+    for k in range(args.warmup):
+        one_pass(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    eng.reset_stats()
+    kernel_ms = []
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ex.step(eng, spaces, args.warmup + k, stream, events=ev[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kernel_ms = [a.elapsed_time(b) for a, b in ev]
+    st = eng.stats()
+    commits = st["leader_commits"]
+    esc = st["escalations"]
+    if world > 1:
+        t = torch.tensor([commits, esc], dtype=torch.float64, device=dev)
+        dist.all_reduce(t)
+        commits, esc = int(t[0].item()), int(t[1].item())
+    value = commits / elapsed
+    kavg = sum(kernel_ms) / len(kernel_ms)
+    groups_total = G * world
+    achieved = b_round(R) * G / (kavg * 1e-3) / 1e9  # GB/s, per launch of the step kernel
+    if rank == 0:
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "commit-index updates/sec (1M groups x 3 replicas) + achieved HBM GB/s",
+            "value": value,
+            "unit": "commit-index updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic steady-state groups (BASELINE config 4 shape), 16-B proposals",
+            "config": {"workload": f"{G} groups x {R} replicas per GPU, replicas {placement}, "
+                                   f"1 proposal per leader per pass", "groups_total": groups_total,
+                       "replicas": R, "placement": placement},
+            "escalations": esc,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "gr_step_kernel<3>", "kernel_ms": kavg,
+                         "algorithmic_bytes_per_launch": b_round(R) * G},
+        }
+        if args.cpu_baseline == "on" and world == 1:
+            try:
+                line["cpu_baseline"] = cpu_baseline(args, R)
+            except Exception as e:  # baseline is reported, not required
+                line["cpu_baseline"] = {"value": None, "error": str(e)}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

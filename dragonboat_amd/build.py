@@ -1,0 +1,75 @@
+"""Build recipes for the native parts (run by __graft_entry__.build()).
+
+- libgpuraft.so: the product, HIP for gfx950 (hipcc).
+- liboracle.so, kat_tests: the CPU oracle (g++), test infrastructure.
+- libhostlane.so: the engine's lane code compiled for the host, test-only.
+Outputs stay in-tree (git-ignored) so they travel to the GPU box.
+"""
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+ENGINE_SRC = [os.path.join(ROOT, "dragonboat_amd", "csrc", "gr_engine.hip")]
+ENGINE_DEPS = ENGINE_SRC + [os.path.join(ROOT, "dragonboat_amd", "csrc", f)
+                            for f in ("gr_lane.h", "gr_layout.h", "gr_host.h")] + \
+    [os.path.join(ROOT, "include", "gpuraft.h")]
+ENGINE_LIB = os.path.join(ROOT, "dragonboat_amd", "_build", "libgpuraft.so")
+ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+KAT_BIN = os.path.join(ROOT, "oracle", "_build", "kat_tests")
+HOSTLANE_LIB = os.path.join(ROOT, "tests", "_build", "libhostlane.so")
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def build_engine(force=False):
+    os.makedirs(os.path.dirname(ENGINE_LIB), exist_ok=True)
+    if force or _stale(ENGINE_LIB, ENGINE_DEPS):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "dragonboat_amd", "csrc"),
+              *ENGINE_SRC, "-o", ENGINE_LIB])
+    return ENGINE_LIB
+
+
+def build_oracle(force=False):
+    odir = os.path.join(ROOT, "oracle")
+    os.makedirs(os.path.dirname(ORACLE_LIB), exist_ok=True)
+    hdrs = [os.path.join(odir, f) for f in ("raft_oracle.hpp", "oracle_testkit.hpp")] + \
+        [os.path.join(ROOT, "include", "gpuraft.h")]
+    src = os.path.join(odir, "batch.cpp")
+    if force or _stale(ORACLE_LIB, hdrs + [src]):
+        _run(["g++", "-std=c++17", "-O2", "-g", "-fPIC", "-shared", "-I" + odir,
+              "-I" + os.path.join(ROOT, "include"), src, "-o", ORACLE_LIB, "-lpthread"])
+    kat = os.path.join(odir, "kat_tests.cpp")
+    if force or _stale(KAT_BIN, hdrs + [kat]):
+        _run(["g++", "-std=c++17", "-O1", "-g", "-I" + odir, kat, "-o", KAT_BIN])
+    return ORACLE_LIB
+
+
+def build_hostlane(force=False):
+    os.makedirs(os.path.dirname(HOSTLANE_LIB), exist_ok=True)
+    src = os.path.join(ROOT, "tests", "native", "hostlane.hip")
+    if force or _stale(HOSTLANE_LIB, ENGINE_DEPS + [src]):
+        _run([HIPCC, "--cuda-host-only", "-O2", "-g", "-std=c++17", "-fPIC", "-shared",
+              "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "dragonboat_amd", "csrc"),
+              src, "-o", HOSTLANE_LIB])
+    return HOSTLANE_LIB
+
+
+def build_all(force=False):
+    build_engine(force)
+    build_oracle(force)
+    build_hostlane(force)

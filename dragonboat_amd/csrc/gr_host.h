@@ -210,8 +210,9 @@ inline int pack_inbox(const gr_inbox* in, uint32_t S, uint32_t max_peers, Packed
   const uint32_t nl = (uint32_t)pk->peers.size();
   std::vector<uint32_t> mcount((size_t)nl * S, 0);
   for (size_t k = 0; k < in->n_msgs; ++k) {
-    uint32_t& c = mcount[(size_t)pk->lane(in->msgs[k].peer) * S + in->msgs[k].slot];
-    if (++c > GR_C) return GR_ECAPACITY;
+    // more than GR_C messages in one mailbox: the first GR_C travel, the
+    // mailbox is marked overflowed and the receiver escalates there (CAPACITY)
+    ++mcount[(size_t)pk->lane(in->msgs[k].peer) * S + in->msgs[k].slot];
   }
   pk->in_pos.assign((size_t)S * nl, NOPOS);
   uint32_t npos = 0;
@@ -252,6 +253,10 @@ inline void encode_inbox(const gr_inbox* in, const PackedInbox& pk, void* space)
   const SpaceView v = make_view(space, 1, pk.in_positions);
   for (size_t k = 0; k < in->n_msgs; ++k) {
     const Mailbox mb = v.at(pk.msg_pos[k].first);
+    if (pk.msg_pos[k].second >= GR_C) {
+      mb.cnt() = (uint8_t)(GR_C + 1);  // overflow marker
+      continue;
+    }
     encode_msg(mb, pk.msg_pos[k].second, in->msgs[k]);
     mb.cnt() = (uint8_t)(pk.msg_pos[k].second + 1);
   }

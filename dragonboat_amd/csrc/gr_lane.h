@@ -1219,11 +1219,11 @@ struct Lane {
       const uint32_t g = in_gpos(j);
       if (g == NOPOS) continue;
       const Mailbox mb = kp.in.at(g);
-      uint32_t c = mb.cnt();
-      if (c > GR_C) c = GR_C;
+      const uint32_t c = mb.cnt();
 #pragma unroll 1
       for (uint32_t k = 0; k < c; ++k) {
         if (item == limit) { *at = item; return 0; }
+        if (k == GR_C) { *at = item; return GR_ESC_CAPACITY; }  // overflowed mailbox
         InMsg m;
         read_msg(mb, k, m);
         const int e = handle(m, j);

@@ -1,0 +1,141 @@
+"""Device-resident message exchange between passes (the transport's role).
+
+In the reference every Replicate/ReplicateResp leaves a node through
+``transport.Send`` (plugin/transport) and is delivered to the receiving
+node's ``Peer.Handle`` on the next step. Here the engines of all GPUs write
+their outgoing messages straight into mailbox "spaces" in HBM:
+
+* ``local`` placement — all replicas of a group on one GPU: two spaces,
+  ping-ponged; the kernel of pass k reads space k%2 and writes space (k+1)%2.
+  No copy, no collective.
+* ``spread`` placement — replica r of the groups homed on rank h lives on
+  rank (h + r) % N. The out space has one chunk per destination rank, the in
+  space one chunk per source rank, and one RCCL ``all_to_all_single`` with
+  equal chunk splits moves every mailbox across xGMI once per pass.
+
+Peers on a rank are laid out replica-major: peer r*G + g is replica r of the
+group (home = (rank - r) % N, index g), so a wave's accesses stay contiguous.
+"""
+import numpy as np
+
+from . import populations as P
+
+NOPOS = 0xFFFFFFFF
+
+
+def pad_positions(positions):
+    """gr_layout.h space_pad_positions: chunks hold a multiple of 64 mailboxes."""
+    return (positions + 63) & ~63
+
+
+def offset_pairs(R, N):
+    """(sender replica r, receiver replica j) pairs per rank offset (j - r) % N."""
+    pairs = {o: [] for o in range(N)}
+    for r in range(R):
+        for j in range(R):
+            if j != r:
+                pairs[(j - r) % N].append((r, j))
+    return pairs
+
+
+def spread_routes(G, R, S, N, rank):
+    """Route tables for spread placement on `rank`.
+
+    Returns (in_pos [S][R*G], out_pos [S][R*G], positions per chunk). The
+    sender on rank a writes its mailbox for (r -> j, group g) at chunk
+    d = (a - r + j) % N, position pair_index * G + g; all_to_all delivers
+    chunk d of rank a as chunk a of rank d, where the receiver (replica j,
+    same group) reads the same position."""
+    pairs = offset_pairs(R, N)
+    per = max(len(v) for v in pairs.values())
+    positions = per * G
+    pc = pad_positions(positions)
+    index = {}
+    for o, lst in pairs.items():
+        for k, rj in enumerate(lst):
+            index[rj] = k
+    n = R * G
+    g = np.arange(G, dtype=np.int64)
+    in_pos = np.full((S, n), NOPOS, np.uint32)
+    out_pos = np.full((S, n), NOPOS, np.uint32)
+    for r in range(R):
+        for j in range(R):
+            if j == r:
+                continue
+            k = index[(r, j)]
+            # sender: local replica r, slot j -> chunk d
+            d = (rank - r + j) % N
+            out_pos[j, r * G + g] = (d * pc + k * G + g).astype(np.uint32)
+            # receiver: local replica j, slot r <- chunk a (sender rank)
+            a = (rank - j + r) % N
+            in_pos[r, j * G + g] = (a * pc + k * G + g).astype(np.uint32)
+    return in_pos, out_pos, positions
+
+
+def group_seed(seed, home):
+    return [seed, home]
+
+
+def spread_peers(G, R, N, rank, seed=2, **kw):
+    """Peer records for `rank`: replica r of the G groups homed on (rank - r) % N.
+    Every rank regenerates a home's groups from the same seed, so the replicas
+    of one group agree wherever they are placed."""
+    out = np.zeros(R * G, dtype=P.make_groups(1, R).dtype)
+    for r in range(R):
+        h = (rank - r) % N
+        grp = P.make_groups(G, R, seed=int(np.random.SeedSequence(group_seed(seed, h)).generate_state(1)[0]), **kw)
+        out[r * G:(r + 1) * G] = grp[r * G:(r + 1) * G]
+    return out
+
+
+class Exchange:
+    """Spaces + routes for one rank; `step` launches one pass and exchanges."""
+
+    def __init__(self, G, R, S, world, rank, placement, seed=2):
+        self.G, self.R, self.S = G, R, S
+        self.world, self.rank, self.placement = world, rank, placement
+        self.n_peers = R * G
+        self.leader_slots = np.arange(G)  # replica 0 of every hosted group leads
+        if placement == "local":
+            self.peers = P.make_groups(G, R, seed=int(np.random.SeedSequence(group_seed(seed, rank)).generate_state(1)[0]))
+            self.in_pos, self.out_pos = P.Topology(G, R).loopback_routes(S)
+            self.n_chunks = 1
+            self.positions = self.n_peers * S
+        elif placement == "spread":
+            self.peers = spread_peers(G, R, world, rank, seed=seed)
+            self.in_pos, self.out_pos, self.positions = spread_routes(G, R, S, world, rank)
+            self.n_chunks = world
+        else:
+            raise ValueError(placement)
+
+    def allocate(self, eng, device):
+        import torch
+        nbytes = eng.space_bytes(self.n_chunks, self.positions)
+        assert nbytes == self.n_chunks * eng.chunk_bytes(self.positions)
+        a = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+        b = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+        return [a, b]
+
+    def step(self, eng, spaces, k, stream, events=None):
+        """One pass: kernel (optionally bracketed by `events`), then the exchange."""
+        h = stream.cuda_stream
+        if self.placement == "local":
+            src, dst = spaces[k % 2], spaces[(k + 1) % 2]
+        else:
+            src, dst = spaces[0], spaces[1]
+        if events is not None:
+            events[0].record(stream)
+        eng.step_device(src.data_ptr(), dst.data_ptr(), self.n_chunks, self.positions,
+                        self.n_chunks, self.positions, self.n_peers, h)
+        if events is not None:
+            events[1].record(stream)
+        if self.placement == "spread":
+            import torch.distributed as dist
+            if self.world > 1:
+                dist.all_to_all_single(spaces[0], spaces[1])
+            else:
+                spaces[0].copy_(spaces[1])
+
+
+def build_exchange(G, R, S, world, rank, placement, seed=2):
+    return Exchange(G, R, S, world, rank, placement, seed=seed)

@@ -117,3 +117,89 @@ def propose_locals(n_peers, leaders, entries=1, seed=0, pass_index=0, ticks=0, q
     rng = np.random.default_rng([seed, pass_index])
     loc["rand"] = rng.integers(0, 2**63, n_peers, dtype=np.uint64)
     return loc
+
+
+def _push_run(rec, start, term):
+    n = int(rec["n_runs"])
+    if n and int(rec["run_term"][n - 1]) == int(term):
+        return
+    if n < abi.GR_K:
+        rec["run_start"][n] = start
+        rec["run_term"][n] = term
+        rec["n_runs"] = n + 1
+    else:
+        rec["run_start"][:-1] = rec["run_start"][1:].copy()
+        rec["run_term"][:-1] = rec["run_term"][1:].copy()
+        rec["run_start"][-1] = start
+        rec["run_term"][-1] = term
+
+
+def _last_term(rec):
+    n = int(rec["n_runs"])
+    return int(rec["run_term"][n - 1]) if n else 0
+
+
+def inject_leader_change(state, topo, p, rng, max_div=8, max_extra=4):
+    """BASELINE config 5 fault injection on settled groups (one leader, all at term T).
+
+    The old leader L appended d+e entries at term T and replicated the first d
+    only to follower F; F then wins an election for term T+1 (becomeLeader,
+    raft.go:689-702: reset remotes, append a no-op). The third replica keeps its
+    log. Next passes exercise rejects (Hint = lastIndex), decreaseTo/becomeRetry
+    and getConflictIndex truncation of L's divergent suffix. Returns changed slots.
+    """
+    G, R = topo.G, topo.R
+    st = state.reshape(R, G)
+    terms = st["term"]
+    leaders = st["state"] == abi.LEADER
+    settled = (leaders.sum(0) == 1) & np.all(terms == terms[0], axis=0) & \
+        np.all((st["state"] == abi.LEADER) | (st["state"] == abi.FOLLOWER), axis=0)
+    cand = np.nonzero(settled & (rng.random(G) < p))[0]
+    changed = []
+    for g in cand:
+        a = int(np.argmax(leaders[:, g]))
+        b = int(rng.choice([r for r in range(R) if r != a]))
+        L = state[a * G + g]
+        F = state[b * G + g]
+        T = int(L["term"])
+        if _last_term(L) != T or _last_term(F) != T:
+            continue
+        d = int(rng.integers(1, max_div + 1))
+        e = int(rng.integers(1, max_extra + 1))
+        hi_a = int(L["last_index"])
+        if int(F["last_index"]) > hi_a:
+            continue
+        L["last_index"] = hi_a + d + e
+        hf = hi_a + d
+        F["last_index"] = hf
+        # F becomes leader for T+1
+        F["term"] = T + 1
+        F["vote"] = F["node_id"]
+        F["state"] = abi.LEADER
+        F["leader_id"] = F["node_id"]
+        F["election_tick"] = 0
+        F["heartbeat_tick"] = 0
+        et = int(F["election_timeout"])
+        F["randomized_election_timeout"] = et + int(rng.integers(0, et))
+        F["read_index_count"] = 0
+        F["read_index"] = np.zeros(abi.GR_Q, abi.READ_STATUS)
+        F["leader_transfer_target"] = 0
+        F["flags"] = int(F["flags"]) & ~abi.F_PENDING_CONFIG_CHANGE
+        me = int(F["self_slot"])
+        for j in range(R):
+            F["remotes"][j]["next"] = hf + 1
+            F["remotes"][j]["match"] = 0
+            F["remotes"][j]["state"] = abi.RETRY
+            F["remotes"][j]["active"] = 0
+            F["remotes"][j]["snapshot_index"] = 0
+        F["last_index"] = hf + 1
+        _push_run(F, hf + 1, T + 1)
+        F["remotes"][me]["match"] = hf + 1
+        F["remotes"][me]["next"] = hf + 2
+        changed += [a * G + g, b * G + g]
+    return np.array(sorted(changed), np.int64)
+
+
+def current_leaders(state, topo):
+    """Slots of all peers in the leader state (proposal targets)."""
+    return np.nonzero(state["state"] == abi.LEADER)[0]

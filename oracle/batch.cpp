@@ -374,6 +374,33 @@ int ob_create(uint32_t slots, uint64_t max_entry_size, const gr_peer* peers, uin
 
 void ob_destroy(ob_pop* p) { delete p; }
 
+// Rebuild one peer from a record (state injections in simulations).
+int ob_reload(ob_pop* p, uint32_t peer, const gr_peer* rec) {
+  if (!p || !rec || peer >= p->peers.size()) return GR_EINVAL;
+  try {
+    build_peer(*rec, p->S, p->maxEntrySize, &p->peers[peer]);
+  } catch (const std::exception&) {
+    return GR_ESTATE;
+  }
+  return GR_OK;
+}
+
+// 1 if the peer's state fits a gr_peer record exactly (the device can hold
+// it), 0 if the host must keep stepping it: more than GR_Q pending ReadIndex
+// requests, or members outside the slot table.
+int ob_representable(ob_pop* p, uint8_t* out, uint32_t n) {
+  if (!p || n > p->peers.size()) return GR_EINVAL;
+  for (uint32_t k = 0; k < n; ++k) {
+    const OPeer& op = p->peers[k];
+    const raft& r = *op.r;
+    bool ok = r.readIdx.queue.size() <= GR_Q && r.readIdx.pending.size() <= GR_Q;
+    for (auto& kv : r.remotes) ok = ok && op.slotOf(kv.first) != GR_SLOT_NONE;
+    for (auto& kv : r.observers) ok = ok && op.slotOf(kv.first) != GR_SLOT_NONE;
+    out[k] = ok ? 1 : 0;
+  }
+  return GR_OK;
+}
+
 int ob_export(ob_pop* p, gr_peer* out, uint32_t n) {
   if (!p || n > p->peers.size()) return GR_EINVAL;
   for (uint32_t k = 0; k < n; ++k) export_peer(p->peers[k], p->S, &out[k]);

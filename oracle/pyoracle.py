@@ -30,6 +30,8 @@ def oracle_lib():
         lib.ob_destroy.restype = None
         lib.ob_export.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32]
         lib.ob_commit_all.argtypes = [c.c_void_p]
+        lib.ob_representable.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32]
+        lib.ob_reload.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p]
         lib.ob_step.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.c_void_p, c.c_void_p, c.c_void_p,
                                 c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t), c.c_void_p, c.c_uint32,
                                 c.c_char_p, c.c_size_t]
@@ -76,6 +78,20 @@ class OraclePopulation:
         out = np.zeros(self.n, abi.PEER)
         self.lib.ob_export(self._h, out.ctypes.data, self.n)
         return out
+
+    def representable(self):
+        """bool[n]: the peer's state fits a gr_peer record (device-resident)."""
+        out = np.zeros(self.n, np.uint8)
+        self.lib.ob_representable(self._h, out.ctypes.data, self.n)
+        return out.astype(bool)
+
+    def reload(self, idx, recs):
+        """Rebuild peers from records (state injections)."""
+        for p, rec in zip(idx, recs):
+            r = np.array([rec], abi.PEER)
+            rc = self.lib.ob_reload(self._h, int(p), r.ctypes.data)
+            if rc:
+                raise OracleError(f"ob_reload failed {rc}")
 
     def commit_all(self):
         self.lib.ob_commit_all(self._h)

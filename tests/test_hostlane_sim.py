@@ -1,0 +1,50 @@
+"""The kernel's lane code (gr_lane.h, built for the host as tests/_build/libhostlane.so)
+against the oracle, bit-exact after every pass. The same code runs on the GPU
+in tests/test_gpu.py; these CPU runs pin the logic without a device."""
+import numpy as np
+import pytest
+
+from dragonboat_amd import abi, populations as P
+import simulate as SIM
+
+
+def _run(G, passes, seed, locals_fn=None, inject_p=0.0, **mk):
+    R = 3
+    peers = P.make_groups(G, R, seed=seed, **mk)
+    topo = P.Topology(G, R)
+    rng = np.random.default_rng(seed)
+    lf = locals_fn or (lambda k: P.propose_locals(R * G, np.arange(G), pass_index=k))
+    inj = (lambda k, cur: P.inject_leader_change(cur, topo, inject_p, rng)) if inject_p else None
+    return SIM.simulate(SIM.HostlaneBackend, peers, topo, passes, lf, inject_fn=inj)
+
+
+def test_steady_state_commit(built):
+    """BASELINE config 2 shape: leader commits one index per pass after warm-up."""
+    st = _run(64, 6, seed=3)
+    assert st["escalations"] == 0
+    assert st["commits"] > 0
+
+
+def test_leader_change_churn(built):
+    """BASELINE config 5 shape: rejects, decreaseTo, conflict truncation."""
+    st = _run(200, 20, seed=5, inject_p=0.1)
+    assert st["commits"] > 0
+
+
+@pytest.mark.parametrize("check_quorum", [False, True])
+def test_ticks_and_read_index(built, check_quorum):
+    """Tick sweep (heartbeats, election timeouts, checkQuorum) + leader ReadIndex."""
+    G, R = 96, 3
+    rng = np.random.default_rng(9)
+
+    def lf(k):
+        loc = P.propose_locals(R * G, np.arange(G), pass_index=k, ticks=1)
+        loc["ticks"] = rng.integers(0, 3, R * G)
+        ri = rng.random(R * G) < 0.3
+        loc["read_index"] = ri
+        loc["read_ctx_low"] = rng.integers(1, 2**63, R * G, dtype=np.uint64)
+        loc["read_ctx_high"] = k
+        loc["propose_entries"] = np.where(rng.random(R * G) < 0.5, loc["propose_entries"], 0)
+        return loc
+    st = _run(G, 12, seed=7, locals_fn=lf, check_quorum=check_quorum)
+    assert st["msgs"] > 0
