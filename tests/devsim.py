@@ -1,0 +1,78 @@
+"""Device-resident passes (gr_step_device + mailbox spaces, the bench path)
+checked against the oracle after every pass: state, every mailbox of the
+written space, and per-peer results."""
+import numpy as np
+
+from dragonboat_amd import abi
+from dragonboat_amd.engine import Engine, decode_space
+from dragonboat_amd.exchange import Exchange
+from oracle.pyoracle import OraclePopulation
+import parity
+
+
+def inverse_routes(in_pos):
+    """mailbox gpos -> (receiving peer, sender slot) from an in_pos table [S][n]."""
+    S, n = in_pos.shape
+    inv = {}
+    for j in range(S):
+        for p in np.nonzero(in_pos[j] != 0xFFFFFFFF)[0]:
+            inv[int(in_pos[j, p])] = (int(p), j)
+    return inv
+
+
+def run_device(G, R, passes, placement="local", seed=2):
+    import torch
+    S = R
+    ex = Exchange(G, R, S, 1, 0, placement, seed=seed)
+    n = ex.n_peers
+    eng = Engine(n, S)
+    eng.load(ex.peers)
+    eng.bind_routes(ex.in_pos, ex.out_pos)
+    from dragonboat_amd import populations as P
+    loc = P.propose_locals(n, ex.leader_slots, pass_index=0)
+    eng.set_locals(loc)
+    spaces = ex.allocate(eng, torch.device("cuda", 0))
+    stream = torch.cuda.current_stream()
+    pop = OraclePopulation(ex.peers, S)
+    inv = inverse_routes(ex.in_pos)
+    msgs = np.zeros(0, abi.MESSAGE)  # oracle's view of this pass's inbox
+    for k in range(passes):
+        ex.step(eng, spaces, k, stream)
+        torch.cuda.synchronize()
+        o = pop.step(msgs, loc)
+        res = eng.collect_results(n)
+        assert not np.any(res["escalation"]), "unexpected escalation on the device path"
+        dev = eng.sync(n)
+        bad = parity.compare_states(dev, o["mid"], S)
+        assert not bad, f"pass {k}: state {bad[:3]}"
+        # the space the next pass reads
+        nxt = spaces[(k + 1) % 2] if placement == "local" else spaces[0]
+        raw = nxt.cpu().numpy()
+        got = decode_space(raw, ex.n_chunks, ex.positions)
+        for m in got:
+            p, j = inv[int(m["peer"])]
+            m["peer"], m["slot"] = p, j
+        # oracle messages -> (receiver, sender slot) records in arrival order
+        want = route(o["msgs"], ex, G, R)
+        bad = parity.compare_msgs(got, want)
+        assert not bad, f"pass {k}: mailboxes {bad[:3]}"
+        bad = parity.compare_results(res, o["results"])
+        assert not bad, f"pass {k}: results {bad[:3]}"
+        msgs = want
+    final = eng.sync(n)
+    eng.close()
+    return final
+
+
+def route(out, ex, G, R):
+    """Outbox records (sender peer, target slot) -> inbox records (receiver, sender slot),
+    using the placement's peer layout (replica-major in both placements on one rank)."""
+    nxt = out.copy()
+    sender = out["peer"].astype(np.int64)
+    r = sender // G
+    g = sender % G
+    j = out["slot"].astype(np.int64)
+    nxt["peer"] = (j * G + g).astype(np.uint32)
+    nxt["slot"] = r.astype(np.uint8)
+    order = np.lexsort((np.arange(len(nxt)), nxt["slot"], nxt["peer"]))
+    return nxt[order]

@@ -1,0 +1,133 @@
+"""Route tables of the device exchange (dragonboat_amd/exchange.py) and the
+multi-rank all_to_all over gloo (CPU): every sender mailbox lands exactly in
+the receiver's mailbox for the same (group, sender replica)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dragonboat_amd import exchange as X
+from dragonboat_amd import populations as P
+
+
+def _owner(rank, r, N):
+    return (rank - r) % N  # home of the group whose replica r sits on `rank`
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 4, 8])
+def test_spread_routes_bijection(N):
+    G, R, S = 37, 3, 3
+    tables = [X.spread_routes(G, R, S, N, a) for a in range(N)]
+    positions = tables[0][2]
+    pc = X.pad_positions(positions)
+    # sender side: (rank a, chunk d, local pos) -> (home, g, r, j)
+    sent = {}
+    for a in range(N):
+        _, out_pos, _ = tables[a]
+        for j in range(S):
+            for p in range(R * G):
+                v = int(out_pos[j, p])
+                if v == X.NOPOS:
+                    continue
+                r, g = divmod(p, G)
+                d, loc = divmod(v, pc)
+                assert loc < positions
+                key = (a, d, loc)
+                assert key not in sent
+                sent[key] = (_owner(a, r, N), g, r, j)
+    recv = {}
+    for d in range(N):
+        in_pos, _, _ = tables[d]
+        for r in range(S):
+            for p in range(R * G):
+                v = int(in_pos[r, p])
+                if v == X.NOPOS:
+                    continue
+                j, g = divmod(p, G)
+                a, loc = divmod(v, pc)
+                recv[(a, d, loc)] = (_owner(d, j, N), g, r, j)
+    assert sent == recv
+    assert len(sent) == N * G * R * (R - 1)
+
+
+def test_local_routes_match_topology():
+    G, R = 50, 3
+    ex = X.Exchange(G, R, R, 1, 0, "local")
+    inv = {}
+    for j in range(R):
+        for p in range(R * G):
+            v = int(ex.in_pos[j, p])
+            if v != X.NOPOS:
+                inv[v] = (p, j)
+    topo = P.Topology(G, R)
+    for j in range(R):
+        for p in range(R * G):
+            v = int(ex.out_pos[j, p])
+            if v == X.NOPOS:
+                assert p // G == j
+                continue
+            dp, ds = topo.dest(p, j)
+            assert inv[v] == (int(dp), int(ds))
+
+
+def test_spread_peers_agree_across_ranks():
+    """Every replica of a group, wherever placed, starts from the same group state."""
+    G, R, N = 16, 3, 4
+    recs = [X.spread_peers(G, R, N, a, seed=5) for a in range(N)]
+    for h in range(N):
+        reps = [recs[(h + r) % N][r * G:(r + 1) * G] for r in range(R)]
+        for r in range(1, R):
+            for f in ("term", "last_index", "committed"):
+                assert np.array_equal(reps[0][f], reps[r][f])
+            assert np.all(reps[r]["node_id"] == r + 1)
+
+
+def _worker(rank, world, port, G, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    R = S = 3
+    in_pos, out_pos, positions = X.spread_routes(G, R, S, world, rank)
+    pc = X.pad_positions(positions)
+    # each sender writes a tag (rank, replica, group, slot) into its mailboxes
+    out = torch.zeros(world * pc, dtype=torch.int64)
+    for j in range(S):
+        for p in range(R * G):
+            v = int(out_pos[j, p])
+            if v != X.NOPOS:
+                r, g = divmod(p, G)
+                out[v] = 1 + ((rank * 8 + r) * 1000 + g) * 8 + j
+    inp = torch.zeros_like(out)
+    dist.all_to_all_single(inp, out)
+    errs = 0
+    for r in range(S):
+        for p in range(R * G):
+            v = int(in_pos[r, p])
+            if v == X.NOPOS:
+                continue
+            j, g = divmod(p, G)
+            src = (rank - j + r) % world
+            want = 1 + ((src * 8 + r) * 1000 + g) * 8 + j
+            errs += int(inp[v]) != want
+    q.put((rank, errs))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_all_to_all_delivery(world):
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 29, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(e == 0 for _, e in res), res
