@@ -1,0 +1,65 @@
+// PMC calibration: kernels that move a known number of bytes with the access
+// widths gr_step_kernel uses (8-B and 1-B per lane, coalesced), so the
+// FETCH_SIZE / WRITE_SIZE readings of the step kernel can be converted to
+// bytes (MI355X_MICROARCH.md: "calibrate on a known byte count in your own
+// access pattern"). Buffers are 2 GiB, well past the 256 MiB Infinity Cache.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+__global__ void read_u64(const uint64_t* __restrict__ a, uint64_t* __restrict__ out, size_t n) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  uint64_t s = 0;
+  for (; i < n; i += (size_t)gridDim.x * blockDim.x) s ^= a[i];
+  if (s == 0x9e3779b97f4a7c15ull) out[0] = s;  // never true for zeroed input; keeps the loads
+}
+__global__ void read_u8(const uint8_t* __restrict__ a, uint64_t* __restrict__ out, size_t n) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  uint32_t s = 0;
+  for (; i < n; i += (size_t)gridDim.x * blockDim.x) s ^= a[i];
+  if (s == 0xdeadbeefu) out[0] = s;
+}
+__global__ void write_u64(uint64_t* __restrict__ a, size_t n) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  for (; i < n; i += (size_t)gridDim.x * blockDim.x) a[i] = i;
+}
+__global__ void write_u8(uint8_t* __restrict__ a, size_t n) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  for (; i < n; i += (size_t)gridDim.x * blockDim.x) a[i] = (uint8_t)i;
+}
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s\n", hipGetErrorString(e_)); return 1; } } while (0)
+
+int main() {
+  const size_t bytes = 2ull << 30;
+  void* buf;
+  uint64_t* out;
+  CK(hipMalloc(&buf, bytes));
+  CK(hipMalloc(&out, 64));
+  CK(hipMemset(buf, 0, bytes));
+  const int grid = 256 * 64, block = 256;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int rep = 0; rep < 2; ++rep) {
+    float ms[4];
+    CK(hipEventRecord(a));
+    read_u64<<<grid, block>>>((const uint64_t*)buf, out, bytes / 8);
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms[0], a, b));
+    CK(hipEventRecord(a));
+    read_u8<<<grid, block>>>((const uint8_t*)buf, out, bytes);
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms[1], a, b));
+    CK(hipEventRecord(a));
+    write_u64<<<grid, block>>>((uint64_t*)buf, bytes / 8);
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms[2], a, b));
+    CK(hipEventRecord(a));
+    write_u8<<<grid, block>>>((uint8_t*)buf, bytes);
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms[3], a, b));
+    printf("{\"bytes\": %zu, \"read_u64_GBs\": %.1f, \"read_u8_GBs\": %.1f, \"write_u64_GBs\": %.1f, \"write_u8_GBs\": %.1f}\n",
+           bytes, bytes / ms[0] / 1e6, bytes / ms[1] / 1e6, bytes / ms[2] / 1e6, bytes / ms[3] / 1e6);
+    CK(hipMemset(buf, 0, bytes));
+  }
+  CK(hipFree(buf));
+  CK(hipFree(out));
+  return 0;
+}

@@ -1,0 +1,65 @@
+"""Summarise a tools/profile.sh run: per-kernel trace stats, HBM bytes per
+launch of gr_step_kernel from FETCH_SIZE/WRITE_SIZE, calibrated against
+tools/hbm_calib's known byte counts, and SQ occupancy counters."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def rows(pattern):
+    out = []
+    for f in sorted(glob.glob(pattern, recursive=True)):
+        with open(f) as fh:
+            out += list(csv.DictReader(fh))
+    return out
+
+
+def counters(d, kernel_sub):
+    """{counter: [value per dispatch]} for kernels whose name contains kernel_sub."""
+    per = defaultdict(lambda: defaultdict(float))
+    for r in rows(os.path.join(d, "**", "*counter_collection.csv")):
+        if kernel_sub not in r.get("Kernel_Name", ""):
+            continue
+        per[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {k: [v[x] for x in sorted(v, key=int)] for k, v in per.items()}
+
+
+def main(o):
+    s = {}
+    st = rows(os.path.join(o, "trace", "**", "*kernel_stats.csv"))
+    s["kernel_stats"] = [{k: r[k] for k in r} for r in st[:8]]
+    # calibration: bytes per FETCH_SIZE/WRITE_SIZE unit at our access widths
+    cal = {}
+    nbytes = 2 << 30
+    for name in ("read_u64", "read_u8"):
+        v = counters(os.path.join(o, "calib_fetch"), name).get("FETCH_SIZE", [])
+        if v:
+            cal[name + "_bytes_per_unit"] = nbytes / (sum(v) / len(v))
+    for name in ("write_u64", "write_u8"):
+        v = counters(os.path.join(o, "calib_write"), name).get("WRITE_SIZE", [])
+        if v:
+            cal[name + "_bytes_per_unit"] = nbytes / (sum(v) / len(v))
+    s["calibration"] = cal
+    f = counters(os.path.join(o, "fetch"), "gr_step").get("FETCH_SIZE", [])
+    w = counters(os.path.join(o, "write"), "gr_step").get("WRITE_SIZE", [])
+    # steady-state launches only (skip the warm-up passes' first two)
+    f_ss, w_ss = f[3:] or f, w[3:] or w
+    if f_ss and w_ss:
+        fu = sum(f_ss) / len(f_ss)
+        wu = sum(w_ss) / len(w_ss)
+        kf = cal.get("read_u64_bytes_per_unit", 2048.0)
+        kw = cal.get("write_u64_bytes_per_unit", 1024.0)
+        s["step_kernel"] = {"fetch_size_units": fu, "write_size_units": wu,
+                            "read_bytes": fu * kf, "write_bytes": wu * kw,
+                            "hbm_bytes_per_launch": fu * kf + wu * kw, "launches": len(f)}
+    sq = counters(os.path.join(o, "sq"), "gr_step")
+    s["sq"] = {k: sum(v[3:] or v) / len(v[3:] or v) for k, v in sq.items()}
+    json.dump(s, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
