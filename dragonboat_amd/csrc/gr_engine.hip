@@ -22,17 +22,10 @@ namespace gr {
 
 constexpr int kBlock = 256;
 
-template <int S>
-__global__ __launch_bounds__(kBlock) void gr_step_kernel(StepParams kp) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t lc = 0, fc = 0, es = 0, mi = 0, mo = 0;
-  if (i < kp.n_lanes) {
-    const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-    Lane<S> L(kp, i, p);
-    L.step(&lc, &fc, &es, &mi, &mo);
-  }
-  if (!kp.stats) return;
-  // per-workgroup partial counters (no atomics on global memory)
+// Per-workgroup partial counters (no atomics on global memory): row b of the
+// stats block belongs to workgroup b of whichever kernel runs.
+__device__ inline void block_stats(const StepParams& kp, uint32_t lc, uint32_t fc, uint32_t es, uint32_t mi,
+                                   uint32_t mo) {
   __shared__ uint32_t red[5];
   if (threadIdx.x < 5) red[threadIdx.x] = 0;
   __syncthreads();
@@ -59,19 +52,81 @@ __global__ __launch_bounds__(kBlock) void gr_step_kernel(StepParams kp) {
   }
 }
 
+// Pass 1: every lane runs the steady-state subset (Lane<S, true>). Lanes that
+// meet anything else append themselves to bail_list (one atomic per wave;
+// a wave's lanes stay contiguous and ascending) and store nothing.
 template <int S>
-static hipError_t launch(const StepParams& kp, hipStream_t s) {
+__global__ __launch_bounds__(kBlock) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
+                                                         uint32_t* bail_count) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t lc = 0, fc = 0, es = 0, mi = 0, mo = 0;
+  bool bail = false;
+  if (i < kp.n_lanes) {
+    const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+    Lane<S, true> L(kp, i, p);
+    bail = !L.step(&lc, &fc, &es, &mi, &mo);
+  }
+  const uint64_t bm = __ballot(bail);
+  if (bm) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t first = (uint32_t)__ffsll((unsigned long long)bm) - 1;
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(bail_count, (uint32_t)__popcll(bm));
+    base = __shfl(base, (int)first);
+    if (bail) bail_list[base + (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
+  }
+  if (kp.stats) block_stats(kp, lc, fc, es, mi, mo);
+}
+
+// Pass 2: the general lane (every handler, escalation with prefix re-run)
+// over the bailed lanes only. Grid-stride over the list; also clears the
+// counter the next pass's fast kernel will use.
+template <int S>
+__global__ __launch_bounds__(kBlock) void gr_step_kernel(StepParams kp, const uint32_t* bail_list,
+                                                         const uint32_t* bail_count, uint32_t* next_count) {
+  const uint32_t n = *bail_count;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *next_count = 0;
+  uint32_t lc = 0, fc = 0, es = 0, mi = 0, mo = 0;
+  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    const uint32_t x = base + threadIdx.x;
+    if (x < n) {
+      const uint32_t i = bail_list[x];
+      const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+      Lane<S> L(kp, i, p);
+      uint32_t a = 0, b = 0, c = 0, d = 0, e = 0;
+      L.step(&a, &b, &c, &d, &e);
+      lc += a; fc += b; es += c; mi += d; mo += e;
+    }
+  }
+  if (kp.stats) block_stats(kp, lc, fc, es, mi, mo);
+}
+
+// The general kernel's grid: enough workgroups to fill the chip twice over,
+// never more than the stats block has rows for.
+constexpr uint32_t kGeneralBlocks = 2048;
+
+template <int S>
+static hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counts, uint32_t parity,
+                         hipStream_t s) {
   if (kp.n_lanes == 0) return hipSuccess;
   const uint32_t blocks = (kp.n_lanes + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(gr_step_kernel<S>, dim3(blocks), dim3(kBlock), 0, s, kp);
+  uint32_t* cur = counts + (parity & 1);
+  uint32_t* nxt = counts + ((parity + 1) & 1);
+  hipLaunchKernelGGL(gr_fast_kernel<S>, dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  const uint32_t gblocks = blocks < kGeneralBlocks ? blocks : kGeneralBlocks;
+  hipLaunchKernelGGL(gr_step_kernel<S>, dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list,
+                     (const uint32_t*)cur, nxt);
   return hipGetLastError();
 }
 
-static hipError_t launch_slots(uint32_t S, const StepParams& kp, hipStream_t s) {
+static hipError_t launch_slots(uint32_t S, const StepParams& kp, uint32_t* bail_list, uint32_t* counts,
+                               uint32_t parity, hipStream_t s) {
   switch (S) {
-    case 1: return launch<1>(kp, s);
-    case 3: return launch<3>(kp, s);
-    case 5: return launch<5>(kp, s);
+    case 1: return launch<1>(kp, bail_list, counts, parity, s);
+    case 3: return launch<3>(kp, bail_list, counts, parity, s);
+    case 5: return launch<5>(kp, bail_list, counts, parity, s);
   }
   return hipErrorInvalidValue;
 }
@@ -98,6 +153,8 @@ struct gr_engine {
   LaneBase ln{};
   uint64_t* stats = nullptr;
   uint32_t stats_rows = 0;
+  uint32_t* bail = nullptr;  // [cap] bailed lanes, then 2 counters (launch parity)
+  uint64_t launches = 0;     // never reset: selects the live bail counter
   bool routes_bound = false;
   bool locals_set = false;
   uint64_t passes = 0;
@@ -319,7 +376,8 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
   e->stats_rows = (e->cap + kBlock - 1) / kBlock;
   void *ds = nullptr, *dl = nullptr;
   if (hipMalloc(&ds, sb) != hipSuccess || hipMalloc(&dl, lb) != hipSuccess ||
-      hipMalloc((void**)&e->stats, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess) {
+      hipMalloc((void**)&e->stats, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
+      hipMalloc((void**)&e->bail, ((size_t)e->cap + 2) * 4) != hipSuccess) {
     if (ds) (void)hipFree(ds);
     if (dl) (void)hipFree(dl);
     e->st.base = nullptr;
@@ -331,6 +389,7 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
   e->ln.base = (uint8_t*)dl;
   if (hipMemset(ds, 0, sb) != hipSuccess || hipMemset(dl, 0, lb) != hipSuccess ||
       hipMemset(e->stats, 0, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
+      hipMemset(e->bail + e->cap, 0, 8) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     gr_destroy(e);
     return GR_EDEVICE;
@@ -345,6 +404,7 @@ void gr_destroy(gr_engine* e) {
   if (e->st.base) (void)hipFree(e->st.base);
   if (e->ln.base) (void)hipFree(e->ln.base);
   if (e->stats) (void)hipFree(e->stats);
+  if (e->bail) (void)hipFree(e->bail);
   if (e->d_in) (void)hipFree(e->d_in);
   if (e->d_out) (void)hipFree(e->d_out);
   if (e->h_in) (void)hipHostFree(e->h_in);
@@ -448,7 +508,7 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
   kp.in = make_view(e->d_in, 1, pk.in_positions);
   kp.out = make_view(e->d_out, 1, pk.out_positions);
   kp.n_lanes = nl;
-  HIPCHK(launch_slots(S, kp, s));
+  HIPCHK(launch_slots(S, kp, e->bail, e->bail + e->cap, (uint32_t)e->launches++, s));
   e->passes++;
   e->locals_set = false;    // the lane rows now hold this pass's compact locals
   e->routes_bound = false;  // and its compact routes
@@ -542,7 +602,7 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
   kp.in = make_view(in_space, in_chunks, in_positions);
   kp.out = make_view(out_space, out_chunks, out_positions);
   kp.n_lanes = n_peers;
-  HIPCHK(launch_slots(e->S, kp, (hipStream_t)stream));
+  HIPCHK(launch_slots(e->S, kp, e->bail, e->bail + e->cap, (uint32_t)e->launches++, (hipStream_t)stream));
   e->passes++;
   return GR_OK;
 }

@@ -82,7 +82,15 @@ GR_HD uint64_t rb_with(uint64_t rb, uint32_t j, uint32_t off, uint32_t width, ui
   return (rb & ~m) | (((uint64_t)v << (5 * j + off)) & m);
 }
 
-template <int S>
+// Internal code (never reported): a FAST lane met an input outside the fast
+// path and left no trace; the general kernel steps it instead.
+constexpr int ESC_FAST = 0x40;
+
+// FAST = true instantiates the steady-state subset only (the leader's
+// ReplicateResp/Propose, the follower's Replicate, equal terms, no ticks or
+// ReadIndex): the same handler code, with every other branch replaced by an
+// ESC_FAST bail, so the compiler drops the cold paths and their registers.
+template <int S, bool FAST = false>
 struct Lane {
   using R = Rows<S>;
   const StepParams kp;  // by value: small, uniform (SGPRs)
@@ -903,6 +911,7 @@ struct Lane {
           GR_TRY(send_timeout_now(ltt));
       }
     } else {
+      if constexpr (FAST) return ESC_FAST;
       if (decrease_to(j, m.log_index, m.hint)) {
         enter_retry(j);
         GR_TRY(send_replicate(j));
@@ -989,6 +998,9 @@ struct Lane {
     m.term = mb.u64(k, MF_TERM);
     m.n = 0; m.run2 = 0;
     m.log_index = 0; m.log_term = 0; m.commit = 0; m.hint = 0; m.hint_high = 0; m.rt0 = 0; m.rt1 = 0;
+    if constexpr (FAST) {
+      if (m.type != GR_REPLICATE && m.type != GR_REPLICATE_RESP) return;  // bails in handle()
+    }
     switch (m.type) {
       case GR_REPLICATE:
         m.n = mb.n(k);
@@ -1049,6 +1061,20 @@ struct Lane {
   GR_HD int handle(const InMsg& m, uint32_t from) {
     need(G_CORE);
     const uint32_t t = m.type;
+    if constexpr (FAST) {  // the same dispatch as below, for the two hot pairs only
+      if (m.term != term) return ESC_FAST;
+      if (state == GR_LEADER && t == GR_REPLICATE_RESP) {
+        need(G_REM);
+        if (rkind(from) == GR_SLOT_EMPTY) return 0;
+        return leader_replicate_resp(m, from);
+      }
+      if (state == GR_FOLLOWER && t == GR_REPLICATE) {
+        zero_etick();
+        set_leader_from(from);
+        return handle_replicate(m, from);
+      }
+      return ESC_FAST;
+    }
     if (m.term != 0 && m.term != term) {  // onMessageTermNotMatched
       if (m.term > term) {
         if (t == GR_REQUEST_VOTE) return GR_ESC_UNSUPPORTED;  // dropRequestVoteFromHighTermNode + vote
@@ -1236,6 +1262,13 @@ struct Lane {
       const uint8_t lf = kp.ln.u8(LR_LFLAGS)[i];
       const uint32_t nt = kp.ln.u32(LR_TICKS)[i], nq = kp.ln.u32(LR_QTICKS)[i],
                      np = kp.ln.u32(LR_PROPOSE)[i];
+      if constexpr (FAST) {
+        if ((lf & (LF_READ_INDEX | LF_PROPOSE_CC)) || nt || nq) { *at = item; return ESC_FAST; }
+        if (np) {
+          need(G_CORE);
+          if (state != GR_LEADER) { *at = item; return ESC_FAST; }
+        }
+      }
       if (lf & LF_READ_INDEX) {
         if (item == limit) { *at = item; return 0; }
         need(G_CORE);
@@ -1281,17 +1314,24 @@ struct Lane {
 
   // Kernel body for one lane: run, and on escalation re-run the prefix on the
   // pristine state so the escalating item is left entirely to the host.
-  GR_HD void step(uint32_t* stat_leader_commit, uint32_t* stat_follower_commit, uint32_t* stat_esc,
+  // A FAST lane returns false, having stored nothing but message bodies in
+  // its (uncounted) out mailboxes, when any item needs the general path.
+  GR_HD bool step(uint32_t* stat_leader_commit, uint32_t* stat_follower_commit, uint32_t* stat_esc,
                   uint32_t* stat_in, uint32_t* stat_out) {
     uint32_t at = 0, limit = 0xFFFFFFFFu;
     int esc = 0;
-#pragma unroll 1
-    for (int attempt = 0; attempt < 2; ++attempt) {  // one call site keeps run() inlined
+    if constexpr (FAST) {
       begin();
-      const int e = run(limit, &at);
-      if (!e) break;
-      esc = e;  // second attempt re-runs the prefix and cannot escalate
-      limit = at;
+      if (run(limit, &at)) return false;
+    } else {
+#pragma unroll 1
+      for (int attempt = 0; attempt < 2; ++attempt) {  // one call site keeps run() inlined
+        begin();
+        const int e = run(limit, &at);
+        if (!e) break;
+        esc = e;  // second attempt re-runs the prefix and cannot escalate
+        limit = at;
+      }
     }
     store();
 #pragma unroll 1
@@ -1325,6 +1365,7 @@ struct Lane {
     *stat_esc = esc != 0;
     *stat_in = msgs_in;
     *stat_out = msgs_out;
+    return true;
   }
 };
 
