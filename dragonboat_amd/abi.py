@@ -101,6 +101,11 @@ class Stats(ctypes.Structure):
                 ("msgs_in", ctypes.c_uint64), ("msgs_out", ctypes.c_uint64)]
 
 
+class Timing(ctypes.Structure):
+    _fields_ = [("passes", ctypes.c_uint64), ("fast_ms", ctypes.c_double), ("general_ms", ctypes.c_double),
+                ("bailed_lanes", ctypes.c_uint64)]
+
+
 # settings.Soft.MaxEntrySize (internal/settings/soft.go:236)
 MAX_ENTRY_SIZE = 2 * 32 * 1024 * 1024
 
@@ -109,7 +114,7 @@ EXPORTS = [
     "gr_create", "gr_destroy", "gr_strerror", "gr_escalation_name", "gr_load_groups",
     "gr_sync_groups_to_host", "gr_step", "gr_release_outbox", "gr_stats_get", "gr_stats_reset",
     "gr_space_bytes", "gr_space_chunk_bytes", "gr_bind_routes", "gr_set_locals", "gr_step_device",
-    "gr_collect_results", "gr_space_decode", "gr_space_encode",
+    "gr_collect_results", "gr_space_decode", "gr_space_encode", "gr_timing_begin", "gr_timing_end",
 ]
 
 

@@ -86,6 +86,7 @@ __global__ __launch_bounds__(kBlock) void gr_step_kernel(StepParams kp, const ui
                                                          const uint32_t* bail_count, uint32_t* next_count) {
   const uint32_t n = *bail_count;
   if (blockIdx.x == 0 && threadIdx.x == 0) *next_count = 0;
+  if (blockIdx.x * kBlock >= n) return;  // uniform per block: nothing to do, no stats row touched
   uint32_t lc = 0, fc = 0, es = 0, mi = 0, mo = 0;
   for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
     const uint32_t x = base + threadIdx.x;
@@ -103,30 +104,42 @@ __global__ __launch_bounds__(kBlock) void gr_step_kernel(StepParams kp, const ui
 
 // The general kernel's grid: enough workgroups to fill the chip twice over,
 // never more than the stats block has rows for.
-constexpr uint32_t kGeneralBlocks = 2048;
+constexpr uint32_t kGeneralBlocks = 1024;
+
+// Optional per-pass timing: events around the two kernels and a copy of the
+// bail count (pinned host slot), recorded on the pass's stream.
+struct PassTiming {
+  hipEvent_t ev[3];
+  uint32_t* bailed;  // pinned host word
+};
 
 template <int S>
 static hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counts, uint32_t parity,
-                         hipStream_t s) {
+                         hipStream_t s, const PassTiming* t) {
   if (kp.n_lanes == 0) return hipSuccess;
   const uint32_t blocks = (kp.n_lanes + kBlock - 1) / kBlock;
   uint32_t* cur = counts + (parity & 1);
   uint32_t* nxt = counts + ((parity + 1) & 1);
+  hipError_t err;
+  if (t && (err = hipEventRecord(t->ev[0], s)) != hipSuccess) return err;
   hipLaunchKernelGGL(gr_fast_kernel<S>, dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur);
-  hipError_t err = hipGetLastError();
-  if (err != hipSuccess) return err;
+  if ((err = hipGetLastError()) != hipSuccess) return err;
+  if (t && (err = hipEventRecord(t->ev[1], s)) != hipSuccess) return err;
+  if (t && (err = hipMemcpyAsync(t->bailed, cur, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return err;
   const uint32_t gblocks = blocks < kGeneralBlocks ? blocks : kGeneralBlocks;
   hipLaunchKernelGGL(gr_step_kernel<S>, dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list,
                      (const uint32_t*)cur, nxt);
-  return hipGetLastError();
+  if ((err = hipGetLastError()) != hipSuccess) return err;
+  if (t && (err = hipEventRecord(t->ev[2], s)) != hipSuccess) return err;
+  return hipSuccess;
 }
 
 static hipError_t launch_slots(uint32_t S, const StepParams& kp, uint32_t* bail_list, uint32_t* counts,
-                               uint32_t parity, hipStream_t s) {
+                               uint32_t parity, hipStream_t s, const PassTiming* t) {
   switch (S) {
-    case 1: return launch<1>(kp, bail_list, counts, parity, s);
-    case 3: return launch<3>(kp, bail_list, counts, parity, s);
-    case 5: return launch<5>(kp, bail_list, counts, parity, s);
+    case 1: return launch<1>(kp, bail_list, counts, parity, s, t);
+    case 3: return launch<3>(kp, bail_list, counts, parity, s, t);
+    case 5: return launch<5>(kp, bail_list, counts, parity, s, t);
   }
   return hipErrorInvalidValue;
 }
@@ -155,6 +168,8 @@ struct gr_engine {
   uint32_t stats_rows = 0;
   uint32_t* bail = nullptr;  // [cap] bailed lanes, then 2 counters (launch parity)
   uint64_t launches = 0;     // never reset: selects the live bail counter
+  bool timing = false;
+  std::vector<PassTiming> timings;  // one per pass while timing
   bool routes_bound = false;
   bool locals_set = false;
   uint64_t passes = 0;
@@ -170,6 +185,27 @@ struct gr_engine {
   std::vector<gr_peer_result> out_results;
   std::mutex mu;  // one host-path pass at a time per engine
 };
+
+// A fresh timing record for the next pass (nullptr when timing is off or a
+// HIP call fails: the pass then runs untimed and gr_timing_end reports it).
+static PassTiming* next_timing(gr_engine* e) {
+  if (!e->timing) return nullptr;
+  PassTiming t{};
+  for (int k = 0; k < 3; ++k)
+    if (hipEventCreate(&t.ev[k]) != hipSuccess) return nullptr;
+  if (hipHostMalloc((void**)&t.bailed, 4) != hipSuccess) return nullptr;
+  *t.bailed = 0;
+  e->timings.push_back(t);
+  return &e->timings.back();
+}
+
+static void free_timings(gr_engine* e) {
+  for (auto& t : e->timings) {
+    for (int k = 0; k < 3; ++k) (void)hipEventDestroy(t.ev[k]);
+    (void)hipHostFree(t.bailed);
+  }
+  e->timings.clear();
+}
 
 namespace {
 
@@ -405,6 +441,7 @@ void gr_destroy(gr_engine* e) {
   if (e->ln.base) (void)hipFree(e->ln.base);
   if (e->stats) (void)hipFree(e->stats);
   if (e->bail) (void)hipFree(e->bail);
+  free_timings(e);
   if (e->d_in) (void)hipFree(e->d_in);
   if (e->d_out) (void)hipFree(e->d_out);
   if (e->h_in) (void)hipHostFree(e->h_in);
@@ -508,7 +545,7 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
   kp.in = make_view(e->d_in, 1, pk.in_positions);
   kp.out = make_view(e->d_out, 1, pk.out_positions);
   kp.n_lanes = nl;
-  HIPCHK(launch_slots(S, kp, e->bail, e->bail + e->cap, (uint32_t)e->launches++, s));
+  HIPCHK(launch_slots(S, kp, e->bail, e->bail + e->cap, (uint32_t)e->launches++, s, next_timing(e)));
   e->passes++;
   e->locals_set = false;    // the lane rows now hold this pass's compact locals
   e->routes_bound = false;  // and its compact routes
@@ -552,6 +589,33 @@ int gr_stats_get(gr_engine* e, gr_stats* out) {
     out->msgs_in += row[ST_MSGS_IN];
     out->msgs_out += row[ST_MSGS_OUT];
   }
+  return GR_OK;
+}
+
+int gr_timing_begin(gr_engine* e) {
+  if (!e) return GR_EINVAL;
+  HIPCHK(hipDeviceSynchronize());
+  free_timings(e);
+  e->timings.reserve(1 << 16);  // records are referenced by pointer until the pass is enqueued
+  e->timing = true;
+  return GR_OK;
+}
+
+int gr_timing_end(gr_engine* e, gr_timing* out) {
+  if (!e || !out) return GR_EINVAL;
+  HIPCHK(hipDeviceSynchronize());
+  memset(out, 0, sizeof(*out));
+  for (auto& t : e->timings) {
+    float a = 0, b = 0;
+    HIPCHK(hipEventElapsedTime(&a, t.ev[0], t.ev[1]));
+    HIPCHK(hipEventElapsedTime(&b, t.ev[1], t.ev[2]));
+    out->fast_ms += a;
+    out->general_ms += b;
+    out->bailed_lanes += *t.bailed;
+    out->passes++;
+  }
+  free_timings(e);
+  e->timing = false;
   return GR_OK;
 }
 
@@ -602,7 +666,7 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
   kp.in = make_view(in_space, in_chunks, in_positions);
   kp.out = make_view(out_space, out_chunks, out_positions);
   kp.n_lanes = n_peers;
-  HIPCHK(launch_slots(e->S, kp, e->bail, e->bail + e->cap, (uint32_t)e->launches++, (hipStream_t)stream));
+  HIPCHK(launch_slots(e->S, kp, e->bail, e->bail + e->cap, (uint32_t)e->launches++, (hipStream_t)stream, next_timing(e)));
   e->passes++;
   return GR_OK;
 }

@@ -57,6 +57,8 @@ def load_library(path=LIB_PATH):
                                     c.POINTER(c.c_size_t)]
     lib.gr_space_encode.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_void_p, c.c_size_t,
                                     c.c_void_p]
+    lib.gr_timing_begin.argtypes = [c.c_void_p]
+    lib.gr_timing_end.argtypes = [c.c_void_p, c.POINTER(abi.Timing)]
     _lib = lib
     return lib
 
@@ -125,6 +127,15 @@ class Engine:
 
     def reset_stats(self):
         _check(self.lib.gr_stats_reset(self._h), "gr_stats_reset")
+
+    def timing_begin(self):
+        """Record HIP events around each pass's two kernels until timing_end()."""
+        _check(self.lib.gr_timing_begin(self._h), "gr_timing_begin")
+
+    def timing_end(self):
+        t = abi.Timing()
+        _check(self.lib.gr_timing_end(self._h, ctypes.byref(t)), "gr_timing_end")
+        return {k: getattr(t, k) for k, _ in abi.Timing._fields_}
 
     # ---- device-resident path -------------------------------------------------
     def space_bytes(self, n_chunks, positions):

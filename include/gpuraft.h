@@ -248,6 +248,21 @@ int gr_stats_get(gr_engine* e, gr_stats* out);
 int gr_stats_reset(gr_engine* e);
 
 /*
+ * Per-kernel timing (benchmarks/profiling; not in the reference). Between
+ * gr_timing_begin and gr_timing_end every pass records HIP events around its
+ * two kernels on the pass's stream: the steady-state kernel over all lanes and
+ * the general kernel over the lanes the first one handed over ("bailed").
+ */
+typedef struct gr_timing {
+  uint64_t passes;
+  double fast_ms;         /* summed over passes */
+  double general_ms;
+  uint64_t bailed_lanes;  /* summed over passes */
+} gr_timing;
+int gr_timing_begin(gr_engine* e);
+int gr_timing_end(gr_engine* e, gr_timing* out);
+
+/*
  * Device-resident path (benchmarks, multi-GPU exchange). Messages live in
  * "spaces": n_chunks chunks of `positions` mailboxes, each mailbox holding up
  * to GR_C messages in structure-of-arrays form. in_pos[j*max_peers+p] /

@@ -13,11 +13,11 @@ __global__ void read_u64(const uint64_t* __restrict__ a, uint64_t* __restrict__ 
   for (; i < n; i += (size_t)gridDim.x * blockDim.x) s ^= a[i];
   if (s == 0x9e3779b97f4a7c15ull) out[0] = s;  // never true for zeroed input; keeps the loads
 }
-__global__ void read_u8(const uint8_t* __restrict__ a, uint64_t* __restrict__ out, size_t n) {
+__global__ void read_u8(const uint8_t* __restrict__ a, uint64_t* __restrict__ out, size_t n, uint32_t key) {
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   uint32_t s = 0;
-  for (; i < n; i += (size_t)gridDim.x * blockDim.x) s ^= a[i];
-  if (s == 0xdeadbeefu) out[0] = s;
+  for (; i < n; i += (size_t)gridDim.x * blockDim.x) s = s * 31u + a[i];
+  if (s == key) out[0] = s;  // key is never hit for zeroed input (s == 0); keeps the loads
 }
 __global__ void write_u64(uint64_t* __restrict__ a, size_t n) {
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -47,7 +47,7 @@ int main() {
     read_u64<<<grid, block>>>((const uint64_t*)buf, out, bytes / 8);
     CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms[0], a, b));
     CK(hipEventRecord(a));
-    read_u8<<<grid, block>>>((const uint8_t*)buf, out, bytes);
+    read_u8<<<grid, block>>>((const uint8_t*)buf, out, bytes, 0xdeadbeefu);
     CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms[1], a, b));
     CK(hipEventRecord(a));
     write_u64<<<grid, block>>>((uint64_t*)buf, bytes / 8);

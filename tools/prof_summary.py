@@ -43,20 +43,30 @@ def main(o):
         if v:
             cal[name + "_bytes_per_unit"] = nbytes / (sum(v) / len(v))
     s["calibration"] = cal
-    f = counters(os.path.join(o, "fetch"), "gr_step").get("FETCH_SIZE", [])
-    w = counters(os.path.join(o, "write"), "gr_step").get("WRITE_SIZE", [])
-    # steady-state launches only (skip the warm-up passes' first two)
-    f_ss, w_ss = f[3:] or f, w[3:] or w
-    if f_ss and w_ss:
-        fu = sum(f_ss) / len(f_ss)
-        wu = sum(w_ss) / len(w_ss)
-        kf = cal.get("read_u64_bytes_per_unit", 2048.0)
-        kw = cal.get("write_u64_bytes_per_unit", 1024.0)
-        s["step_kernel"] = {"fetch_size_units": fu, "write_size_units": wu,
-                            "read_bytes": fu * kf, "write_bytes": wu * kw,
-                            "hbm_bytes_per_launch": fu * kf + wu * kw, "launches": len(f)}
-    sq = counters(os.path.join(o, "sq"), "gr_step")
-    s["sq"] = {k: sum(v[3:] or v) / len(v[3:] or v) for k, v in sq.items()}
+    kf = cal.get("read_u64_bytes_per_unit", 2048.0)
+    kw = cal.get("write_u64_bytes_per_unit", 1024.0)
+    s["kernels"] = {}
+    for kname in ("gr_fast_kernel", "gr_step_kernel"):
+        f = counters(os.path.join(o, "fetch"), kname).get("FETCH_SIZE", [])
+        w = counters(os.path.join(o, "write"), kname).get("WRITE_SIZE", [])
+        f_ss, w_ss = f[3:] or f, w[3:] or w  # steady-state launches (after warm-up)
+        k = {"launches": len(f)}
+        if f_ss and w_ss:
+            fu = sum(f_ss) / len(f_ss)
+            wu = sum(w_ss) / len(w_ss)
+            k.update({"fetch_size_units": fu, "write_size_units": wu, "read_bytes": fu * kf,
+                      "write_bytes": wu * kw, "hbm_bytes_per_launch": fu * kf + wu * kw})
+        sq = counters(os.path.join(o, "sq"), kname)
+        k["sq"] = {c: sum(v[3:] or v) / len(v[3:] or v) for c, v in sq.items() if v}
+        s["kernels"][kname] = k
+    fk = s["kernels"].get("gr_fast_kernel", {})
+    if "hbm_bytes_per_launch" in fk:
+        groups = int(os.environ.get("GROUPS", "1000000"))
+        with open(os.path.join(o, "pmc_latest.json"), "w") as fh:
+            json.dump({"kernel": "gr_fast_kernel<3>", "groups": groups, "replicas": 3,
+                       "hbm_bytes_per_launch": fk["hbm_bytes_per_launch"],
+                       "read_bytes": fk["read_bytes"], "write_bytes": fk["write_bytes"],
+                       "calibration": cal, "source": os.path.basename(o)}, fh, indent=1)
     json.dump(s, sys.stdout, indent=1)
     print()
 
