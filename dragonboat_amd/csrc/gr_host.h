@@ -214,16 +214,18 @@ inline int pack_inbox(const gr_inbox* in, uint32_t S, uint32_t max_peers, Packed
     // mailbox is marked overflowed and the receiver escalates there (CAPACITY)
     ++mcount[(size_t)pk->lane(in->msgs[k].peer) * S + in->msgs[k].slot];
   }
+  // slot-major positions: consecutive lanes use consecutive mailboxes of
+  // every field array (coalesced on the device)
   pk->in_pos.assign((size_t)S * nl, NOPOS);
   uint32_t npos = 0;
-  for (uint32_t l = 0; l < nl; ++l)
-    for (uint32_t j = 0; j < S; ++j)
+  for (uint32_t j = 0; j < S; ++j)
+    for (uint32_t l = 0; l < nl; ++l)
       if (mcount[(size_t)l * S + j]) pk->in_pos[(size_t)j * nl + l] = npos++;
   pk->in_positions = std::max<uint32_t>(npos, 1);
   pk->out_positions = std::max<uint32_t>(nl * S, 1);
   pk->out_pos.resize((size_t)S * nl);
   for (uint32_t j = 0; j < S; ++j)
-    for (uint32_t l = 0; l < nl; ++l) pk->out_pos[(size_t)j * nl + l] = l * S + j;
+    for (uint32_t l = 0; l < nl; ++l) pk->out_pos[(size_t)j * nl + l] = j * nl + l;
   std::vector<uint32_t> fill((size_t)nl * S, 0);
   pk->msg_pos.resize(in->n_msgs);
   for (size_t k = 0; k < in->n_msgs; ++k) {
@@ -267,7 +269,7 @@ inline void decode_outbox(const void* space, const PackedInbox& pk, uint32_t S, 
   const uint32_t nl = (uint32_t)pk.peers.size();
   for (uint32_t l = 0; l < nl; ++l) {
     for (uint32_t j = 0; j < S; ++j) {
-      const Mailbox mb = v.at(l * S + j);
+      const Mailbox mb = v.at(j * nl + l);
       const uint32_t c = std::min<uint32_t>(mb.cnt(), GR_C);
       for (uint32_t k = 0; k < c; ++k) {
         gr_message m = decode_msg(mb, k);

@@ -415,10 +415,10 @@ struct Lane {
 
   // ---------------------------------------------------------------- emission
   GR_HD uint32_t out_gpos(uint32_t j) const {
-    return kp.has_routes ? kp.ln.out_pos()[(uint64_t)j * kp.ln.lcap + i] : i * (uint32_t)S + j;
+    return kp.has_routes ? kp.ln.out_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
   }
   GR_HD uint32_t in_gpos(uint32_t j) const {
-    return kp.has_routes ? kp.ln.in_pos()[(uint64_t)j * kp.ln.lcap + i] : i * (uint32_t)S + j;
+    return kp.has_routes ? kp.ln.in_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
   }
   // raft.send (raft.go:457-461): From is implied by the mailbox; Term is
   // r.term unless the type is a request (finalizeMessageTerm :444-455).

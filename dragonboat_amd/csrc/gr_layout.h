@@ -174,7 +174,8 @@ enum StatField : uint32_t {
 
 // Kernel argument (small, passed by value, lives in SGPRs).
 // Lane i steps peer lane_peer[i] (identity when has_lane_peer == 0). Route
-// tables live in the lane block; has_routes == 0 => identity i*S + j.
+// tables live in the lane block; has_routes == 0 => identity j*n_lanes + i
+// (slot-major, so a wave touches consecutive mailboxes).
 struct StepParams {
   StateBase st;
   LaneBase ln;

@@ -93,16 +93,20 @@ class Topology:
         return nxt[order]
 
     def loopback_routes(self, S):
-        """in_pos/out_pos tables [S][n] for a one-space loopback: mailbox p*S + j."""
+        """in_pos/out_pos tables [S][n] for a one-space loopback.
+
+        Mailbox (receiver q, sender slot j) sits at position j*n + q (slot-major),
+        so the 64 lanes of a wave read and write 64 consecutive positions of
+        every message field array (coalesced), receivers and senders alike."""
         n = self.R * self.G
         p = np.arange(n, dtype=np.int64)
         in_pos = np.full((S, n), NOPOS, np.uint32)
         out_pos = np.full((S, n), NOPOS, np.uint32)
         for j in range(self.R):
             other = self.replica != j
-            in_pos[j, other] = (p[other] * S + j).astype(np.uint32)
+            in_pos[j, other] = (j * n + p[other]).astype(np.uint32)
             dp = j * self.G + self.group
-            out_pos[j, other] = (dp[other] * S + self.replica[other]).astype(np.uint32)
+            out_pos[j, other] = (self.replica[other] * n + dp[other]).astype(np.uint32)
         return in_pos, out_pos
 
 
