@@ -127,6 +127,16 @@ struct Lane {
   uint64_t committed0 = 0;
   uint32_t msgs_in = 0, msgs_out = 0;
 
+  // FAST only: everything run_fast() prefetches (see there)
+  static constexpr int FM = 4;  // messages per lane on the fast path
+  uint32_t fm_n = 0;
+  uint32_t fm_hdr[FAST ? FM : 1];  // type | flags << 8 | slot << 16
+  uint32_t fm_ne[FAST ? FM : 1];   // Replicate entry count
+  uint64_t fm_term[FAST ? FM : 1], fm_a[FAST ? FM : 1], fm_b[FAST ? FM : 1], fm_c[FAST ? FM : 1],
+      fm_d[FAST ? FM : 1];
+  uint64_t fm_rid[FAST ? S : 1];   // node ids of the slots that sent messages (follower)
+  uint32_t fm_gout[FAST ? S : 1];  // out mailbox per slot
+
   GR_HD Lane(const StepParams& k, uint32_t lane, uint32_t peer) : kp(k), p(peer), i(lane) {}
 
   GR_HD uint64_t& s64(uint32_t row) const { return kp.st.u64(row)[p]; }
@@ -415,6 +425,7 @@ struct Lane {
 
   // ---------------------------------------------------------------- emission
   GR_HD uint32_t out_gpos(uint32_t j) const {
+    if constexpr (FAST) return sel(fm_gout, j);
     return kp.has_routes ? kp.ln.out_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
   }
   GR_HD uint32_t in_gpos(uint32_t j) const {
@@ -539,7 +550,8 @@ struct Lane {
     return 0;
   }
   GR_HD void set_leader_from(uint32_t j) {  // setLeaderID(m.From), raft.go:239-244
-    leader_id = remote_id(j);
+    if constexpr (FAST) leader_id = sel(fm_rid, j);
+    else leader_id = remote_id(j);
     loaded |= G_LID;
     dirty |= D_LEADER;
   }
@@ -1236,9 +1248,119 @@ struct Lane {
     msgs_out = 0;
     outcnt = 0;
   }
+  // ---------------------------------------------------------------- FAST lane
+  // The steady-state lane issues every load before its first store: gfx9
+  // counts loads and stores in one vmcnt, so a load consumed after a store
+  // also waits for that store to complete. Three dependent load rounds:
+  //   routes + core + window + locals -> mailbox counts + leader remotes ->
+  //   message fields + sender ids;
+  // then the same handlers as the general lane run on registers only, and
+  // their stores (messages, state) drain at the end. Anything else bails.
+  GR_HD void fast_msg(uint32_t x, InMsg& m) const {
+    const uint32_t h = sel(fm_hdr, x);
+    m.type = (uint8_t)(h & 0xFFu);
+    m.flags = (uint8_t)((h >> 8) & 0xFFu);
+    m.term = sel(fm_term, x);
+    m.n = 0; m.run2 = 0;
+    m.log_term = 0; m.commit = 0; m.hint = 0; m.hint_high = 0; m.rt0 = 0; m.rt1 = 0;
+    m.log_index = sel(fm_a, x);
+    if (m.type == GR_REPLICATE) {  // read_msg's fields for the two types
+      m.n = sel(fm_ne, x);
+      m.log_term = sel(fm_b, x);
+      m.commit = sel(fm_c, x);
+      if (m.n) m.rt0 = sel(fm_d, x);
+    } else {
+      m.hint = sel(fm_b, x);
+    }
+  }
+  GR_HD int run_fast(uint32_t* at) {
+    *at = 0;
+    // round 1
+    uint32_t gin[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      gin[j] = kp.has_routes ? kp.ln.in_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
+      fm_gout[j] = kp.has_routes ? kp.ln.out_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
+    }
+    need(G_CORE | G_WIN);
+    uint32_t lf = 0, nt = 0, nq = 0, np = 0;
+    if (kp.has_locals) {
+      lf = kp.ln.u8(LR_LFLAGS)[i];
+      nt = kp.ln.u32(LR_TICKS)[i];
+      nq = kp.ln.u32(LR_QTICKS)[i];
+      np = kp.ln.u32(LR_PROPOSE)[i];
+    }
+    // round 2
+    const bool leader = state == GR_LEADER;
+    if (leader) need(G_REM | G_LTT | G_EUB);
+    uint32_t cnt[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) cnt[j] = gin[j] != NOPOS ? (uint32_t)kp.in.at(gin[j]).cnt() : 0u;
+    if (!leader && state != GR_FOLLOWER) return ESC_FAST;
+    if ((lf & (LF_READ_INDEX | LF_PROPOSE_CC)) || nt || nq || (np && !leader)) return ESC_FAST;
+    if (leader && ltt != 0) return ESC_FAST;
+    // round 3
+    uint32_t total = 0;
+    bool over = false;
+    fm_n = 0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      total += cnt[j];
+      over = over || cnt[j] > 2;
+      fm_rid[j] = (!leader && cnt[j]) ? remote_id((uint32_t)j) : 0;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if ((uint32_t)k < cnt[j] && fm_n < (uint32_t)FM) {
+          const Mailbox mb = kp.in.at(gin[j]);
+          const uint32_t x = fm_n;
+          put(fm_hdr, x, (uint32_t)mb.type(k) | ((uint32_t)mb.flags(k) << 8) | ((uint32_t)j << 16));
+          put(fm_term, x, mb.u64(k, MF_TERM));
+          put(fm_a, x, mb.u64(k, MF_LOG_INDEX));
+          if (leader) {  // ReplicateResp expected
+            put(fm_b, x, mb.u64(k, MF_HINT));
+          } else {       // Replicate expected
+            put(fm_ne, x, mb.n(k));
+            put(fm_b, x, mb.u64(k, MF_LOG_TERM));
+            put(fm_c, x, mb.u64(k, MF_COMMIT));
+            put(fm_d, x, mb.u64(k, MF_RT0));
+          }
+          fm_n++;
+        }
+      }
+    }
+    if (over || total > (uint32_t)FM) return ESC_FAST;
+#pragma unroll
+    for (int x = 0; x < FM; ++x) {
+      if ((uint32_t)x < fm_n) {
+        const uint32_t t = fm_hdr[x] & 0xFFu, fl = (fm_hdr[x] >> 8) & 0xFFu;
+        if (t != (leader ? (uint32_t)GR_REPLICATE_RESP : (uint32_t)GR_REPLICATE)) return ESC_FAST;
+        if (!leader && ((fl >> MFL_RUNS_SHIFT) & 3u) > 1) return ESC_FAST;
+      }
+    }
+    // compute (stores drain from here on)
+    uint32_t item = 0;
+#pragma unroll 1
+    for (uint32_t x = 0; x < fm_n; ++x) {
+      InMsg m;
+      fast_msg(x, m);
+      const int e = handle(m, (sel(fm_hdr, x) >> 16) & 0xFFu);
+      if (e) { *at = item; return e; }
+      msgs_in++;
+      item++;
+    }
+    if (np) {
+      const int e = propose(np, false);
+      if (e) { *at = item; return e; }
+      item++;
+    }
+    *at = item;
+    return 0;
+  }
+
   // Process items [0, limit); returns an escalation code and the item index
   // where it stopped (*at), or 0 with *at = number of items processed.
   GR_HD int run(uint32_t limit, uint32_t* at) {
+    if constexpr (FAST) return run_fast(at);
     uint32_t item = 0;
 #pragma unroll 1
     for (uint32_t j = 0; j < (uint32_t)S; ++j) {
