@@ -15,6 +15,7 @@
 #include <new>
 #include <vector>
 
+#include "gr_fast.h"
 #include "gr_host.h"
 #include "gr_lane.h"
 
@@ -52,9 +53,9 @@ __device__ inline void block_stats(const StepParams& kp, uint32_t lc, uint32_t f
   }
 }
 
-// Pass 1: every lane runs the steady-state subset (Lane<S, true>). Lanes that
+// Pass 1: every lane runs the lean steady-state lane (gr_fast.h). Lanes that
 // meet anything else append themselves to bail_list (one atomic per wave;
-// a wave's lanes stay contiguous and ascending) and store nothing.
+// a wave's lanes stay contiguous and ascending) and store no state.
 template <int S>
 __global__ __launch_bounds__(kBlock) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
                                                          uint32_t* bail_count) {
@@ -63,8 +64,7 @@ __global__ __launch_bounds__(kBlock) void gr_fast_kernel(StepParams kp, uint32_t
   bool bail = false;
   if (i < kp.n_lanes) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-    Lane<S, true> L(kp, i, p);
-    bail = !L.step(&lc, &fc, &es, &mi, &mo);
+    bail = !fast_step<S>(kp, i, p, &lc, &fc, &mi, &mo);
   }
   const uint64_t bm = __ballot(bail);
   if (bm) {
@@ -171,6 +171,9 @@ struct gr_engine {
   bool timing = false;
   std::vector<PassTiming> timings;  // one per pass while timing
   bool routes_bound = false;
+  uint8_t route_mode = RT_TABLE;  // of the bound routes (RT_TABLE or RT_AFFINE)
+  uint32_t route_g = 0;
+  uint32_t* route_base = nullptr;  // device [2][GR_SMAX][GR_SMAX]
   bool locals_set = false;
   uint64_t passes = 0;
 
@@ -413,7 +416,8 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
   void *ds = nullptr, *dl = nullptr;
   if (hipMalloc(&ds, sb) != hipSuccess || hipMalloc(&dl, lb) != hipSuccess ||
       hipMalloc((void**)&e->stats, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
-      hipMalloc((void**)&e->bail, ((size_t)e->cap + 2) * 4) != hipSuccess) {
+      hipMalloc((void**)&e->bail, ((size_t)e->cap + 2) * 4) != hipSuccess ||
+      hipMalloc((void**)&e->route_base, 2 * GR_SMAX * GR_SMAX * 4) != hipSuccess) {
     if (ds) (void)hipFree(ds);
     if (dl) (void)hipFree(dl);
     e->st.base = nullptr;
@@ -441,6 +445,7 @@ void gr_destroy(gr_engine* e) {
   if (e->ln.base) (void)hipFree(e->ln.base);
   if (e->stats) (void)hipFree(e->stats);
   if (e->bail) (void)hipFree(e->bail);
+  if (e->route_base) (void)hipFree(e->route_base);
   free_timings(e);
   if (e->d_in) (void)hipFree(e->d_in);
   if (e->d_out) (void)hipFree(e->d_out);
@@ -541,7 +546,7 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
   StepParams kp = base_params(e);
   kp.has_locals = 1;
   kp.has_lane_peer = 1;
-  kp.has_routes = 1;
+  kp.route_mode = RT_TABLE;
   kp.in = make_view(e->d_in, 1, pk.in_positions);
   kp.out = make_view(e->d_out, 1, pk.out_positions);
   kp.n_lanes = nl;
@@ -630,6 +635,16 @@ int gr_stats_reset(gr_engine* e) {
 int gr_bind_routes(gr_engine* e, const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n_peers) {
   if (!e || !in_pos || !out_pos || n_peers > e->cfg.max_peers) return GR_EINVAL;
   HIPCHK(hipDeviceSynchronize());
+  std::vector<uint32_t> base(2 * GR_SMAX * GR_SMAX, NOPOS);
+  uint32_t g = 0;
+  if (detect_affine_routes(in_pos, out_pos, n_peers, e->S, base.data(), &g)) {
+    HIPCHK(hipMemcpy(e->route_base, base.data(), base.size() * 4, hipMemcpyHostToDevice));
+    e->route_mode = RT_AFFINE;
+    e->route_g = g;
+  } else {
+    e->route_mode = RT_TABLE;
+    e->route_g = 0;
+  }
   for (uint32_t j = 0; j < e->S; ++j) {
     HIPCHK(hipMemcpy(e->ln.in_pos() + (size_t)j * e->cap, in_pos + (size_t)j * n_peers, (size_t)n_peers * 4,
                      hipMemcpyHostToDevice));
@@ -662,7 +677,9 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
   StepParams kp = base_params(e);
   kp.has_locals = e->locals_set ? 1 : 0;
   kp.has_lane_peer = 0;
-  kp.has_routes = e->routes_bound ? 1 : 0;
+  kp.route_mode = e->routes_bound ? e->route_mode : RT_IDENTITY;
+  kp.route_g = e->route_g;
+  kp.route_base = e->route_base;
   kp.in = make_view(in_space, in_chunks, in_positions);
   kp.out = make_view(out_space, out_chunks, out_positions);
   kp.n_lanes = n_peers;

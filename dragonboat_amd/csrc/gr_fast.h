@@ -1,0 +1,467 @@
+// gr_fast.h — the lean steady-state lane of the step kernel.
+//
+// Most lanes of a pass are in one of two steady states:
+//   leader:   ReplicateResp accepts at the current term, then ProposeEntries
+//             (raft.go:1205-1227 handleLeaderReplicateResp, tryCommit
+//             :625-641, broadcastReplicateMessage :534-546, handleLeaderPropose
+//             :1125-1146);
+//   follower: Replicate at the current term from one remote, appending at the
+//             end of its log (raft.go:1359-1363, handleReplicateMessage
+//             :953-976, logentry.go:281-312 tryAppend/getConflictIndex).
+// fast_step<S> restates exactly that subset of the general lane (gr_lane.h,
+// same field semantics, same message fields) with every remote slot a
+// compile-time index, the term window reduced to its newest run, and all
+// loads issued in three rounds before any store. Anything else — another
+// message type, a term mismatch, a reject, a lookup below the newest run, a
+// truncation, ticks, ReadIndex, more than two messages in a mailbox — returns
+// false before the first state store; the general lane then steps the lane
+// from its untouched state (message bodies this lane may have written to its
+// out mailboxes are overwritten there, and their counts were never written).
+#pragma once
+#include "gr_layout.h"
+
+namespace gr {
+
+#define GF_HD __host__ __device__ inline __attribute__((always_inline))
+// A condition outside the steady state clears `ok`; the lane keeps computing
+// (branch-light, no early exits: keeps the exec-mask nesting shallow) and
+// hands over at the end. Nothing but uncounted message bodies is stored
+// before `ok` is checked.
+#define GF_BAIL(c) (ok = ok && !(c))
+
+template <int S>
+struct FastLane {
+  using Rw = Rows<S>;
+  static constexpr int MK = 2;  // messages per mailbox handled here
+
+  const StepParams& kp;
+  const uint32_t i, p;
+  // core
+  uint32_t state = 0, self = 0, nruns = 0;
+  uint64_t term = 0, committed = 0, committed0 = 0, hi = 0, hi0 = 0, lo = 0;
+  uint64_t rsn = 0, rtn = 0;  // newest term run (start, term)
+  bool pushed = false;        // a run was appended this pass (row nruns-1)
+  bool ok = true;             // still on the steady-state path
+  // leader remotes
+  uint64_t match[S], next[S];
+  uint32_t rst[S], ract[S], rkind[S];
+  bool rem_dirty = false;
+  uint32_t snapz = 0;
+  // emission
+  uint32_t gout[S];
+  uint32_t outc[S];
+  uint32_t nmo = 0, nmi = 0;
+  // results
+  uint64_t append_from = 0, propose_first = 0;
+  uint32_t prop_result = 0;
+
+  GF_HD FastLane(const StepParams& k, uint32_t lane, uint32_t peer) : kp(k), i(lane), p(peer) {}
+
+  GF_HD uint64_t& s64(uint32_t row) const { return kp.st.u64(row)[p]; }
+  GF_HD uint8_t& s8(uint32_t row) const { return kp.st.u8(row)[p]; }
+
+  // entryLog.term (logentry.go:141-157) when the answer is in the newest run;
+  // an older run (or the host's LogReader) hands the lane over.
+  GF_HD uint64_t term_of(uint64_t x) {
+    const bool out = x < lo || x > hi;
+    GF_BAIL(!out && (nruns == 0 || x < rsn));
+    return out ? 0 : rtn;
+  }
+  // win_push (gr_lane.h) for one new run per pass, no window shift.
+  GF_HD void win_push(uint64_t start, uint64_t t) {
+    if (nruns > 0 && rtn == t) return;
+    GF_BAIL(pushed || nruns >= (uint32_t)GR_K);
+    rsn = start;
+    rtn = t;
+    nruns++;
+    pushed = true;
+  }
+  // raft.send (raft.go:457-461) of a Replicate into slot j.
+  GF_HD void emit_replicate(int j, uint64_t log_index, uint64_t log_term, uint32_t n, uint64_t rt0) {
+    GF_BAIL(gout[j] == NOPOS || outc[j] >= (uint32_t)GR_C);
+    if (!ok) return;
+    const Mailbox mb = kp.out.at(gout[j]);
+    const uint32_t c = outc[j];
+    mb.type(c) = GR_REPLICATE;
+    mb.flags(c) = (uint8_t)(n ? (1u << MFL_RUNS_SHIFT) : 0u);
+    mb.u64(c, MF_TERM) = term;
+    mb.n(c) = n;
+    mb.u64(c, MF_LOG_INDEX) = log_index;
+    mb.u64(c, MF_LOG_TERM) = log_term;
+    mb.u64(c, MF_COMMIT) = committed;
+    if (n) mb.u64(c, MF_RT0) = rt0;
+    outc[j] = c + 1;
+    nmo++;
+  }
+  // ... and of a ReplicateResp into the mailbox at gpos.
+  GF_HD void emit_resp(uint32_t gpos, uint32_t* cnt, uint64_t log_index, bool reject, uint64_t hint) {
+    GF_BAIL(gpos == NOPOS || *cnt >= (uint32_t)GR_C);
+    if (!ok) return;
+    const Mailbox mb = kp.out.at(gpos);
+    const uint32_t c = *cnt;
+    mb.type(c) = GR_REPLICATE_RESP;
+    mb.flags(c) = (uint8_t)(reject ? MFL_REJECT : 0u);
+    mb.u64(c, MF_TERM) = term;
+    mb.u64(c, MF_LOG_INDEX) = log_index;
+    if (reject) mb.u64(c, MF_HINT) = hint;
+    *cnt = c + 1;
+    nmo++;
+  }
+
+  // ------------------------------------------------------------- leader
+  // raft.tryCommit + sortMatchValues + entryLog.tryCommit (raft.go:600-641,
+  // logentry.go:359-374): order statistic of the voting match values by an
+  // odd-even transposition network; non-voters sort to the end as +inf.
+  GF_HD bool try_commit() {
+    uint64_t m[S];
+    int nv = 0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const bool v = rkind[j] == GR_SLOT_VOTER;
+      m[j] = v ? match[j] : ~0ull;
+      nv += v;
+    }
+    GF_BAIL(nv == 0);
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+#pragma unroll
+      for (int x = (r & 1); x + 1 < S; x += 2) {
+        const uint64_t a = m[x], b = m[x + 1];
+        m[x] = a < b ? a : b;
+        m[x + 1] = a < b ? b : a;
+      }
+    }
+    const int qi = nv - (nv / 2 + 1);
+    uint64_t q = m[0];
+#pragma unroll
+    for (int x = 1; x < S; ++x) q = (x == qi) ? m[x] : q;
+    if (q <= committed) return false;
+    const uint64_t lt = term_of(q);
+    if (lt != term) return false;
+    GF_BAIL(q > hi);  // commitTo panics (logentry.go:318-321)
+    committed = q;
+    return true;
+  }
+  // sendReplicateMessage / makeReplicateMessage (raft.go:474-532), one entry at most.
+  GF_HD void send_replicate(int j) {
+    if (rst[j] == GR_WAIT || rst[j] == GR_SNAPSHOT_ST) return;  // isPaused, remote.go:158-171
+    const uint64_t nx = next[j];
+    const uint64_t lt = term_of(nx - 1);
+    uint32_t n = 0;
+    if (nx <= hi) {
+      GF_BAIL(nx <= lo);                // InstallSnapshot path
+      GF_BAIL(nruns == 0 || nx < rsn);  // entries in an older run
+      GF_BAIL(hi - nx + 1 > 1);         // several entries: MaxEntrySize check
+      GF_BAIL(rst[j] != GR_REPLICATE_ST && rst[j] != GR_RETRY);
+      n = 1;
+      if (rst[j] == GR_REPLICATE_ST) next[j] = hi + 1;  // remote.progress, remote.go:120-128
+      else rst[j] = GR_WAIT;
+      rem_dirty = true;
+    }
+    emit_replicate(j, nx - 1, lt, n, rtn);
+  }
+  GF_HD void broadcast() {  // raft.go:534-546: voters (not self), then observers
+#pragma unroll
+    for (int j = 0; j < S; ++j)
+      if (rkind[j] == GR_SLOT_VOTER && (uint32_t)j != self) send_replicate(j);
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      if (rkind[j] == GR_SLOT_OBSERVER) {
+        GF_BAIL((uint32_t)j == self);
+        send_replicate(j);
+      }
+    }
+  }
+  // remote.tryUpdate (remote.go:108-118)
+  GF_HD bool try_update(int j, uint64_t index) {
+    if (next[j] < index + 1) next[j] = index + 1;
+    if (match[j] < index) {
+      if (rst[j] == GR_WAIT) rst[j] = GR_RETRY;
+      match[j] = index;
+      return true;
+    }
+    return false;
+  }
+  // handleLeaderReplicateResp, accept path (raft.go:1205-1221); no leader transfer.
+  GF_HD void replicate_resp(int j, uint64_t index) {
+    ract[j] = 1;
+    rem_dirty = true;
+    const bool paused = rst[j] == GR_WAIT || rst[j] == GR_SNAPSHOT_ST;
+    if (!try_update(j, index)) return;
+    GF_BAIL(rst[j] == GR_SNAPSHOT_ST);
+    if (rst[j] == GR_RETRY) {  // respondedTo -> becomeReplicate (remote.go:92-96,130-138)
+      next[j] = match[j] + 1;
+      snapz |= 1u << j;
+      rst[j] = GR_REPLICATE_ST;
+    }
+    if (try_commit()) broadcast();
+    else if (paused) send_replicate(j);
+  }
+  // handleLeaderPropose + appendEntries (raft.go:1125-1146, 643-654)
+  GF_HD void propose(uint32_t np) {
+    uint32_t sk = GR_SLOT_EMPTY;
+#pragma unroll
+    for (int j = 0; j < S; ++j) sk = ((uint32_t)j == self) ? rkind[j] : sk;
+    if (sk != GR_SLOT_VOTER) {  // selfRemoved: dropped (raft.go:1126-1129)
+      prop_result = GR_PROP_DROPPED;
+      return;
+    }
+    GF_BAIL(nruns > 0 && rtn > term);  // checkEntriesToAppend would panic
+    const uint64_t first = hi + 1;
+    win_push(first, term);
+    hi += np;
+#pragma unroll
+    for (int j = 0; j < S; ++j)
+      if ((uint32_t)j == self) try_update(j, hi);
+    rem_dirty = true;
+    int nv = 0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) nv += rkind[j] == GR_SLOT_VOTER;
+    if (nv / 2 + 1 == 1) try_commit();
+    broadcast();
+    prop_result = GR_PROP_APPENDED;
+    propose_first = first;
+  }
+
+  // ------------------------------------------------------------- step
+  GF_HD bool step(uint32_t* st_lc, uint32_t* st_fc, uint32_t* st_mi, uint32_t* st_mo) {
+    // ---- round 1: core, locals, routes
+    state = s8(Rw::B_STATE);
+    self = s8(Rw::B_SELF);
+    nruns = s8(Rw::B_NRUNS);
+    term = s64(SR_TERM);
+    committed = s64(SR_COMMITTED);
+    hi = s64(SR_LAST_INDEX);
+    lo = s64(SR_LO);
+    uint32_t lf = 0, nt = 0, nq = 0, np = 0;
+    if (kp.has_locals) {
+      lf = kp.ln.u8(LR_LFLAGS)[i];
+      nt = kp.ln.u32(LR_TICKS)[i];
+      nq = kp.ln.u32(LR_QTICKS)[i];
+      np = kp.ln.u32(LR_PROPOSE)[i];
+    }
+    uint32_t gin[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      gin[j] = route_of(kp, 0, j, i);
+      gout[j] = route_of(kp, 1, j, i);
+      outc[j] = 0;
+    }
+    // ---- round 2: mailbox counts, newest run, leader remotes
+    uint32_t cnt[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) cnt[j] = gin[j] != NOPOS ? (uint32_t)kp.in.at(gin[j]).cnt() : 0u;
+    if (nruns) {
+      rsn = s64(SR_RUN_START + nruns - 1);
+      rtn = s64(SR_RUN_TERM + nruns - 1);
+    }
+    const bool leader = state == GR_LEADER;
+    uint64_t ltt = 0;
+    if (leader) {
+      ltt = s64(SR_LTT);
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        match[j] = s64(Rw::MATCH + j);
+        next[j] = s64(Rw::NEXT + j);
+        rst[j] = s8(Rw::B_RSTATE + j) & 3u;
+        ract[j] = s8(Rw::B_RACTIVE + j) & 1u;
+        rkind[j] = s8(Rw::B_RKIND + j) & 3u;
+      }
+    }
+    // ---- round 3: message fields
+    // leader: ReplicateResp (type, flags, term, LogIndex) from every slot
+    uint32_t lh[S][MK];
+    uint64_t lterm[S][MK], lidx[S][MK];
+    // follower: Replicate fields from the one slot L that sent, + its node id
+    uint32_t L = 0, nsrc = 0, c = 0, gl = 0, go = NOPOS;
+    uint32_t fh[MK], fn[MK];
+    uint64_t fterm[MK], fidx[MK], flt[MK], fcom[MK], frt0[MK];
+    uint64_t rid = 0;
+    if (leader) {
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+#pragma unroll
+        for (int k = 0; k < MK; ++k) {
+          lh[j][k] = 0;
+          lterm[j][k] = 0;
+          lidx[j][k] = 0;
+          if ((uint32_t)k < cnt[j]) {
+            const Mailbox mb = kp.in.at(gin[j]);
+            lh[j][k] = (uint32_t)mb.type(k) | ((uint32_t)mb.flags(k) << 8);
+            lterm[j][k] = mb.u64(k, MF_TERM);
+            lidx[j][k] = mb.u64(k, MF_LOG_INDEX);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        if (cnt[j]) {
+          L = (uint32_t)j;
+          c = cnt[j];
+          gl = gin[j];
+          go = gout[j];
+          nsrc++;
+        }
+      }
+      const uint32_t cc = c < (uint32_t)MK ? c : (uint32_t)MK;
+#pragma unroll
+      for (int k = 0; k < MK; ++k) {
+        fh[k] = 0; fn[k] = 0; fterm[k] = 0; fidx[k] = 0; flt[k] = 0; fcom[k] = 0; frt0[k] = 0;
+        if ((uint32_t)k < cc) {
+          const Mailbox mb = kp.in.at(gl);
+          fh[k] = (uint32_t)mb.type(k) | ((uint32_t)mb.flags(k) << 8);
+          fn[k] = mb.n(k);
+          fterm[k] = mb.u64(k, MF_TERM);
+          fidx[k] = mb.u64(k, MF_LOG_INDEX);
+          flt[k] = mb.u64(k, MF_LOG_TERM);
+          fcom[k] = mb.u64(k, MF_COMMIT);
+          frt0[k] = mb.u64(k, MF_RT0);
+        }
+      }
+      if (c) rid = s64(Rw::RID + L);
+    }
+    // ---- checks: anything outside the steady state goes to the general lane
+    GF_BAIL(!leader && state != GR_FOLLOWER);
+    GF_BAIL((lf & (LF_READ_INDEX | LF_PROPOSE_CC)) || nt || nq || (np && !leader));
+    committed0 = committed;
+    hi0 = hi;
+    if (leader) {
+      GF_BAIL(ltt != 0);  // leader transfer in progress
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        GF_BAIL(cnt[j] > (uint32_t)MK);
+#pragma unroll
+        for (int k = 0; k < MK; ++k)
+          if ((uint32_t)k < cnt[j]) GF_BAIL(lh[j][k] != GR_REPLICATE_RESP || lterm[j][k] != term);
+      }
+      // messages in node.handleReceivedMessages order: slot, then arrival
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+#pragma unroll
+        for (int k = 0; k < MK; ++k) {
+          if ((uint32_t)k < cnt[j]) {
+            nmi++;
+            if (rkind[j] != GR_SLOT_EMPTY) replicate_resp(j, lidx[j][k]);
+          }
+        }
+      }
+      if (np) propose(np);
+    } else {
+      GF_BAIL(nsrc > 1 || c > (uint32_t)MK);
+#pragma unroll
+      for (int k = 0; k < MK; ++k) {
+        if ((uint32_t)k < c) {
+          GF_BAIL((fh[k] & 0xFFu) != GR_REPLICATE || fterm[k] != term);
+          const uint32_t nr = (fh[k] >> (8 + MFL_RUNS_SHIFT)) & 3u;
+          GF_BAIL(fn[k] != 0 && nr != 1);
+        }
+      }
+      uint32_t oc = 0;
+#pragma unroll
+      for (int k = 0; k < MK; ++k) {
+        if ((uint32_t)k < c) {
+          nmi++;
+          replicate(fidx[k], flt[k], fcom[k], fn[k], frt0[k], go, &oc);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < S; ++j) outc[j] = ((uint32_t)j == L) ? oc : 0u;
+    }
+    if (!ok) return false;
+    // ---- stores (nothing above this line has written state)
+    if (committed != committed0) s64(SR_COMMITTED) = committed;
+    if (hi != hi0) s64(SR_LAST_INDEX) = hi;
+    if (pushed) {
+      s64(SR_RUN_START + nruns - 1) = rsn;
+      s64(SR_RUN_TERM + nruns - 1) = rtn;
+      s8(Rw::B_NRUNS) = (uint8_t)nruns;
+    }
+    if (leader) {
+      if (rem_dirty) {
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          s64(Rw::MATCH + j) = match[j];
+          s64(Rw::NEXT + j) = next[j];
+          s8(Rw::B_RSTATE + j) = (uint8_t)rst[j];
+          s8(Rw::B_RACTIVE + j) = (uint8_t)ract[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < S; ++j)
+        if ((snapz >> j) & 1u) s64(Rw::SNAP + j) = 0;
+    } else if (c) {
+      s64(SR_ETICK) = 0;        // electionTick = 0 (raft.go:1360)
+      s64(SR_LEADER_ID) = rid;  // setLeaderID(m.From)
+    }
+#pragma unroll
+    for (int j = 0; j < S; ++j)
+      if (gout[j] != NOPOS) kp.out.at(gout[j]).cnt() = (uint8_t)outc[j];
+    uint8_t rf = 0;
+    if (prop_result) {
+      rf |= RF_PROPOSE;
+      kp.ln.u8(LR_PROP_RESULT)[i] = (uint8_t)prop_result;
+      kp.ln.u64(LR_PROPOSE_FIRST)[i] = propose_first;
+    }
+    if (append_from) {
+      rf |= RF_APPEND;
+      kp.ln.u64(LR_APPEND_FROM)[i] = append_from;
+    }
+    kp.ln.u8(LR_RFLAGS)[i] = rf;
+    const bool adv = committed > committed0;
+    *st_lc = adv && leader;
+    *st_fc = adv && !leader;
+    *st_mi = nmi;
+    *st_mo = nmo;
+    return true;
+  }
+
+  // handleReplicateMessage (raft.go:953-976) for an append at the log's end.
+  GF_HD void replicate(uint64_t li, uint64_t lterm, uint64_t mcommit, uint32_t n, uint64_t rt0, uint32_t go,
+                       uint32_t* oc) {
+    if (li < committed) {
+      emit_resp(go, oc, committed, false, 0);
+      return;
+    }
+    if (term_of(li) != lterm) {
+      emit_resp(go, oc, li, true, hi);
+      return;
+    }
+    uint64_t ci = 0;
+    if (n) {  // getConflictIndex over the newest run (logentry.go:305-312)
+      const uint64_t a = li + 1, b = li + n;
+      GF_BAIL(a < lo);
+      if (a <= hi) {
+        GF_BAIL(nruns == 0 || a < rsn);
+        if (rtn != rt0) ci = a;
+      }
+      if (ci == 0 && b > hi && rt0 != 0) ci = a > hi + 1 ? a : hi + 1;
+    }
+    if (ci) {
+      GF_BAIL(ci <= committed || ci != hi + 1);  // panic / truncation: general lane
+      GF_BAIL(nruns && rsn > hi);                // a run beyond lastIndex would be truncated
+      const uint64_t tprev = (ci - 1 == li) ? lterm : rt0;
+      GF_BAIL(tprev > rt0);  // checkEntriesToAppend
+      win_push(ci, rt0);
+      hi = li + n;
+      append_from = append_from ? (append_from < ci ? append_from : ci) : ci;
+    }
+    const uint64_t last = li + n;
+    const uint64_t cm = last < mcommit ? last : mcommit;
+    if (cm > committed) {  // commitTo (logentry.go:314-323)
+      GF_BAIL(cm > hi);
+      committed = cm;
+    }
+    emit_resp(go, oc, last, false, 0);
+  }
+};
+
+// Kernel-side entry: the lean lane for lane i; false = hand the lane to the general kernel.
+template <int S>
+GF_HD bool fast_step(const StepParams& kp, uint32_t i, uint32_t p, uint32_t* lc, uint32_t* fc, uint32_t* mi,
+                     uint32_t* mo) {
+  FastLane<S> L(kp, i, p);
+  return L.step(lc, fc, mi, mo);
+}
+
+}  // namespace gr

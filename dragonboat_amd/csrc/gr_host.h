@@ -149,9 +149,9 @@ inline gr_message decode_msg(const Mailbox& mb, uint32_t k) {
         m.run_term[1] = mb.u64(k, MF_RT1);
       }
       break;
-    case GR_REPLICATE_RESP:
+    case GR_REPLICATE_RESP:  // the device writes Hint only on a reject
       m.log_index = mb.u64(k, MF_LOG_INDEX);
-      m.hint = mb.u64(k, MF_HINT);
+      if (m.reject) m.hint = mb.u64(k, MF_HINT);
       break;
     case GR_HEARTBEAT:
       m.commit = mb.u64(k, MF_COMMIT);
@@ -279,6 +279,40 @@ inline void decode_outbox(const void* space, const PackedInbox& pk, uint32_t S, 
       }
     }
   }
+}
+
+// Route tables of a replica-major population (lane i = r*G + g) whose every
+// entry is base[dir][r][j] + g (or NOPOS for the whole (r, j) block) become
+// RT_AFFINE: the kernel computes positions instead of reading 8*S bytes of
+// tables per lane. Tries each replica count R <= S that divides n.
+inline bool detect_affine_routes(const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n, uint32_t S,
+                                 uint32_t* base /* [2][GR_SMAX][GR_SMAX] */, uint32_t* g_out) {
+  if (n == 0) return false;
+  for (uint32_t R = 1; R <= S && R <= GR_SMAX; ++R) {
+    if (n % R) continue;
+    const uint32_t G = n / R;
+    bool ok = true;
+    for (uint32_t d = 0; d < 2 && ok; ++d) {
+      const uint32_t* t = d ? out_pos : in_pos;
+      for (uint32_t r = 0; r < R && ok; ++r) {
+        for (uint32_t j = 0; j < S && ok; ++j) {
+          const uint32_t* row = t + (size_t)j * n + (size_t)r * G;
+          const uint32_t b = row[0];
+          if (b != NOPOS && (uint64_t)b + G - 1 >= NOPOS) { ok = false; break; }
+          for (uint32_t x = 0; x < G; ++x) {
+            const uint32_t want = b == NOPOS ? NOPOS : b + x;
+            if (row[x] != want) { ok = false; break; }
+          }
+          base[(d * GR_SMAX + r) * GR_SMAX + j] = b;
+        }
+      }
+    }
+    if (ok) {
+      *g_out = G;
+      return true;
+    }
+  }
+  return false;
 }
 
 // Local-input rows of a lane block (host copies).

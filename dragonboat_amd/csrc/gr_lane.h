@@ -82,15 +82,10 @@ GR_HD uint64_t rb_with(uint64_t rb, uint32_t j, uint32_t off, uint32_t width, ui
   return (rb & ~m) | (((uint64_t)v << (5 * j + off)) & m);
 }
 
-// Internal code (never reported): a FAST lane met an input outside the fast
-// path and left no trace; the general kernel steps it instead.
-constexpr int ESC_FAST = 0x40;
-
-// FAST = true instantiates the steady-state subset only (the leader's
-// ReplicateResp/Propose, the follower's Replicate, equal terms, no ticks or
-// ReadIndex): the same handler code, with every other branch replaced by an
-// ESC_FAST bail, so the compiler drops the cold paths and their registers.
-template <int S, bool FAST = false>
+// The general lane: every handler of the device path. The steady-state
+// subset runs first in the lean lane of gr_fast.h; this lane steps the lanes
+// that one hands over.
+template <int S>
 struct Lane {
   using R = Rows<S>;
   const StepParams kp;  // by value: small, uniform (SGPRs)
@@ -127,15 +122,6 @@ struct Lane {
   uint64_t committed0 = 0;
   uint32_t msgs_in = 0, msgs_out = 0;
 
-  // FAST only: everything run_fast() prefetches (see there)
-  static constexpr int FM = 4;  // messages per lane on the fast path
-  uint32_t fm_n = 0;
-  uint32_t fm_hdr[FAST ? FM : 1];  // type | flags << 8 | slot << 16
-  uint32_t fm_ne[FAST ? FM : 1];   // Replicate entry count
-  uint64_t fm_term[FAST ? FM : 1], fm_a[FAST ? FM : 1], fm_b[FAST ? FM : 1], fm_c[FAST ? FM : 1],
-      fm_d[FAST ? FM : 1];
-  uint64_t fm_rid[FAST ? S : 1];   // node ids of the slots that sent messages (follower)
-  uint32_t fm_gout[FAST ? S : 1];  // out mailbox per slot
 
   GR_HD Lane(const StepParams& k, uint32_t lane, uint32_t peer) : kp(k), p(peer), i(lane) {}
 
@@ -424,13 +410,8 @@ struct Lane {
   }
 
   // ---------------------------------------------------------------- emission
-  GR_HD uint32_t out_gpos(uint32_t j) const {
-    if constexpr (FAST) return sel(fm_gout, j);
-    return kp.has_routes ? kp.ln.out_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
-  }
-  GR_HD uint32_t in_gpos(uint32_t j) const {
-    return kp.has_routes ? kp.ln.in_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
-  }
+  GR_HD uint32_t out_gpos(uint32_t j) const { return route_of(kp, 1, j, i); }
+  GR_HD uint32_t in_gpos(uint32_t j) const { return route_of(kp, 0, j, i); }
   // raft.send (raft.go:457-461): From is implied by the mailbox; Term is
   // r.term unless the type is a request (finalizeMessageTerm :444-455).
   GR_HD int emit(uint32_t j, const OutMsg& m) {
@@ -458,9 +439,9 @@ struct Lane {
           }
         }
         break;
-      case GR_REPLICATE_RESP:
+      case GR_REPLICATE_RESP:  // Hint is only read on a reject (decreaseTo, raft.go:1219)
         mb.u64(c, MF_LOG_INDEX) = m.log_index;
-        mb.u64(c, MF_HINT) = m.hint;
+        if (m.flags & MFL_REJECT) mb.u64(c, MF_HINT) = m.hint;
         break;
       case GR_HEARTBEAT:
         mb.u64(c, MF_COMMIT) = m.commit;
@@ -550,8 +531,7 @@ struct Lane {
     return 0;
   }
   GR_HD void set_leader_from(uint32_t j) {  // setLeaderID(m.From), raft.go:239-244
-    if constexpr (FAST) leader_id = sel(fm_rid, j);
-    else leader_id = remote_id(j);
+    leader_id = remote_id(j);
     loaded |= G_LID;
     dirty |= D_LEADER;
   }
@@ -887,7 +867,7 @@ struct Lane {
           win_push(ci, m.rt0);
         }
         hi = m.log_index + m.n;
-        dirty |= D_HI | D_WIN;
+        dirty |= D_HI;  // the window is dirty only if win_truncate/win_push changed it
         append_from = append_from ? umin(append_from, ci) : ci;
       }
       const uint64_t last_idx = m.log_index + m.n;
@@ -923,7 +903,6 @@ struct Lane {
           GR_TRY(send_timeout_now(ltt));
       }
     } else {
-      if constexpr (FAST) return ESC_FAST;
       if (decrease_to(j, m.log_index, m.hint)) {
         enter_retry(j);
         GR_TRY(send_replicate(j));
@@ -1010,9 +989,6 @@ struct Lane {
     m.term = mb.u64(k, MF_TERM);
     m.n = 0; m.run2 = 0;
     m.log_index = 0; m.log_term = 0; m.commit = 0; m.hint = 0; m.hint_high = 0; m.rt0 = 0; m.rt1 = 0;
-    if constexpr (FAST) {
-      if (m.type != GR_REPLICATE && m.type != GR_REPLICATE_RESP) return;  // bails in handle()
-    }
     switch (m.type) {
       case GR_REPLICATE:
         m.n = mb.n(k);
@@ -1029,7 +1005,7 @@ struct Lane {
         break;
       case GR_REPLICATE_RESP:
         m.log_index = mb.u64(k, MF_LOG_INDEX);
-        m.hint = mb.u64(k, MF_HINT);
+        if (m.flags & MFL_REJECT) m.hint = mb.u64(k, MF_HINT);
         break;
       case GR_HEARTBEAT:
         m.commit = mb.u64(k, MF_COMMIT);
@@ -1073,20 +1049,6 @@ struct Lane {
   GR_HD int handle(const InMsg& m, uint32_t from) {
     need(G_CORE);
     const uint32_t t = m.type;
-    if constexpr (FAST) {  // the same dispatch as below, for the two hot pairs only
-      if (m.term != term) return ESC_FAST;
-      if (state == GR_LEADER && t == GR_REPLICATE_RESP) {
-        need(G_REM);
-        if (rkind(from) == GR_SLOT_EMPTY) return 0;
-        return leader_replicate_resp(m, from);
-      }
-      if (state == GR_FOLLOWER && t == GR_REPLICATE) {
-        zero_etick();
-        set_leader_from(from);
-        return handle_replicate(m, from);
-      }
-      return ESC_FAST;
-    }
     if (m.term != 0 && m.term != term) {  // onMessageTermNotMatched
       if (m.term > term) {
         if (t == GR_REQUEST_VOTE) return GR_ESC_UNSUPPORTED;  // dropRequestVoteFromHighTermNode + vote
@@ -1248,119 +1210,9 @@ struct Lane {
     msgs_out = 0;
     outcnt = 0;
   }
-  // ---------------------------------------------------------------- FAST lane
-  // The steady-state lane issues every load before its first store: gfx9
-  // counts loads and stores in one vmcnt, so a load consumed after a store
-  // also waits for that store to complete. Three dependent load rounds:
-  //   routes + core + window + locals -> mailbox counts + leader remotes ->
-  //   message fields + sender ids;
-  // then the same handlers as the general lane run on registers only, and
-  // their stores (messages, state) drain at the end. Anything else bails.
-  GR_HD void fast_msg(uint32_t x, InMsg& m) const {
-    const uint32_t h = sel(fm_hdr, x);
-    m.type = (uint8_t)(h & 0xFFu);
-    m.flags = (uint8_t)((h >> 8) & 0xFFu);
-    m.term = sel(fm_term, x);
-    m.n = 0; m.run2 = 0;
-    m.log_term = 0; m.commit = 0; m.hint = 0; m.hint_high = 0; m.rt0 = 0; m.rt1 = 0;
-    m.log_index = sel(fm_a, x);
-    if (m.type == GR_REPLICATE) {  // read_msg's fields for the two types
-      m.n = sel(fm_ne, x);
-      m.log_term = sel(fm_b, x);
-      m.commit = sel(fm_c, x);
-      if (m.n) m.rt0 = sel(fm_d, x);
-    } else {
-      m.hint = sel(fm_b, x);
-    }
-  }
-  GR_HD int run_fast(uint32_t* at) {
-    *at = 0;
-    // round 1
-    uint32_t gin[S];
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-      gin[j] = kp.has_routes ? kp.ln.in_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
-      fm_gout[j] = kp.has_routes ? kp.ln.out_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
-    }
-    need(G_CORE | G_WIN);
-    uint32_t lf = 0, nt = 0, nq = 0, np = 0;
-    if (kp.has_locals) {
-      lf = kp.ln.u8(LR_LFLAGS)[i];
-      nt = kp.ln.u32(LR_TICKS)[i];
-      nq = kp.ln.u32(LR_QTICKS)[i];
-      np = kp.ln.u32(LR_PROPOSE)[i];
-    }
-    // round 2
-    const bool leader = state == GR_LEADER;
-    if (leader) need(G_REM | G_LTT | G_EUB);
-    uint32_t cnt[S];
-#pragma unroll
-    for (int j = 0; j < S; ++j) cnt[j] = gin[j] != NOPOS ? (uint32_t)kp.in.at(gin[j]).cnt() : 0u;
-    if (!leader && state != GR_FOLLOWER) return ESC_FAST;
-    if ((lf & (LF_READ_INDEX | LF_PROPOSE_CC)) || nt || nq || (np && !leader)) return ESC_FAST;
-    if (leader && ltt != 0) return ESC_FAST;
-    // round 3
-    uint32_t total = 0;
-    bool over = false;
-    fm_n = 0;
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-      total += cnt[j];
-      over = over || cnt[j] > 2;
-      fm_rid[j] = (!leader && cnt[j]) ? remote_id((uint32_t)j) : 0;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        if ((uint32_t)k < cnt[j] && fm_n < (uint32_t)FM) {
-          const Mailbox mb = kp.in.at(gin[j]);
-          const uint32_t x = fm_n;
-          put(fm_hdr, x, (uint32_t)mb.type(k) | ((uint32_t)mb.flags(k) << 8) | ((uint32_t)j << 16));
-          put(fm_term, x, mb.u64(k, MF_TERM));
-          put(fm_a, x, mb.u64(k, MF_LOG_INDEX));
-          if (leader) {  // ReplicateResp expected
-            put(fm_b, x, mb.u64(k, MF_HINT));
-          } else {       // Replicate expected
-            put(fm_ne, x, mb.n(k));
-            put(fm_b, x, mb.u64(k, MF_LOG_TERM));
-            put(fm_c, x, mb.u64(k, MF_COMMIT));
-            put(fm_d, x, mb.u64(k, MF_RT0));
-          }
-          fm_n++;
-        }
-      }
-    }
-    if (over || total > (uint32_t)FM) return ESC_FAST;
-#pragma unroll
-    for (int x = 0; x < FM; ++x) {
-      if ((uint32_t)x < fm_n) {
-        const uint32_t t = fm_hdr[x] & 0xFFu, fl = (fm_hdr[x] >> 8) & 0xFFu;
-        if (t != (leader ? (uint32_t)GR_REPLICATE_RESP : (uint32_t)GR_REPLICATE)) return ESC_FAST;
-        if (!leader && ((fl >> MFL_RUNS_SHIFT) & 3u) > 1) return ESC_FAST;
-      }
-    }
-    // compute (stores drain from here on)
-    uint32_t item = 0;
-#pragma unroll 1
-    for (uint32_t x = 0; x < fm_n; ++x) {
-      InMsg m;
-      fast_msg(x, m);
-      const int e = handle(m, (sel(fm_hdr, x) >> 16) & 0xFFu);
-      if (e) { *at = item; return e; }
-      msgs_in++;
-      item++;
-    }
-    if (np) {
-      const int e = propose(np, false);
-      if (e) { *at = item; return e; }
-      item++;
-    }
-    *at = item;
-    return 0;
-  }
-
   // Process items [0, limit); returns an escalation code and the item index
   // where it stopped (*at), or 0 with *at = number of items processed.
   GR_HD int run(uint32_t limit, uint32_t* at) {
-    if constexpr (FAST) return run_fast(at);
     uint32_t item = 0;
 #pragma unroll 1
     for (uint32_t j = 0; j < (uint32_t)S; ++j) {
@@ -1384,13 +1236,6 @@ struct Lane {
       const uint8_t lf = kp.ln.u8(LR_LFLAGS)[i];
       const uint32_t nt = kp.ln.u32(LR_TICKS)[i], nq = kp.ln.u32(LR_QTICKS)[i],
                      np = kp.ln.u32(LR_PROPOSE)[i];
-      if constexpr (FAST) {
-        if ((lf & (LF_READ_INDEX | LF_PROPOSE_CC)) || nt || nq) { *at = item; return ESC_FAST; }
-        if (np) {
-          need(G_CORE);
-          if (state != GR_LEADER) { *at = item; return ESC_FAST; }
-        }
-      }
       if (lf & LF_READ_INDEX) {
         if (item == limit) { *at = item; return 0; }
         need(G_CORE);
@@ -1436,24 +1281,17 @@ struct Lane {
 
   // Kernel body for one lane: run, and on escalation re-run the prefix on the
   // pristine state so the escalating item is left entirely to the host.
-  // A FAST lane returns false, having stored nothing but message bodies in
-  // its (uncounted) out mailboxes, when any item needs the general path.
   GR_HD bool step(uint32_t* stat_leader_commit, uint32_t* stat_follower_commit, uint32_t* stat_esc,
                   uint32_t* stat_in, uint32_t* stat_out) {
     uint32_t at = 0, limit = 0xFFFFFFFFu;
     int esc = 0;
-    if constexpr (FAST) {
-      begin();
-      if (run(limit, &at)) return false;
-    } else {
 #pragma unroll 1
-      for (int attempt = 0; attempt < 2; ++attempt) {  // one call site keeps run() inlined
-        begin();
-        const int e = run(limit, &at);
-        if (!e) break;
-        esc = e;  // second attempt re-runs the prefix and cannot escalate
-        limit = at;
-      }
+    for (int attempt = 0; attempt < 2; ++attempt) {  // one call site keeps run() inlined
+      begin();
+      const int e = run(limit, &at);
+      if (!e) break;
+      esc = e;  // second attempt re-runs the prefix and cannot escalate
+      limit = at;
     }
     store();
 #pragma unroll 1

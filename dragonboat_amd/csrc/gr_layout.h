@@ -172,21 +172,41 @@ enum StatField : uint32_t {
   ST_MSGS_IN = 4, ST_MSGS_OUT = 5, NSTAT = 8
 };
 
+// Route modes: where lane i reads (dir 0) / writes (dir 1) the mailbox of
+// remote slot j.
+//   RT_IDENTITY: j*n_lanes + i (slot-major, so a wave touches consecutive mailboxes)
+//   RT_TABLE:    in_pos/out_pos tables [S][lcap] in the lane block
+//   RT_AFFINE:   replica-major populations (lane i = r*G + g): base[dir][r][j] + g,
+//                base NOPOS = no mailbox. Detected by gr_bind_routes from the
+//                tables; saves the 8*S bytes of route reads per lane.
+constexpr uint8_t RT_IDENTITY = 0, RT_TABLE = 1, RT_AFFINE = 2;
+
 // Kernel argument (small, passed by value, lives in SGPRs).
-// Lane i steps peer lane_peer[i] (identity when has_lane_peer == 0). Route
-// tables live in the lane block; has_routes == 0 => identity j*n_lanes + i
-// (slot-major, so a wave touches consecutive mailboxes).
+// Lane i steps peer lane_peer[i] (identity when has_lane_peer == 0).
 struct StepParams {
   StateBase st;
   LaneBase ln;
   SpaceView in, out;
   uint64_t* stats;     // [gridDim.x][NSTAT] or nullptr
+  const uint32_t* route_base;  // RT_AFFINE: [2][GR_SMAX][GR_SMAX]
   uint64_t max_entry_size;
   uint32_t n_lanes;
+  uint32_t route_g;    // RT_AFFINE: groups per replica block
   uint8_t has_locals;
   uint8_t has_lane_peer;
-  uint8_t has_routes;
+  uint8_t route_mode;
   uint8_t pad;
 };
+
+__host__ __device__ inline uint32_t route_of(const StepParams& kp, uint32_t dir, uint32_t j, uint32_t i) {
+  if (kp.route_mode == RT_TABLE)
+    return (dir ? kp.ln.out_pos() : kp.ln.in_pos())[(uint64_t)j * kp.ln.lcap + i];
+  if (kp.route_mode == RT_AFFINE) {
+    const uint32_t r = i / kp.route_g, g = i - r * kp.route_g;
+    const uint32_t b = kp.route_base[(dir * GR_SMAX + r) * GR_SMAX + j];
+    return b == NOPOS ? NOPOS : b + g;
+  }
+  return j * kp.n_lanes + i;
+}
 
 }  // namespace gr

@@ -47,6 +47,11 @@ def hostlane_lib():
         lib.hl_step.argtypes = [c.c_uint32, c.c_uint64, c.c_void_p, c.c_uint32, c.POINTER(abi.Inbox),
                                 c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t), c.c_void_p,
                                 c.POINTER(c.c_size_t)]
+        lib.hl_counters.argtypes = [c.POINTER(c.c_uint64), c.POINTER(c.c_uint64)]
+        lib.hl_counters.restype = None
+        lib.hl_detect_affine.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32, c.c_void_p,
+                                         c.POINTER(c.c_uint32)]
+        lib.hl_detect_affine.restype = c.c_int
         _hlib = lib
     return _hlib
 
@@ -138,3 +143,23 @@ def hostlane_step(peers, msgs=None, locals_=None, slots=3, max_entry_size=abi.MA
     if rc:
         raise OracleError(f"hl_step rc={rc}")
     return peers, out[:n_out.value], res[:n_res.value]
+
+
+def hostlane_counters():
+    """(lanes finished by the lean steady-state lane, lanes it handed to the general lane)."""
+    lib = hostlane_lib()
+    f, b = ctypes.c_uint64(), ctypes.c_uint64()
+    lib.hl_counters(ctypes.byref(f), ctypes.byref(b))
+    return f.value, b.value
+
+
+def hostlane_affine_routes(in_pos, out_pos, slots):
+    """gr_bind_routes' affine detection (test-only host build): (base [2][8][8], G) or None."""
+    lib = hostlane_lib()
+    in_pos = np.ascontiguousarray(in_pos, np.uint32)
+    out_pos = np.ascontiguousarray(out_pos, np.uint32)
+    base = np.zeros((2, abi.GR_SMAX, abi.GR_SMAX), np.uint32)
+    g = ctypes.c_uint32()
+    ok = lib.hl_detect_affine(in_pos.ctypes.data, out_pos.ctypes.data, in_pos.shape[1], slots,
+                              base.ctypes.data, ctypes.byref(g))
+    return (base, g.value) if ok else None

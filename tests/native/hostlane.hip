@@ -8,6 +8,7 @@
 #include <cstring>
 #include <vector>
 
+#include "gr_fast.h"
 #include "gr_host.h"
 #include "gr_lane.h"
 
@@ -25,9 +26,8 @@ void run_lanes(const StepParams& kp) {
   std::vector<uint32_t> bailed;
   for (uint32_t i = 0; i < kp.n_lanes; ++i) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-    Lane<S, true> F(kp, i, p);
-    uint32_t a, b, c, d, e;
-    if (!F.step(&a, &b, &c, &d, &e)) bailed.push_back(i);
+    uint32_t a, b, c, d;
+    if (!fast_step<S>(kp, i, p, &a, &b, &c, &d)) bailed.push_back(i);
   }
   for (uint32_t i : bailed) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
@@ -89,7 +89,7 @@ extern "C" int hl_step(uint32_t slots, uint64_t max_entry_size, gr_peer* peers, 
   kp.n_lanes = nl;
   kp.has_locals = 1;
   kp.has_lane_peer = 1;
-  kp.has_routes = 1;
+  kp.route_mode = RT_TABLE;
   if (S == 1) run_lanes<1>(kp);
   else if (S == 3) run_lanes<3>(kp);
   else run_lanes<5>(kp);
@@ -138,4 +138,11 @@ extern "C" int hl_step(uint32_t slots, uint64_t max_entry_size, gr_peer* peers, 
 extern "C" void hl_counters(uint64_t* fast, uint64_t* bailed) {
   *fast = g_fast_lanes;
   *bailed = g_bailed_lanes;
+}
+
+// gr_bind_routes' affine-route detection, for the CPU tests
+extern "C" int hl_detect_affine(const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n, uint32_t S,
+                                uint32_t* base, uint32_t* g) {
+  for (uint32_t k = 0; k < 2 * GR_SMAX * GR_SMAX; ++k) base[k] = NOPOS;
+  return detect_affine_routes(in_pos, out_pos, n, S, base, g) ? 1 : 0;
 }

@@ -131,3 +131,39 @@ def test_gloo_all_to_all_delivery(world):
     for p in procs:
         p.join(timeout=60)
     assert all(e == 0 for _, e in res), res
+
+
+@pytest.mark.parametrize("placement,N,rank", [("local", 1, 0), ("spread", 1, 0), ("spread", 2, 1),
+                                              ("spread", 8, 5)])
+def test_routes_are_affine(built, placement, N, rank):
+    """gr_bind_routes turns the bench topologies into RT_AFFINE routes:
+    position = base[dir][replica][slot] + group, reproducing the tables exactly."""
+    from oracle.pyoracle import hostlane_affine_routes
+    G, R, S = 96, 3, 3
+    if placement == "local":
+        in_pos, out_pos = P.Topology(G, R).loopback_routes(S)
+    else:
+        in_pos, out_pos, _ = X.spread_routes(G, R, S, N, rank)
+    got = hostlane_affine_routes(in_pos, out_pos, S)
+    assert got is not None
+    base, g = got
+    assert g == G
+    for d, t in enumerate((in_pos, out_pos)):
+        for j in range(S):
+            for r in range(R):
+                b = int(base[d, r, j])
+                want = t[j, r * G:(r + 1) * G]
+                if b == 0xFFFFFFFF:
+                    assert np.all(want == 0xFFFFFFFF)
+                else:
+                    assert np.array_equal(want, b + np.arange(G, dtype=np.uint32))
+
+
+def test_routes_not_affine_fall_back(built):
+    """A table that is not replica-major affine keeps RT_TABLE."""
+    from oracle.pyoracle import hostlane_affine_routes
+    G, R, S = 64, 3, 3
+    in_pos, out_pos = P.Topology(G, R).loopback_routes(S)
+    in_pos = in_pos.copy()
+    in_pos[1, 5], in_pos[1, 6] = in_pos[1, 6], in_pos[1, 5]
+    assert hostlane_affine_routes(in_pos, out_pos, S) is None
