@@ -1,5 +1,5 @@
 """Headline benchmark: commit-index updates/sec for 1M Raft groups x 3 replicas
-(BASELINE.json configs[3]), one device pass per step, inputs resident in HBM.
+(BASELINE.json configs[3]'s shape), one device pass per step, inputs resident in HBM.
 
 A step = one pass of the batched raft step over every replica of every group:
 leaders ingest the previous pass's ReplicateResp batch, run the quorum commit
@@ -9,10 +9,22 @@ round trip). In steady state every group's leader advances committed by one
 index per pass; `value` counts those advances (device stats) per second.
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
-per GPU, each owning its own 1M groups ("scaling": "weak"). Replicas of a group
-are placed on ranks g, g+1, g+2 (mod N) when --placement spread (default for
-N > 1) and Replicate/ReplicateResp mailboxes cross GPUs with one RCCL
-all_to_all_single per pass; --placement local keeps replicas on one rank.
+per GPU, each owning its own 1M groups sharded by clusterID ("scaling": "weak",
+no data-path collective: the groups are independent, partition.go:34-36).
+--placement spread is BASELINE config 4's synthetic multi-replica variant:
+replica r of a group homed on rank h lives on rank (h + r) % N and the
+Replicate/ReplicateResp mailboxes cross GPUs with one RCCL all_to_all_single
+per pass (dragonboat_amd/exchange.py).
+
+Roofline accounting: algorithmic bytes are SURVEY.md §8d's
+per-unit figures times the units the launch processed, counted on the device:
+69 B per message a leader ingests (B_resp), 65 B per message a leader emits
+(B_emit), 122 + 16 n B per Replicate of n entries a follower matches
+(B_match with ov + ap = n), and 8R + 48 B per group for the quorum commit
+(B_commit). In steady state each follower gets two Replicates per pass (the
+commit-carrying broadcast of raft.go:1214 and the proposal's), so one
+group-round is 1,128 B at R = 3; SURVEY's B_round (616 B) assumes one, and is
+reported beside it as "canonical_round_bytes".
 """
 import argparse
 import json
@@ -27,6 +39,16 @@ sys.path.insert(0, ROOT)
 # widths): B_round(R) = (R-1)*(69 + 65 + 138) + 8R + 48 -> R=3: 616 B.
 def b_round(R):
     return (R - 1) * (69 + 65 + 138) + 8 * R + 48
+
+
+B_RESP, B_EMIT, B_MATCH0, B_ENTRY = 69, 65, 122, 16
+
+
+def algorithmic_bytes(st, groups, R):
+    """SURVEY.md §8d per-unit bytes x the units counted by the device stats."""
+    follower_in = st["msgs_in"] - st["leader_msgs_in"]
+    return (B_RESP * st["leader_msgs_in"] + B_EMIT * st["leader_msgs_out"] + B_MATCH0 * follower_in
+            + B_ENTRY * st["replicate_entries"] + (8 * R + 48) * groups)
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, spec
@@ -106,7 +128,7 @@ def main():
     R = args.replicas
     S = R
     G = args.groups
-    placement = args.placement or ("spread" if world > 1 else "local")
+    placement = args.placement or "local"
     ex = build_exchange(G, R, S, world, rank, placement)
     n = ex.n_peers
     eng = Engine(n, S, device=local_rank)
@@ -151,17 +173,22 @@ def main():
         dist.all_reduce(t)
         commits, esc = int(t[0].item()), int(t[1].item())
     value = commits / elapsed
-    kavg = tm["fast_ms"] / max(1, tm["passes"])  # the dominant kernel
-    gavg = tm["general_ms"] / max(1, tm["passes"])
+    passes = max(1, tm["passes"])
+    kavg = tm["fast_ms"] / passes  # the dominant kernel
+    gavg = tm["general_ms"] / passes
     groups_total = G * world
-    achieved = b_round(R) * G / (kavg * 1e-3) / 1e9  # GB/s: algorithmic bytes of the launch / its time
+    alg = algorithmic_bytes(st, G, R) / args.steps  # per launch (this rank)
+    achieved = alg / (kavg * 1e-3) / 1e9  # GB/s: algorithmic bytes of the launch / its time
+    canon = b_round(R) * G
     if rank == 0:
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
         if os.path.exists(pmc):  # tools/profile.sh: calibrated FETCH_SIZE + WRITE_SIZE of this kernel
             try:
+                from dragonboat_amd.build import source_digest
                 rec = json.load(open(pmc))
-                if rec.get("groups") == G and rec.get("replicas") == R:
+                if rec.get("groups") == G and rec.get("replicas") == R and \
+                        rec.get("source_digest") == source_digest():  # measured on this very kernel
                     traffic = rec.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
@@ -185,9 +212,15 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"gr_fast_kernel<{S}>", "kernel_ms": kavg,
-                         "algorithmic_bytes_per_launch": b_round(R) * G,
+                         "algorithmic_bytes_per_launch": alg,
+                         "units_per_launch": {k: st[k] / args.steps for k in
+                                              ("leader_msgs_in", "leader_msgs_out", "msgs_in",
+                                               "replicate_entries")},
+                         "canonical_round_bytes": canon,
+                         "canonical_frac": canon / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "hbm_traffic_GBs": (traffic / (kavg * 1e-3) / 1e9) if traffic else None,
                          "general_kernel_ms": gavg,
-                         "bailed_lanes_per_pass": tm["bailed_lanes"] / max(1, tm["passes"])},
+                         "bailed_lanes_per_pass": tm["bailed_lanes"] / passes},
         }
         if args.cpu_baseline == "on" and world == 1:
             try:

@@ -35,7 +35,7 @@ F_CHECK_QUORUM, F_IS_LEADER_TRANSFER_TARGET, F_PENDING_CONFIG_CHANGE = 1, 2, 4
 PROP_NONE, PROP_APPENDED, PROP_DROPPED, PROP_FORWARDED = 0, 1, 2, 3
 
 ESC_NAMES = ["none", "term_window", "random", "unsupported", "election", "panic", "capacity",
-             "snapshot", "entry_size", "msg_runs", "nonmember", "config_change"]
+             "snapshot", "entry_size", "msg_runs", "nonmember", "config_change", "wide_term"]
 
 u8, u32, u64 = np.uint8, np.uint32, np.uint64
 
@@ -98,7 +98,9 @@ class Outbox(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("passes", ctypes.c_uint64), ("leader_commits", ctypes.c_uint64),
                 ("follower_commits", ctypes.c_uint64), ("escalations", ctypes.c_uint64),
-                ("msgs_in", ctypes.c_uint64), ("msgs_out", ctypes.c_uint64)]
+                ("msgs_in", ctypes.c_uint64), ("msgs_out", ctypes.c_uint64),
+                ("leader_msgs_in", ctypes.c_uint64), ("leader_msgs_out", ctypes.c_uint64),
+                ("replicate_entries", ctypes.c_uint64)]
 
 
 class Timing(ctypes.Structure):

@@ -14,12 +14,22 @@ ARCH = "gfx950"
 
 ENGINE_SRC = [os.path.join(ROOT, "dragonboat_amd", "csrc", "gr_engine.hip")]
 ENGINE_DEPS = ENGINE_SRC + [os.path.join(ROOT, "dragonboat_amd", "csrc", f)
-                            for f in ("gr_lane.h", "gr_layout.h", "gr_host.h")] + \
+                            for f in ("gr_lane.h", "gr_layout.h", "gr_host.h", "gr_fast.h")] + \
     [os.path.join(ROOT, "include", "gpuraft.h")]
 ENGINE_LIB = os.path.join(ROOT, "dragonboat_amd", "_build", "libgpuraft.so")
 ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
 KAT_BIN = os.path.join(ROOT, "oracle", "_build", "kat_tests")
 HOSTLANE_LIB = os.path.join(ROOT, "tests", "_build", "libhostlane.so")
+
+
+def source_digest():
+    """Digest of the engine sources: ties a PMC measurement (profiles/) to the build it measured."""
+    import hashlib
+    h = hashlib.sha1()
+    for f in sorted(ENGINE_DEPS):
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def _stale(out, deps):

@@ -25,22 +25,19 @@ constexpr int kBlock = 256;
 
 // Per-workgroup partial counters (no atomics on global memory): row b of the
 // stats block belongs to workgroup b of whichever kernel runs.
-__device__ inline void block_stats(const StepParams& kp, uint32_t lc, uint32_t fc, uint32_t es, uint32_t mi,
-                                   uint32_t mo) {
-  __shared__ uint32_t red[5];
-  if (threadIdx.x < 5) red[threadIdx.x] = 0;
+__device__ inline void block_stats(const StepParams& kp, const LaneStats& ls) {
+  constexpr int N = 8;
+  __shared__ uint32_t red[N];
+  if (threadIdx.x < N) red[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t bl = __ballot(lc != 0), bf = __ballot(fc != 0), be = __ballot(es != 0);
-  for (int off = 32; off > 0; off >>= 1) {
-    mi += __shfl_xor(mi, off);
-    mo += __shfl_xor(mo, off);
-  }
+  uint32_t v[N] = {ls.leader_commit, ls.follower_commit, ls.escalated, ls.msgs_in,
+                   ls.msgs_out,      ls.leader_in,       ls.leader_out, ls.entries};
+#pragma unroll
+  for (int f = 0; f < N; ++f)
+    for (int off = 32; off > 0; off >>= 1) v[f] += __shfl_xor(v[f], off);
   if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&red[0], (uint32_t)__popcll(bl));
-    atomicAdd(&red[1], (uint32_t)__popcll(bf));
-    atomicAdd(&red[2], (uint32_t)__popcll(be));
-    atomicAdd(&red[3], mi);
-    atomicAdd(&red[4], mo);
+#pragma unroll
+    for (int f = 0; f < N; ++f) atomicAdd(&red[f], v[f]);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -50,6 +47,9 @@ __device__ inline void block_stats(const StepParams& kp, uint32_t lc, uint32_t f
     row[ST_ESCALATIONS] += red[2];
     row[ST_MSGS_IN] += red[3];
     row[ST_MSGS_OUT] += red[4];
+    row[ST_LEADER_MSGS_IN] += red[5];
+    row[ST_LEADER_MSGS_OUT] += red[6];
+    row[ST_REPLICATE_ENTRIES] += red[7];
   }
 }
 
@@ -60,11 +60,12 @@ template <int S>
 __global__ __launch_bounds__(kBlock) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
                                                          uint32_t* bail_count) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t lc = 0, fc = 0, es = 0, mi = 0, mo = 0;
+  LaneStats ls;
   bool bail = false;
   if (i < kp.n_lanes) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-    bail = !fast_step<S>(kp, i, p, &lc, &fc, &mi, &mo);
+    bail = !fast_step<S>(kp, i, p, &ls);
+    if (bail) ls = LaneStats();
   }
   const uint64_t bm = __ballot(bail);
   if (bm) {
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(kBlock) void gr_fast_kernel(StepParams kp, uint32_t
     base = __shfl(base, (int)first);
     if (bail) bail_list[base + (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
   }
-  if (kp.stats) block_stats(kp, lc, fc, es, mi, mo);
+  if (kp.stats) block_stats(kp, ls);
 }
 
 // Pass 2: the general lane (every handler, escalation with prefix re-run)
@@ -87,24 +88,32 @@ __global__ __launch_bounds__(kBlock) void gr_step_kernel(StepParams kp, const ui
   const uint32_t n = *bail_count;
   if (blockIdx.x == 0 && threadIdx.x == 0) *next_count = 0;
   if (blockIdx.x * kBlock >= n) return;  // uniform per block: nothing to do, no stats row touched
-  uint32_t lc = 0, fc = 0, es = 0, mi = 0, mo = 0;
+  LaneStats acc;
   for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
     const uint32_t x = base + threadIdx.x;
     if (x < n) {
       const uint32_t i = bail_list[x];
       const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
       Lane<S> L(kp, i, p);
-      uint32_t a = 0, b = 0, c = 0, d = 0, e = 0;
-      L.step(&a, &b, &c, &d, &e);
-      lc += a; fc += b; es += c; mi += d; mo += e;
+      LaneStats ls;
+      L.step(&ls);
+      acc.leader_commit += ls.leader_commit;
+      acc.follower_commit += ls.follower_commit;
+      acc.escalated += ls.escalated;
+      acc.msgs_in += ls.msgs_in;
+      acc.msgs_out += ls.msgs_out;
+      acc.leader_in += ls.leader_in;
+      acc.leader_out += ls.leader_out;
+      acc.entries += ls.entries;
     }
   }
-  if (kp.stats) block_stats(kp, lc, fc, es, mi, mo);
+  if (kp.stats) block_stats(kp, acc);
 }
 
-// The general kernel's grid: enough workgroups to fill the chip twice over,
-// never more than the stats block has rows for.
-constexpr uint32_t kGeneralBlocks = 1024;
+// The general kernel's grid: one 256-lane workgroup per CU fills the chip at
+// its occupancy (1 wave per SIMD); never more than the stats block has rows for.
+// Kept small because with no bailed lanes the launch is pure overhead.
+constexpr uint32_t kGeneralBlocks = 256;
 
 // Optional per-pass timing: events around the two kernels and a copy of the
 // bail count (pinned host slot), recorded on the pass's stream.
@@ -293,24 +302,17 @@ int grow_pinned(uint8_t** p, size_t* have, size_t want) {
 
 // Upload per-lane local inputs for lanes [0, n) in lane order.
 int upload_locals(gr_engine* e, const std::vector<gr_local_input>& byLane, uint32_t n, hipStream_t s) {
-  std::vector<uint32_t> lt(n, 0), lq(n, 0), lp(n, 0);
+  std::vector<uint32_t> lt(n, 0), lq(n, 0), lp(n, 0), lw(n, 0);
   std::vector<uint8_t> lf(n, 0);
   std::vector<uint64_t> llo(n, 0), lhi(n, 0), lr(n, 0);
-  for (uint32_t l = 0; l < n; ++l) {
-    const gr_local_input& x = byLane[l];
-    lt[l] = x.ticks;
-    lq[l] = x.quiesced_ticks;
-    lp[l] = x.propose_entries;
-    lf[l] = (uint8_t)((x.read_index ? LF_READ_INDEX : 0) | (x.propose_has_config_change ? LF_PROPOSE_CC : 0));
-    llo[l] = x.read_ctx_low;
-    lhi[l] = x.read_ctx_high;
-    lr[l] = x.rand;
-  }
+  for (uint32_t l = 0; l < n; ++l)
+    locals_to_rows(byLane[l], &lt[l], &lq[l], &lp[l], &lf[l], &llo[l], &lhi[l], &lr[l], &lw[l]);
   const LaneBase& L = e->ln;
   HIPCHK(hipMemcpyAsync(L.u32(LR_TICKS), lt.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(L.u32(LR_QTICKS), lq.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(L.u32(LR_PROPOSE), lp.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(L.u8(LR_LFLAGS), lf.data(), (size_t)n, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(L.u32(LR_LWORD), lw.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(L.u64(LR_RI_LO), llo.data(), (size_t)n * 8, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(L.u64(LR_RI_HI), lhi.data(), (size_t)n * 8, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(L.u64(LR_RAND), lr.data(), (size_t)n * 8, hipMemcpyHostToDevice, s));
@@ -324,15 +326,23 @@ int download_results(gr_engine* e, uint32_t first, uint32_t n, std::vector<gr_pe
   const LaneBase& L = e->ln;
   std::vector<uint8_t> rflags(n), esc(n), pres(n), rtrc(n);
   std::vector<uint32_t> escitem(n);
-  std::vector<uint64_t> afrom(n), pfirst(n), rti((size_t)GR_Q * n), rtl((size_t)GR_Q * n),
+  std::vector<uint64_t> afrom(n), hi(n), rti((size_t)GR_Q * n), rtl((size_t)GR_Q * n),
       rth((size_t)GR_Q * n);
+  std::vector<uint32_t> nprop(n);
   HIPCHK(hipMemcpy(rflags.data(), L.u8(LR_RFLAGS) + first, n, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(esc.data(), L.u8(LR_ESC_REASON) + first, n, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(pres.data(), L.u8(LR_PROP_RESULT) + first, n, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(rtrc.data(), L.u8(LR_RTR_COUNT) + first, n, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(escitem.data(), L.u32(LR_ESC_ITEM) + first, (size_t)n * 4, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(afrom.data(), L.u64(LR_APPEND_FROM) + first, (size_t)n * 8, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(pfirst.data(), L.u64(LR_PROPOSE_FIRST) + first, (size_t)n * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(nprop.data(), L.u32(LR_PROPOSE) + first, (size_t)n * 4, hipMemcpyDeviceToHost));
+  if (peer_of_lane) {  // last_index of each lane's peer
+    std::vector<uint64_t> all(e->cfg.max_peers);
+    HIPCHK(hipMemcpy(all.data(), e->st.u64(SR_LAST_INDEX), all.size() * 8, hipMemcpyDeviceToHost));
+    for (uint32_t l = 0; l < n; ++l) hi[l] = all[peer_of_lane[l]];
+  } else {
+    HIPCHK(hipMemcpy(hi.data(), e->st.u64(SR_LAST_INDEX) + first, (size_t)n * 8, hipMemcpyDeviceToHost));
+  }
   for (int q = 0; q < GR_Q; ++q) {
     HIPCHK(hipMemcpy(rti.data() + (size_t)q * n, L.u64(LR_RTR_INDEX + q) + first, (size_t)n * 8,
                      hipMemcpyDeviceToHost));
@@ -353,7 +363,7 @@ int download_results(gr_engine* e, uint32_t first, uint32_t n, std::vector<gr_pe
     }
     if (rf & RF_PROPOSE) {
       pr.propose_result = pres[l];
-      pr.propose_first = pfirst[l];
+      if (pr.propose_result == GR_PROP_APPENDED) pr.propose_first = hi[l] - nprop[l] + 1;
     }
     if (rf & RF_APPEND) pr.append_from = afrom[l];
     if (rf & RF_READY) {
@@ -388,8 +398,8 @@ const char* gr_strerror(int err) {
 const char* gr_escalation_name(int esc) {
   static const char* names[] = {"none", "term_window", "random", "unsupported", "election", "panic",
                                 "capacity", "snapshot", "entry_size", "msg_runs", "nonmember",
-                                "config_change"};
-  if (esc < 0 || esc > GR_ESC_CONFIG_CHANGE) return "unknown";
+                                "config_change", "wide_term"};
+  if (esc < 0 || esc > GR_ESC_WIDE_TERM) return "unknown";
   return names[esc];
 }
 
@@ -593,6 +603,9 @@ int gr_stats_get(gr_engine* e, gr_stats* out) {
     out->escalations += row[ST_ESCALATIONS];
     out->msgs_in += row[ST_MSGS_IN];
     out->msgs_out += row[ST_MSGS_OUT];
+    out->leader_msgs_in += row[ST_LEADER_MSGS_IN];
+    out->leader_msgs_out += row[ST_LEADER_MSGS_OUT];
+    out->replicate_entries += row[ST_REPLICATE_ENTRIES];
   }
   return GR_OK;
 }

@@ -45,14 +45,15 @@ struct FastLane {
   // leader remotes
   uint64_t match[S], next[S];
   uint32_t rst[S], ract[S], rkind[S];
-  bool rem_dirty = false;
+  uint32_t mdirty = 0;  // slots whose match/next changed
+  uint32_t sdirty = 0;  // slots whose state/active byte changed
   uint32_t snapz = 0;
   // emission
   uint32_t gout[S];
   uint32_t outc[S];
-  uint32_t nmo = 0, nmi = 0;
+  uint32_t nmo = 0, nmi = 0, nent = 0;
   // results
-  uint64_t append_from = 0, propose_first = 0;
+  uint64_t append_from = 0;
   uint32_t prop_result = 0;
 
   GF_HD FastLane(const StepParams& k, uint32_t lane, uint32_t peer) : kp(k), i(lane), p(peer) {}
@@ -79,29 +80,31 @@ struct FastLane {
   // raft.send (raft.go:457-461) of a Replicate into slot j.
   GF_HD void emit_replicate(int j, uint64_t log_index, uint64_t log_term, uint32_t n, uint64_t rt0) {
     GF_BAIL(gout[j] == NOPOS || outc[j] >= (uint32_t)GR_C);
+    GF_BAIL(wide_term(term, log_term, n ? rt0 : 0, 0));  // GR_ESC_WIDE_TERM in the general lane
     if (!ok) return;
     const Mailbox mb = kp.out.at(gout[j]);
     const uint32_t c = outc[j];
     mb.type(c) = GR_REPLICATE;
     mb.flags(c) = (uint8_t)(n ? (1u << MFL_RUNS_SHIFT) : 0u);
-    mb.u64(c, MF_TERM) = term;
+    mb.t32(c, MT_TERM) = (uint32_t)(term);
     mb.n(c) = n;
     mb.u64(c, MF_LOG_INDEX) = log_index;
-    mb.u64(c, MF_LOG_TERM) = log_term;
+    mb.t32(c, MT_LOG_TERM) = (uint32_t)(log_term);
     mb.u64(c, MF_COMMIT) = committed;
-    if (n) mb.u64(c, MF_RT0) = rt0;
+    if (n) mb.t32(c, MT_RT0) = (uint32_t)(rt0);
     outc[j] = c + 1;
     nmo++;
   }
   // ... and of a ReplicateResp into the mailbox at gpos.
   GF_HD void emit_resp(uint32_t gpos, uint32_t* cnt, uint64_t log_index, bool reject, uint64_t hint) {
     GF_BAIL(gpos == NOPOS || *cnt >= (uint32_t)GR_C);
+    GF_BAIL(wide_term(term, 0, 0, 0));
     if (!ok) return;
     const Mailbox mb = kp.out.at(gpos);
     const uint32_t c = *cnt;
     mb.type(c) = GR_REPLICATE_RESP;
     mb.flags(c) = (uint8_t)(reject ? MFL_REJECT : 0u);
-    mb.u64(c, MF_TERM) = term;
+    mb.t32(c, MT_TERM) = (uint32_t)(term);
     mb.u64(c, MF_LOG_INDEX) = log_index;
     if (reject) mb.u64(c, MF_HINT) = hint;
     *cnt = c + 1;
@@ -154,9 +157,13 @@ struct FastLane {
       GF_BAIL(hi - nx + 1 > 1);         // several entries: MaxEntrySize check
       GF_BAIL(rst[j] != GR_REPLICATE_ST && rst[j] != GR_RETRY);
       n = 1;
-      if (rst[j] == GR_REPLICATE_ST) next[j] = hi + 1;  // remote.progress, remote.go:120-128
-      else rst[j] = GR_WAIT;
-      rem_dirty = true;
+      if (rst[j] == GR_REPLICATE_ST) {  // remote.progress, remote.go:120-128
+        next[j] = hi + 1;
+        mdirty |= 1u << j;
+      } else {
+        rst[j] = GR_WAIT;
+        sdirty |= 1u << j;
+      }
     }
     emit_replicate(j, nx - 1, lt, n, rtn);
   }
@@ -174,18 +181,27 @@ struct FastLane {
   }
   // remote.tryUpdate (remote.go:108-118)
   GF_HD bool try_update(int j, uint64_t index) {
-    if (next[j] < index + 1) next[j] = index + 1;
+    if (next[j] < index + 1) {
+      next[j] = index + 1;
+      mdirty |= 1u << j;
+    }
     if (match[j] < index) {
-      if (rst[j] == GR_WAIT) rst[j] = GR_RETRY;
+      if (rst[j] == GR_WAIT) {
+        rst[j] = GR_RETRY;
+        sdirty |= 1u << j;
+      }
       match[j] = index;
+      mdirty |= 1u << j;
       return true;
     }
     return false;
   }
   // handleLeaderReplicateResp, accept path (raft.go:1205-1221); no leader transfer.
   GF_HD void replicate_resp(int j, uint64_t index) {
-    ract[j] = 1;
-    rem_dirty = true;
+    if (!ract[j]) {
+      ract[j] = 1;
+      sdirty |= 1u << j;
+    }
     const bool paused = rst[j] == GR_WAIT || rst[j] == GR_SNAPSHOT_ST;
     if (!try_update(j, index)) return;
     GF_BAIL(rst[j] == GR_SNAPSHOT_ST);
@@ -193,6 +209,8 @@ struct FastLane {
       next[j] = match[j] + 1;
       snapz |= 1u << j;
       rst[j] = GR_REPLICATE_ST;
+      mdirty |= 1u << j;
+      sdirty |= 1u << j;
     }
     if (try_commit()) broadcast();
     else if (paused) send_replicate(j);
@@ -213,18 +231,16 @@ struct FastLane {
 #pragma unroll
     for (int j = 0; j < S; ++j)
       if ((uint32_t)j == self) try_update(j, hi);
-    rem_dirty = true;
     int nv = 0;
 #pragma unroll
     for (int j = 0; j < S; ++j) nv += rkind[j] == GR_SLOT_VOTER;
     if (nv / 2 + 1 == 1) try_commit();
     broadcast();
     prop_result = GR_PROP_APPENDED;
-    propose_first = first;
   }
 
   // ------------------------------------------------------------- step
-  GF_HD bool step(uint32_t* st_lc, uint32_t* st_fc, uint32_t* st_mi, uint32_t* st_mo) {
+  GF_HD bool step(LaneStats* ls) {
     // ---- round 1: core, locals, routes
     state = s8(Rw::B_STATE);
     self = s8(Rw::B_SELF);
@@ -233,13 +249,8 @@ struct FastLane {
     committed = s64(SR_COMMITTED);
     hi = s64(SR_LAST_INDEX);
     lo = s64(SR_LO);
-    uint32_t lf = 0, nt = 0, nq = 0, np = 0;
-    if (kp.has_locals) {
-      lf = kp.ln.u8(LR_LFLAGS)[i];
-      nt = kp.ln.u32(LR_TICKS)[i];
-      nq = kp.ln.u32(LR_QTICKS)[i];
-      np = kp.ln.u32(LR_PROPOSE)[i];
-    }
+    const uint32_t flags = s8(Rw::B_FLAGS);
+    const uint32_t lw = kp.has_locals ? kp.ln.u32(LR_LWORD)[i] : 0u;  // packed locals (gr_layout.h)
     uint32_t gin[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
@@ -256,9 +267,8 @@ struct FastLane {
       rtn = s64(SR_RUN_TERM + nruns - 1);
     }
     const bool leader = state == GR_LEADER;
-    uint64_t ltt = 0;
+    const uint32_t np = lw & 0xFFFFu;
     if (leader) {
-      ltt = s64(SR_LTT);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         match[j] = s64(Rw::MATCH + j);
@@ -288,7 +298,7 @@ struct FastLane {
           if ((uint32_t)k < cnt[j]) {
             const Mailbox mb = kp.in.at(gin[j]);
             lh[j][k] = (uint32_t)mb.type(k) | ((uint32_t)mb.flags(k) << 8);
-            lterm[j][k] = mb.u64(k, MF_TERM);
+            lterm[j][k] = (uint64_t)mb.t32(k, MT_TERM);
             lidx[j][k] = mb.u64(k, MF_LOG_INDEX);
           }
         }
@@ -312,22 +322,22 @@ struct FastLane {
           const Mailbox mb = kp.in.at(gl);
           fh[k] = (uint32_t)mb.type(k) | ((uint32_t)mb.flags(k) << 8);
           fn[k] = mb.n(k);
-          fterm[k] = mb.u64(k, MF_TERM);
+          fterm[k] = (uint64_t)mb.t32(k, MT_TERM);
           fidx[k] = mb.u64(k, MF_LOG_INDEX);
-          flt[k] = mb.u64(k, MF_LOG_TERM);
+          flt[k] = (uint64_t)mb.t32(k, MT_LOG_TERM);
           fcom[k] = mb.u64(k, MF_COMMIT);
-          frt0[k] = mb.u64(k, MF_RT0);
+          frt0[k] = (uint64_t)mb.t32(k, MT_RT0);
         }
       }
       if (c) rid = s64(Rw::RID + L);
     }
     // ---- checks: anything outside the steady state goes to the general lane
     GF_BAIL(!leader && state != GR_FOLLOWER);
-    GF_BAIL((lf & (LF_READ_INDEX | LF_PROPOSE_CC)) || nt || nq || (np && !leader));
+    GF_BAIL((lw & LW_OTHER) || (np && !leader));
     committed0 = committed;
     hi0 = hi;
     if (leader) {
-      GF_BAIL(ltt != 0);  // leader transfer in progress
+      GF_BAIL(flags & F_LTT);  // leader transfer in progress
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         GF_BAIL(cnt[j] > (uint32_t)MK);
@@ -378,11 +388,13 @@ struct FastLane {
       s8(Rw::B_NRUNS) = (uint8_t)nruns;
     }
     if (leader) {
-      if (rem_dirty) {
 #pragma unroll
-        for (int j = 0; j < S; ++j) {
+      for (int j = 0; j < S; ++j) {
+        if ((mdirty >> j) & 1u) {
           s64(Rw::MATCH + j) = match[j];
           s64(Rw::NEXT + j) = next[j];
+        }
+        if ((sdirty >> j) & 1u) {
           s8(Rw::B_RSTATE + j) = (uint8_t)rst[j];
           s8(Rw::B_RACTIVE + j) = (uint8_t)ract[j];
         }
@@ -398,10 +410,9 @@ struct FastLane {
     for (int j = 0; j < S; ++j)
       if (gout[j] != NOPOS) kp.out.at(gout[j]).cnt() = (uint8_t)outc[j];
     uint8_t rf = 0;
-    if (prop_result) {
+    if (prop_result) {  // propose_first = last_index - n + 1 (gr_layout.h)
       rf |= RF_PROPOSE;
       kp.ln.u8(LR_PROP_RESULT)[i] = (uint8_t)prop_result;
-      kp.ln.u64(LR_PROPOSE_FIRST)[i] = propose_first;
     }
     if (append_from) {
       rf |= RF_APPEND;
@@ -409,16 +420,21 @@ struct FastLane {
     }
     kp.ln.u8(LR_RFLAGS)[i] = rf;
     const bool adv = committed > committed0;
-    *st_lc = adv && leader;
-    *st_fc = adv && !leader;
-    *st_mi = nmi;
-    *st_mo = nmo;
+    ls->leader_commit = adv && leader;
+    ls->follower_commit = adv && !leader;
+    ls->escalated = 0;
+    ls->msgs_in = nmi;
+    ls->msgs_out = nmo;
+    ls->leader_in = leader ? nmi : 0;
+    ls->leader_out = leader ? nmo : 0;
+    ls->entries = nent;
     return true;
   }
 
   // handleReplicateMessage (raft.go:953-976) for an append at the log's end.
   GF_HD void replicate(uint64_t li, uint64_t lterm, uint64_t mcommit, uint32_t n, uint64_t rt0, uint32_t go,
                        uint32_t* oc) {
+    nent += n;
     if (li < committed) {
       emit_resp(go, oc, committed, false, 0);
       return;
@@ -458,10 +474,9 @@ struct FastLane {
 
 // Kernel-side entry: the lean lane for lane i; false = hand the lane to the general kernel.
 template <int S>
-GF_HD bool fast_step(const StepParams& kp, uint32_t i, uint32_t p, uint32_t* lc, uint32_t* fc, uint32_t* mi,
-                     uint32_t* mo) {
+GF_HD bool fast_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls) {
   FastLane<S> L(kp, i, p);
-  return L.step(lc, fc, mi, mo);
+  return L.step(ls);
 }
 
 }  // namespace gr

@@ -67,7 +67,7 @@ inline void set_u64_row(gr_peer& g, uint32_t row, uint32_t S, uint64_t v) {
 inline uint8_t get_u8_row(const gr_peer& g, uint32_t row, uint32_t S) {
   switch (row) {
     case 0: return g.state;
-    case 1: return g.flags;
+    case 1: return (uint8_t)((g.flags & ~F_LTT) | (g.leader_transfer_target ? F_LTT : 0u));
     case 2: return g.self_slot;
     case 3: return g.n_runs;
     case 4: return g.read_index_count;
@@ -86,7 +86,7 @@ inline uint8_t get_u8_row(const gr_peer& g, uint32_t row, uint32_t S) {
 inline void set_u8_row(gr_peer& g, uint32_t row, uint32_t S, uint8_t v) {
   switch (row) {
     case 0: g.state = v; return;
-    case 1: g.flags = v; return;
+    case 1: g.flags = (uint8_t)(v & ~F_LTT); return;
     case 2: g.self_slot = v; return;
     case 3: g.n_runs = v; return;
     case 4: g.read_index_count = v; return;
@@ -114,18 +114,22 @@ inline int validate_msg(const gr_message& m, uint32_t S, uint32_t cap) {
 }
 
 inline void encode_msg(const Mailbox& mb, uint32_t k, const gr_message& m) {
+  if (wide_term(m.term, m.log_term, m.run_term[0], m.run_term[1])) {  // cannot travel: receiver escalates
+    mb.type(k) = MT_WIDE;
+    return;
+  }
   mb.type(k) = m.type;
   mb.flags(k) = (uint8_t)((m.reject ? MFL_REJECT : 0) | (m.n_runs << MFL_RUNS_SHIFT));
   mb.n(k) = m.n_entries;
   mb.run2(k) = m.run2_offset;
-  mb.u64(k, MF_TERM) = m.term;
+  mb.t32(k, MT_TERM) = (uint32_t)(m.term);
   mb.u64(k, MF_LOG_INDEX) = m.log_index;
-  mb.u64(k, MF_LOG_TERM) = m.log_term;
+  mb.t32(k, MT_LOG_TERM) = (uint32_t)(m.log_term);
   mb.u64(k, MF_COMMIT) = m.commit;
   mb.u64(k, MF_HINT) = m.hint;
   mb.u64(k, MF_HINT_HIGH) = m.hint_high;
-  mb.u64(k, MF_RT0) = m.run_term[0];
-  mb.u64(k, MF_RT1) = m.run_term[1];
+  mb.t32(k, MT_RT0) = (uint32_t)(m.run_term[0]);
+  mb.t32(k, MT_RT1) = (uint32_t)(m.run_term[1]);
 }
 
 // Decode one message; fields a type does not carry on the device are zero.
@@ -136,17 +140,17 @@ inline gr_message decode_msg(const Mailbox& mb, uint32_t k) {
   const uint8_t fl = mb.flags(k);
   m.reject = (fl & MFL_REJECT) ? 1 : 0;
   m.n_runs = (fl >> MFL_RUNS_SHIFT) & 3u;
-  m.term = mb.u64(k, MF_TERM);
+  m.term = (uint64_t)mb.t32(k, MT_TERM);
   switch (m.type) {
     case GR_REPLICATE:
       m.n_entries = mb.n(k);
       m.log_index = mb.u64(k, MF_LOG_INDEX);
-      m.log_term = mb.u64(k, MF_LOG_TERM);
+      m.log_term = (uint64_t)mb.t32(k, MT_LOG_TERM);
       m.commit = mb.u64(k, MF_COMMIT);
-      if (m.n_entries) m.run_term[0] = mb.u64(k, MF_RT0);
+      if (m.n_entries) m.run_term[0] = (uint64_t)mb.t32(k, MT_RT0);
       if (m.n_runs == 2) {
         m.run2_offset = mb.run2(k);
-        m.run_term[1] = mb.u64(k, MF_RT1);
+        m.run_term[1] = (uint64_t)mb.t32(k, MT_RT1);
       }
       break;
     case GR_REPLICATE_RESP:  // the device writes Hint only on a reject
@@ -166,12 +170,12 @@ inline gr_message decode_msg(const Mailbox& mb, uint32_t k) {
       m.n_entries = mb.n(k);
       m.run2_offset = mb.run2(k);
       m.log_index = mb.u64(k, MF_LOG_INDEX);
-      m.log_term = mb.u64(k, MF_LOG_TERM);
+      m.log_term = (uint64_t)mb.t32(k, MT_LOG_TERM);
       m.commit = mb.u64(k, MF_COMMIT);
       m.hint = mb.u64(k, MF_HINT);
       m.hint_high = mb.u64(k, MF_HINT_HIGH);
-      m.run_term[0] = mb.u64(k, MF_RT0);
-      m.run_term[1] = mb.u64(k, MF_RT1);
+      m.run_term[0] = (uint64_t)mb.t32(k, MT_RT0);
+      m.run_term[1] = (uint64_t)mb.t32(k, MT_RT1);
       break;
   }
   return m;
@@ -317,7 +321,7 @@ inline bool detect_affine_routes(const uint32_t* in_pos, const uint32_t* out_pos
 
 // Local-input rows of a lane block (host copies).
 inline void locals_to_rows(const gr_local_input& x, uint32_t* ticks, uint32_t* qticks, uint32_t* prop,
-                           uint8_t* lflags, uint64_t* rlo, uint64_t* rhi, uint64_t* rnd) {
+                           uint8_t* lflags, uint64_t* rlo, uint64_t* rhi, uint64_t* rnd, uint32_t* lword) {
   *ticks = x.ticks;
   *qticks = x.quiesced_ticks;
   *prop = x.propose_entries;
@@ -325,6 +329,7 @@ inline void locals_to_rows(const gr_local_input& x, uint32_t* ticks, uint32_t* q
   *rlo = x.read_ctx_low;
   *rhi = x.read_ctx_high;
   *rnd = x.rand;
+  *lword = local_word(*ticks, *qticks, *prop, *lflags);
 }
 
 }  // namespace host

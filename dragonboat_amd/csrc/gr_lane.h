@@ -120,7 +120,7 @@ struct Lane {
   bool rand_used = false;
   uint64_t append_from = 0, propose_first = 0;
   uint64_t committed0 = 0;
-  uint32_t msgs_in = 0, msgs_out = 0;
+  uint32_t msgs_in = 0, msgs_out = 0, entries_in = 0;
 
 
   GR_HD Lane(const StepParams& k, uint32_t lane, uint32_t peer) : kp(k), p(peer), i(lane) {}
@@ -196,6 +196,13 @@ struct Lane {
   }
 
   GR_HD void store() {
+    if (dirty & D_LTT) {  // keep the device-internal F_LTT bit of the flags row in step
+      const uint32_t nf = (flags & ~F_LTT) | (ltt ? F_LTT : 0u);
+      if (nf != flags) {
+        flags = nf;
+        dirty |= D_FLAGS;
+      }
+    }
     if (dirty & D_TERM) s64(SR_TERM) = term;
     if (dirty & D_VOTE) s64(SR_VOTE) = 0;  // reset() on a term change is the only vote write here
     if (dirty & D_COMMITTED) s64(SR_COMMITTED) = committed;
@@ -421,21 +428,23 @@ struct Lane {
     if (g == NOPOS) return GR_ESC_NONMEMBER;
     const uint32_t c = (outcnt >> (3 * j)) & 7u;
     if (c >= GR_C) return GR_ESC_CAPACITY;
+    const uint64_t mterm = is_request_message(m.type) ? m.term : term;
+    if (wide_term(mterm, m.log_term, m.rt0, m.rt1)) return GR_ESC_WIDE_TERM;
     const Mailbox mb = kp.out.at(g);
     mb.type(c) = m.type;
     mb.flags(c) = m.flags;
-    mb.u64(c, MF_TERM) = is_request_message(m.type) ? m.term : term;
+    mb.t32(c, MT_TERM) = (uint32_t)mterm;
     switch (m.type) {  // write the fields the receiver reads (read_msg)
       case GR_REPLICATE:
         mb.n(c) = m.n;
         mb.u64(c, MF_LOG_INDEX) = m.log_index;
-        mb.u64(c, MF_LOG_TERM) = m.log_term;
+        mb.t32(c, MT_LOG_TERM) = (uint32_t)(m.log_term);
         mb.u64(c, MF_COMMIT) = m.commit;
         if (m.n) {
-          mb.u64(c, MF_RT0) = m.rt0;
+          mb.t32(c, MT_RT0) = (uint32_t)(m.rt0);
           if (((m.flags >> MFL_RUNS_SHIFT) & 3u) == 2) {
             mb.run2(c) = m.run2;
-            mb.u64(c, MF_RT1) = m.rt1;
+            mb.t32(c, MT_RT1) = (uint32_t)(m.rt1);
           }
         }
         break;
@@ -456,12 +465,12 @@ struct Lane {
         mb.n(c) = m.n;
         mb.run2(c) = m.run2;
         mb.u64(c, MF_LOG_INDEX) = m.log_index;
-        mb.u64(c, MF_LOG_TERM) = m.log_term;
+        mb.t32(c, MT_LOG_TERM) = (uint32_t)(m.log_term);
         mb.u64(c, MF_COMMIT) = m.commit;
         mb.u64(c, MF_HINT) = m.hint;
         mb.u64(c, MF_HINT_HIGH) = m.hint_high;
-        mb.u64(c, MF_RT0) = m.rt0;
-        mb.u64(c, MF_RT1) = m.rt1;
+        mb.t32(c, MT_RT0) = (uint32_t)(m.rt0);
+        mb.t32(c, MT_RT1) = (uint32_t)(m.rt1);
         break;
     }
     outcnt += 1u << (3 * j);
@@ -841,6 +850,7 @@ struct Lane {
   // append / inMemory.merge (logentry.go:281-303, inmemory.go:157-177).
   GR_HD int handle_replicate(const InMsg& m, uint32_t from) {
     need(G_CORE | G_WIN);
+    entries_in += m.n;
     OutMsg r;
     r.type = GR_REPLICATE_RESP;
     if (m.log_index < committed) {
@@ -986,20 +996,20 @@ struct Lane {
   GR_HD void read_msg(const Mailbox& mb, uint32_t k, InMsg& m) const {
     m.type = mb.type(k);
     m.flags = mb.flags(k);
-    m.term = mb.u64(k, MF_TERM);
+    m.term = (uint64_t)mb.t32(k, MT_TERM);
     m.n = 0; m.run2 = 0;
     m.log_index = 0; m.log_term = 0; m.commit = 0; m.hint = 0; m.hint_high = 0; m.rt0 = 0; m.rt1 = 0;
     switch (m.type) {
       case GR_REPLICATE:
         m.n = mb.n(k);
         m.log_index = mb.u64(k, MF_LOG_INDEX);
-        m.log_term = mb.u64(k, MF_LOG_TERM);
+        m.log_term = (uint64_t)mb.t32(k, MT_LOG_TERM);
         m.commit = mb.u64(k, MF_COMMIT);
         if (m.n) {
-          m.rt0 = mb.u64(k, MF_RT0);
+          m.rt0 = (uint64_t)mb.t32(k, MT_RT0);
           if (((m.flags >> MFL_RUNS_SHIFT) & 3u) == 2) {
             m.run2 = mb.run2(k);
-            m.rt1 = mb.u64(k, MF_RT1);
+            m.rt1 = (uint64_t)mb.t32(k, MT_RT1);
           }
         }
         break;
@@ -1020,12 +1030,12 @@ struct Lane {
         m.n = mb.n(k);
         m.run2 = mb.run2(k);
         m.log_index = mb.u64(k, MF_LOG_INDEX);
-        m.log_term = mb.u64(k, MF_LOG_TERM);
+        m.log_term = (uint64_t)mb.t32(k, MT_LOG_TERM);
         m.commit = mb.u64(k, MF_COMMIT);
         m.hint = mb.u64(k, MF_HINT);
         m.hint_high = mb.u64(k, MF_HINT_HIGH);
-        m.rt0 = mb.u64(k, MF_RT0);
-        m.rt1 = mb.u64(k, MF_RT1);
+        m.rt0 = (uint64_t)mb.t32(k, MT_RT0);
+        m.rt1 = (uint64_t)mb.t32(k, MT_RT1);
         break;
     }
   }
@@ -1208,6 +1218,7 @@ struct Lane {
     propose_first = 0;
     msgs_in = 0;
     msgs_out = 0;
+    entries_in = 0;
     outcnt = 0;
   }
   // Process items [0, limit); returns an escalation code and the item index
@@ -1226,6 +1237,7 @@ struct Lane {
         if (k == GR_C) { *at = item; return GR_ESC_CAPACITY; }  // overflowed mailbox
         InMsg m;
         read_msg(mb, k, m);
+        if (m.type == MT_WIDE) { *at = item; return GR_ESC_WIDE_TERM; }  // terms >= 2^32: host path
         const int e = handle(m, j);
         if (e) { *at = item; return e; }
         msgs_in++;
@@ -1281,8 +1293,7 @@ struct Lane {
 
   // Kernel body for one lane: run, and on escalation re-run the prefix on the
   // pristine state so the escalating item is left entirely to the host.
-  GR_HD bool step(uint32_t* stat_leader_commit, uint32_t* stat_follower_commit, uint32_t* stat_esc,
-                  uint32_t* stat_in, uint32_t* stat_out) {
+  GR_HD bool step(LaneStats* ls) {
     uint32_t at = 0, limit = 0xFFFFFFFFu;
     int esc = 0;
 #pragma unroll 1
@@ -1305,10 +1316,9 @@ struct Lane {
       kp.ln.u8(LR_ESC_REASON)[i] = (uint8_t)esc;
       kp.ln.u32(LR_ESC_ITEM)[i] = at;
     }
-    if (prop_result) {
+    if (prop_result) {  // propose_first = last_index - n + 1 (gr_layout.h)
       rf |= RF_PROPOSE;
       kp.ln.u8(LR_PROP_RESULT)[i] = (uint8_t)prop_result;
-      kp.ln.u64(LR_PROPOSE_FIRST)[i] = propose_first;
     }
     if (rtrc) {
       rf |= RF_READY;
@@ -1320,11 +1330,15 @@ struct Lane {
     }
     kp.ln.u8(LR_RFLAGS)[i] = rf;
     const bool adv = (dirty & D_COMMITTED) && committed > committed0;
-    *stat_leader_commit = adv && state == GR_LEADER;
-    *stat_follower_commit = adv && state != GR_LEADER;
-    *stat_esc = esc != 0;
-    *stat_in = msgs_in;
-    *stat_out = msgs_out;
+    const bool lead = state == GR_LEADER;
+    ls->leader_commit = adv && lead;
+    ls->follower_commit = adv && !lead;
+    ls->escalated = esc != 0;
+    ls->msgs_in = msgs_in;
+    ls->msgs_out = msgs_out;
+    ls->leader_in = lead ? msgs_in : 0;
+    ls->leader_out = lead ? msgs_out : 0;
+    ls->entries = entries_in;
     return true;
   }
 };

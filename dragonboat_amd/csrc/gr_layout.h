@@ -16,7 +16,11 @@
 // chunk so a wave of lanes reading "message k of its mailbox" is coalesced.
 // Chunk layout (pc = positions per chunk, a multiple of 64):
 //   [cnt u8 x pc] then for k < GR_C: [type u8 x pc][flags u8 x pc]
-//   [n u32 x pc][run2 u32 x pc][8 x (u64 x pc)] — u64 fields below.
+//   [n u32 x pc][run2 u32 x pc][4 x (u32 x pc) terms][4 x (u64 x pc) indexes]
+// Terms travel as 32 bits: a message whose term, log term or entry-run terms
+// reach 2^32 never enters a mailbox (the sender escalates GR_ESC_WIDE_TERM;
+// a host-encoded inbox marks it MT_WIDE and the receiver escalates there), so
+// every value read back is exact. Indexes, commit and ReadIndex contexts stay 64-bit.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -76,13 +80,13 @@ struct StateBase {
 // ---------------------------------------------------------------- lane rows
 // Per-pass arrays indexed by lane: local inputs and results.
 enum LaneU64Row : uint32_t {
-  LR_RI_LO = 0, LR_RI_HI, LR_RAND, LR_APPEND_FROM, LR_PROPOSE_FIRST,
+  LR_RI_LO = 0, LR_RI_HI, LR_RAND, LR_APPEND_FROM,
   LR_RTR_INDEX,                         // + q
   LR_RTR_LO = LR_RTR_INDEX + GR_Q,      // + q
   LR_RTR_HI = LR_RTR_LO + GR_Q,         // + q
   LR_NU64 = LR_RTR_HI + GR_Q,
 };
-enum LaneU32Row : uint32_t { LR_TICKS = 0, LR_QTICKS, LR_PROPOSE, LR_ESC_ITEM, LR_LANE_PEER, LR_NU32 };
+enum LaneU32Row : uint32_t { LR_TICKS = 0, LR_QTICKS, LR_PROPOSE, LR_ESC_ITEM, LR_LANE_PEER, LR_LWORD, LR_NU32 };
 enum LaneU8Row : uint32_t { LR_LFLAGS = 0, LR_RFLAGS, LR_ESC_REASON, LR_PROP_RESULT, LR_RTR_COUNT, LR_NU8 };
 __host__ __device__ inline uint64_t lane_bytes(uint32_t S, uint32_t lcap) {
   // + in_pos / out_pos route tables [S][lcap] u32 each
@@ -108,23 +112,42 @@ struct LaneBase {
 };
 constexpr uint8_t LF_READ_INDEX = 0x01;
 constexpr uint8_t LF_PROPOSE_CC = 0x02;
+// LR_LWORD: a lane's local inputs packed for the lean lane (4 bytes instead
+// of 13): bits 0-15 the ProposeEntries count, bit 16 set when there is
+// anything else (ReadIndex, config change, ticks, quiesced ticks, or a count
+// >= 2^16), which the lean lane hands to the general lane.
+constexpr uint32_t LW_OTHER = 0x10000u;
+__host__ __device__ inline uint32_t local_word(uint32_t ticks, uint32_t qticks, uint32_t propose, uint32_t lflags) {
+  const bool other = ticks || qticks || lflags || propose > 0xFFFFu;
+  return other ? LW_OTHER : propose;
+}
+// Device-internal bit of the state flags row: leaderTransferTarget != 0, so the
+// lean lane tests one byte instead of loading the 8-byte target. Never visible
+// in gr_peer.flags (gr_host.h masks it).
+constexpr uint32_t F_LTT = 0x80u;
+// The result record's propose_first is not stored: ProposeEntries is the last
+// item of a pass, so it is last_index - propose_entries + 1 after the pass.
 constexpr uint8_t RF_ESCALATED = 0x01;
 constexpr uint8_t RF_PROPOSE = 0x02;
 constexpr uint8_t RF_READY = 0x04;
 constexpr uint8_t RF_APPEND = 0x08;
 
 // ---------------------------------------------------------------- message spaces
-enum U64Field : uint32_t {
-  MF_TERM = 0, MF_LOG_INDEX = 1, MF_LOG_TERM = 2, MF_COMMIT = 3,
-  MF_HINT = 4, MF_HINT_HIGH = 5, MF_RT0 = 6, MF_RT1 = 7, MF_NUM_U64 = 8
-};
+enum U64Field : uint32_t { MF_LOG_INDEX = 0, MF_COMMIT = 1, MF_HINT = 2, MF_HINT_HIGH = 3, MF_NUM_U64 = 4 };
+enum T32Field : uint32_t { MT_TERM = 0, MT_LOG_TERM = 1, MT_RT0 = 2, MT_RT1 = 3, MT_NUM = 4 };
 constexpr uint8_t MFL_REJECT = 0x01;
 constexpr uint8_t MFL_RUNS_SHIFT = 1;  // bits 1..2: n_runs
+constexpr uint8_t MT_WIDE = 0xFF;      // type of a host-encoded message whose terms do not fit 32 bits
+__host__ __device__ inline bool wide_term(uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
+  return ((a | b | c | d) >> 32) != 0;
+}
 
 __host__ __device__ inline uint32_t space_pad_positions(uint32_t positions) {
   return (positions + 63u) & ~63u;
 }
-__host__ __device__ inline uint64_t space_k_bytes(uint32_t pc) { return (uint64_t)pc * (2 + 8 + 8 * MF_NUM_U64); }
+__host__ __device__ inline uint64_t space_k_bytes(uint32_t pc) {
+  return (uint64_t)pc * (2 + 8 + 4 * MT_NUM + 8 * MF_NUM_U64);
+}
 __host__ __device__ inline uint64_t space_chunk_bytes_pc(uint32_t pc) {
   uint64_t b = (uint64_t)pc + GR_C * space_k_bytes(pc);
   return (b + 255u) & ~(uint64_t)255u;
@@ -146,8 +169,11 @@ struct Mailbox {
   __host__ __device__ inline uint32_t& run2(uint32_t k) const {
     return reinterpret_cast<uint32_t*>(kblock(k) + 6ull * pc)[local];
   }
+  __host__ __device__ inline uint32_t& t32(uint32_t k, uint32_t f) const {
+    return reinterpret_cast<uint32_t*>(kblock(k) + 10ull * pc + (uint64_t)f * 4ull * pc)[local];
+  }
   __host__ __device__ inline uint64_t& u64(uint32_t k, uint32_t f) const {
-    return reinterpret_cast<uint64_t*>(kblock(k) + 10ull * pc + (uint64_t)f * 8ull * pc)[local];
+    return reinterpret_cast<uint64_t*>(kblock(k) + (10ull + 4 * MT_NUM) * pc + (uint64_t)f * 8ull * pc)[local];
   }
 };
 
@@ -169,7 +195,15 @@ struct SpaceView {
 // Stats partials: one row of NSTAT u64 per workgroup, owned by that workgroup.
 enum StatField : uint32_t {
   ST_PASSES = 0, ST_LEADER_COMMITS = 1, ST_FOLLOWER_COMMITS = 2, ST_ESCALATIONS = 3,
-  ST_MSGS_IN = 4, ST_MSGS_OUT = 5, NSTAT = 8
+  ST_MSGS_IN = 4, ST_MSGS_OUT = 5, ST_LEADER_MSGS_IN = 6, ST_LEADER_MSGS_OUT = 7,
+  ST_REPLICATE_ENTRIES = 8, NSTAT = 16
+};
+// Per-lane counters of one pass (reduced per workgroup into the stats rows).
+// "leader" = the lane ended the pass as leader; entries = sum of n over the
+// Replicate messages the lane handled (the units of SURVEY.md §8d).
+struct LaneStats {
+  uint32_t leader_commit = 0, follower_commit = 0, escalated = 0;
+  uint32_t msgs_in = 0, msgs_out = 0, leader_in = 0, leader_out = 0, entries = 0;
 };
 
 // Route modes: where lane i reads (dir 0) / writes (dir 1) the mailbox of

@@ -80,7 +80,8 @@ enum gr_escalation {
   GR_ESC_ENTRY_SIZE = 8,     /* settings.Soft.MaxEntrySize may bind (raft.go:513) */
   GR_ESC_MSG_RUNS = 9,       /* Replicate entries span more than 2 term runs */
   GR_ESC_NONMEMBER = 10,     /* target node id has no remote slot */
-  GR_ESC_CONFIG_CHANGE = 11  /* proposal carries a ConfigChangeEntry (raft.go:1134-1143) */
+  GR_ESC_CONFIG_CHANGE = 11, /* proposal carries a ConfigChangeEntry (raft.go:1134-1143) */
+  GR_ESC_WIDE_TERM = 12      /* a message term >= 2^32 (device mailboxes carry 32-bit terms) */
 };
 
 enum gr_error {
@@ -226,6 +227,8 @@ typedef struct gr_stats {
   uint64_t follower_commits;
   uint64_t escalations;
   uint64_t msgs_in, msgs_out;
+  uint64_t leader_msgs_in, leader_msgs_out; /* of lanes that ended the pass as leader */
+  uint64_t replicate_entries;               /* sum of n over Replicate messages handled */
 } gr_stats;
 
 typedef struct gr_engine gr_engine;

@@ -26,14 +26,14 @@ void run_lanes(const StepParams& kp) {
   std::vector<uint32_t> bailed;
   for (uint32_t i = 0; i < kp.n_lanes; ++i) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-    uint32_t a, b, c, d;
-    if (!fast_step<S>(kp, i, p, &a, &b, &c, &d)) bailed.push_back(i);
+    LaneStats ls;
+    if (!fast_step<S>(kp, i, p, &ls)) bailed.push_back(i);
   }
   for (uint32_t i : bailed) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     Lane<S> L(kp, i, p);
-    uint32_t a, b, c, d, e;
-    L.step(&a, &b, &c, &d, &e);
+    LaneStats ls;
+    L.step(&ls);
   }
   g_fast_lanes += kp.n_lanes - bailed.size();
   g_bailed_lanes += bailed.size();
@@ -70,7 +70,8 @@ extern "C" int hl_step(uint32_t slots, uint64_t max_entry_size, gr_peer* peers, 
   for (uint32_t l = 0; l < nl; ++l) {
     ln.u32(LR_LANE_PEER)[l] = pk.peers[l];
     locals_to_rows(pk.locals[l], &ln.u32(LR_TICKS)[l], &ln.u32(LR_QTICKS)[l], &ln.u32(LR_PROPOSE)[l],
-                   &ln.u8(LR_LFLAGS)[l], &ln.u64(LR_RI_LO)[l], &ln.u64(LR_RI_HI)[l], &ln.u64(LR_RAND)[l]);
+                   &ln.u8(LR_LFLAGS)[l], &ln.u64(LR_RI_LO)[l], &ln.u64(LR_RI_HI)[l], &ln.u64(LR_RAND)[l],
+                   &ln.u32(LR_LWORD)[l]);
     for (uint32_t j = 0; j < S; ++j) {
       ln.in_pos()[(size_t)j * ln.lcap + l] = pk.in_pos[(size_t)j * nl + l];
       ln.out_pos()[(size_t)j * ln.lcap + l] = pk.out_pos[(size_t)j * nl + l];
@@ -118,7 +119,8 @@ extern "C" int hl_step(uint32_t slots, uint64_t max_entry_size, gr_peer* peers, 
       }
       if (rf & RF_PROPOSE) {
         pr.propose_result = ln.u8(LR_PROP_RESULT)[l];
-        pr.propose_first = ln.u64(LR_PROPOSE_FIRST)[l];
+        if (pr.propose_result == GR_PROP_APPENDED)
+          pr.propose_first = st.u64(SR_LAST_INDEX)[pk.peers[l]] - ln.u32(LR_PROPOSE)[l] + 1;
       }
       if (rf & RF_APPEND) pr.append_from = ln.u64(LR_APPEND_FROM)[l];
       if (rf & RF_READY) {

@@ -54,3 +54,12 @@ def test_ticks_and_read_index(built, check_quorum):
         return loc
     st = _run(G, 12, seed=7, locals_fn=lf, check_quorum=check_quorum)
     assert st["msgs"] > 0
+
+
+def test_wide_terms_escalate(built):
+    """Terms >= 2^32 never enter a device mailbox (32-bit term fields): the sender
+    escalates GR_ESC_WIDE_TERM, a host-encoded inbox message escalates at the
+    receiver, and every applied item still matches the oracle bit for bit."""
+    st = _run(32, 5, seed=4, term_lo=2**32 - 1, term_hi=2**32 + 2)
+    assert st["esc_reasons"].get("wide_term", 0) > 0
+    assert st["commits"] > 0  # groups whose terms still fit keep committing on the device

@@ -62,8 +62,11 @@ def main(o):
     fk = s["kernels"].get("gr_fast_kernel", {})
     if "hbm_bytes_per_launch" in fk:
         groups = int(os.environ.get("GROUPS", "1000000"))
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from dragonboat_amd.build import source_digest
         with open(os.path.join(o, "pmc_latest.json"), "w") as fh:
             json.dump({"kernel": "gr_fast_kernel<3>", "groups": groups, "replicas": 3,
+                       "source_digest": source_digest(),
                        "hbm_bytes_per_launch": fk["hbm_bytes_per_launch"],
                        "read_bytes": fk["read_bytes"], "write_bytes": fk["write_bytes"],
                        "calibration": cal, "source": os.path.basename(o)}, fh, indent=1)
