@@ -44,11 +44,11 @@ def b_round(R):
 B_RESP, B_EMIT, B_MATCH0, B_ENTRY = 69, 65, 122, 16
 
 
-def algorithmic_bytes(st, groups, R):
-    """SURVEY.md §8d per-unit bytes x the units counted by the device stats."""
+def algorithmic_bytes(st, groups, R, passes):
+    """SURVEY.md §8d per-unit bytes x the units counted by the device stats over `passes` passes."""
     follower_in = st["msgs_in"] - st["leader_msgs_in"]
     return (B_RESP * st["leader_msgs_in"] + B_EMIT * st["leader_msgs_out"] + B_MATCH0 * follower_in
-            + B_ENTRY * st["replicate_entries"] + (8 * R + 48) * groups)
+            + B_ENTRY * st["replicate_entries"] + (8 * R + 48) * groups * passes)
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, spec
@@ -177,7 +177,7 @@ def main():
     kavg = tm["fast_ms"] / passes  # the dominant kernel
     gavg = tm["general_ms"] / passes
     groups_total = G * world
-    alg = algorithmic_bytes(st, G, R) / args.steps  # per launch (this rank)
+    alg = algorithmic_bytes(st, G, R, args.steps) / args.steps  # per launch (this rank)
     achieved = alg / (kavg * 1e-3) / 1e9  # GB/s: algorithmic bytes of the launch / its time
     canon = b_round(R) * G
     if rank == 0:
