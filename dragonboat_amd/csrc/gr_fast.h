@@ -280,12 +280,12 @@ struct FastLane {
     }
     // ---- round 3: message fields
     // leader: ReplicateResp (type, flags, term, LogIndex) from every slot
-    uint32_t lh[S][MK];
-    uint64_t lterm[S][MK], lidx[S][MK];
+    uint32_t lh[S][MK], lterm[S][MK];
+    uint64_t lidx[S][MK];
     // follower: Replicate fields from the one slot L that sent, + its node id
     uint32_t L = 0, nsrc = 0, c = 0, gl = 0, go = NOPOS;
-    uint32_t fh[MK], fn[MK];
-    uint64_t fterm[MK], fidx[MK], flt[MK], fcom[MK], frt0[MK];
+    uint32_t fh[MK], fn[MK], fterm[MK], flt[MK], frt0[MK];
+    uint64_t fidx[MK], fcom[MK];
     uint64_t rid = 0;
     if (leader) {
 #pragma unroll
@@ -298,7 +298,7 @@ struct FastLane {
           if ((uint32_t)k < cnt[j]) {
             const Mailbox mb = kp.in.at(gin[j]);
             lh[j][k] = (uint32_t)mb.type(k) | ((uint32_t)mb.flags(k) << 8);
-            lterm[j][k] = (uint64_t)mb.t32(k, MT_TERM);
+            lterm[j][k] = mb.t32(k, MT_TERM);
             lidx[j][k] = mb.u64(k, MF_LOG_INDEX);
           }
         }
@@ -322,11 +322,11 @@ struct FastLane {
           const Mailbox mb = kp.in.at(gl);
           fh[k] = (uint32_t)mb.type(k) | ((uint32_t)mb.flags(k) << 8);
           fn[k] = mb.n(k);
-          fterm[k] = (uint64_t)mb.t32(k, MT_TERM);
+          fterm[k] = mb.t32(k, MT_TERM);
           fidx[k] = mb.u64(k, MF_LOG_INDEX);
-          flt[k] = (uint64_t)mb.t32(k, MT_LOG_TERM);
+          flt[k] = mb.t32(k, MT_LOG_TERM);
           fcom[k] = mb.u64(k, MF_COMMIT);
-          frt0[k] = (uint64_t)mb.t32(k, MT_RT0);
+          frt0[k] = mb.t32(k, MT_RT0);
         }
       }
       if (c) rid = s64(Rw::RID + L);
@@ -343,7 +343,7 @@ struct FastLane {
         GF_BAIL(cnt[j] > (uint32_t)MK);
 #pragma unroll
         for (int k = 0; k < MK; ++k)
-          if ((uint32_t)k < cnt[j]) GF_BAIL(lh[j][k] != GR_REPLICATE_RESP || lterm[j][k] != term);
+          if ((uint32_t)k < cnt[j]) GF_BAIL(lh[j][k] != GR_REPLICATE_RESP || (uint64_t)lterm[j][k] != term);
       }
       // messages in node.handleReceivedMessages order: slot, then arrival
 #pragma unroll
@@ -362,7 +362,7 @@ struct FastLane {
 #pragma unroll
       for (int k = 0; k < MK; ++k) {
         if ((uint32_t)k < c) {
-          GF_BAIL((fh[k] & 0xFFu) != GR_REPLICATE || fterm[k] != term);
+          GF_BAIL((fh[k] & 0xFFu) != GR_REPLICATE || (uint64_t)fterm[k] != term);
           const uint32_t nr = (fh[k] >> (8 + MFL_RUNS_SHIFT)) & 3u;
           GF_BAIL(fn[k] != 0 && nr != 1);
         }
@@ -372,7 +372,7 @@ struct FastLane {
       for (int k = 0; k < MK; ++k) {
         if ((uint32_t)k < c) {
           nmi++;
-          replicate(fidx[k], flt[k], fcom[k], fn[k], frt0[k], go, &oc);
+          replicate(fidx[k], (uint64_t)flt[k], fcom[k], fn[k], (uint64_t)frt0[k], go, &oc);
         }
       }
 #pragma unroll
