@@ -57,7 +57,10 @@ __device__ inline void block_stats(const StepParams& kp, const LaneStats& ls) {
 // meet anything else append themselves to bail_list (one atomic per wave;
 // a wave's lanes stay contiguous and ascending) and store no state.
 template <int S>
-__global__ __launch_bounds__(kBlock) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
+#ifndef GR_FAST_MIN_WAVES
+#define GR_FAST_MIN_WAVES 1  // waves per SIMD the register allocation must allow (A/B builds)
+#endif
+__global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
                                                          uint32_t* bail_count) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   LaneStats ls;

@@ -38,7 +38,7 @@ struct FastLane {
   const uint32_t i, p;
   // core
   uint32_t state = 0, self = 0, nruns = 0;
-  uint64_t term = 0, committed = 0, committed0 = 0, hi = 0, hi0 = 0, lo = 0;
+  uint64_t term = 0, committed = 0, committed0 = 0, hi = 0, hi0 = 0;
   uint64_t rsn = 0, rtn = 0;  // newest term run (start, term)
   bool pushed = false;        // a run was appended this pass (row nruns-1)
   bool ok = true;             // still on the steady-state path
@@ -61,12 +61,14 @@ struct FastLane {
   GF_HD uint64_t& s64(uint32_t row) const { return kp.st.u64(row)[p]; }
   GF_HD uint8_t& s8(uint32_t row) const { return kp.st.u8(row)[p]; }
 
-  // entryLog.term (logentry.go:141-157) when the answer is in the newest run;
-  // an older run (or the host's LogReader) hands the lane over.
+  // entryLog.term (logentry.go:141-157) when the answer is in the newest run.
+  // The lane only runs with NR_GE_LO (newest run start >= firstIndex-1), so
+  // x >= rsn is inside [firstIndex-1, lastIndex]; anything below the newest
+  // run (an older run, or below firstIndex-1) hands the lane over.
   GF_HD uint64_t term_of(uint64_t x) {
-    const bool out = x < lo || x > hi;
-    GF_BAIL(!out && (nruns == 0 || x < rsn));
-    return out ? 0 : rtn;
+    if (x > hi) return 0;
+    GF_BAIL(nruns == 0 || x < rsn);
+    return rtn;
   }
   // win_push (gr_lane.h) for one new run per pass, no window shift.
   GF_HD void win_push(uint64_t start, uint64_t t) {
@@ -84,13 +86,16 @@ struct FastLane {
     if (!ok) return;
     const Mailbox mb = kp.out.at(gout[j]);
     const uint32_t c = outc[j];
+    uint32_t cd;
+    const bool narrow = commit_delta(committed, log_index, &cd);
     mb.type(c) = GR_REPLICATE;
-    mb.flags(c) = (uint8_t)(n ? (1u << MFL_RUNS_SHIFT) : 0u);
+    mb.flags(c) = (uint8_t)((n ? (1u << MFL_RUNS_SHIFT) : 0u) | (narrow ? 0u : MFL_WIDE_COMMIT));
     mb.t32(c, MT_TERM) = (uint32_t)(term);
     mb.n(c) = n;
     mb.u64(c, MF_LOG_INDEX) = log_index;
     mb.t32(c, MT_LOG_TERM) = (uint32_t)(log_term);
-    mb.u64(c, MF_COMMIT) = committed;
+    if (narrow) mb.t32(c, MT_CDELTA) = cd;
+    else mb.u64(c, MF_COMMIT) = committed;
     if (n) mb.t32(c, MT_RT0) = (uint32_t)(rt0);
     outc[j] = c + 1;
     nmo++;
@@ -152,8 +157,9 @@ struct FastLane {
     const uint64_t lt = term_of(nx - 1);
     uint32_t n = 0;
     if (nx <= hi) {
-      GF_BAIL(nx <= lo);                // InstallSnapshot path
-      GF_BAIL(nruns == 0 || nx < rsn);  // entries in an older run
+      // nx <= rsn covers entries in an older run and nx <= firstIndex-1
+      // (InstallSnapshot path): with NR_GE_LO, nx > rsn implies nx > firstIndex-1
+      GF_BAIL(nruns == 0 || nx <= rsn);
       GF_BAIL(hi - nx + 1 > 1);         // several entries: MaxEntrySize check
       GF_BAIL(rst[j] != GR_REPLICATE_ST && rst[j] != GR_RETRY);
       n = 1;
@@ -244,11 +250,11 @@ struct FastLane {
     // ---- round 1: core, locals, routes
     state = s8(Rw::B_STATE);
     self = s8(Rw::B_SELF);
-    nruns = s8(Rw::B_NRUNS);
+    const uint32_t nbyte = s8(Rw::B_NRUNS);
+    nruns = nbyte & NR_MASK;
     term = s64(SR_TERM);
     committed = s64(SR_COMMITTED);
     hi = s64(SR_LAST_INDEX);
-    lo = s64(SR_LO);
     const uint32_t flags = s8(Rw::B_FLAGS);
     const uint32_t lw = kp.has_locals ? kp.ln.u32(LR_LWORD)[i] : 0u;  // packed locals (gr_layout.h)
     uint32_t gin[S];
@@ -284,8 +290,8 @@ struct FastLane {
     uint64_t lidx[S][MK];
     // follower: Replicate fields from the one slot L that sent, + its node id
     uint32_t L = 0, nsrc = 0, c = 0, gl = 0, go = NOPOS;
-    uint32_t fh[MK], fn[MK], fterm[MK], flt[MK], frt0[MK];
-    uint64_t fidx[MK], fcom[MK];
+    uint32_t fh[MK], fn[MK], fterm[MK], flt[MK], frt0[MK], fcd[MK];
+    uint64_t fidx[MK];
     uint64_t rid = 0;
     if (leader) {
 #pragma unroll
@@ -317,7 +323,7 @@ struct FastLane {
       const uint32_t cc = c < (uint32_t)MK ? c : (uint32_t)MK;
 #pragma unroll
       for (int k = 0; k < MK; ++k) {
-        fh[k] = 0; fn[k] = 0; fterm[k] = 0; fidx[k] = 0; flt[k] = 0; fcom[k] = 0; frt0[k] = 0;
+        fh[k] = 0; fn[k] = 0; fterm[k] = 0; fidx[k] = 0; flt[k] = 0; fcd[k] = 0; frt0[k] = 0;
         if ((uint32_t)k < cc) {
           const Mailbox mb = kp.in.at(gl);
           fh[k] = (uint32_t)mb.type(k) | ((uint32_t)mb.flags(k) << 8);
@@ -325,15 +331,21 @@ struct FastLane {
           fterm[k] = mb.t32(k, MT_TERM);
           fidx[k] = mb.u64(k, MF_LOG_INDEX);
           flt[k] = mb.t32(k, MT_LOG_TERM);
-          fcom[k] = mb.u64(k, MF_COMMIT);
+          fcd[k] = mb.t32(k, MT_CDELTA);
           frt0[k] = mb.t32(k, MT_RT0);
         }
       }
-      if (c) rid = s64(Rw::RID + L);
+      // electionTick = 0 and leaderID = remote_id(L) are usually already so
+      // (F_ETZ, F_LSLOT): then neither is loaded nor rewritten
+      if (c && ((flags & F_LSLOT) >> F_LSLOT_SHIFT) != L + 1) rid = s64(Rw::RID + L);
     }
     // ---- checks: anything outside the steady state goes to the general lane
     GF_BAIL(!leader && state != GR_FOLLOWER);
     GF_BAIL((lw & LW_OTHER) || (np && !leader));
+    bool any_input = np != 0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) any_input = any_input || cnt[j] != 0;
+    GF_BAIL(any_input && !(nbyte & NR_GE_LO));  // the window test needs firstIndex-1
     committed0 = committed;
     hi0 = hi;
     if (leader) {
@@ -363,6 +375,7 @@ struct FastLane {
       for (int k = 0; k < MK; ++k) {
         if ((uint32_t)k < c) {
           GF_BAIL((fh[k] & 0xFFu) != GR_REPLICATE || (uint64_t)fterm[k] != term);
+          GF_BAIL(fh[k] & ((uint32_t)MFL_WIDE_COMMIT << 8));
           const uint32_t nr = (fh[k] >> (8 + MFL_RUNS_SHIFT)) & 3u;
           GF_BAIL(fn[k] != 0 && nr != 1);
         }
@@ -372,7 +385,7 @@ struct FastLane {
       for (int k = 0; k < MK; ++k) {
         if ((uint32_t)k < c) {
           nmi++;
-          replicate(fidx[k], (uint64_t)flt[k], fcom[k], fn[k], (uint64_t)frt0[k], go, &oc);
+          replicate(fidx[k], (uint64_t)flt[k], commit_of(fcd[k], fidx[k]), fn[k], (uint64_t)frt0[k], go, &oc);
         }
       }
 #pragma unroll
@@ -382,10 +395,10 @@ struct FastLane {
     // ---- stores (nothing above this line has written state)
     if (committed != committed0) s64(SR_COMMITTED) = committed;
     if (hi != hi0) s64(SR_LAST_INDEX) = hi;
-    if (pushed) {
+    if (pushed) {  // the new run starts above the old newest run: NR_GE_LO still holds
       s64(SR_RUN_START + nruns - 1) = rsn;
       s64(SR_RUN_TERM + nruns - 1) = rtn;
-      s8(Rw::B_NRUNS) = (uint8_t)nruns;
+      s8(Rw::B_NRUNS) = (uint8_t)(nruns | NR_GE_LO);
     }
     if (leader) {
 #pragma unroll
@@ -403,8 +416,16 @@ struct FastLane {
       for (int j = 0; j < S; ++j)
         if ((snapz >> j) & 1u) s64(Rw::SNAP + j) = 0;
     } else if (c) {
-      s64(SR_ETICK) = 0;        // electionTick = 0 (raft.go:1360)
-      s64(SR_LEADER_ID) = rid;  // setLeaderID(m.From)
+      uint32_t nf = flags;
+      if (!(flags & F_ETZ)) {
+        s64(SR_ETICK) = 0;  // electionTick = 0 (raft.go:1360)
+        nf |= F_ETZ;
+      }
+      if (((flags & F_LSLOT) >> F_LSLOT_SHIFT) != L + 1) {
+        s64(SR_LEADER_ID) = rid;  // setLeaderID(m.From)
+        nf = (nf & ~F_LSLOT) | ((L + 1) << F_LSLOT_SHIFT);
+      }
+      if (nf != flags) s8(Rw::B_FLAGS) = (uint8_t)nf;
     }
 #pragma unroll
     for (int j = 0; j < S; ++j)
@@ -445,8 +466,7 @@ struct FastLane {
     }
     uint64_t ci = 0;
     if (n) {  // getConflictIndex over the newest run (logentry.go:305-312)
-      const uint64_t a = li + 1, b = li + n;
-      GF_BAIL(a < lo);
+      const uint64_t a = li + 1, b = li + n;  // a >= rsn >= firstIndex-1 below (NR_GE_LO)
       if (a <= hi) {
         GF_BAIL(nruns == 0 || a < rsn);
         if (rtn != rt0) ci = a;

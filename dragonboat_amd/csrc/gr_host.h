@@ -67,9 +67,17 @@ inline void set_u64_row(gr_peer& g, uint32_t row, uint32_t S, uint64_t v) {
 inline uint8_t get_u8_row(const gr_peer& g, uint32_t row, uint32_t S) {
   switch (row) {
     case 0: return g.state;
-    case 1: return (uint8_t)((g.flags & ~F_LTT) | (g.leader_transfer_target ? F_LTT : 0u));
+    case 1: {
+      uint32_t sl = 0;
+      for (uint32_t j = 0; j < S && j < 7 && g.leader_id; ++j)
+        if (!sl && g.remote_id[j] == g.leader_id) sl = j + 1;
+      return (uint8_t)((g.flags & F_PUBLIC) | (g.leader_transfer_target ? F_LTT : 0u) |
+                       (g.election_tick == 0 ? F_ETZ : 0u) | (sl << F_LSLOT_SHIFT));
+    }
     case 2: return g.self_slot;
-    case 3: return g.n_runs;
+    case 3:
+      return (uint8_t)(g.n_runs | (g.n_runs && g.n_runs <= GR_K && g.run_start[g.n_runs - 1] >= g.first_index_m1
+                                       ? NR_GE_LO : 0u));
     case 4: return g.read_index_count;
   }
   uint32_t r = row - 5;
@@ -86,9 +94,9 @@ inline uint8_t get_u8_row(const gr_peer& g, uint32_t row, uint32_t S) {
 inline void set_u8_row(gr_peer& g, uint32_t row, uint32_t S, uint8_t v) {
   switch (row) {
     case 0: g.state = v; return;
-    case 1: g.flags = (uint8_t)(v & ~F_LTT); return;
+    case 1: g.flags = (uint8_t)(v & F_PUBLIC); return;
     case 2: g.self_slot = v; return;
-    case 3: g.n_runs = v; return;
+    case 3: g.n_runs = (uint8_t)(v & NR_MASK); return;
     case 4: g.read_index_count = v; return;
   }
   uint32_t r = row - 5;
@@ -119,7 +127,13 @@ inline void encode_msg(const Mailbox& mb, uint32_t k, const gr_message& m) {
     return;
   }
   mb.type(k) = m.type;
-  mb.flags(k) = (uint8_t)((m.reject ? MFL_REJECT : 0) | (m.n_runs << MFL_RUNS_SHIFT));
+  uint8_t fl = (uint8_t)((m.reject ? MFL_REJECT : 0) | (m.n_runs << MFL_RUNS_SHIFT));
+  if (m.type == GR_REPLICATE) {
+    uint32_t cd;
+    if (commit_delta(m.commit, m.log_index, &cd)) mb.t32(k, MT_CDELTA) = cd;
+    else fl |= MFL_WIDE_COMMIT;
+  }
+  mb.flags(k) = fl;
   mb.n(k) = m.n_entries;
   mb.run2(k) = m.run2_offset;
   mb.t32(k, MT_TERM) = (uint32_t)(m.term);
@@ -146,7 +160,7 @@ inline gr_message decode_msg(const Mailbox& mb, uint32_t k) {
       m.n_entries = mb.n(k);
       m.log_index = mb.u64(k, MF_LOG_INDEX);
       m.log_term = (uint64_t)mb.t32(k, MT_LOG_TERM);
-      m.commit = mb.u64(k, MF_COMMIT);
+      m.commit = (fl & MFL_WIDE_COMMIT) ? mb.u64(k, MF_COMMIT) : commit_of(mb.t32(k, MT_CDELTA), m.log_index);
       if (m.n_entries) m.run_term[0] = (uint64_t)mb.t32(k, MT_RT0);
       if (m.n_runs == 2) {
         m.run2_offset = mb.run2(k);

@@ -156,7 +156,7 @@ struct Lane {
     }
     if (miss & G_WIN) {
       lo = s64(SR_LO);
-      nruns = s8(R::B_NRUNS);
+      nruns = s8(R::B_NRUNS) & NR_MASK;
 #pragma unroll
       for (int r = 0; r < GR_K; ++r) {
         rs[r] = s64(SR_RUN_START + r);
@@ -196,8 +196,18 @@ struct Lane {
   }
 
   GR_HD void store() {
-    if (dirty & D_LTT) {  // keep the device-internal F_LTT bit of the flags row in step
-      const uint32_t nf = (flags & ~F_LTT) | (ltt ? F_LTT : 0u);
+    if (dirty & (D_LTT | D_ETICK | D_LEADER)) {  // device-internal flag bits (gr_layout.h)
+      need(G_CORE);
+      uint32_t nf = flags;
+      if (dirty & D_LTT) nf = (nf & ~F_LTT) | (ltt ? F_LTT : 0u);
+      if (dirty & D_ETICK) nf = (nf & ~F_ETZ) | (etick == 0 ? F_ETZ : 0u);
+      if (dirty & D_LEADER) {
+        uint32_t sl = 0;
+#pragma unroll 1
+        for (uint32_t j = 0; j < (uint32_t)S && j < 7 && leader_id; ++j)
+          if (!sl && remote_id(j) == leader_id) sl = j + 1;
+        nf = (nf & ~F_LSLOT) | (sl << F_LSLOT_SHIFT);
+      }
       if (nf != flags) {
         flags = nf;
         dirty |= D_FLAGS;
@@ -215,7 +225,10 @@ struct Lane {
     if (dirty & D_STATE) s8(R::B_STATE) = (uint8_t)state;
     if (dirty & D_FLAGS) s8(R::B_FLAGS) = (uint8_t)flags;
     if (dirty & D_WIN) {
-      s8(R::B_NRUNS) = (uint8_t)nruns;
+      uint64_t last_start = 0;
+#pragma unroll
+      for (int r = 0; r < GR_K; ++r) last_start = ((uint32_t)r + 1 == nruns) ? rs[r] : last_start;
+      s8(R::B_NRUNS) = (uint8_t)(nruns | (nruns && last_start >= lo ? NR_GE_LO : 0u));
 #pragma unroll
       for (int r = 0; r < GR_K; ++r) {
         s64(SR_RUN_START + r) = rs[r];
@@ -435,11 +448,17 @@ struct Lane {
     mb.flags(c) = m.flags;
     mb.t32(c, MT_TERM) = (uint32_t)mterm;
     switch (m.type) {  // write the fields the receiver reads (read_msg)
-      case GR_REPLICATE:
+      case GR_REPLICATE: {
         mb.n(c) = m.n;
         mb.u64(c, MF_LOG_INDEX) = m.log_index;
         mb.t32(c, MT_LOG_TERM) = (uint32_t)(m.log_term);
-        mb.u64(c, MF_COMMIT) = m.commit;
+        uint32_t cd;
+        if (commit_delta(m.commit, m.log_index, &cd)) {
+          mb.t32(c, MT_CDELTA) = cd;
+        } else {
+          mb.flags(c) = (uint8_t)(m.flags | MFL_WIDE_COMMIT);
+          mb.u64(c, MF_COMMIT) = m.commit;
+        }
         if (m.n) {
           mb.t32(c, MT_RT0) = (uint32_t)(m.rt0);
           if (((m.flags >> MFL_RUNS_SHIFT) & 3u) == 2) {
@@ -448,6 +467,7 @@ struct Lane {
           }
         }
         break;
+      }
       case GR_REPLICATE_RESP:  // Hint is only read on a reject (decreaseTo, raft.go:1219)
         mb.u64(c, MF_LOG_INDEX) = m.log_index;
         if (m.flags & MFL_REJECT) mb.u64(c, MF_HINT) = m.hint;
@@ -1004,7 +1024,8 @@ struct Lane {
         m.n = mb.n(k);
         m.log_index = mb.u64(k, MF_LOG_INDEX);
         m.log_term = (uint64_t)mb.t32(k, MT_LOG_TERM);
-        m.commit = mb.u64(k, MF_COMMIT);
+        m.commit = (m.flags & MFL_WIDE_COMMIT) ? mb.u64(k, MF_COMMIT)
+                                               : commit_of(mb.t32(k, MT_CDELTA), m.log_index);
         if (m.n) {
           m.rt0 = (uint64_t)mb.t32(k, MT_RT0);
           if (((m.flags >> MFL_RUNS_SHIFT) & 3u) == 2) {

@@ -121,10 +121,21 @@ __host__ __device__ inline uint32_t local_word(uint32_t ticks, uint32_t qticks, 
   const bool other = ticks || qticks || lflags || propose > 0xFFFFu;
   return other ? LW_OTHER : propose;
 }
-// Device-internal bit of the state flags row: leaderTransferTarget != 0, so the
-// lean lane tests one byte instead of loading the 8-byte target. Never visible
-// in gr_peer.flags (gr_host.h masks it).
+// Device-internal bits of the state flags row (never visible in gr_peer.flags:
+// gr_host.h masks them; GR_F_* use bits 0-2). They let the lean lane test one
+// byte instead of loading or rewriting 8-byte fields:
+//   F_LTT    leaderTransferTarget != 0
+//   F_ETZ    electionTick == 0
+//   F_LSLOT  0, or s + 1 for a remote slot s < 7 with remote_id[s] == leaderID
+// Every device write of those fields updates the bits (Lane::store, FastLane).
+constexpr uint32_t F_PUBLIC = 0x07u;
 constexpr uint32_t F_LTT = 0x80u;
+constexpr uint32_t F_ETZ = 0x40u;
+constexpr uint32_t F_LSLOT_SHIFT = 3, F_LSLOT = 0x38u;
+// Device-internal bit of the n_runs row: the newest run starts at or above
+// firstIndex-1, so every index at or above it is inside the log window and
+// the lean lane never needs firstIndex-1 (lo). n_runs itself is bits 0-2.
+constexpr uint32_t NR_MASK = 0x07u, NR_GE_LO = 0x80u;
 // The result record's propose_first is not stored: ProposeEntries is the last
 // item of a pass, so it is last_index - propose_entries + 1 after the pass.
 constexpr uint8_t RF_ESCALATED = 0x01;
@@ -134,9 +145,22 @@ constexpr uint8_t RF_APPEND = 0x08;
 
 // ---------------------------------------------------------------- message spaces
 enum U64Field : uint32_t { MF_LOG_INDEX = 0, MF_COMMIT = 1, MF_HINT = 2, MF_HINT_HIGH = 3, MF_NUM_U64 = 4 };
-enum T32Field : uint32_t { MT_TERM = 0, MT_LOG_TERM = 1, MT_RT0 = 2, MT_RT1 = 3, MT_NUM = 4 };
+enum T32Field : uint32_t { MT_TERM = 0, MT_LOG_TERM = 1, MT_RT0 = 2, MT_RT1 = 3, MT_CDELTA = 4, MT_NUM = 5 };
 constexpr uint8_t MFL_REJECT = 0x01;
-constexpr uint8_t MFL_RUNS_SHIFT = 1;  // bits 1..2: n_runs
+constexpr uint8_t MFL_RUNS_SHIFT = 1;     // bits 1..2: n_runs
+constexpr uint8_t MFL_WIDE_COMMIT = 0x08; // Replicate: Commit in MF_COMMIT (else MT_CDELTA)
+// A Replicate's Commit travels as a 32-bit offset from its LogIndex when
+// |Commit - LogIndex| < 2^31 (always, unless a follower lags by 2^31 entries);
+// otherwise in full with MFL_WIDE_COMMIT. Both decode exactly.
+__host__ __device__ inline bool commit_delta(uint64_t commit, uint64_t log_index, uint32_t* cd) {
+  const uint64_t d = commit - log_index + 0x80000000ull;  // mod 2^64
+  if (d >> 32) return false;
+  *cd = (uint32_t)d;
+  return true;
+}
+__host__ __device__ inline uint64_t commit_of(uint32_t cd, uint64_t log_index) {
+  return log_index + (uint64_t)cd - 0x80000000ull;
+}
 constexpr uint8_t MT_WIDE = 0xFF;      // type of a host-encoded message whose terms do not fit 32 bits
 __host__ __device__ inline bool wide_term(uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
   return ((a | b | c | d) >> 32) != 0;

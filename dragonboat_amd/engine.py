@@ -14,7 +14,7 @@ import numpy as np
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libgpuraft.so")
+LIB_PATH = os.environ.get("GPURAFT_LIB") or os.path.join(_HERE, "_build", "libgpuraft.so")  # env: A/B builds
 _lib = None
 
 
