@@ -116,10 +116,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(local_rank)  # before the process group: RCCL binds the current device
     dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
     from dragonboat_amd import abi, populations as P
     from dragonboat_amd.engine import Engine
