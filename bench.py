@@ -116,10 +116,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)  # before the process group: RCCL binds the current device
-    dev = torch.device("cuda", local_rank)
+    # Rehearsal knobs (not used by the driver): GR_BENCH_BACKEND=gloo with
+    # GR_BENCH_ONE_DEVICE=1 runs N ranks on one GPU to exercise the N > 1 path
+    # of this script on a one-GPU box (RCCL itself refuses two ranks per device).
+    backend = os.environ.get("GR_BENCH_BACKEND", "nccl")
+    ordinal = 0 if os.environ.get("GR_BENCH_ONE_DEVICE") == "1" else local_rank
+    torch.cuda.set_device(ordinal)  # before the process group: RCCL binds the current device
+    dev = torch.device("cuda", ordinal)
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # where the control collectives run
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from dragonboat_amd import abi, populations as P
     from dragonboat_amd.engine import Engine
@@ -131,7 +140,7 @@ def main():
     placement = args.placement or "local"
     ex = build_exchange(G, R, S, world, rank, placement)
     n = ex.n_peers
-    eng = Engine(n, S, device=local_rank)
+    eng = Engine(n, S, device=ordinal)
     eng.load(ex.peers)
     eng.bind_routes(ex.in_pos, ex.out_pos)
     loc = P.propose_locals(n, ex.leader_slots, pass_index=0)
@@ -161,7 +170,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     tm = eng.timing_end()
@@ -169,7 +178,7 @@ def main():
     commits = st["leader_commits"]
     esc = st["escalations"]
     if world > 1:
-        t = torch.tensor([commits, esc], dtype=torch.float64, device=dev)
+        t = torch.tensor([commits, esc], dtype=torch.float64, device=cdev)
         dist.all_reduce(t)
         commits, esc = int(t[0].item()), int(t[1].item())
     value = commits / elapsed

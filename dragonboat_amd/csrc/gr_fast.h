@@ -33,6 +33,9 @@ template <int S>
 struct FastLane {
   using Rw = Rows<S>;
   static constexpr int MK = 2;  // messages per mailbox handled here
+  // Leaders with input run here for up to 3 slots; wider groups' leaders take
+  // the general lane (keeps this kernel's code and registers small for S = 5)
+  static constexpr bool kLeaderPath = S <= 3;
 
   const StepParams& kp;
   const uint32_t i, p;
@@ -274,7 +277,10 @@ struct FastLane {
     }
     const bool leader = state == GR_LEADER;
     const uint32_t np = lw & 0xFFFFu;
-    if (leader) {
+    const uint32_t nq = (lw >> LW_QT_SHIFT) & LW_QT_MAX;
+    uint64_t etick = 0;
+    if (nq) etick = s64(SR_ETICK);
+    if (kLeaderPath && leader) {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         match[j] = s64(Rw::MATCH + j);
@@ -293,7 +299,7 @@ struct FastLane {
     uint32_t fh[MK], fn[MK], fterm[MK], flt[MK], frt0[MK], fcd[MK];
     uint64_t fidx[MK];
     uint64_t rid = 0;
-    if (leader) {
+    if (kLeaderPath && leader) {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
 #pragma unroll
@@ -340,15 +346,33 @@ struct FastLane {
       if (c && ((flags & F_LSLOT) >> F_LSLOT_SHIFT) != L + 1) rid = s64(Rw::RID + L);
     }
     // ---- checks: anything outside the steady state goes to the general lane
-    GF_BAIL(!leader && state != GR_FOLLOWER);
-    GF_BAIL((lw & LW_OTHER) || (np && !leader));
     bool any_input = np != 0;
 #pragma unroll
     for (int j = 0; j < S; ++j) any_input = any_input || cnt[j] != 0;
+    GF_BAIL(lw & LW_OTHER);
+    if (nq) {
+      // QuiescedTick x nq alone (raft.go:431-433: electionTick++ in every
+      // state), the bulk of a quiesced population; combined with other
+      // inputs it goes to the general lane
+      GF_BAIL(any_input);
+      if (!ok) return false;
+      etick += nq;
+      s64(SR_ETICK) = etick;
+      if (flags & F_ETZ) s8(Rw::B_FLAGS) = (uint8_t)(flags & ~F_ETZ);
+#pragma unroll
+      for (int j = 0; j < S; ++j)
+        if (gout[j] != NOPOS) kp.out.at(gout[j]).cnt() = 0;
+      kp.ln.u8(LR_RFLAGS)[i] = 0;
+      *ls = LaneStats();
+      return true;
+    }
+    GF_BAIL(!leader && state != GR_FOLLOWER);
+    GF_BAIL(np && !leader);
+    GF_BAIL(!kLeaderPath && leader && any_input);
     GF_BAIL(any_input && !(nbyte & NR_GE_LO));  // the window test needs firstIndex-1
     committed0 = committed;
     hi0 = hi;
-    if (leader) {
+    if (kLeaderPath && leader) {
       GF_BAIL(flags & F_LTT);  // leader transfer in progress
 #pragma unroll
       for (int j = 0; j < S; ++j) {
@@ -400,7 +424,7 @@ struct FastLane {
       s64(SR_RUN_TERM + nruns - 1) = rtn;
       s8(Rw::B_NRUNS) = (uint8_t)(nruns | NR_GE_LO);
     }
-    if (leader) {
+    if (kLeaderPath && leader) {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         if ((mdirty >> j) & 1u) {

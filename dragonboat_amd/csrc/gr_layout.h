@@ -113,13 +113,14 @@ struct LaneBase {
 constexpr uint8_t LF_READ_INDEX = 0x01;
 constexpr uint8_t LF_PROPOSE_CC = 0x02;
 // LR_LWORD: a lane's local inputs packed for the lean lane (4 bytes instead
-// of 13): bits 0-15 the ProposeEntries count, bit 16 set when there is
-// anything else (ReadIndex, config change, ticks, quiesced ticks, or a count
-// >= 2^16), which the lean lane hands to the general lane.
+// of 13): bits 0-15 the ProposeEntries count, bits 17-24 the QuiescedTick
+// count, bit 16 set when there is anything else (ReadIndex, config change,
+// ticks, or a count that does not fit), which the lean lane hands over.
 constexpr uint32_t LW_OTHER = 0x10000u;
+constexpr uint32_t LW_QT_SHIFT = 17, LW_QT_MAX = 0xFFu;
 __host__ __device__ inline uint32_t local_word(uint32_t ticks, uint32_t qticks, uint32_t propose, uint32_t lflags) {
-  const bool other = ticks || qticks || lflags || propose > 0xFFFFu;
-  return other ? LW_OTHER : propose;
+  const bool other = ticks || lflags || propose > 0xFFFFu || qticks > LW_QT_MAX;
+  return other ? LW_OTHER : (propose | (qticks << LW_QT_SHIFT));
 }
 // Device-internal bits of the state flags row (never visible in gr_peer.flags:
 // gr_host.h masks them; GR_F_* use bits 0-2). They let the lean lane test one

@@ -207,3 +207,44 @@ def inject_leader_change(state, topo, p, rng, max_div=8, max_extra=4):
 def current_leaders(state, topo):
     """Slots of all peers in the leader state (proposal targets)."""
     return np.nonzero(state["state"] == abi.LEADER)[0]
+
+
+def config3(G, R=5, seed=3, active_frac=0.1, election=10, heartbeat=1):
+    """BASELINE config 3: G groups x R replicas, 90% quiesced, 10% active with a
+    ReadIndex pending each pass; electionTick uniform in [0, ET), ET=10, HT=1,
+    checkQuorum on for half of the groups (seed 3). Returns (peers, active[G])."""
+    peers = make_groups(G, R, seed=seed, election=election, heartbeat=heartbeat)
+    rng = np.random.default_rng([seed, 1])
+    cq = rng.random(G) < 0.5
+    active = rng.random(G) < active_frac
+    for r in range(R):
+        v = peers[r * G:(r + 1) * G]
+        v["flags"] = np.where(cq, v["flags"] | abi.F_CHECK_QUORUM, v["flags"])
+        v["election_tick"] = rng.integers(0, election, G)
+    return peers, active
+
+
+def config3_locals(G, R, active, pass_index, seed=3):
+    """Per-pass inputs of config 3: quiesced groups get one QuiescedTick per
+    replica; active groups one Tick per replica and a ReadIndex on the leader."""
+    n = R * G
+    rng = np.random.default_rng([seed, 2, pass_index])
+    act = np.tile(active, R)
+    loc = np.zeros(n, abi.LOCAL)
+    loc["peer"] = np.arange(n, dtype=np.uint32)
+    loc["quiesced_ticks"] = np.where(act, 0, 1)
+    loc["ticks"] = np.where(act, 1, 0)
+    lead = act & (np.arange(n) < G)
+    loc["read_index"] = lead
+    loc["read_ctx_low"] = np.where(lead, rng.integers(1, 2**63, n, dtype=np.uint64), 0)
+    loc["read_ctx_high"] = np.where(lead, pass_index + 1, 0)
+    loc["rand"] = rng.integers(0, 2**63, n, dtype=np.uint64)
+    return loc
+
+
+def drop_acks(msgs, p, rng):
+    """Drop each HeartbeatResp with probability p (config 3: followers ack with 1 - p)."""
+    if len(msgs) == 0:
+        return msgs
+    keep = ~((msgs["type"] == abi.HEARTBEAT_RESP) & (rng.random(len(msgs)) < p))
+    return msgs[keep]

@@ -54,13 +54,13 @@ class GpuBackend:
 
 
 def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, check=True,
-             max_report=3):
+             max_report=3, drop_fn=None):
     """Run `passes` passes; returns a dict of counters. Raises AssertionError on divergence."""
     pop = OraclePopulation(peers, slots)
     eng = backend(peers, slots)
     n = len(peers)
     msgs = np.zeros(0, abi.MESSAGE)
-    stats = {"msgs": 0, "escalations": 0, "esc_reasons": {}, "commits": 0}
+    stats = {"msgs": 0, "escalations": 0, "esc_reasons": {}, "commits": 0, "ready": 0}
     parked = np.zeros(n, bool)
     for k in range(passes):
         if inject_fn is not None:
@@ -77,6 +77,7 @@ def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, c
         lim = parity.limits_from(res, n)
         o = pop.step(msgs, loc, lim)
         esc = res[res["escalation"] != 0]
+        stats["ready"] += int(res["n_ready"].sum())
         stats["escalations"] += len(esc)
         for r in esc:
             nm = abi.ESC_NAMES[r["escalation"]]
@@ -104,4 +105,6 @@ def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, c
         if len(idx):
             eng.load(idx, full[idx])
         msgs = topo.route_messages(o["msgs"])
+        if drop_fn is not None:
+            msgs = drop_fn(k, msgs)
     return stats

@@ -79,3 +79,14 @@ def test_bench_runs(gpu):
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["value"] > 0 and line["escalations"] == 0
     assert line["roofline"]["achieved"] > 0
+
+
+def test_gpu_config3_read_index_quiesced(gpu):
+    """BASELINE config 3 shape on the GPU (R=5, slots=5 kernels)."""
+    R, G = 5, 1000
+    peers, active = P.config3(G, R)
+    topo = P.Topology(G, R)
+    rng = np.random.default_rng(33)
+    st = SIM.simulate(SIM.GpuBackend, peers, topo, 8, lambda k: P.config3_locals(G, R, active, k),
+                      slots=R, drop_fn=lambda k, m: P.drop_acks(m, 0.1, rng))
+    assert st["ready"] > 0

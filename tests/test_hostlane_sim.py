@@ -63,3 +63,31 @@ def test_wide_terms_escalate(built):
     st = _run(32, 5, seed=4, term_lo=2**32 - 1, term_hi=2**32 + 2)
     assert st["esc_reasons"].get("wide_term", 0) > 0
     assert st["commits"] > 0  # groups whose terms still fit keep committing on the device
+
+
+def _config3(backend, G, passes):
+    R = 5
+    peers, active = P.config3(G, R)
+    topo = P.Topology(G, R)
+    rng = np.random.default_rng(33)
+    return SIM.simulate(backend, peers, topo, passes, lambda k: P.config3_locals(G, R, active, k),
+                        slots=R, drop_fn=lambda k, m: P.drop_acks(m, 0.1, rng))
+
+
+def test_config3_read_index_quiesced(built):
+    """BASELINE config 3 shape (R=5): 90% quiesced groups (QuiescedTick only, the
+    lean lane), 10% active with a ReadIndex per pass, heartbeat acks dropped
+    with p=0.1, checkQuorum on half: bit-exact vs the oracle every pass."""
+    from oracle.pyoracle import hostlane_counters
+    f0, _ = hostlane_counters()
+    st = _config3(SIM.HostlaneBackend, 300, 10)
+    f1, _ = hostlane_counters()
+    assert st["ready"] > 0  # ReadIndex confirmations reached ReadyToRead
+    assert f1 - f0 > 0.8 * 300 * 5 * 10 * 0.9 * 0.9  # quiesced lanes stay on the lean lane
+
+
+def test_config1_single_group(built):
+    """BASELINE config 1 shape: one group x 3 replicas, one 1-entry proposal per
+    pass for 300 passes, committed traced against the oracle every pass."""
+    st = _run(1, 300, seed=1)
+    assert st["escalations"] == 0 and st["commits"] >= 290 * 3 - 10
