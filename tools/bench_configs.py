@@ -1,0 +1,113 @@
+"""Per-config measurements beside the headline bench (BASELINE.json configs 2, 3, 5)
+on one GPU, device-resident path (gr_step_device + mailbox spaces in HBM).
+
+Each pass's host work (new local inputs, config 5's injected leader changes and
+reloads) happens outside the timed region; the reported time is the sum of the
+two kernels' HIP-event durations per pass (gr_timing), i.e. the device pass.
+
+  config 2: 10k groups x 3, one 1-entry proposal per leader per pass
+  config 3: 100k groups x 5, 90% quiesced (QuiescedTick), 10% active: a Tick per
+            replica and a ReadIndex on the leader per pass (all acks delivered:
+            the device path has no drop filter)
+  config 5: 100k groups x 3, one proposal per leader per pass, and with p = 0.1
+            per group per pass an injected leader change with a divergent
+            suffix of 1..8 entries on the old leader (populations.inject_leader_change)
+Escalated lanes are counted; the host replay of escalations is not part of
+this device measurement (config 5 reloads the changed groups each pass).
+
+Usage: python tools/bench_configs.py [--passes N] > gpurun_out/configs.json
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def run(name, peers, G, R, passes, warmup, prepare):
+    """prepare(k, eng, n_peers) -> local inputs of pass k (may also reload groups)."""
+    import torch
+    from dragonboat_amd.engine import Engine
+    from dragonboat_amd.exchange import Exchange
+
+    S = R
+    ex = Exchange(G, R, S, 1, 0, "local")
+    eng = Engine(ex.n_peers, S)
+    eng.load(peers)
+    eng.bind_routes(ex.in_pos, ex.out_pos)
+    spaces = ex.allocate(eng, torch.device("cuda", 0))
+    stream = torch.cuda.current_stream()
+    fast = gen = 0.0
+    bailed = 0
+    t_host = 0.0
+    for k in range(warmup + passes):
+        if k == warmup:
+            torch.cuda.synchronize()
+            eng.reset_stats()
+        th = time.perf_counter()
+        eng.set_locals(prepare(k, eng, ex.n_peers))
+        t_host += time.perf_counter() - th
+        if k >= warmup:
+            eng.timing_begin()
+        ex.step(eng, spaces, k, stream)
+        if k >= warmup:
+            tm = eng.timing_end()
+            fast += tm["fast_ms"]
+            gen += tm["general_ms"]
+            bailed += tm["bailed_lanes"]
+    st = eng.stats()
+    ms = (fast + gen) / passes
+    out = {"config": name, "groups": G, "replicas": R, "passes": passes,
+           "device_ms_per_pass": ms, "fast_ms": fast / passes, "general_ms": gen / passes,
+           "bailed_lanes_per_pass": bailed / passes, "lanes": ex.n_peers,
+           "lanes_per_s": ex.n_peers / (ms * 1e-3),
+           "leader_commits_per_s": st["leader_commits"] / (passes * ms * 1e-3),
+           "escalations_per_pass": st["escalations"] / passes,
+           "msgs_in_per_pass": st["msgs_in"] / passes, "host_s": t_host}
+    eng.close()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--passes", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--only", default="2,3,5")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    torch.cuda.set_device(0)
+    from dragonboat_amd import populations as P
+    res = []
+    want = set(args.only.split(","))
+    if "2" in want:
+        G, R = 10_000, 3
+        peers = P.make_groups(G, R, seed=2)
+        res.append(run("2: 10k x 3, uniform proposals", peers, G, R, args.passes, args.warmup,
+                       lambda k, eng, n: P.propose_locals(n, np.arange(G), pass_index=k)))
+    if "3" in want:
+        G, R = 100_000, 5
+        peers, active = P.config3(G, R)
+        res.append(run("3: 100k x 5, 90% quiesced, ReadIndex + ticks", peers, G, R, args.passes,
+                       args.warmup, lambda k, eng, n: P.config3_locals(G, R, active, k)))
+    if "5" in want:
+        G, R = 100_000, 3
+        peers = P.make_groups(G, R, seed=5)
+        topo = P.Topology(G, R)
+        rng = np.random.default_rng(5)
+
+        def prepare5(k, eng, n):
+            cur = eng.sync(n)
+            if k >= args.warmup and len(P.inject_leader_change(cur, topo, 0.1, rng)):
+                eng.load(cur)  # host-side fault injection, reloaded before the pass
+            return P.propose_locals(n, P.current_leaders(cur, topo), pass_index=k)
+        res.append(run("5: 100k x 3, leader churn p=0.1", peers, G, R, args.passes, args.warmup, prepare5))
+    for r in res:
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
