@@ -221,7 +221,7 @@ struct SpaceView {
 enum StatField : uint32_t {
   ST_PASSES = 0, ST_LEADER_COMMITS = 1, ST_FOLLOWER_COMMITS = 2, ST_ESCALATIONS = 3,
   ST_MSGS_IN = 4, ST_MSGS_OUT = 5, ST_LEADER_MSGS_IN = 6, ST_LEADER_MSGS_OUT = 7,
-  ST_REPLICATE_ENTRIES = 8, NSTAT = 16
+  ST_REPLICATE_ENTRIES = 8, ST_BAILED = 9, NSTAT = 16
 };
 // Per-lane counters of one pass (reduced per workgroup into the stats rows).
 // "leader" = the lane ended the pass as leader; entries = sum of n over the
@@ -229,6 +229,7 @@ enum StatField : uint32_t {
 struct LaneStats {
   uint32_t leader_commit = 0, follower_commit = 0, escalated = 0;
   uint32_t msgs_in = 0, msgs_out = 0, leader_in = 0, leader_out = 0, entries = 0;
+  uint32_t bailed = 0;  // stepped by the general kernel
 };
 
 // Route modes: where lane i reads (dir 0) / writes (dir 1) the mailbox of
