@@ -55,19 +55,20 @@ __device__ inline void block_stats(const StepParams& kp, const LaneStats& ls) {
 }
 
 // Pass 1: every lane runs the lean steady-state lane (gr_fast.h). Lanes that
-// meet anything else store no state and are handed to pass 2 through this
-// workgroup's own region of the bail list: bail_list[b*kBlock + k], k <
-// bail_count[b], ascending within the block. No global atomics: a single
-// shared counter serialised every workgroup of a population whose waves all
-// carry a few bailing lanes (measured: 105 us vs the lanes' own ~20 us).
+// meet anything else store no state and are appended to one of kBailLists
+// lists (list = workgroup % kBailLists, one returning atomic per wave with a
+// bailing lane, a wave's lanes contiguous and ascending). Spreading the
+// appends over 16 counters 256 B apart keeps them from serialising when every
+// wave bails a few lanes (one shared counter: 105 us instead of 37 us on
+// config 3); no barrier, so waves of steady-state populations retire freely.
+constexpr uint32_t kBailLists = 16, kCounterStride = 64;  // counters 256 B apart
+
 template <int S>
 #ifndef GR_FAST_MIN_WAVES
 #define GR_FAST_MIN_WAVES 1  // waves per SIMD the register allocation must allow (A/B builds)
 #endif
 __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
-                                                                             uint32_t* bail_count) {
-  constexpr int W = kBlock / 64;
-  __shared__ uint32_t wave_bails[W];
+                                                                             uint32_t* counters, uint32_t list_cap) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   LaneStats ls;
   bool bail = false;
@@ -76,35 +77,44 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
     bail = !fast_step<S>(kp, i, p, &ls);
     if (bail) ls = LaneStats();
   }
-  const uint64_t bm = __ballot(bail);  // (wave_bails below is per 64-lane wave)
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) wave_bails[wave] = (uint32_t)__popcll(bm);
-  __syncthreads();
-  uint32_t base = 0, total = 0;
-#pragma unroll
-  for (int w = 0; w < W; ++w) {
-    base += (uint32_t)w < wave ? wave_bails[w] : 0u;
-    total += wave_bails[w];
+  const uint64_t bm = __ballot(bail);
+  if (bm) {
+    const uint32_t list = blockIdx.x % kBailLists;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t first = (uint32_t)__ffsll((unsigned long long)bm) - 1;
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(counters + list * kCounterStride, (uint32_t)__popcll(bm));
+    base = __shfl(base, (int)first);
+    if (bail) bail_list[(uint64_t)list * list_cap + base + (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
   }
-  if (bail) bail_list[blockIdx.x * kBlock + base + (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
-  if (threadIdx.x == 0) bail_count[blockIdx.x] = total;
   if (kp.stats) block_stats(kp, ls);
 }
 
 // Pass 2: the general lane (every handler, escalation with prefix re-run)
-// over the bailed lanes only: workgroup g takes the regions of pass-1
-// workgroups g, g + gridDim.x, ...
+// over the bailed lanes only, grid-stride over the concatenated lists; also
+// clears the counters the next pass's fast kernel will use.
 template <int S>
 __global__ __launch_bounds__(kBlock) void gr_step_kernel(StepParams kp, const uint32_t* bail_list,
-                                                         const uint32_t* bail_count, uint32_t fast_blocks) {
+                                                         const uint32_t* counters, uint32_t* next_counters,
+                                                         uint32_t list_cap) {
+  uint32_t start[kBailLists + 1];
+  start[0] = 0;
+#pragma unroll
+  for (uint32_t l = 0; l < kBailLists; ++l) start[l + 1] = start[l] + counters[l * kCounterStride];
+  const uint32_t n = start[kBailLists];
+  if (blockIdx.x == 0 && threadIdx.x < kBailLists) next_counters[threadIdx.x * kCounterStride] = 0;
+  if (blockIdx.x * kBlock >= n) return;  // uniform per block: nothing to do, no stats row touched
   LaneStats acc;
-  bool any = false;
-  for (uint32_t b = blockIdx.x; b < fast_blocks; b += gridDim.x) {
-    const uint32_t n = bail_count[b];  // uniform per workgroup
-    if (n == 0) continue;
-    any = true;
-    if (threadIdx.x < n) {
-      const uint32_t i = bail_list[b * kBlock + threadIdx.x];
+  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    const uint32_t x = base + threadIdx.x;
+    if (x < n) {
+      uint32_t l = 0;
+#pragma unroll
+      for (uint32_t k = 1; k < kBailLists; ++k) l = x >= start[k] ? k : l;
+      uint32_t off = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kBailLists; ++k) off = (k == l) ? x - start[k] : off;
+      const uint32_t i = bail_list[(uint64_t)l * list_cap + off];
       const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
       Lane<S> L(kp, i, p);
       LaneStats ls;
@@ -120,7 +130,7 @@ __global__ __launch_bounds__(kBlock) void gr_step_kernel(StepParams kp, const ui
       acc.bailed += 1;
     }
   }
-  if (any && kp.stats) block_stats(kp, acc);  // `any` is uniform per workgroup
+  if (kp.stats) block_stats(kp, acc);
 }
 
 // The general kernel's grid: one 256-lane workgroup per CU fills the chip at
@@ -135,29 +145,31 @@ struct PassTiming {
 };
 
 template <int S>
-static hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* bail_count, hipStream_t s,
-                         const PassTiming* t) {
+static hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters, uint32_t list_cap,
+                         uint32_t parity, hipStream_t s, const PassTiming* t) {
   if (kp.n_lanes == 0) return hipSuccess;
   const uint32_t blocks = (kp.n_lanes + kBlock - 1) / kBlock;
+  uint32_t* cur = counters + (parity & 1) * kBailLists * kCounterStride;
+  uint32_t* nxt = counters + ((parity + 1) & 1) * kBailLists * kCounterStride;
   hipError_t err;
   if (t && (err = hipEventRecord(t->ev[0], s)) != hipSuccess) return err;
-  hipLaunchKernelGGL(gr_fast_kernel<S>, dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, bail_count);
+  hipLaunchKernelGGL(gr_fast_kernel<S>, dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
   if ((err = hipGetLastError()) != hipSuccess) return err;
   if (t && (err = hipEventRecord(t->ev[1], s)) != hipSuccess) return err;
   const uint32_t gblocks = blocks < kGeneralBlocks ? blocks : kGeneralBlocks;
   hipLaunchKernelGGL(gr_step_kernel<S>, dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list,
-                     (const uint32_t*)bail_count, blocks);
+                     (const uint32_t*)cur, nxt, list_cap);
   if ((err = hipGetLastError()) != hipSuccess) return err;
   if (t && (err = hipEventRecord(t->ev[2], s)) != hipSuccess) return err;
   return hipSuccess;
 }
 
-static hipError_t launch_slots(uint32_t S, const StepParams& kp, uint32_t* bail_list, uint32_t* bail_count,
-                               hipStream_t s, const PassTiming* t) {
+static hipError_t launch_slots(uint32_t S, const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
+                               uint32_t list_cap, uint32_t parity, hipStream_t s, const PassTiming* t) {
   switch (S) {
-    case 1: return launch<1>(kp, bail_list, bail_count, s, t);
-    case 3: return launch<3>(kp, bail_list, bail_count, s, t);
-    case 5: return launch<5>(kp, bail_list, bail_count, s, t);
+    case 1: return launch<1>(kp, bail_list, counters, list_cap, parity, s, t);
+    case 3: return launch<3>(kp, bail_list, counters, list_cap, parity, s, t);
+    case 5: return launch<5>(kp, bail_list, counters, list_cap, parity, s, t);
   }
   return hipErrorInvalidValue;
 }
@@ -184,8 +196,10 @@ struct gr_engine {
   LaneBase ln{};
   uint64_t* stats = nullptr;
   uint32_t stats_rows = 0;
-  uint32_t* bail = nullptr;  // [cap] bailed lanes by pass-1 workgroup, then [stats_rows] counts
-  uint64_t timing_bailed0 = 0;  // ST_BAILED when timing began
+  uint32_t* bail = nullptr;      // kBailLists lists of cap lanes each
+  uint32_t* counters = nullptr;  // [2 (pass parity)][kBailLists][kCounterStride]
+  uint64_t launches = 0;         // never reset: selects the live counter set
+  uint64_t timing_bailed0 = 0;   // ST_BAILED when timing began
   bool timing = false;
   std::vector<PassTiming> timings;  // one per pass while timing
   bool routes_bound = false;
@@ -432,7 +446,8 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
   void *ds = nullptr, *dl = nullptr;
   if (hipMalloc(&ds, sb) != hipSuccess || hipMalloc(&dl, lb) != hipSuccess ||
       hipMalloc((void**)&e->stats, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
-      hipMalloc((void**)&e->bail, ((size_t)e->cap + e->stats_rows) * 4) != hipSuccess ||
+      hipMalloc((void**)&e->bail, (size_t)kBailLists * e->cap * 4) != hipSuccess ||
+      hipMalloc((void**)&e->counters, 2 * kBailLists * kCounterStride * 4) != hipSuccess ||
       hipMalloc((void**)&e->route_base, 2 * GR_SMAX * GR_SMAX * 4) != hipSuccess) {
     if (ds) (void)hipFree(ds);
     if (dl) (void)hipFree(dl);
@@ -445,7 +460,7 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
   e->ln.base = (uint8_t*)dl;
   if (hipMemset(ds, 0, sb) != hipSuccess || hipMemset(dl, 0, lb) != hipSuccess ||
       hipMemset(e->stats, 0, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
-      hipMemset(e->bail + e->cap, 0, (size_t)e->stats_rows * 4) != hipSuccess ||
+      hipMemset(e->counters, 0, 2 * kBailLists * kCounterStride * 4) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     gr_destroy(e);
     return GR_EDEVICE;
@@ -461,6 +476,7 @@ void gr_destroy(gr_engine* e) {
   if (e->ln.base) (void)hipFree(e->ln.base);
   if (e->stats) (void)hipFree(e->stats);
   if (e->bail) (void)hipFree(e->bail);
+  if (e->counters) (void)hipFree(e->counters);
   if (e->route_base) (void)hipFree(e->route_base);
   free_timings(e);
   if (e->d_in) (void)hipFree(e->d_in);
@@ -566,7 +582,7 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
   kp.in = make_view(e->d_in, 1, pk.in_positions);
   kp.out = make_view(e->d_out, 1, pk.out_positions);
   kp.n_lanes = nl;
-  HIPCHK(launch_slots(S, kp, e->bail, e->bail + e->cap, s, next_timing(e)));
+  HIPCHK(launch_slots(S, kp, e->bail, e->counters, e->cap, (uint32_t)e->launches++, s, next_timing(e)));
   e->passes++;
   e->locals_set = false;    // the lane rows now hold this pass's compact locals
   e->routes_bound = false;  // and its compact routes
@@ -716,7 +732,8 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
   kp.in = make_view(in_space, in_chunks, in_positions);
   kp.out = make_view(out_space, out_chunks, out_positions);
   kp.n_lanes = n_peers;
-  HIPCHK(launch_slots(e->S, kp, e->bail, e->bail + e->cap, (hipStream_t)stream, next_timing(e)));
+  HIPCHK(launch_slots(e->S, kp, e->bail, e->counters, e->cap, (uint32_t)e->launches++, (hipStream_t)stream,
+                      next_timing(e)));
   e->passes++;
   return GR_OK;
 }
