@@ -25,19 +25,31 @@ constexpr int kBlock = 256;
 
 // Per-workgroup partial counters (no atomics on global memory): row b of the
 // stats block belongs to workgroup b of whichever kernel runs.
+__device__ inline uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
 __device__ inline void block_stats(const StepParams& kp, const LaneStats& ls) {
   constexpr int N = 9;
   __shared__ uint32_t red[N];
   if (threadIdx.x < N) red[threadIdx.x] = 0;
   __syncthreads();
-  uint32_t v[N] = {ls.leader_commit, ls.follower_commit, ls.escalated, ls.msgs_in,  ls.msgs_out,
-                   ls.leader_in,     ls.leader_out,      ls.entries,   ls.bailed};
-#pragma unroll
-  for (int f = 0; f < N; ++f)
-    for (int off = 32; off > 0; off >>= 1) v[f] += __shfl_xor(v[f], off);
+  // one named field at a time: a register array indexed in a loop was put in scratch
+  const uint32_t f0 = wave_sum(ls.leader_commit), f1 = wave_sum(ls.follower_commit),
+                 f2 = wave_sum(ls.escalated), f3 = wave_sum(ls.msgs_in), f4 = wave_sum(ls.msgs_out),
+                 f5 = wave_sum(ls.leader_in), f6 = wave_sum(ls.leader_out), f7 = wave_sum(ls.entries),
+                 f8 = wave_sum(ls.bailed);
   if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-    for (int f = 0; f < N; ++f) atomicAdd(&red[f], v[f]);
+    atomicAdd(&red[0], f0);
+    atomicAdd(&red[1], f1);
+    atomicAdd(&red[2], f2);
+    atomicAdd(&red[3], f3);
+    atomicAdd(&red[4], f4);
+    atomicAdd(&red[5], f5);
+    atomicAdd(&red[6], f6);
+    atomicAdd(&red[7], f7);
+    atomicAdd(&red[8], f8);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -74,8 +86,7 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
   bool bail = false;
   if (i < kp.n_lanes) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-    bail = !fast_step<S>(kp, i, p, &ls);
-    if (bail) ls = LaneStats();
+    bail = !fast_step<S>(kp, i, p, &ls);  // leaves ls zero when it bails
   }
   const uint64_t bm = __ballot(bail);
   if (bm) {

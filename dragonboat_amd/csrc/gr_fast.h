@@ -363,8 +363,7 @@ struct FastLane {
       for (int j = 0; j < S; ++j)
         if (gout[j] != NOPOS) kp.out.at(gout[j]).cnt() = 0;
       kp.ln.u8(LR_RFLAGS)[i] = 0;
-      *ls = LaneStats();
-      return true;
+      return true;  // *ls stays zero
     }
     GF_BAIL(!leader && state != GR_FOLLOWER);
     GF_BAIL(np && !leader);
