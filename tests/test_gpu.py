@@ -90,3 +90,53 @@ def test_gpu_config3_read_index_quiesced(gpu):
     st = SIM.simulate(SIM.GpuBackend, peers, topo, 8, lambda k: P.config3_locals(G, R, active, k),
                       slots=R, drop_fn=lambda k, m: P.drop_acks(m, 0.1, rng))
     assert st["ready"] > 0
+
+
+def test_full_size_properties(gpu):
+    """The bench population at full size (1M groups x 3, device-resident path, 8
+    passes): no escalation or hand-over, every group's commit and log advanced by
+    the same amounts, and a 64-group sample equal field by field to the oracle run
+    on the same records and inputs."""
+    import torch
+    from dragonboat_amd.engine import Engine
+    from dragonboat_amd.exchange import Exchange
+    from oracle.pyoracle import OraclePopulation
+    import parity
+    from dragonboat_amd import abi
+    G, R, S, K = 1_000_000, 3, 3, 8
+    ex = Exchange(G, R, S, 1, 0, "local")
+    n = ex.n_peers
+    eng = Engine(n, S)
+    eng.load(ex.peers)
+    eng.bind_routes(ex.in_pos, ex.out_pos)
+    eng.set_locals(P.propose_locals(n, ex.leader_slots, pass_index=0))
+    spaces = ex.allocate(eng, torch.device("cuda", 0))
+    stream = torch.cuda.current_stream()
+    for k in range(K):
+        ex.step(eng, spaces, k, stream)
+    torch.cuda.synchronize()
+    st = eng.stats()
+    assert st["escalations"] == 0
+    final = eng.sync(n)
+    eng.close()
+    hi0 = ex.peers["last_index"].astype(np.int64)
+    dc = final["committed"].astype(np.int64) - hi0
+    dl = final["last_index"].astype(np.int64) - hi0
+    for r in range(R):
+        blk = slice(r * G, (r + 1) * G)
+        assert np.all(dc[blk] == dc[r * G]), f"replica {r}: committed deltas differ"
+        assert np.all(dl[blk] == dl[r * G]), f"replica {r}: lastIndex deltas differ"
+    # leader: K proposals, commit two passes behind; followers one pass behind the leader
+    assert (dc[0], dl[0]) == (K - 2, K) and (dc[G], dl[G]) == (K - 3, K - 1)
+    # oracle on a 64-group sample of the same records (replica-major re-indexed)
+    g0 = 64
+    idx = np.concatenate([np.arange(r * G, r * G + g0) for r in range(R)])
+    sample = ex.peers[idx].copy()
+    pop = OraclePopulation(sample, S)
+    topo = P.Topology(g0, R)
+    msgs = np.zeros(0, abi.MESSAGE)
+    for k in range(K):
+        o = pop.step(msgs, P.propose_locals(R * g0, np.arange(g0), pass_index=0))
+        msgs = topo.route_messages(o["msgs"])
+    bad = parity.compare_states(final[idx], pop.export(), S)
+    assert not bad, bad[:3]
