@@ -521,7 +521,7 @@ int gr_space_encode(void* space_host, uint32_t n_chunks, uint32_t positions, con
     const uint32_t g = pos_of_msg[k];
     if (g / v.pc >= n_chunks || g % v.pc >= positions) return GR_ERANGE;
     const Mailbox mb = v.at(g);
-    const uint8_t c = mb.cnt();
+    const uint8_t c = mb.cnt() & MB_COUNT;
     if (c >= GR_C) return GR_ECAPACITY;
     encode_msg(mb, c, msgs[k]);
     mb.cnt() = (uint8_t)(c + 1);
@@ -538,7 +538,7 @@ int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t position
     for (uint32_t l = 0; l < positions; ++l) {
       const uint32_t g = c * v.pc + l;
       const Mailbox mb = v.at(g);
-      const uint32_t cnt = std::min<uint32_t>(mb.cnt(), GR_C);
+      const uint32_t cnt = std::min<uint32_t>(mb.cnt() & MB_COUNT, GR_C);
       for (uint32_t k = 0; k < cnt; ++k) {
         if (out && n < cap) {
           out[n] = decode_msg(mb, k);

@@ -54,6 +54,8 @@ struct FastLane {
   // emission
   uint32_t gout[S];
   uint32_t outc[S];
+  uint32_t outnc = 0;    // out mailboxes holding a message that is not compact (MB_ALLCOMPACT)
+  bool resp_nc = false;  // a reject (carries Hint) went out
   uint32_t nmo = 0, nmi = 0, nent = 0;
   // results
   uint64_t append_from = 0;
@@ -91,15 +93,21 @@ struct FastLane {
     const uint32_t c = outc[j];
     uint32_t cd;
     const bool narrow = commit_delta(committed, log_index, &cd);
+    const bool compact = narrow && log_term == term && (n == 0 || rt0 == term);  // n <= 1 here
+    uint32_t fl = (n ? (1u << MFL_RUNS_SHIFT) : 0u) | (narrow ? 0u : MFL_WIDE_COMMIT);
+    if (compact) fl |= MFL_COMPACT | (n ? MFL_N1 : 0u);
+    else outnc |= 1u << j;
     mb.type(c) = GR_REPLICATE;
-    mb.flags(c) = (uint8_t)((n ? (1u << MFL_RUNS_SHIFT) : 0u) | (narrow ? 0u : MFL_WIDE_COMMIT));
+    mb.flags(c) = (uint8_t)fl;
     mb.t32(c, MT_TERM) = (uint32_t)(term);
-    mb.n(c) = n;
     mb.u64(c, MF_LOG_INDEX) = log_index;
-    mb.t32(c, MT_LOG_TERM) = (uint32_t)(log_term);
     if (narrow) mb.t32(c, MT_CDELTA) = cd;
     else mb.u64(c, MF_COMMIT) = committed;
-    if (n) mb.t32(c, MT_RT0) = (uint32_t)(rt0);
+    if (!compact) {
+      mb.n(c) = n;
+      mb.t32(c, MT_LOG_TERM) = (uint32_t)(log_term);
+      if (n) mb.t32(c, MT_RT0) = (uint32_t)(rt0);
+    }
     outc[j] = c + 1;
     nmo++;
   }
@@ -114,7 +122,10 @@ struct FastLane {
     mb.flags(c) = (uint8_t)(reject ? MFL_REJECT : 0u);
     mb.t32(c, MT_TERM) = (uint32_t)(term);
     mb.u64(c, MF_LOG_INDEX) = log_index;
-    if (reject) mb.u64(c, MF_HINT) = hint;
+    if (reject) {
+      mb.u64(c, MF_HINT) = hint;
+      resp_nc = true;
+    }
     *cnt = c + 1;
     nmo++;
   }
@@ -269,8 +280,13 @@ struct FastLane {
     }
     // ---- round 2: mailbox counts, newest run, leader remotes
     uint32_t cnt[S];
+    uint32_t allc = 0;  // in mailboxes whose messages are all compact (MB_ALLCOMPACT)
 #pragma unroll
-    for (int j = 0; j < S; ++j) cnt[j] = gin[j] != NOPOS ? (uint32_t)kp.in.at(gin[j]).cnt() : 0u;
+    for (int j = 0; j < S; ++j) {
+      const uint32_t b = gin[j] != NOPOS ? (uint32_t)kp.in.at(gin[j]).cnt() : 0u;
+      cnt[j] = b & MB_COUNT;
+      allc |= (b & MB_ALLCOMPACT) ? (1u << j) : 0u;
+    }
     if (nruns) {
       rsn = s64(SR_RUN_START + nruns - 1);
       rtn = s64(SR_RUN_TERM + nruns - 1);
@@ -295,7 +311,7 @@ struct FastLane {
     uint32_t lh[S][MK], lterm[S][MK];
     uint64_t lidx[S][MK];
     // follower: Replicate fields from the one slot L that sent, + its node id
-    uint32_t L = 0, nsrc = 0, c = 0, gl = 0, go = NOPOS;
+    uint32_t L = 0, nsrc = 0, c = 0, gl = 0, go = NOPOS, lc = 0;
     uint32_t fh[MK], fn[MK], fterm[MK], flt[MK], frt0[MK], fcd[MK];
     uint64_t fidx[MK];
     uint64_t rid = 0;
@@ -323,6 +339,7 @@ struct FastLane {
           c = cnt[j];
           gl = gin[j];
           go = gout[j];
+          lc = (allc >> j) & 1u;
           nsrc++;
         }
       }
@@ -333,12 +350,14 @@ struct FastLane {
         if ((uint32_t)k < cc) {
           const Mailbox mb = kp.in.at(gl);
           fh[k] = (uint32_t)mb.type(k) | ((uint32_t)mb.flags(k) << 8);
-          fn[k] = mb.n(k);
           fterm[k] = mb.t32(k, MT_TERM);
           fidx[k] = mb.u64(k, MF_LOG_INDEX);
-          flt[k] = mb.t32(k, MT_LOG_TERM);
           fcd[k] = mb.t32(k, MT_CDELTA);
-          frt0[k] = mb.t32(k, MT_RT0);
+          if (!lc) {  // a compact mailbox carries none of these
+            fn[k] = mb.n(k);
+            flt[k] = mb.t32(k, MT_LOG_TERM);
+            frt0[k] = mb.t32(k, MT_RT0);
+          }
         }
       }
       // electionTick = 0 and leaderID = remote_id(L) are usually already so
@@ -399,6 +418,11 @@ struct FastLane {
         if ((uint32_t)k < c) {
           GF_BAIL((fh[k] & 0xFFu) != GR_REPLICATE || (uint64_t)fterm[k] != term);
           GF_BAIL(fh[k] & ((uint32_t)MFL_WIDE_COMMIT << 8));
+          if (fh[k] & ((uint32_t)MFL_COMPACT << 8)) {  // LogTerm = Term, <= 1 entry at Term
+            fn[k] = (fh[k] & ((uint32_t)MFL_N1 << 8)) ? 1u : 0u;
+            flt[k] = fterm[k];
+            frt0[k] = fterm[k];
+          }
           const uint32_t nr = (fh[k] >> (8 + MFL_RUNS_SHIFT)) & 3u;
           GF_BAIL(fn[k] != 0 && nr != 1);
         }
@@ -413,6 +437,7 @@ struct FastLane {
       }
 #pragma unroll
       for (int j = 0; j < S; ++j) outc[j] = ((uint32_t)j == L) ? oc : 0u;
+      if (resp_nc) outnc |= 1u << L;
     }
     if (!ok) return false;
     // ---- stores (nothing above this line has written state)
@@ -452,7 +477,8 @@ struct FastLane {
     }
 #pragma unroll
     for (int j = 0; j < S; ++j)
-      if (gout[j] != NOPOS) kp.out.at(gout[j]).cnt() = (uint8_t)outc[j];
+      if (gout[j] != NOPOS)
+        kp.out.at(gout[j]).cnt() = (uint8_t)(outc[j] | (((outnc >> j) & 1u) ? 0u : MB_ALLCOMPACT));
     uint8_t rf = 0;
     if (prop_result) {  // propose_first = last_index - n + 1 (gr_layout.h)
       rf |= RF_PROPOSE;

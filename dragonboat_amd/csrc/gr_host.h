@@ -157,6 +157,15 @@ inline gr_message decode_msg(const Mailbox& mb, uint32_t k) {
   m.term = (uint64_t)mb.t32(k, MT_TERM);
   switch (m.type) {
     case GR_REPLICATE:
+      if (fl & MFL_COMPACT) {  // gr_layout.h: LogTerm = Term, <= 1 entry at Term, narrow Commit
+        m.log_index = mb.u64(k, MF_LOG_INDEX);
+        m.n_entries = (fl & MFL_N1) ? 1u : 0u;
+        m.n_runs = m.n_entries ? 1u : 0u;
+        m.log_term = m.term;
+        m.commit = commit_of(mb.t32(k, MT_CDELTA), m.log_index);
+        if (m.n_entries) m.run_term[0] = m.term;
+        break;
+      }
       m.n_entries = mb.n(k);
       m.log_index = mb.u64(k, MF_LOG_INDEX);
       m.log_term = (uint64_t)mb.t32(k, MT_LOG_TERM);
@@ -288,7 +297,7 @@ inline void decode_outbox(const void* space, const PackedInbox& pk, uint32_t S, 
   for (uint32_t l = 0; l < nl; ++l) {
     for (uint32_t j = 0; j < S; ++j) {
       const Mailbox mb = v.at(j * nl + l);
-      const uint32_t c = std::min<uint32_t>(mb.cnt(), GR_C);
+      const uint32_t c = std::min<uint32_t>(mb.cnt() & MB_COUNT, GR_C);
       for (uint32_t k = 0; k < c; ++k) {
         gr_message m = decode_msg(mb, k);
         m.peer = pk.peers[l];

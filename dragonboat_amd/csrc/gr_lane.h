@@ -1021,8 +1021,15 @@ struct Lane {
     m.log_index = 0; m.log_term = 0; m.commit = 0; m.hint = 0; m.hint_high = 0; m.rt0 = 0; m.rt1 = 0;
     switch (m.type) {
       case GR_REPLICATE:
-        m.n = mb.n(k);
         m.log_index = mb.u64(k, MF_LOG_INDEX);
+        if (m.flags & MFL_COMPACT) {  // LogTerm = Term, <= 1 entry at Term, narrow Commit
+          m.n = (m.flags & MFL_N1) ? 1u : 0u;
+          m.log_term = m.term;
+          m.commit = commit_of(mb.t32(k, MT_CDELTA), m.log_index);
+          m.rt0 = m.n ? m.term : 0;
+          break;
+        }
+        m.n = mb.n(k);
         m.log_term = (uint64_t)mb.t32(k, MT_LOG_TERM);
         m.commit = (m.flags & MFL_WIDE_COMMIT) ? mb.u64(k, MF_COMMIT)
                                                : commit_of(mb.t32(k, MT_CDELTA), m.log_index);
@@ -1251,7 +1258,7 @@ struct Lane {
       const uint32_t g = in_gpos(j);
       if (g == NOPOS) continue;
       const Mailbox mb = kp.in.at(g);
-      const uint32_t c = mb.cnt();
+      const uint32_t c = mb.cnt() & MB_COUNT;
 #pragma unroll 1
       for (uint32_t k = 0; k < c; ++k) {
         if (item == limit) { *at = item; return 0; }

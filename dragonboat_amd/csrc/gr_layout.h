@@ -150,6 +150,15 @@ enum T32Field : uint32_t { MT_TERM = 0, MT_LOG_TERM = 1, MT_RT0 = 2, MT_RT1 = 3,
 constexpr uint8_t MFL_REJECT = 0x01;
 constexpr uint8_t MFL_RUNS_SHIFT = 1;     // bits 1..2: n_runs
 constexpr uint8_t MFL_WIDE_COMMIT = 0x08; // Replicate: Commit in MF_COMMIT (else MT_CDELTA)
+// Compact Replicate (the steady state): LogTerm == Term, at most one entry,
+// whose term is Term, narrow Commit. Only type, flags, Term, LogIndex and the
+// Commit offset are written; MFL_N1 gives the entry count (0 or 1).
+constexpr uint8_t MFL_COMPACT = 0x10;
+constexpr uint8_t MFL_N1 = 0x20;
+// The mailbox count byte: bits 0-2 the count (GR_C + 1 marks an overflowed
+// host-encoded mailbox), bit 3 set when every message in it is a compact
+// Replicate or a non-reject ReplicateResp, so a reader can skip the other fields.
+constexpr uint8_t MB_COUNT = 0x07, MB_ALLCOMPACT = 0x08;
 // A Replicate's Commit travels as a 32-bit offset from its LogIndex when
 // |Commit - LogIndex| < 2^31 (always, unless a follower lags by 2^31 entries);
 // otherwise in full with MFL_WIDE_COMMIT. Both decode exactly.
