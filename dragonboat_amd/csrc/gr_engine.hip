@@ -214,8 +214,8 @@ struct gr_engine {
   bool timing = false;
   std::vector<PassTiming> timings;  // one per pass while timing
   bool routes_bound = false;
-  uint8_t route_mode = RT_TABLE;  // of the bound routes (RT_TABLE or RT_AFFINE)
-  uint32_t route_g = 0;
+  uint8_t route_mode = RT_TABLE;  // of the bound routes (RT_TABLE, RT_AFFINE or RT_LOOPBACK)
+  uint32_t route_g = 0, route_r = 0;
   uint32_t* route_base = nullptr;  // device [2][GR_SMAX][GR_SMAX]
   bool locals_set = false;
   uint64_t passes = 0;
@@ -696,11 +696,12 @@ int gr_bind_routes(gr_engine* e, const uint32_t* in_pos, const uint32_t* out_pos
   if (!e || !in_pos || !out_pos || n_peers > e->cfg.max_peers) return GR_EINVAL;
   HIPCHK(hipDeviceSynchronize());
   std::vector<uint32_t> base(2 * GR_SMAX * GR_SMAX, NOPOS);
-  uint32_t g = 0;
-  if (detect_affine_routes(in_pos, out_pos, n_peers, e->S, base.data(), &g)) {
+  uint32_t g = 0, rr = 0;
+  if (detect_affine_routes(in_pos, out_pos, n_peers, e->S, base.data(), &g, &rr)) {
     HIPCHK(hipMemcpy(e->route_base, base.data(), base.size() * 4, hipMemcpyHostToDevice));
-    e->route_mode = RT_AFFINE;
+    e->route_mode = is_loopback(base.data(), g, rr, e->S) ? RT_LOOPBACK : RT_AFFINE;
     e->route_g = g;
+    e->route_r = rr;
   } else {
     e->route_mode = RT_TABLE;
     e->route_g = 0;
@@ -739,6 +740,7 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
   kp.has_lane_peer = 0;
   kp.route_mode = e->routes_bound ? e->route_mode : RT_IDENTITY;
   kp.route_g = e->route_g;
+  kp.route_r = e->route_r;
   kp.route_base = e->route_base;
   kp.in = make_view(in_space, in_chunks, in_positions);
   kp.out = make_view(out_space, out_chunks, out_positions);

@@ -313,7 +313,7 @@ inline void decode_outbox(const void* space, const PackedInbox& pk, uint32_t S, 
 // RT_AFFINE: the kernel computes positions instead of reading 8*S bytes of
 // tables per lane. Tries each replica count R <= S that divides n.
 inline bool detect_affine_routes(const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n, uint32_t S,
-                                 uint32_t* base /* [2][GR_SMAX][GR_SMAX] */, uint32_t* g_out) {
+                                 uint32_t* base /* [2][GR_SMAX][GR_SMAX] */, uint32_t* g_out, uint32_t* r_out) {
   if (n == 0) return false;
   for (uint32_t R = 1; R <= S && R <= GR_SMAX; ++R) {
     if (n % R) continue;
@@ -336,10 +336,25 @@ inline bool detect_affine_routes(const uint32_t* in_pos, const uint32_t* out_pos
     }
     if (ok) {
       *g_out = G;
+      *r_out = R;
       return true;
     }
   }
   return false;
+}
+
+// An affine route table that is exactly the replica-major loopback (RT_LOOPBACK).
+inline bool is_loopback(const uint32_t* base, uint32_t G, uint32_t R, uint32_t S) {
+  const uint64_t n = (uint64_t)R * G;
+  for (uint32_t r = 0; r < R; ++r)
+    for (uint32_t j = 0; j < S; ++j) {
+      const bool none = j == r || j >= R;
+      const uint64_t bi = none ? NOPOS : j * n + (uint64_t)r * G;
+      const uint64_t bo = none ? NOPOS : r * n + (uint64_t)j * G;
+      if (base[(0 * GR_SMAX + r) * GR_SMAX + j] != bi || base[(1 * GR_SMAX + r) * GR_SMAX + j] != bo)
+        return false;
+    }
+  return true;
 }
 
 // Local-input rows of a lane block (host copies).

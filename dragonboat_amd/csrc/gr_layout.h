@@ -248,7 +248,11 @@ struct LaneStats {
 //   RT_AFFINE:   replica-major populations (lane i = r*G + g): base[dir][r][j] + g,
 //                base NOPOS = no mailbox. Detected by gr_bind_routes from the
 //                tables; saves the 8*S bytes of route reads per lane.
-constexpr uint8_t RT_IDENTITY = 0, RT_TABLE = 1, RT_AFFINE = 2;
+//   RT_LOOPBACK: the one-space replica-major loopback (all replicas of a group in
+//                this engine, route_r blocks of route_g lanes): in = j*n + i,
+//                out = r*n + j*G + g, none when j == r or j >= route_r. No table
+//                load, so the mailbox counts load in the first round.
+constexpr uint8_t RT_IDENTITY = 0, RT_TABLE = 1, RT_AFFINE = 2, RT_LOOPBACK = 3;
 
 // Kernel argument (small, passed by value, lives in SGPRs).
 // Lane i steps peer lane_peer[i] (identity when has_lane_peer == 0).
@@ -260,7 +264,8 @@ struct StepParams {
   const uint32_t* route_base;  // RT_AFFINE: [2][GR_SMAX][GR_SMAX]
   uint64_t max_entry_size;
   uint32_t n_lanes;
-  uint32_t route_g;    // RT_AFFINE: groups per replica block
+  uint32_t route_g;    // RT_AFFINE / RT_LOOPBACK: groups per replica block
+  uint32_t route_r;    // RT_LOOPBACK: replica blocks
   uint8_t has_locals;
   uint8_t has_lane_peer;
   uint8_t route_mode;
@@ -270,6 +275,12 @@ struct StepParams {
 __host__ __device__ inline uint32_t route_of(const StepParams& kp, uint32_t dir, uint32_t j, uint32_t i) {
   if (kp.route_mode == RT_TABLE)
     return (dir ? kp.ln.out_pos() : kp.ln.in_pos())[(uint64_t)j * kp.ln.lcap + i];
+  if (kp.route_mode == RT_LOOPBACK) {
+    const uint32_t r = i / kp.route_g;
+    if (j == r || j >= kp.route_r) return NOPOS;
+    const uint32_t n = kp.route_r * kp.route_g;
+    return dir ? r * n + j * kp.route_g + (i - r * kp.route_g) : j * n + i;
+  }
   if (kp.route_mode == RT_AFFINE) {
     const uint32_t r = i / kp.route_g, g = i - r * kp.route_g;
     const uint32_t b = kp.route_base[(dir * GR_SMAX + r) * GR_SMAX + j];

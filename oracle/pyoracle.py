@@ -154,12 +154,12 @@ def hostlane_counters():
 
 
 def hostlane_affine_routes(in_pos, out_pos, slots):
-    """gr_bind_routes' affine detection (test-only host build): (base [2][8][8], G) or None."""
+    """gr_bind_routes' route detection (test-only host build): (base [2][8][8], G, mode) or None."""
     lib = hostlane_lib()
     in_pos = np.ascontiguousarray(in_pos, np.uint32)
     out_pos = np.ascontiguousarray(out_pos, np.uint32)
     base = np.zeros((2, abi.GR_SMAX, abi.GR_SMAX), np.uint32)
     g = ctypes.c_uint32()
-    ok = lib.hl_detect_affine(in_pos.ctypes.data, out_pos.ctypes.data, in_pos.shape[1], slots,
-                              base.ctypes.data, ctypes.byref(g))
-    return (base, g.value) if ok else None
+    mode = lib.hl_detect_affine(in_pos.ctypes.data, out_pos.ctypes.data, in_pos.shape[1], slots,
+                                base.ctypes.data, ctypes.byref(g))
+    return (base, g.value, "loopback" if mode == 2 else "affine") if mode else None

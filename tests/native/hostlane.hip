@@ -146,5 +146,7 @@ extern "C" void hl_counters(uint64_t* fast, uint64_t* bailed) {
 extern "C" int hl_detect_affine(const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n, uint32_t S,
                                 uint32_t* base, uint32_t* g) {
   for (uint32_t k = 0; k < 2 * GR_SMAX * GR_SMAX; ++k) base[k] = NOPOS;
-  return detect_affine_routes(in_pos, out_pos, n, S, base, g) ? 1 : 0;
+  uint32_t r = 0;
+  if (!detect_affine_routes(in_pos, out_pos, n, S, base, g, &r)) return 0;
+  return is_loopback(base, *g, r, S) ? 2 : 1;
 }

@@ -146,8 +146,9 @@ def test_routes_are_affine(built, placement, N, rank):
         in_pos, out_pos, _ = X.spread_routes(G, R, S, N, rank)
     got = hostlane_affine_routes(in_pos, out_pos, S)
     assert got is not None
-    base, g = got
+    base, g, mode = got
     assert g == G
+    assert mode == ("loopback" if placement == "local" else "affine")
     for d, t in enumerate((in_pos, out_pos)):
         for j in range(S):
             for r in range(R):
