@@ -18,6 +18,7 @@
 #include "gr_fast.h"
 #include "gr_host.h"
 #include "gr_lane.h"
+#include "gr_tick.h"
 
 namespace gr {
 
@@ -104,8 +105,11 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
 // Pass 2: the general lane (every handler, escalation with prefix re-run)
 // over the bailed lanes only, grid-stride over the concatenated lists; also
 // clears the counters the next pass's fast kernel will use.
+#ifndef GR_GENERAL_MIN_WAVES
+#define GR_GENERAL_MIN_WAVES 1  // A/B builds: waves per SIMD for the general kernel
+#endif
 template <int S>
-__global__ __launch_bounds__(kBlock) void gr_step_kernel(StepParams kp, const uint32_t* bail_list,
+__global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(StepParams kp, const uint32_t* bail_list,
                                                          const uint32_t* counters, uint32_t* next_counters,
                                                          uint32_t list_cap) {
   uint32_t start[kBailLists + 1];
@@ -127,9 +131,11 @@ __global__ __launch_bounds__(kBlock) void gr_step_kernel(StepParams kp, const ui
       for (uint32_t k = 0; k < kBailLists; ++k) off = (k == l) ? x - start[k] : off;
       const uint32_t i = bail_list[(uint64_t)l * list_cap + off];
       const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-      Lane<S> L(kp, i, p);
       LaneStats ls;
-      L.step(&ls);
+      if (!tick_step<S>(kp, i, p, &ls)) {  // heartbeat / ReadIndex / tick lanes, else the general lane
+        Lane<S> L(kp, i, p);
+        L.step(&ls);
+      }
       acc.leader_commit += ls.leader_commit;
       acc.follower_commit += ls.follower_commit;
       acc.escalated += ls.escalated;

@@ -1,0 +1,434 @@
+// gr_tick.h — the lean lane for heartbeat, ReadIndex and tick traffic: the
+// north-star's ReadIndex quorum-ack reduction and election/heartbeat tick
+// sweep, for lanes the steady-state lane (gr_fast.h) hands over.
+//
+//   follower: Heartbeats at the current term from one remote (raft.go:1365-1369,
+//             handleHeartbeatMessage :923-931: electionTick = 0, leaderID,
+//             commitTo(m.Commit), HeartbeatResp echoing the context), then
+//             Tick x n without reaching the randomized election timeout
+//             (nonLeaderTick :386-401);
+//   leader:   HeartbeatResps at the current term from caught-up remotes
+//             (handleLeaderHeartbeatResp :1229-1240 + readIndex.confirm,
+//             readindex.go:77-116: ack bit, popcount quorum test, prefix
+//             release into ReadyToRead), a local ReadIndex (handleLeaderReadIndex
+//             :1171-1203: readIndex.addRequest + broadcastHeartbeatMessageWithHint
+//             :575-587), then at most one Tick (leaderTick :403-429 with
+//             CheckQuorum :1117-1123, 262-271 and the heartbeat broadcast).
+// It restates that subset of the general lane (gr_lane.h) with compile-time
+// remote slots. Anything else (an election or step-down, a lagging remote, a
+// ReadIndex from another node, FIFO or mailbox capacity, other inputs) clears
+// `ok`; the lane then stores no state and the general lane steps it. It runs in
+// the general kernel, in front of the general lane, on the lanes pass 1 handed
+// over, so it costs the steady-state kernel nothing.
+#pragma once
+#include "gr_layout.h"
+
+namespace gr {
+
+#define GT_HD __host__ __device__ inline __attribute__((always_inline))
+#define GT_BAIL(c) (ok = ok && !(c))
+
+GT_HD uint32_t gt_popc8(uint32_t x) {
+  x &= 0xFFu;
+  x = x - ((x >> 1) & 0x55u);
+  x = (x & 0x33u) + ((x >> 2) & 0x33u);
+  return (x + (x >> 4)) & 0x0Fu;
+}
+
+template <int S>
+struct TickLane {
+  using Rw = Rows<S>;
+  static constexpr int MK = 2;  // messages per mailbox handled here
+
+  const StepParams& kp;
+  const uint32_t i, p;
+  bool ok = true;
+  uint32_t state = 0, self = 0, flags = 0, nruns = 0, nbyte = 0;
+  uint64_t term = 0, committed = 0, committed0 = 0, hi = 0, rsn = 0, rtn = 0;
+  uint64_t etick = 0, etick0 = 0;
+  // leader
+  uint64_t match[S];
+  uint32_t rst[S], ract[S], rkind[S], sdirty = 0;
+  uint64_t htick = 0, htick0 = 0, etimeout = 0, htimeout = 0;
+  uint32_t ric = 0, rifrom = 0, riack = 0;
+  uint64_t rii[GR_Q], rilo[GR_Q], rihi[GR_Q];
+  bool fifo_dirty = false;
+  uint32_t rtrc = 0;
+  uint64_t rdi[GR_Q], rdl[GR_Q], rdh[GR_Q];
+  // emission
+  uint32_t gout[S], outc[S];
+  uint32_t nmi = 0, nmo = 0;
+
+  GT_HD TickLane(const StepParams& k, uint32_t lane, uint32_t peer) : kp(k), i(lane), p(peer) {}
+  GT_HD uint64_t& s64(uint32_t row) const { return kp.st.u64(row)[p]; }
+  GT_HD uint8_t& s8(uint32_t row) const { return kp.st.u8(row)[p]; }
+
+  GT_HD void emit(int j, uint8_t type, uint64_t commit, uint64_t hint, uint64_t hint_high) {
+    GT_BAIL(gout[j] == NOPOS || outc[j] >= (uint32_t)GR_C || wide_term(term, 0, 0, 0));
+    if (!ok) return;
+    const Mailbox mb = kp.out.at(gout[j]);
+    const uint32_t c = outc[j];
+    mb.type(c) = type;
+    mb.flags(c) = 0;
+    mb.t32(c, MT_TERM) = (uint32_t)term;
+    if (type == GR_HEARTBEAT) mb.u64(c, MF_COMMIT) = commit;
+    mb.u64(c, MF_HINT) = hint;
+    mb.u64(c, MF_HINT_HIGH) = hint_high;
+    outc[j] = c + 1;
+    nmo++;
+  }
+  GT_HD int quorum() const {
+    int nv = 0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) nv += rkind[j] == GR_SLOT_VOTER;
+    return nv / 2 + 1;
+  }
+  GT_HD void add_ready(uint64_t index, uint64_t lo, uint64_t hi_) {  // raft.go:1163-1169
+    GT_BAIL(rtrc >= (uint32_t)GR_Q);
+    if (!ok) return;
+#pragma unroll
+    for (int q = 0; q < GR_Q; ++q) {
+      const bool hit = (uint32_t)q == rtrc;
+      rdi[q] = hit ? index : rdi[q];
+      rdl[q] = hit ? lo : rdl[q];
+      rdh[q] = hit ? hi_ : rdh[q];
+    }
+    rtrc++;
+  }
+  // broadcastHeartbeatMessageWithHint (raft.go:575-587)
+  GT_HD void broadcast_heartbeat(uint64_t clo, uint64_t chi) {
+#pragma unroll
+    for (int j = 0; j < S; ++j)
+      if (rkind[j] == GR_SLOT_VOTER && (uint32_t)j != self)
+        emit(j, GR_HEARTBEAT, match[j] < committed ? match[j] : committed, clo, chi);
+    if (clo == 0 && chi == 0) {
+#pragma unroll
+      for (int j = 0; j < S; ++j)
+        if (rkind[j] == GR_SLOT_OBSERVER) emit(j, GR_HEARTBEAT, match[j] < committed ? match[j] : committed, 0, 0);
+    }
+  }
+  // readIndex.confirm + handleReadIndexLeaderConfirmation (readindex.go:77-116, raft.go:1264-1284)
+  GT_HD void ri_confirm(uint64_t clo, uint64_t chi, uint32_t from) {
+    int pos = -1;
+#pragma unroll
+    for (int q = 0; q < GR_Q; ++q)
+      pos = (pos < 0 && (uint32_t)q < ric && rilo[q] == clo && rihi[q] == chi) ? q : pos;
+    if (pos < 0) return;
+    riack |= (1u << from) << (8 * pos);
+    fifo_dirty = true;
+    const uint32_t ack = (riack >> (8 * pos)) & 0xFFu;
+    if ((int)gt_popc8(ack) + 1 < quorum()) return;
+    uint64_t sidx = 0;
+#pragma unroll
+    for (int q = 0; q < GR_Q; ++q) sidx = (q == pos) ? rii[q] : sidx;
+#pragma unroll
+    for (int q = 0; q < GR_Q; ++q) {
+      if (q <= pos) {
+        GT_BAIL(rii[q] > sidx);  // panic in the reference
+        const uint32_t f = (rifrom >> (8 * q)) & 0xFFu;
+        GT_BAIL(f != GR_SLOT_NONE && f != self);  // ReadIndexResp to another node: general lane
+        add_ready(sidx, rilo[q], rihi[q]);
+      }
+    }
+    const uint32_t drop = (uint32_t)pos + 1;
+#pragma unroll
+    for (int q = 0; q < GR_Q; ++q) {  // queue = queue[done:]
+      uint64_t a = 0, b = 0, c = 0;
+#pragma unroll
+      for (int d = 1; d + q < GR_Q; ++d) {
+        const bool hit = (uint32_t)d == drop;
+        a = hit ? rii[q + d] : a;
+        b = hit ? rilo[q + d] : b;
+        c = hit ? rihi[q + d] : c;
+      }
+      rii[q] = a;
+      rilo[q] = b;
+      rihi[q] = c;
+    }
+    rifrom = drop >= 4 ? 0u : (rifrom >> (8 * drop));
+    riack = drop >= 4 ? 0u : (riack >> (8 * drop));
+    ric -= drop;
+  }
+  // handleLeaderHeartbeatResp (raft.go:1229-1240) for a caught-up remote
+  GT_HD void heartbeat_resp(int j, uint64_t clo, uint64_t chi) {
+    if (!ract[j]) {
+      ract[j] = 1;
+      sdirty |= 1u << j;
+    }
+    if (rst[j] == GR_WAIT) {  // waitToRetry
+      rst[j] = GR_RETRY;
+      sdirty |= 1u << j;
+    }
+    GT_BAIL(match[j] < hi);  // sendReplicateMessage: general lane
+    if (clo != 0) ri_confirm(clo, chi, (uint32_t)j);
+  }
+  // handleLeaderReadIndex (raft.go:1171-1203) for a local request (From = NoNode)
+  GT_HD void read_index(uint64_t clo, uint64_t chi) {
+    if (quorum() == 1) {  // single-voter cluster: ready at once
+      add_ready(committed, clo, chi);
+      return;
+    }
+    GT_BAIL(term == 0);
+    // hasCommittedEntryAtCurrentTerm: term(committed) from the newest run; with
+    // NR_GE_LO every index at or above it lies in [firstIndex-1, lastIndex]
+    GT_BAIL(!(nbyte & NR_GE_LO) || committed > hi || nruns == 0 || committed < rsn);
+    if (rtn != term) return;
+    bool dup = false;
+#pragma unroll
+    for (int q = 0; q < GR_Q; ++q) dup = dup || ((uint32_t)q < ric && rilo[q] == clo && rihi[q] == chi);
+    if (!dup) {  // readIndex.addRequest ignores a duplicate context
+      uint64_t last = 0;
+#pragma unroll
+      for (int q = 0; q < GR_Q; ++q) last = ((uint32_t)q + 1 == ric) ? rii[q] : last;
+      GT_BAIL(ric > 0 && committed < last);  // index moved backward: panic
+      GT_BAIL(ric >= (uint32_t)GR_Q);          // FIFO capacity
+      if (!ok) return;
+#pragma unroll
+      for (int q = 0; q < GR_Q; ++q) {
+        const bool hit = (uint32_t)q == ric;
+        rii[q] = hit ? committed : rii[q];
+        rilo[q] = hit ? clo : rilo[q];
+        rihi[q] = hit ? chi : rihi[q];
+      }
+      rifrom = (rifrom & ~(0xFFu << (8 * ric))) | ((uint32_t)GR_SLOT_NONE << (8 * ric));
+      riack &= ~(0xFFu << (8 * ric));
+      ric++;
+      fifo_dirty = true;
+    }
+    broadcast_heartbeat(clo, chi);  // also for a duplicate (raft.go:1200-1201)
+  }
+
+  GT_HD bool step(LaneStats* ls) {
+    // ---- round 1
+    state = s8(Rw::B_STATE);
+    self = s8(Rw::B_SELF);
+    flags = s8(Rw::B_FLAGS);
+    nbyte = s8(Rw::B_NRUNS);
+    nruns = nbyte & NR_MASK;
+    term = s64(SR_TERM);
+    committed = s64(SR_COMMITTED);
+    hi = s64(SR_LAST_INDEX);
+    uint32_t lf = 0, nt = 0, nq = 0, np = 0;
+    uint64_t rclo = 0, rchi = 0;
+    if (kp.has_locals) {
+      lf = kp.ln.u8(LR_LFLAGS)[i];
+      nt = kp.ln.u32(LR_TICKS)[i];
+      nq = kp.ln.u32(LR_QTICKS)[i];
+      np = kp.ln.u32(LR_PROPOSE)[i];
+      rclo = kp.ln.u64(LR_RI_LO)[i];
+      rchi = kp.ln.u64(LR_RI_HI)[i];
+    }
+    uint32_t gin[S], cnt[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      gin[j] = route_of(kp, 0, j, i);
+      gout[j] = route_of(kp, 1, j, i);
+      outc[j] = 0;
+      cnt[j] = gin[j] != NOPOS ? (uint32_t)(kp.in.at(gin[j]).cnt() & MB_COUNT) : 0u;
+    }
+    const bool leader = state == GR_LEADER;
+    GT_BAIL(!leader && state != GR_FOLLOWER);
+    GT_BAIL((lf & LF_PROPOSE_CC) || nq || np);
+    // ---- round 2
+    etick = s64(SR_ETICK);
+    uint64_t retimeout = 0;
+    if (nruns) {
+      rsn = s64(SR_RUN_START + nruns - 1);
+      rtn = s64(SR_RUN_TERM + nruns - 1);
+    }
+    uint32_t mh[S][MK];
+    uint64_t mterm[S][MK], mcom[S][MK], mlo[S][MK], mhi[S][MK];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+#pragma unroll
+      for (int k = 0; k < MK; ++k) {
+        mh[j][k] = 0; mterm[j][k] = 0; mcom[j][k] = 0; mlo[j][k] = 0; mhi[j][k] = 0;
+        if ((uint32_t)k < cnt[j]) {
+          const Mailbox mb = kp.in.at(gin[j]);
+          mh[j][k] = mb.type(k);
+          mterm[j][k] = mb.t32(k, MT_TERM);
+          if (!leader) mcom[j][k] = mb.u64(k, MF_COMMIT);
+          mlo[j][k] = mb.u64(k, MF_HINT);
+          mhi[j][k] = mb.u64(k, MF_HINT_HIGH);
+        }
+      }
+    }
+    if (leader) {
+      htick = s64(SR_HTICK);
+      etimeout = s64(SR_ETIMEOUT);
+      htimeout = s64(SR_HTIMEOUT);
+      ric = s8(Rw::B_RIC);
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        match[j] = s64(Rw::MATCH + j);
+        rst[j] = s8(Rw::B_RSTATE + j) & 3u;
+        ract[j] = s8(Rw::B_RACTIVE + j) & 1u;
+        rkind[j] = s8(Rw::B_RKIND + j) & 3u;
+      }
+#pragma unroll
+      for (int q = 0; q < GR_Q; ++q) {
+        rii[q] = s64(Rw::RI_INDEX + q);
+        rilo[q] = s64(Rw::RI_LO + q);
+        rihi[q] = s64(Rw::RI_HI + q);
+        rifrom |= (uint32_t)s8(Rw::B_RIFROM + q) << (8 * q);
+        riack |= (uint32_t)s8(Rw::B_RIACK + q) << (8 * q);
+      }
+    } else {
+      retimeout = s64(SR_RETIMEOUT);
+    }
+    committed0 = committed;
+    etick0 = etick;
+    htick0 = htick;
+    // ---- messages (node.handleReceivedMessages order: slot, then arrival)
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      GT_BAIL(cnt[j] > (uint32_t)MK);
+#pragma unroll
+      for (int k = 0; k < MK; ++k)
+        if ((uint32_t)k < cnt[j])
+          GT_BAIL(mterm[j][k] != term ||
+                  mh[j][k] != (uint32_t)(leader ? GR_HEARTBEAT_RESP : GR_HEARTBEAT));
+    }
+    uint32_t L = 0, nsrc = 0;
+    if (leader) {
+      GT_BAIL(flags & F_LTT);  // leader transfer
+      GT_BAIL(nt > 1);
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+#pragma unroll
+        for (int k = 0; k < MK; ++k) {
+          if ((uint32_t)k < cnt[j]) {
+            nmi++;
+            if (rkind[j] != GR_SLOT_EMPTY) heartbeat_resp(j, mlo[j][k], mhi[j][k]);
+          }
+        }
+      }
+      if (lf & LF_READ_INDEX) read_index(rclo, rchi);
+      if (nt) {  // leaderTick (raft.go:403-429)
+        etick++;
+        if (etick >= etimeout) {
+          etick = 0;
+          if (flags & GR_F_CHECK_QUORUM) {  // leaderHasQuorum (raft.go:262-271)
+            int c = 0;
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+              if (rkind[j] == GR_SLOT_VOTER && ((uint32_t)j == self || ract[j])) {
+                c++;
+                if (ract[j]) {
+                  ract[j] = 0;
+                  sdirty |= 1u << j;
+                }
+              }
+            }
+            GT_BAIL(c < quorum());  // step down: general lane
+          }
+        }
+        htick++;
+        if (htick >= htimeout) {
+          htick = 0;
+          uint64_t clo = 0, chi = 0;
+#pragma unroll
+          for (int q = 0; q < GR_Q; ++q) {
+            clo = ((uint32_t)q + 1 == ric) ? rilo[q] : clo;
+            chi = ((uint32_t)q + 1 == ric) ? rihi[q] : chi;
+          }
+          broadcast_heartbeat(clo, chi);
+        }
+      }
+    } else {
+      GT_BAIL(lf & LF_READ_INDEX);  // forwarded to the leader: general lane
+#pragma unroll
+      for (int j = 0; j < S; ++j)
+        if (cnt[j]) {
+          L = (uint32_t)j;
+          nsrc++;
+        }
+      GT_BAIL(nsrc > 1);
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+#pragma unroll
+        for (int k = 0; k < MK; ++k) {
+          if ((uint32_t)k < cnt[j]) {
+            nmi++;
+            etick = 0;
+            if (mcom[j][k] > committed) {  // commitTo (logentry.go:314-323)
+              GT_BAIL(mcom[j][k] > hi);
+              committed = mcom[j][k];
+            }
+            emit(j, GR_HEARTBEAT_RESP, 0, mlo[j][k], mhi[j][k]);
+          }
+        }
+      }
+      // nonLeaderTick x nt: an election timeout (or the selfRemoved test) goes to the general lane
+      GT_BAIL(nt > 0 && etick + nt >= retimeout);
+      etick += nt;
+    }
+    if (!ok) return false;
+    // ---- stores
+    if (committed != committed0) s64(SR_COMMITTED) = committed;
+    uint32_t nf = flags;
+    if (etick != etick0) {
+      s64(SR_ETICK) = etick;
+      nf = (nf & ~F_ETZ) | (etick == 0 ? F_ETZ : 0u);
+    }
+    if (!leader && nsrc && ((flags & F_LSLOT) >> F_LSLOT_SHIFT) != L + 1) {
+      s64(SR_LEADER_ID) = s64(Rw::RID + L);  // setLeaderID(m.From)
+      nf = (nf & ~F_LSLOT) | ((L + 1) << F_LSLOT_SHIFT);
+    }
+    if (nf != flags) s8(Rw::B_FLAGS) = (uint8_t)nf;
+    if (leader) {
+      if (htick != htick0) s64(SR_HTICK) = htick;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        if ((sdirty >> j) & 1u) {
+          s8(Rw::B_RSTATE + j) = (uint8_t)rst[j];
+          s8(Rw::B_RACTIVE + j) = (uint8_t)ract[j];
+        }
+      }
+      if (fifo_dirty) {
+        s8(Rw::B_RIC) = (uint8_t)ric;
+#pragma unroll
+        for (int q = 0; q < GR_Q; ++q) {
+          s64(Rw::RI_INDEX + q) = rii[q];
+          s64(Rw::RI_LO + q) = rilo[q];
+          s64(Rw::RI_HI + q) = rihi[q];
+          s8(Rw::B_RIFROM + q) = (uint8_t)(rifrom >> (8 * q));
+          s8(Rw::B_RIACK + q) = (uint8_t)(riack >> (8 * q));
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < S; ++j)
+      if (gout[j] != NOPOS) kp.out.at(gout[j]).cnt() = (uint8_t)outc[j];
+    uint8_t rf = 0;
+    if (rtrc) {
+      rf |= RF_READY;
+      kp.ln.u8(LR_RTR_COUNT)[i] = (uint8_t)rtrc;
+#pragma unroll
+      for (int q = 0; q < GR_Q; ++q) {
+        if ((uint32_t)q < rtrc) {
+          kp.ln.u64(LR_RTR_INDEX + q)[i] = rdi[q];
+          kp.ln.u64(LR_RTR_LO + q)[i] = rdl[q];
+          kp.ln.u64(LR_RTR_HI + q)[i] = rdh[q];
+        }
+      }
+    }
+    kp.ln.u8(LR_RFLAGS)[i] = rf;
+    const bool adv = committed > committed0;
+    ls->leader_commit = adv && leader;
+    ls->follower_commit = adv && !leader;
+    ls->msgs_in = nmi;
+    ls->msgs_out = nmo;
+    ls->leader_in = leader ? nmi : 0;
+    ls->leader_out = leader ? nmo : 0;
+    return true;
+  }
+};
+
+template <int S>
+GT_HD bool tick_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls) {
+  TickLane<S> L(kp, i, p);
+  return L.step(ls);
+}
+
+}  // namespace gr

@@ -11,13 +11,14 @@
 #include "gr_fast.h"
 #include "gr_host.h"
 #include "gr_lane.h"
+#include "gr_tick.h"
 
 using namespace gr;
 using namespace gr::host;
 
 namespace {
 
-static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0;
+static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0, g_tick_lanes = 0;
 
 template <int S>
 void run_lanes(const StepParams& kp) {
@@ -31,8 +32,12 @@ void run_lanes(const StepParams& kp) {
   }
   for (uint32_t i : bailed) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-    Lane<S> L(kp, i, p);
     LaneStats ls;
+    if (tick_step<S>(kp, i, p, &ls)) {
+      g_tick_lanes++;
+      continue;
+    }
+    Lane<S> L(kp, i, p);
     L.step(&ls);
   }
   g_fast_lanes += kp.n_lanes - bailed.size();
@@ -141,6 +146,9 @@ extern "C" void hl_counters(uint64_t* fast, uint64_t* bailed) {
   *fast = g_fast_lanes;
   *bailed = g_bailed_lanes;
 }
+
+// lanes the heartbeat/ReadIndex/tick lane finished (of the bailed ones)
+extern "C" uint64_t hl_tick_lanes() { return g_tick_lanes; }
 
 // gr_bind_routes' affine-route detection, for the CPU tests
 extern "C" int hl_detect_affine(const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n, uint32_t S,

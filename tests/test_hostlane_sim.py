@@ -78,12 +78,16 @@ def test_config3_read_index_quiesced(built):
     """BASELINE config 3 shape (R=5): 90% quiesced groups (QuiescedTick only, the
     lean lane), 10% active with a ReadIndex per pass, heartbeat acks dropped
     with p=0.1, checkQuorum on half: bit-exact vs the oracle every pass."""
-    from oracle.pyoracle import hostlane_counters
-    f0, _ = hostlane_counters()
+    from oracle.pyoracle import hostlane_counters, hostlane_tick_lanes
+    f0, b0 = hostlane_counters()
+    t0 = hostlane_tick_lanes()
     st = _config3(SIM.HostlaneBackend, 300, 10)
-    f1, _ = hostlane_counters()
+    f1, b1 = hostlane_counters()
+    t1 = hostlane_tick_lanes()
     assert st["ready"] > 0  # ReadIndex confirmations reached ReadyToRead
     assert f1 - f0 > 0.8 * 300 * 5 * 10 * 0.9 * 0.9  # quiesced lanes stay on the lean lane
+    # the active groups' heartbeat / ReadIndex / tick lanes mostly take the tick lane (gr_tick.h)
+    assert t1 - t0 > 0.6 * (b1 - b0), (t1 - t0, b1 - b0)
 
 
 def test_config1_single_group(built):

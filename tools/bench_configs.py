@@ -117,6 +117,7 @@ def main():
             return P.propose_locals(n, P.current_leaders(cur, topo), pass_index=k)
         res.append(run("5: 100k x 3, leader churn p=0.1", peers, G, R, args.passes, args.warmup, prepare5))
     for r in res:
+        r["lib"] = os.path.basename(os.environ.get("GPURAFT_LIB", "libgpuraft.so"))
         print(json.dumps(r), flush=True)
 
 
