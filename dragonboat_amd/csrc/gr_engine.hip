@@ -132,7 +132,10 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
       const uint32_t i = bail_list[(uint64_t)l * list_cap + off];
       const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
       LaneStats ls;
-      if (!tick_step<S>(kp, i, p, &ls)) {  // heartbeat / ReadIndex / tick lanes, else the general lane
+      // lanes with ticks or a ReadIndex (LW_OTHER) try the heartbeat/ReadIndex/tick
+      // lane first; the rest (and its hand-overs) take the general lane
+      const bool tickish = kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
+      if (!tickish || !tick_step<S>(kp, i, p, &ls)) {
         Lane<S> L(kp, i, p);
         L.step(&ls);
       }

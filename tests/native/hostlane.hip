@@ -33,7 +33,8 @@ void run_lanes(const StepParams& kp) {
   for (uint32_t i : bailed) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     LaneStats ls;
-    if (tick_step<S>(kp, i, p, &ls)) {
+    const bool tickish = kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
+    if (tickish && tick_step<S>(kp, i, p, &ls)) {
       g_tick_lanes++;
       continue;
     }
