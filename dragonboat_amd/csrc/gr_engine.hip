@@ -517,37 +517,40 @@ int gr_sync_groups_to_host(gr_engine* e, uint32_t first, gr_peer* out, size_t n)
   return transfer_state(e, first, n, out, false);
 }
 
-uint64_t gr_space_chunk_bytes(uint32_t positions) { return space_chunk_bytes_pc(space_pad_positions(positions)); }
-uint64_t gr_space_bytes(uint32_t n_chunks, uint32_t positions) {
-  return (uint64_t)n_chunks * gr_space_chunk_bytes(positions);
+uint64_t gr_space_chunk_bytes(uint32_t positions, uint32_t depth) {
+  if (depth == 0 || depth > GR_C) return 0;
+  return space_chunk_bytes_pc(space_pad_positions(positions), depth);
+}
+uint64_t gr_space_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth) {
+  return (uint64_t)n_chunks * gr_space_chunk_bytes(positions, depth);
 }
 
-int gr_space_encode(void* space_host, uint32_t n_chunks, uint32_t positions, const gr_message* msgs,
-                    size_t n, const uint32_t* pos_of_msg) {
-  if (!space_host || (n && (!msgs || !pos_of_msg))) return GR_EINVAL;
-  const SpaceView v = make_view(space_host, n_chunks, positions);
+int gr_space_encode(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
+                    const gr_message* msgs, size_t n, const uint32_t* pos_of_msg) {
+  if (!space_host || (n && (!msgs || !pos_of_msg)) || depth == 0 || depth > GR_C) return GR_EINVAL;
+  const SpaceView v = make_view(space_host, n_chunks, positions, depth);
   for (size_t k = 0; k < n; ++k) {
     const uint32_t g = pos_of_msg[k];
     if (g / v.pc >= n_chunks || g % v.pc >= positions) return GR_ERANGE;
     const Mailbox mb = v.at(g);
     const uint8_t c = mb.cnt() & MB_COUNT;
-    if (c >= GR_C) return GR_ECAPACITY;
+    if (c >= depth) return GR_ECAPACITY;
     encode_msg(mb, c, msgs[k]);
     mb.cnt() = (uint8_t)(c + 1);
   }
   return GR_OK;
 }
 
-int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t positions, gr_message* out,
-                    size_t cap, size_t* n_out) {
-  if (!space_host || !n_out) return GR_EINVAL;
-  const SpaceView v = make_view(space_host, n_chunks, positions);
+int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
+                    gr_message* out, size_t cap, size_t* n_out) {
+  if (!space_host || !n_out || depth == 0 || depth > GR_C) return GR_EINVAL;
+  const SpaceView v = make_view(space_host, n_chunks, positions, depth);
   size_t n = 0;
   for (uint32_t c = 0; c < n_chunks; ++c) {
     for (uint32_t l = 0; l < positions; ++l) {
       const uint32_t g = c * v.pc + l;
       const Mailbox mb = v.at(g);
-      const uint32_t cnt = std::min<uint32_t>(mb.cnt() & MB_COUNT, GR_C);
+      const uint32_t cnt = std::min<uint32_t>(mb.cnt() & MB_COUNT, depth);
       for (uint32_t k = 0; k < cnt; ++k) {
         if (out && n < cap) {
           out[n] = decode_msg(mb, k);
@@ -577,8 +580,8 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
   if (r) return r;
   const uint32_t nl = (uint32_t)pk.peers.size();
   if (nl == 0) return GR_OK;
-  const size_t in_bytes = gr_space_bytes(1, pk.in_positions);
-  const size_t out_bytes = gr_space_bytes(1, pk.out_positions);
+  const size_t in_bytes = gr_space_bytes(1, pk.in_positions, GR_C);
+  const size_t out_bytes = gr_space_bytes(1, pk.out_positions, GR_C);
   if ((r = grow_pinned(&e->h_in, &e->h_in_bytes, in_bytes))) return r;
   if ((r = grow_pinned(&e->h_out, &e->h_out_bytes, out_bytes))) return r;
   if ((r = grow_device(&e->d_in, &e->d_in_bytes, in_bytes))) return r;
@@ -741,9 +744,10 @@ int gr_set_locals(gr_engine* e, const gr_local_input* locals, size_t n) {
 }
 
 int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t in_chunks,
-                   uint32_t in_positions, uint32_t out_chunks, uint32_t out_positions, uint32_t n_peers,
-                   void* stream) {
-  if (!e || !in_space || !out_space || n_peers > e->cfg.max_peers) return GR_EINVAL;
+                   uint32_t in_positions, uint32_t out_chunks, uint32_t out_positions, uint32_t depth,
+                   uint32_t n_peers, void* stream) {
+  if (!e || !in_space || !out_space || n_peers > e->cfg.max_peers || depth == 0 || depth > GR_C)
+    return GR_EINVAL;
   StepParams kp = base_params(e);
   kp.has_locals = e->locals_set ? 1 : 0;
   kp.has_lane_peer = 0;
@@ -751,8 +755,8 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
   kp.route_g = e->route_g;
   kp.route_r = e->route_r;
   kp.route_base = e->route_base;
-  kp.in = make_view(in_space, in_chunks, in_positions);
-  kp.out = make_view(out_space, out_chunks, out_positions);
+  kp.in = make_view(in_space, in_chunks, in_positions, depth);
+  kp.out = make_view(out_space, out_chunks, out_positions, depth);
   kp.n_lanes = n_peers;
   HIPCHK(launch_slots(e->S, kp, e->bail, e->counters, e->cap, (uint32_t)e->launches++, (hipStream_t)stream,
                       next_timing(e)));

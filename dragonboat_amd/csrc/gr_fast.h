@@ -86,7 +86,7 @@ struct FastLane {
   }
   // raft.send (raft.go:457-461) of a Replicate into slot j.
   GF_HD void emit_replicate(int j, uint64_t log_index, uint64_t log_term, uint32_t n, uint64_t rt0) {
-    GF_BAIL(gout[j] == NOPOS || outc[j] >= (uint32_t)GR_C);
+    GF_BAIL(gout[j] == NOPOS || outc[j] >= kp.out.depth);
     GF_BAIL(wide_term(term, log_term, n ? rt0 : 0, 0));  // GR_ESC_WIDE_TERM in the general lane
     if (!ok) return;
     const Mailbox mb = kp.out.at(gout[j]);
@@ -113,7 +113,7 @@ struct FastLane {
   }
   // ... and of a ReplicateResp into the mailbox at gpos.
   GF_HD void emit_resp(uint32_t gpos, uint32_t* cnt, uint64_t log_index, bool reject, uint64_t hint) {
-    GF_BAIL(gpos == NOPOS || *cnt >= (uint32_t)GR_C);
+    GF_BAIL(gpos == NOPOS || *cnt >= kp.out.depth);
     GF_BAIL(wide_term(term, 0, 0, 0));
     if (!ok) return;
     const Mailbox mb = kp.out.at(gpos);

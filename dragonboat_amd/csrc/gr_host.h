@@ -265,16 +265,17 @@ inline int pack_inbox(const gr_inbox* in, uint32_t S, uint32_t max_peers, Packed
   return GR_OK;
 }
 
-inline uint64_t space_total_bytes(uint32_t n_chunks, uint32_t positions) {
-  return (uint64_t)n_chunks * space_chunk_bytes_pc(space_pad_positions(positions));
+inline uint64_t space_total_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth = GR_C) {
+  return (uint64_t)n_chunks * space_chunk_bytes_pc(space_pad_positions(positions), depth);
 }
 
-inline SpaceView make_view(const void* base, uint32_t n_chunks, uint32_t positions) {
+inline SpaceView make_view(const void* base, uint32_t n_chunks, uint32_t positions, uint32_t depth = GR_C) {
   SpaceView v;
   v.base = (uint8_t*)base;
   v.n_chunks = n_chunks;
   v.pc = space_pad_positions(positions);
-  v.chunk_bytes = space_chunk_bytes_pc(v.pc);
+  v.chunk_bytes = space_chunk_bytes_pc(v.pc, depth);
+  v.depth = depth;
   return v;
 }
 

@@ -440,7 +440,7 @@ struct Lane {
     const uint32_t g = out_gpos(j);
     if (g == NOPOS) return GR_ESC_NONMEMBER;
     const uint32_t c = (outcnt >> (3 * j)) & 7u;
-    if (c >= GR_C) return GR_ESC_CAPACITY;
+    if (c >= kp.out.depth) return GR_ESC_CAPACITY;
     const uint64_t mterm = is_request_message(m.type) ? m.term : term;
     if (wide_term(mterm, m.log_term, m.rt0, m.rt1)) return GR_ESC_WIDE_TERM;
     const Mailbox mb = kp.out.at(g);
@@ -1262,7 +1262,7 @@ struct Lane {
 #pragma unroll 1
       for (uint32_t k = 0; k < c; ++k) {
         if (item == limit) { *at = item; return 0; }
-        if (k == GR_C) { *at = item; return GR_ESC_CAPACITY; }  // overflowed mailbox
+        if (k == kp.in.depth) { *at = item; return GR_ESC_CAPACITY; }  // overflowed mailbox
         InMsg m;
         read_msg(mb, k, m);
         if (m.type == MT_WIDE) { *at = item; return GR_ESC_WIDE_TERM; }  // terms >= 2^32: host path

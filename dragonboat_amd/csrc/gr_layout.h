@@ -182,8 +182,10 @@ __host__ __device__ inline uint32_t space_pad_positions(uint32_t positions) {
 __host__ __device__ inline uint64_t space_k_bytes(uint32_t pc) {
   return (uint64_t)pc * (2 + 8 + 4 * MT_NUM + 8 * MF_NUM_U64);
 }
-__host__ __device__ inline uint64_t space_chunk_bytes_pc(uint32_t pc) {
-  uint64_t b = (uint64_t)pc + GR_C * space_k_bytes(pc);
+// A space's mailbox depth (1..GR_C) fixes its chunk size: spaces that cross
+// xGMI use the depth the steady state needs (2) and move half the bytes.
+__host__ __device__ inline uint64_t space_chunk_bytes_pc(uint32_t pc, uint32_t depth = GR_C) {
+  uint64_t b = (uint64_t)pc + depth * space_k_bytes(pc);
   return (b + 255u) & ~(uint64_t)255u;
 }
 
@@ -216,6 +218,7 @@ struct SpaceView {
   uint32_t n_chunks;
   uint32_t pc;
   uint64_t chunk_bytes;
+  uint32_t depth;  // messages per mailbox (1..GR_C); emitting more escalates CAPACITY
   __host__ __device__ inline Mailbox at(uint32_t gpos) const {
     uint32_t c = gpos / pc;
     Mailbox m;

@@ -64,7 +64,7 @@ struct TickLane {
   GT_HD uint8_t& s8(uint32_t row) const { return kp.st.u8(row)[p]; }
 
   GT_HD void emit(int j, uint8_t type, uint64_t commit, uint64_t hint, uint64_t hint_high) {
-    GT_BAIL(gout[j] == NOPOS || outc[j] >= (uint32_t)GR_C || wide_term(term, 0, 0, 0));
+    GT_BAIL(gout[j] == NOPOS || outc[j] >= kp.out.depth || wide_term(term, 0, 0, 0));
     if (!ok) return;
     const Mailbox mb = kp.out.at(gout[j]);
     const uint32_t c = outc[j];

@@ -16,6 +16,7 @@ from . import abi
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GPURAFT_LIB") or os.path.join(_HERE, "_build", "libgpuraft.so")  # env: A/B builds
 _lib = None
+MAILBOX_DEPTH = abi.GR_C  # full-depth spaces; exchange.py uses 2 for spaces that cross GPUs
 
 
 class GpuRaftError(RuntimeError):
@@ -45,17 +46,17 @@ def load_library(path=LIB_PATH):
     lib.gr_stats_get.argtypes = [c.c_void_p, c.POINTER(abi.Stats)]
     lib.gr_stats_reset.argtypes = [c.c_void_p]
     lib.gr_space_bytes.restype = c.c_uint64
-    lib.gr_space_bytes.argtypes = [c.c_uint32, c.c_uint32]
+    lib.gr_space_bytes.argtypes = [c.c_uint32, c.c_uint32, c.c_uint32]
     lib.gr_space_chunk_bytes.restype = c.c_uint64
-    lib.gr_space_chunk_bytes.argtypes = [c.c_uint32]
+    lib.gr_space_chunk_bytes.argtypes = [c.c_uint32, c.c_uint32]
     lib.gr_bind_routes.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32]
     lib.gr_set_locals.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_step_device.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32,
-                                   c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p]
+                                   c.c_uint32, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p]
     lib.gr_collect_results.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p, c.c_size_t]
-    lib.gr_space_decode.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_void_p, c.c_size_t,
+    lib.gr_space_decode.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_size_t,
                                     c.POINTER(c.c_size_t)]
-    lib.gr_space_encode.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_void_p, c.c_size_t,
+    lib.gr_space_encode.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_size_t,
                                     c.c_void_p]
     lib.gr_timing_begin.argtypes = [c.c_void_p]
     lib.gr_timing_end.argtypes = [c.c_void_p, c.POINTER(abi.Timing)]
@@ -138,11 +139,11 @@ class Engine:
         return {k: getattr(t, k) for k, _ in abi.Timing._fields_}
 
     # ---- device-resident path -------------------------------------------------
-    def space_bytes(self, n_chunks, positions):
-        return int(self.lib.gr_space_bytes(n_chunks, positions))
+    def space_bytes(self, n_chunks, positions, depth=MAILBOX_DEPTH):
+        return int(self.lib.gr_space_bytes(n_chunks, positions, depth))
 
-    def chunk_bytes(self, positions):
-        return int(self.lib.gr_space_chunk_bytes(positions))
+    def chunk_bytes(self, positions, depth=MAILBOX_DEPTH):
+        return int(self.lib.gr_space_chunk_bytes(positions, depth))
 
     def bind_routes(self, in_pos, out_pos):
         """in_pos/out_pos: uint32 arrays [slots][n_peers] (mailbox positions, 0xFFFFFFFF = none)."""
@@ -157,9 +158,9 @@ class Engine:
                                       len(locals_)), "gr_set_locals")
 
     def step_device(self, in_ptr, out_ptr, in_chunks, in_positions, out_chunks, out_positions,
-                    n_peers, stream=0):
+                    n_peers, stream=0, depth=MAILBOX_DEPTH):
         _check(self.lib.gr_step_device(self._h, in_ptr, out_ptr, in_chunks, in_positions, out_chunks,
-                                       out_positions, n_peers, stream), "gr_step_device")
+                                       out_positions, depth, n_peers, stream), "gr_step_device")
 
     def collect_results(self, n=None, first=0):
         n = self.max_peers - first if n is None else n
@@ -168,16 +169,17 @@ class Engine:
         return out
 
 
-def decode_space(buf, n_chunks, positions):
+def decode_space(buf, n_chunks, positions, depth=MAILBOX_DEPTH):
     """Decode a host copy of a message space (bytes/uint8 array) into records.
 
     peer = mailbox position, slot = index within the mailbox."""
     lib = load_library()
     buf = np.ascontiguousarray(buf, np.uint8)
     n = ctypes.c_size_t()
-    _check(lib.gr_space_decode(buf.ctypes.data, n_chunks, positions, None, 0, ctypes.byref(n)), "decode")
+    _check(lib.gr_space_decode(buf.ctypes.data, n_chunks, positions, depth, None, 0, ctypes.byref(n)),
+           "decode")
     out = np.zeros(n.value, abi.MESSAGE)
     if n.value:
-        _check(lib.gr_space_decode(buf.ctypes.data, n_chunks, positions, out.ctypes.data, n.value,
+        _check(lib.gr_space_decode(buf.ctypes.data, n_chunks, positions, depth, out.ctypes.data, n.value,
                                    ctypes.byref(n)), "decode")
     return out

@@ -9,9 +9,14 @@ their outgoing messages straight into mailbox "spaces" in HBM:
   ping-ponged; the kernel of pass k reads space k%2 and writes space (k+1)%2.
   No copy, no collective.
 * ``spread`` placement — replica r of the groups homed on rank h lives on
-  rank (h + r) % N. The out space has one chunk per destination rank, the in
-  space one chunk per source rank, and one RCCL ``all_to_all_single`` with
-  equal chunk splits moves every mailbox across xGMI once per pass.
+  rank (h + r) % N, so replica r talks to replica j only across the rank
+  offset (j - r) % N. The out space has one chunk per destination rank that
+  some pair reaches (ordered by rank), the in space one per source rank, and
+  one RCCL ``all_to_all_single`` with split sizes (0 for ranks no pair
+  reaches) moves every mailbox across xGMI once per pass. At R = 3 that is
+  4 of N chunks for N ≥ 5, and the spaces hold depth-2 mailboxes (the steady
+  state's two Replicates per follower per pass; a third message escalates
+  CAPACITY): the exchange moves 125 B per mailbox instead of 249.
 
 Peers on a rank are laid out replica-major: peer r*G + g is replica r of the
 group (home = (rank - r) % N, index g), so a wave's accesses stay contiguous.
@@ -38,14 +43,22 @@ def offset_pairs(R, N):
     return pairs
 
 
+def spread_peer_ranks(R, N, rank):
+    """(destination ranks, source ranks) of `rank`'s chunks, each sorted: the
+    ranks some (r -> j) pair reaches at offset (j - r) % N, and back."""
+    offs = [o for o, lst in offset_pairs(R, N).items() if lst]
+    return sorted({(rank + o) % N for o in offs}), sorted({(rank - o) % N for o in offs})
+
+
 def spread_routes(G, R, S, N, rank):
     """Route tables for spread placement on `rank`.
 
     Returns (in_pos [S][R*G], out_pos [S][R*G], positions per chunk). The
-    sender on rank a writes its mailbox for (r -> j, group g) at chunk
-    d = (a - r + j) % N, position pair_index * G + g; all_to_all delivers
-    chunk d of rank a as chunk a of rank d, where the receiver (replica j,
-    same group) reads the same position."""
+    sender on rank a writes its mailbox for (r -> j, group g) into the chunk
+    of destination d = (a - r + j) % N (chunk index = d's place among a's
+    destinations), position pair_index * G + g; all_to_all delivers it into
+    the chunk of source a on rank d (a's place among d's sources), where the
+    receiver (replica j, same group) reads the same position."""
     pairs = offset_pairs(R, N)
     per = max(len(v) for v in pairs.values())
     positions = per * G
@@ -54,6 +67,9 @@ def spread_routes(G, R, S, N, rank):
     for o, lst in pairs.items():
         for k, rj in enumerate(lst):
             index[rj] = k
+    dests, srcs = spread_peer_ranks(R, N, rank)
+    dslot = {d: c for c, d in enumerate(dests)}
+    sslot = {a: c for c, a in enumerate(srcs)}
     n = R * G
     g = np.arange(G, dtype=np.int64)
     in_pos = np.full((S, n), NOPOS, np.uint32)
@@ -65,10 +81,10 @@ def spread_routes(G, R, S, N, rank):
             k = index[(r, j)]
             # sender: local replica r, slot j -> chunk d
             d = (rank - r + j) % N
-            out_pos[j, r * G + g] = (d * pc + k * G + g).astype(np.uint32)
+            out_pos[j, r * G + g] = (dslot[d] * pc + k * G + g).astype(np.uint32)
             # receiver: local replica j, slot r <- chunk a (sender rank)
             a = (rank - j + r) % N
-            in_pos[r, j * G + g] = (a * pc + k * G + g).astype(np.uint32)
+            in_pos[r, j * G + g] = (sslot[a] * pc + k * G + g).astype(np.uint32)
     return in_pos, out_pos, positions
 
 
@@ -101,17 +117,26 @@ class Exchange:
             self.in_pos, self.out_pos = P.Topology(G, R).loopback_routes(S)
             self.n_chunks = 1
             self.positions = self.n_peers * S
+            self.depth = 4  # GR_C: nothing crosses a link, keep the full mailbox
+            self.in_chunks = self.out_chunks = 1
         elif placement == "spread":
             self.peers = spread_peers(G, R, world, rank, seed=seed)
             self.in_pos, self.out_pos, self.positions = spread_routes(G, R, S, world, rank)
-            self.n_chunks = world
+            self.dests, self.srcs = spread_peer_ranks(R, world, rank)
+            self.n_chunks = len(self.dests)
+            assert len(self.srcs) == self.n_chunks
+            self.depth = 2
         else:
             raise ValueError(placement)
 
     def allocate(self, eng, device):
         import torch
-        nbytes = eng.space_bytes(self.n_chunks, self.positions)
-        assert nbytes == self.n_chunks * eng.chunk_bytes(self.positions)
+        nbytes = eng.space_bytes(self.n_chunks, self.positions, self.depth)
+        cb = eng.chunk_bytes(self.positions, self.depth)
+        assert nbytes == self.n_chunks * cb and cb > 0
+        if self.placement == "spread":  # all_to_all split sizes, bytes per peer rank
+            self.out_splits = [cb if d in self.dests else 0 for d in range(self.world)]
+            self.in_splits = [cb if a in self.srcs else 0 for a in range(self.world)]
         a = torch.zeros(nbytes, dtype=torch.uint8, device=device)
         b = torch.zeros(nbytes, dtype=torch.uint8, device=device)
         return [a, b]
@@ -126,13 +151,14 @@ class Exchange:
         if events is not None:
             events[0].record(stream)
         eng.step_device(src.data_ptr(), dst.data_ptr(), self.n_chunks, self.positions,
-                        self.n_chunks, self.positions, self.n_peers, h)
+                        self.n_chunks, self.positions, self.n_peers, h, depth=self.depth)
         if events is not None:
             events[1].record(stream)
         if self.placement == "spread":
             import torch.distributed as dist
             if self.world > 1:
-                dist.all_to_all_single(spaces[0], spaces[1])
+                dist.all_to_all_single(spaces[0], spaces[1], output_split_sizes=self.in_splits,
+                                       input_split_sizes=self.out_splits)
             else:
                 spaces[0].copy_(spaces[1])
 

@@ -268,26 +268,31 @@ int gr_timing_end(gr_engine* e, gr_timing* out);
 /*
  * Device-resident path (benchmarks, multi-GPU exchange). Messages live in
  * "spaces": n_chunks chunks of `positions` mailboxes, each mailbox holding up
- * to GR_C messages in structure-of-arrays form. in_pos[j*max_peers+p] /
+ * to `depth` (1..GR_C) messages in structure-of-arrays form; a lane that would
+ * put more into one mailbox escalates GR_ESC_CAPACITY. Spaces that cross GPUs
+ * use depth 2 (the steady state's two Replicates per follower per pass) and
+ * move 2/GR_C of the bytes a full-depth space would. in_pos[j*max_peers+p] /
  * out_pos[j*max_peers+p] give the mailbox that peer p reads from / writes to
  * for remote slot j (0xFFFFFFFF = none). A chunk is one contiguous byte range,
  * so chunked spaces can be exchanged with one all-to-all.
  */
-uint64_t gr_space_bytes(uint32_t n_chunks, uint32_t positions);
-uint64_t gr_space_chunk_bytes(uint32_t positions);
+/* 0 when depth is not in 1..GR_C. */
+uint64_t gr_space_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth);
+uint64_t gr_space_chunk_bytes(uint32_t positions, uint32_t depth);
 int gr_bind_routes(gr_engine* e, const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n_peers);
 int gr_set_locals(gr_engine* e, const gr_local_input* locals, size_t n);
 /* Launch one pass on `stream` (a hipStream_t, may be NULL) without syncing.
- * in_space/out_space are device pointers laid out by gr_space_bytes(). */
+ * in_space/out_space are device pointers laid out by gr_space_bytes() with
+ * the same `depth`. */
 int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t in_chunks,
                    uint32_t in_positions, uint32_t out_chunks, uint32_t out_positions,
-                   uint32_t n_peers, void* stream);
+                   uint32_t depth, uint32_t n_peers, void* stream);
 /* Copy per-peer results of the last device pass for peers [first, first+n). */
 int gr_collect_results(gr_engine* e, uint32_t first, gr_peer_result* out, size_t n);
 /* Decode the messages of a device space into gr_message records (testing). */
-int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t positions,
+int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
                     gr_message* out, size_t cap, size_t* n_out);
-int gr_space_encode(void* space_host, uint32_t n_chunks, uint32_t positions,
+int gr_space_encode(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
                     const gr_message* msgs, size_t n, const uint32_t* pos_of_msg);
 
 #ifdef __cplusplus

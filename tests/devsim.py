@@ -48,7 +48,7 @@ def run_device(G, R, passes, placement="local", seed=2):
         # the space the next pass reads
         nxt = spaces[(k + 1) % 2] if placement == "local" else spaces[0]
         raw = nxt.cpu().numpy()
-        got = decode_space(raw, ex.n_chunks, ex.positions)
+        got = decode_space(raw, ex.n_chunks, ex.positions, ex.depth)
         for m in got:
             p, j = inv[int(m["peer"])]
             m["peer"], m["slot"] = p, j

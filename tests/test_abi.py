@@ -31,7 +31,9 @@ def test_library_exports_every_symbol(built):
     lib.gr_strerror.restype = ctypes.c_char_p
     assert lib.gr_strerror(-5) == b"mailbox capacity exceeded"
     lib.gr_space_chunk_bytes.restype = ctypes.c_uint64
-    assert lib.gr_space_chunk_bytes(1) % 256 == 0
+    assert lib.gr_space_chunk_bytes(1, 4) % 256 == 0
+    assert lib.gr_space_chunk_bytes(1, 0) == 0
+    assert lib.gr_space_chunk_bytes(64, 2) < lib.gr_space_chunk_bytes(64, 4)
 
 
 def _c_layout(tmp_path):

@@ -17,10 +17,11 @@ def _owner(rank, r, N):
     return (rank - r) % N  # home of the group whose replica r sits on `rank`
 
 
-@pytest.mark.parametrize("N", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 8])
 def test_spread_routes_bijection(N):
     G, R, S = 37, 3, 3
     tables = [X.spread_routes(G, R, S, N, a) for a in range(N)]
+    ranks = [X.spread_peer_ranks(R, N, a) for a in range(N)]
     positions = tables[0][2]
     pc = X.pad_positions(positions)
     # sender side: (rank a, chunk d, local pos) -> (home, g, r, j)
@@ -33,7 +34,8 @@ def test_spread_routes_bijection(N):
                 if v == X.NOPOS:
                     continue
                 r, g = divmod(p, G)
-                d, loc = divmod(v, pc)
+                c, loc = divmod(v, pc)
+                d = ranks[a][0][c]  # chunk slot -> destination rank
                 assert loc < positions
                 key = (a, d, loc)
                 assert key not in sent
@@ -47,10 +49,20 @@ def test_spread_routes_bijection(N):
                 if v == X.NOPOS:
                     continue
                 j, g = divmod(p, G)
-                a, loc = divmod(v, pc)
+                c, loc = divmod(v, pc)
+                a = ranks[d][1][c]  # chunk slot -> source rank
                 recv[(a, d, loc)] = (_owner(d, j, N), g, r, j)
     assert sent == recv
     assert len(sent) == N * G * R * (R - 1)
+
+
+@pytest.mark.parametrize("N,want", [(1, 1), (2, 2), (3, 2), (4, 3), (5, 4), (8, 4), (16, 4)])
+def test_spread_chunks_only_for_reached_ranks(N, want):
+    """At R = 3 a rank exchanges with the ranks at offsets +-1, +-2 only."""
+    for a in range(N):
+        d, s = X.spread_peer_ranks(3, N, a)
+        assert len(d) == len(s) == want
+        assert d == sorted(d) and s == sorted(s)
 
 
 def test_local_routes_match_topology():
@@ -90,17 +102,20 @@ def _worker(rank, world, port, G, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     R = S = 3
     in_pos, out_pos, positions = X.spread_routes(G, R, S, world, rank)
+    dests, srcs = X.spread_peer_ranks(R, world, rank)
     pc = X.pad_positions(positions)
     # each sender writes a tag (rank, replica, group, slot) into its mailboxes
-    out = torch.zeros(world * pc, dtype=torch.int64)
+    out = torch.zeros(len(dests) * pc, dtype=torch.int64)
     for j in range(S):
         for p in range(R * G):
             v = int(out_pos[j, p])
             if v != X.NOPOS:
                 r, g = divmod(p, G)
                 out[v] = 1 + ((rank * 8 + r) * 1000 + g) * 8 + j
-    inp = torch.zeros_like(out)
-    dist.all_to_all_single(inp, out)
+    inp = torch.zeros(len(srcs) * pc, dtype=torch.int64)
+    # the split sizes Exchange.step passes (in elements here, bytes there)
+    dist.all_to_all_single(inp, out, output_split_sizes=[pc if a in srcs else 0 for a in range(world)],
+                           input_split_sizes=[pc if d in dests else 0 for d in range(world)])
     errs = 0
     for r in range(S):
         for p in range(R * G):
@@ -115,7 +130,7 @@ def _worker(rank, world, port, G, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 5])
 def test_gloo_all_to_all_delivery(world):
     import socket
     s = socket.socket()
