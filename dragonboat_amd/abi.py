@@ -66,8 +66,8 @@ LOCAL = np.dtype([
 ])
 READY = np.dtype([("index", u64), ("ctx_low", u64), ("ctx_high", u64)])
 RESULT = np.dtype([
-    ("peer", u32), ("escalation", u8), ("propose_result", u8), ("n_ready", u8), ("pad", u8),
-    ("esc_item", u32), ("pad2", u32), ("append_from", u64), ("propose_first", u64),
+    ("peer", u32), ("escalation", u8), ("propose_result", u8), ("n_ready", u8), ("n_forwarded", u8),
+    ("esc_item", u32), ("forwarded_entries", u32), ("append_from", u64), ("propose_first", u64),
     ("ready", READY, (GR_Q,)),
 ])
 SIZES = {"gr_peer": 640, "gr_message": 80, "gr_local_input": 48, "gr_peer_result": 128,

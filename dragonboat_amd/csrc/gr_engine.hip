@@ -364,8 +364,8 @@ int upload_locals(gr_engine* e, const std::vector<gr_local_input>& byLane, uint3
 int download_results(gr_engine* e, uint32_t first, uint32_t n, std::vector<gr_peer_result>* out,
                      const uint32_t* peer_of_lane) {
   const LaneBase& L = e->ln;
-  std::vector<uint8_t> rflags(n), esc(n), pres(n), rtrc(n);
-  std::vector<uint32_t> escitem(n);
+  std::vector<uint8_t> rflags(n), esc(n), pres(n), rtrc(n), fwdn(n);
+  std::vector<uint32_t> escitem(n), fwde(n);
   std::vector<uint64_t> afrom(n), hi(n), rti((size_t)GR_Q * n), rtl((size_t)GR_Q * n),
       rth((size_t)GR_Q * n);
   std::vector<uint32_t> nprop(n);
@@ -376,6 +376,8 @@ int download_results(gr_engine* e, uint32_t first, uint32_t n, std::vector<gr_pe
   HIPCHK(hipMemcpy(escitem.data(), L.u32(LR_ESC_ITEM) + first, (size_t)n * 4, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(afrom.data(), L.u64(LR_APPEND_FROM) + first, (size_t)n * 8, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(nprop.data(), L.u32(LR_PROPOSE) + first, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(fwdn.data(), L.u8(LR_FWD_COUNT) + first, n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(fwde.data(), L.u32(LR_FWD_ENTRIES) + first, (size_t)n * 4, hipMemcpyDeviceToHost));
   if (peer_of_lane) {  // last_index of each lane's peer
     std::vector<uint64_t> all(e->cfg.max_peers);
     HIPCHK(hipMemcpy(all.data(), e->st.u64(SR_LAST_INDEX), all.size() * 8, hipMemcpyDeviceToHost));
@@ -401,10 +403,7 @@ int download_results(gr_engine* e, uint32_t first, uint32_t n, std::vector<gr_pe
       pr.escalation = esc[l];
       pr.esc_item = escitem[l];
     }
-    if (rf & RF_PROPOSE) {
-      pr.propose_result = pres[l];
-      if (pr.propose_result == GR_PROP_APPENDED) pr.propose_first = hi[l] - nprop[l] + 1;
-    }
+    derive_proposals(&pr, rf, pres[l], hi[l], nprop[l], fwdn[l], fwde[l]);
     if (rf & RF_APPEND) pr.append_from = afrom[l];
     if (rf & RF_READY) {
       pr.n_ready = rtrc[l];

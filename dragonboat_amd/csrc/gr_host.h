@@ -265,6 +265,24 @@ inline int pack_inbox(const gr_inbox* in, uint32_t S, uint32_t max_peers, Packed
   return GR_OK;
 }
 
+// The proposal fields of a result record from the lane rows (gr_layout.h RF_*):
+// propose_first is not stored, it follows from last_index since proposals are
+// the only appends of a pass that reports them.
+inline void derive_proposals(gr_peer_result* pr, uint8_t rf, uint8_t pres, uint64_t last_index,
+                             uint32_t local_n, uint8_t fwd_n, uint32_t fwd_entries) {
+  uint64_t n = 0;
+  if (rf & RF_PROPOSE) {
+    pr->propose_result = pres;
+    if (pres == GR_PROP_APPENDED) n += local_n;
+  }
+  if (rf & RF_FORWARDED) {
+    pr->n_forwarded = fwd_n;
+    pr->forwarded_entries = fwd_entries;
+    n += fwd_entries;
+  }
+  if (n) pr->propose_first = last_index - n + 1;
+}
+
 inline uint64_t space_total_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth = GR_C) {
   return (uint64_t)n_chunks * space_chunk_bytes_pc(space_pad_positions(positions), depth);
 }

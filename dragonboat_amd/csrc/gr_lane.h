@@ -119,6 +119,7 @@ struct Lane {
   uint32_t rtrc = 0, prop_result = 0;
   bool rand_used = false;
   uint64_t append_from = 0, propose_first = 0;
+  uint32_t fwd_n = 0, fwd_entries = 0;  // forwarded Propose batches appended this pass
   uint64_t committed0 = 0;
   uint32_t msgs_in = 0, msgs_out = 0, entries_in = 0;
 
@@ -547,6 +548,9 @@ struct Lane {
     return 0;
   }
   GR_HD int become_follower(uint64_t t, uint64_t lid) {  // raft.go:669-674
+    // a step-down after appending forwarded proposals: the host attributes
+    // those entries from propose_first, which only holds while this lane leads
+    if (fwd_n) return GR_ESC_UNSUPPORTED;
     need(G_CORE);
     state = GR_FOLLOWER;
     dirty |= D_STATE;
@@ -1134,7 +1138,7 @@ struct Lane {
         case GR_LEADER_HEARTBEAT: return broadcast_heartbeat();
         case GR_CHECK_QUORUM: return check_quorum();
         case GR_ELECTION: return 0;
-        case GR_PROPOSE:
+        case GR_PROPOSE: return leader_forwarded_propose(m);
         case GR_REQUEST_VOTE: return GR_ESC_UNSUPPORTED;
         default: return 0;  // nil handler
       }
@@ -1176,7 +1180,10 @@ struct Lane {
         case GR_ELECTION:
           if (obs) return 0;
           return handle_election();
-        case GR_PROPOSE:
+        case GR_PROPOSE: {  // handleFollowerPropose / handleObserverPropose (raft.go:1346-1357, 1322)
+          bool d;
+          return forward_to_leader(as_out(m), &d);
+        }
         case GR_INSTALL_SNAPSHOT: return GR_ESC_UNSUPPORTED;
         case GR_REQUEST_VOTE:
         case GR_TIMEOUT_NOW:
@@ -1197,6 +1204,36 @@ struct Lane {
     }
   }
 
+  // appendEntries + broadcastReplicateMessage (raft.go:643-654, 1144-1145)
+  GR_HD int append_proposal(uint32_t n) {
+    need(G_WIN | G_REM);
+    if (nruns > 0 && last_run_term() > term) return GR_ESC_PANIC;  // checkEntriesToAppend
+    const uint64_t first = hi + 1;
+    win_push(first, term);
+    hi += n;
+    dirty |= D_HI | D_REM;
+    try_update(self, hi);
+    if (quorum() == 1) {
+      bool c;
+      GR_TRY(try_commit(&c));
+    }
+    GR_TRY(broadcast_replicate());
+    if (!propose_first) propose_first = first;
+    return 0;
+  }
+  // handleLeaderPropose (raft.go:1125-1146) for a batch a follower forwarded
+  // (handleFollowerPropose :1346-1357). The device takes only appends, so the
+  // host can attribute the entries (gr_peer_result.propose_first): a drop
+  // (selfRemoved, leader transfer) or a config change goes to the host.
+  GR_HD int leader_forwarded_propose(const InMsg& m) {
+    if (m.flags & MFL_REJECT) return GR_ESC_CONFIG_CHANGE;
+    if (m.n == 0 || self_removed() || leader_transfering()) return GR_ESC_UNSUPPORTED;
+    GR_TRY(append_proposal(m.n));
+    fwd_n++;
+    fwd_entries += m.n;
+    return 0;
+  }
+
   // raft.handleLeaderPropose + appendEntries (raft.go:1125-1146, 643-654), or
   // the follower/observer forward and the candidate drop.
   GR_HD int propose(uint32_t n, bool has_cc) {
@@ -1205,20 +1242,8 @@ struct Lane {
       if (self_removed()) { prop_result = GR_PROP_DROPPED; return 0; }
       if (leader_transfering()) { prop_result = GR_PROP_DROPPED; return 0; }
       if (has_cc) return GR_ESC_CONFIG_CHANGE;
-      need(G_WIN | G_REM);
-      if (nruns > 0 && last_run_term() > term) return GR_ESC_PANIC;  // checkEntriesToAppend
-      const uint64_t first = hi + 1;
-      win_push(first, term);
-      hi += n;
-      dirty |= D_HI | D_REM;
-      try_update(self, hi);
-      if (quorum() == 1) {
-        bool c;
-        GR_TRY(try_commit(&c));
-      }
-      GR_TRY(broadcast_replicate());
+      GR_TRY(append_proposal(n));
       prop_result = GR_PROP_APPENDED;
-      propose_first = first;
       return 0;
     }
     if (state == GR_CANDIDATE) {
@@ -1228,6 +1253,7 @@ struct Lane {
     OutMsg o;
     o.type = GR_PROPOSE;
     o.n = n;
+    if (has_cc) o.flags = MFL_REJECT;  // a Propose record's reject bit: the batch holds a ConfigChangeEntry
     bool dropped;
     GR_TRY(forward_to_leader(o, &dropped));
     prop_result = dropped ? GR_PROP_DROPPED : GR_PROP_FORWARDED;
@@ -1244,6 +1270,8 @@ struct Lane {
     rand_used = false;
     append_from = 0;
     propose_first = 0;
+    fwd_n = 0;
+    fwd_entries = 0;
     msgs_in = 0;
     msgs_out = 0;
     entries_in = 0;
@@ -1355,6 +1383,11 @@ struct Lane {
     if (append_from) {
       rf |= RF_APPEND;
       kp.ln.u64(LR_APPEND_FROM)[i] = append_from;
+    }
+    if (fwd_n) {
+      rf |= RF_FORWARDED;
+      kp.ln.u8(LR_FWD_COUNT)[i] = (uint8_t)fwd_n;
+      kp.ln.u32(LR_FWD_ENTRIES)[i] = fwd_entries;
     }
     kp.ln.u8(LR_RFLAGS)[i] = rf;
     const bool adv = (dirty & D_COMMITTED) && committed > committed0;

@@ -86,8 +86,10 @@ enum LaneU64Row : uint32_t {
   LR_RTR_HI = LR_RTR_LO + GR_Q,         // + q
   LR_NU64 = LR_RTR_HI + GR_Q,
 };
-enum LaneU32Row : uint32_t { LR_TICKS = 0, LR_QTICKS, LR_PROPOSE, LR_ESC_ITEM, LR_LANE_PEER, LR_LWORD, LR_NU32 };
-enum LaneU8Row : uint32_t { LR_LFLAGS = 0, LR_RFLAGS, LR_ESC_REASON, LR_PROP_RESULT, LR_RTR_COUNT, LR_NU8 };
+enum LaneU32Row : uint32_t { LR_TICKS = 0, LR_QTICKS, LR_PROPOSE, LR_ESC_ITEM, LR_LANE_PEER, LR_LWORD, LR_FWD_ENTRIES,
+                             LR_NU32 };
+enum LaneU8Row : uint32_t { LR_LFLAGS = 0, LR_RFLAGS, LR_ESC_REASON, LR_PROP_RESULT, LR_RTR_COUNT, LR_FWD_COUNT,
+                            LR_NU8 };
 __host__ __device__ inline uint64_t lane_bytes(uint32_t S, uint32_t lcap) {
   // + in_pos / out_pos route tables [S][lcap] u32 each
   return (uint64_t)lcap * (8ull * LR_NU64 + 4ull * LR_NU32 + LR_NU8 + 8ull * S);
@@ -143,6 +145,7 @@ constexpr uint8_t RF_ESCALATED = 0x01;
 constexpr uint8_t RF_PROPOSE = 0x02;
 constexpr uint8_t RF_READY = 0x04;
 constexpr uint8_t RF_APPEND = 0x08;
+constexpr uint8_t RF_FORWARDED = 0x10;  // forwarded Propose batches appended: LR_FWD_COUNT, LR_FWD_ENTRIES
 
 // ---------------------------------------------------------------- message spaces
 enum U64Field : uint32_t { MF_LOG_INDEX = 0, MF_COMMIT = 1, MF_HINT = 2, MF_HINT_HIGH = 3, MF_NUM_U64 = 4 };

@@ -199,11 +199,16 @@ typedef struct gr_peer_result {
   uint8_t escalation;      /* gr_escalation */
   uint8_t propose_result;  /* gr_propose_result */
   uint8_t n_ready;
-  uint8_t pad;
+  uint8_t n_forwarded;     /* Propose messages from remotes (handleFollowerPropose forwards) appended this pass */
   uint32_t esc_item;       /* first item NOT applied on device (messages, read index, ticks, qticks, propose) */
-  uint32_t pad2;
+  uint32_t forwarded_entries; /* entries those n_forwarded batches appended */
   uint64_t append_from;    /* lowest index appended by Replicate this pass (0 = none): persist [append_from, last] */
-  uint64_t propose_first;  /* index of the first proposed entry when appended */
+  /* Index of the first entry a proposal appended this pass (0 = none). Proposals
+   * append in item order and nothing else appends on a leader, so
+   * [propose_first, propose_first + forwarded_entries) hold the forwarded
+   * batches in arrival order (slot, then mailbox order) and the local
+   * ProposeEntries batch, when propose_result == GR_PROP_APPENDED, follows. */
+  uint64_t propose_first;
   gr_ready_to_read ready[GR_Q];
 } gr_peer_result;
 

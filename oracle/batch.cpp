@@ -313,6 +313,8 @@ bool to_record(const OPeer& op, uint32_t peer, const Message& m, gr_message* o) 
   o->hint = m.Hint;
   o->hint_high = m.HintHigh;
   o->n_entries = (uint32_t)m.Entries.size();
+  if (m.Type == Propose)  // a Propose record's reject bit: the batch holds a ConfigChangeEntry
+    for (const Entry& e : m.Entries) o->reject |= e.Type == ConfigChangeEntry ? 1 : 0;
   bool ok = o->slot != GR_SLOT_NONE;
   if (!m.Entries.empty()) {
     o->n_runs = 1;
@@ -348,6 +350,10 @@ Message from_record(const OPeer& op, const gr_message& g) {
     e.Term = (g.n_runs == 2 && k >= g.run2_offset) ? g.run_term[1] : g.run_term[0];
     e.Cmd.assign(payload, 0);
     m.Entries.push_back(std::move(e));
+  }
+  if (m.Type == Propose && m.Reject) {  // see to_record
+    m.Reject = false;
+    if (!m.Entries.empty()) m.Entries[0].Type = ConfigChangeEntry;
   }
   return m;
 }
@@ -507,9 +513,15 @@ int ob_step(ob_pop* p, const gr_inbox* in, const uint32_t* limits, gr_peer* mid,
           for (const gr_message* gm : box[pi][j]) {
             if (item == limit) take_mid();
             Message m = from_record(op, *gm);
+            const u64 before = r.log->lastIndex();
             // Peer.Handle (peer.go:199-209)
             bool member = op.kinds[j] != GR_SLOT_EMPTY;
             if (member || !isResponseMessageType(m.Type)) r.Handle(m);
+            if (m.Type == Propose && !midTaken && r.log->lastIndex() > before) {  // forwarded batch appended
+              if (!res.propose_first) res.propose_first = before + 1;
+              res.n_forwarded++;
+              res.forwarded_entries += (uint32_t)m.Entries.size();
+            }
             flush(item);
             item++;
           }
@@ -558,7 +570,7 @@ int ob_step(ob_pop* p, const gr_inbox* in, const uint32_t* limits, gr_peer* mid,
             if (!midTaken) {
               if (r.log->lastIndex() > before) {
                 res.propose_result = GR_PROP_APPENDED;
-                res.propose_first = before + 1;
+                if (!res.propose_first) res.propose_first = before + 1;
               } else {
                 res.propose_result = fwd ? GR_PROP_FORWARDED : GR_PROP_DROPPED;
               }

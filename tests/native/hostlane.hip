@@ -123,11 +123,8 @@ extern "C" int hl_step(uint32_t slots, uint64_t max_entry_size, gr_peer* peers, 
         pr.escalation = ln.u8(LR_ESC_REASON)[l];
         pr.esc_item = ln.u32(LR_ESC_ITEM)[l];
       }
-      if (rf & RF_PROPOSE) {
-        pr.propose_result = ln.u8(LR_PROP_RESULT)[l];
-        if (pr.propose_result == GR_PROP_APPENDED)
-          pr.propose_first = st.u64(SR_LAST_INDEX)[pk.peers[l]] - ln.u32(LR_PROPOSE)[l] + 1;
-      }
+      derive_proposals(&pr, rf, ln.u8(LR_PROP_RESULT)[l], st.u64(SR_LAST_INDEX)[pk.peers[l]],
+                       ln.u32(LR_PROPOSE)[l], ln.u8(LR_FWD_COUNT)[l], ln.u32(LR_FWD_ENTRIES)[l]);
       if (rf & RF_APPEND) pr.append_from = ln.u64(LR_APPEND_FROM)[l];
       if (rf & RF_READY) {
         pr.n_ready = ln.u8(LR_RTR_COUNT)[l];

@@ -124,7 +124,8 @@ def compare_results(eng_res, orc_res, limit=20):
     for r in eng_res:
         p = int(r["peer"])
         o = orc_res[p]
-        fields = ["propose_result", "propose_first", "append_from", "n_ready"]
+        fields = ["propose_result", "propose_first", "append_from", "n_ready", "n_forwarded",
+                  "forwarded_entries"]
         d = [f"{f}: engine={r[f]} oracle={o[f]}" for f in fields if r[f] != o[f]]
         for q in range(min(int(r["n_ready"]), abi.GR_Q)):
             if tuple(r["ready"][q]) != tuple(o["ready"][q]):

@@ -60,7 +60,7 @@ def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, c
     eng = backend(peers, slots)
     n = len(peers)
     msgs = np.zeros(0, abi.MESSAGE)
-    stats = {"msgs": 0, "escalations": 0, "esc_reasons": {}, "commits": 0, "ready": 0}
+    stats = {"msgs": 0, "escalations": 0, "esc_reasons": {}, "commits": 0, "ready": 0, "forwarded": 0}
     parked = np.zeros(n, bool)
     for k in range(passes):
         if inject_fn is not None:
@@ -78,6 +78,7 @@ def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, c
         o = pop.step(msgs, loc, lim)
         esc = res[res["escalation"] != 0]
         stats["ready"] += int(res["n_ready"].sum())
+        stats["forwarded"] += int(res["n_forwarded"].sum())
         stats["escalations"] += len(esc)
         for r in esc:
             nm = abi.ESC_NAMES[r["escalation"]]

@@ -37,6 +37,26 @@ def test_leader_change_churn(built):
     assert st["commits"] > 0
 
 
+def test_forwarded_proposals(built):
+    """ProposeEntries on every replica: followers forward (handleFollowerPropose,
+    raft.go:1346-1357) and the leader appends the forwarded batches on the device
+    (handleLeaderPropose :1125-1146), reported as n_forwarded/forwarded_entries
+    with propose_first at the first of them. A forwarded batch holding a config
+    change escalates CONFIG_CHANGE; leader churn mixes in stepped-down leaders."""
+    G, R = 120, 3
+
+    def lf(k):
+        rng = np.random.default_rng([7, k])
+        loc = P.propose_locals(R * G, np.arange(R * G), pass_index=k)
+        loc["propose_entries"] = rng.integers(1, 4, R * G)
+        loc["propose_has_config_change"] = rng.random(R * G) < 0.02
+        return loc
+    st = _run(G, 10, seed=9, locals_fn=lf, inject_p=0.05)
+    assert st["forwarded"] > G, st
+    assert "unsupported" not in st["esc_reasons"] or st["esc_reasons"]["unsupported"] < G // 10, st
+    assert st["esc_reasons"].get("config_change", 0) > 0, st
+
+
 @pytest.mark.parametrize("check_quorum", [False, True])
 def test_ticks_and_read_index(built, check_quorum):
     """Tick sweep (heartbeats, election timeouts, checkQuorum) + leader ReadIndex."""
