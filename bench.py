@@ -54,6 +54,27 @@ def algorithmic_bytes(st, groups, R, passes):
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, spec
 
 
+def stream_copy_gbs(torch, dev, nbytes=1 << 30, reps=5):
+    """Achievable HBM bandwidth on this box: a device-to-device copy of 1 GiB
+    (read + write = 2 GiB moved per copy, past the 256 MiB Infinity Cache),
+    best of `reps`, HIP events. Reported beside the spec peak, never instead of it."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1)
+    b.copy_(a)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    del a, b
+    return 2 * nbytes / (best * 1e-3) / 1e9
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -180,6 +201,7 @@ def main():
     for k in range(args.steps):
         ex.step(eng, spaces, args.warmup + args.steps + k, stream)
     tm = eng.timing_end()
+    copy_gbs = stream_copy_gbs(torch, dev)
     commits = st["leader_commits"]
     esc = st["escalations"]
     if world > 1:
@@ -233,6 +255,9 @@ def main():
                          "canonical_round_bytes": canon,
                          "canonical_frac": canon / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "hbm_traffic_GBs": (traffic / (kavg * 1e-3) / 1e9) if traffic else None,
+                         "stream_copy_GBs": copy_gbs,
+                         "hbm_traffic_frac_of_stream_copy": ((traffic / (kavg * 1e-3) / 1e9) / copy_gbs)
+                         if traffic else None,
                          "general_kernel_ms": gavg,
                          "bailed_lanes_per_pass": tm["bailed_lanes"] / passes},
         }
