@@ -15,8 +15,11 @@
 #include <new>
 #include <vector>
 
+#include <rocprim/rocprim.hpp>  // device-wide scan and radix sort of the boundary passes (gr_io.h)
+
 #include "gr_fast.h"
 #include "gr_host.h"
+#include "gr_io.h"
 #include "gr_lane.h"
 #include "gr_tick.h"
 
@@ -229,15 +232,23 @@ struct gr_engine {
   bool locals_set = false;
   uint64_t passes = 0;
 
-  // host-path staging
-  void* d_in = nullptr;
-  void* d_out = nullptr;
-  size_t d_in_bytes = 0, d_out_bytes = 0;
-  uint8_t* h_in = nullptr;
-  uint8_t* h_out = nullptr;
-  size_t h_in_bytes = 0, h_out_bytes = 0;
-  std::vector<gr_message> out_msgs;
-  std::vector<gr_peer_result> out_results;
+  // gr_step buffers (gr_io.h), grown on demand and reused
+  struct Buf {
+    void* p = nullptr;
+    size_t n = 0;
+  };
+  Buf d_in, d_out;          // mailbox spaces
+  Buf d_msgs, d_locals;     // caller records, as given
+  Buf d_mark, d_lop;        // [max_peers] input flags, lane of peer
+  Buf d_keys, d_idx, d_skeys, d_sidx;  // mailbox sort
+  Buf d_win, d_oc, d_off;   // [lanes]
+  Buf d_tmp;                // rocprim scratch
+  Buf d_scal;               // lane count, error, outbox total
+  Buf d_outmsgs, d_results; // packed outbox
+  uint8_t* h_outmsgs = nullptr;  // pinned: returned to the caller until gr_release_outbox
+  uint8_t* h_results = nullptr;
+  uint8_t* h_scal = nullptr;
+  size_t h_outmsgs_bytes = 0, h_results_bytes = 0, h_scal_bytes = 0;
   std::mutex mu;  // one host-path pass at a time per engine
 };
 
@@ -340,82 +351,23 @@ int grow_pinned(uint8_t** p, size_t* have, size_t want) {
   return GR_OK;
 }
 
-// Upload per-lane local inputs for lanes [0, n) in lane order.
-int upload_locals(gr_engine* e, const std::vector<gr_local_input>& byLane, uint32_t n, hipStream_t s) {
-  std::vector<uint32_t> lt(n, 0), lq(n, 0), lp(n, 0), lw(n, 0);
-  std::vector<uint8_t> lf(n, 0);
-  std::vector<uint64_t> llo(n, 0), lhi(n, 0), lr(n, 0);
-  for (uint32_t l = 0; l < n; ++l)
-    locals_to_rows(byLane[l], &lt[l], &lq[l], &lp[l], &lf[l], &llo[l], &lhi[l], &lr[l], &lw[l]);
-  const LaneBase& L = e->ln;
-  HIPCHK(hipMemcpyAsync(L.u32(LR_TICKS), lt.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(L.u32(LR_QTICKS), lq.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(L.u32(LR_PROPOSE), lp.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(L.u8(LR_LFLAGS), lf.data(), (size_t)n, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(L.u32(LR_LWORD), lw.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(L.u64(LR_RI_LO), llo.data(), (size_t)n * 8, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(L.u64(LR_RI_HI), lhi.data(), (size_t)n * 8, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(L.u64(LR_RAND), lr.data(), (size_t)n * 8, hipMemcpyHostToDevice, s));
-  HIPCHK(hipStreamSynchronize(s));  // the host vectors go out of scope
+// Grid of a boundary pass (grid-stride loops): enough workgroups to fill the chip.
+uint32_t io_grid(size_t n) {
+  const size_t b = (n + io::kIoBlock - 1) / io::kIoBlock;
+  return (uint32_t)std::max<size_t>(1, std::min<size_t>(b, 4096));
+}
+
+// Exclusive sum of n u32 on `s` (rocprim), scratch grown on demand.
+int io_scan(gr_engine* e, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s) {
+  size_t tb = 0;
+  HIPCHK(rocprim::exclusive_scan(nullptr, tb, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
+  const int r = grow_device(&e->d_tmp.p, &e->d_tmp.n, tb);
+  if (r) return r;
+  tb = e->d_tmp.n;
+  HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tb, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
   return GR_OK;
 }
 
-// Download per-lane results for lanes [first, first+n).
-int download_results(gr_engine* e, uint32_t first, uint32_t n, std::vector<gr_peer_result>* out,
-                     const uint32_t* peer_of_lane) {
-  const LaneBase& L = e->ln;
-  std::vector<uint8_t> rflags(n), esc(n), pres(n), rtrc(n), fwdn(n);
-  std::vector<uint32_t> escitem(n), fwde(n);
-  std::vector<uint64_t> afrom(n), hi(n), rti((size_t)GR_Q * n), rtl((size_t)GR_Q * n),
-      rth((size_t)GR_Q * n);
-  std::vector<uint32_t> nprop(n);
-  HIPCHK(hipMemcpy(rflags.data(), L.u8(LR_RFLAGS) + first, n, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(esc.data(), L.u8(LR_ESC_REASON) + first, n, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(pres.data(), L.u8(LR_PROP_RESULT) + first, n, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(rtrc.data(), L.u8(LR_RTR_COUNT) + first, n, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(escitem.data(), L.u32(LR_ESC_ITEM) + first, (size_t)n * 4, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(afrom.data(), L.u64(LR_APPEND_FROM) + first, (size_t)n * 8, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(nprop.data(), L.u32(LR_PROPOSE) + first, (size_t)n * 4, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(fwdn.data(), L.u8(LR_FWD_COUNT) + first, n, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(fwde.data(), L.u32(LR_FWD_ENTRIES) + first, (size_t)n * 4, hipMemcpyDeviceToHost));
-  if (peer_of_lane) {  // last_index of each lane's peer
-    std::vector<uint64_t> all(e->cfg.max_peers);
-    HIPCHK(hipMemcpy(all.data(), e->st.u64(SR_LAST_INDEX), all.size() * 8, hipMemcpyDeviceToHost));
-    for (uint32_t l = 0; l < n; ++l) hi[l] = all[peer_of_lane[l]];
-  } else {
-    HIPCHK(hipMemcpy(hi.data(), e->st.u64(SR_LAST_INDEX) + first, (size_t)n * 8, hipMemcpyDeviceToHost));
-  }
-  for (int q = 0; q < GR_Q; ++q) {
-    HIPCHK(hipMemcpy(rti.data() + (size_t)q * n, L.u64(LR_RTR_INDEX + q) + first, (size_t)n * 8,
-                     hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(rtl.data() + (size_t)q * n, L.u64(LR_RTR_LO + q) + first, (size_t)n * 8,
-                     hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(rth.data() + (size_t)q * n, L.u64(LR_RTR_HI + q) + first, (size_t)n * 8,
-                     hipMemcpyDeviceToHost));
-  }
-  out->resize(n);
-  for (uint32_t l = 0; l < n; ++l) {
-    gr_peer_result& pr = (*out)[l];
-    memset(&pr, 0, sizeof(pr));
-    pr.peer = peer_of_lane ? peer_of_lane[l] : first + l;
-    const uint8_t rf = rflags[l];
-    if (rf & RF_ESCALATED) {
-      pr.escalation = esc[l];
-      pr.esc_item = escitem[l];
-    }
-    derive_proposals(&pr, rf, pres[l], hi[l], nprop[l], fwdn[l], fwde[l]);
-    if (rf & RF_APPEND) pr.append_from = afrom[l];
-    if (rf & RF_READY) {
-      pr.n_ready = rtrc[l];
-      for (int q = 0; q < pr.n_ready && q < GR_Q; ++q) {
-        pr.ready[q].index = rti[(size_t)q * n + l];
-        pr.ready[q].ctx_low = rtl[(size_t)q * n + l];
-        pr.ready[q].ctx_high = rth[(size_t)q * n + l];
-      }
-    }
-  }
-  return GR_OK;
-}
 
 }  // namespace
 
@@ -498,10 +450,12 @@ void gr_destroy(gr_engine* e) {
   if (e->counters) (void)hipFree(e->counters);
   if (e->route_base) (void)hipFree(e->route_base);
   free_timings(e);
-  if (e->d_in) (void)hipFree(e->d_in);
-  if (e->d_out) (void)hipFree(e->d_out);
-  if (e->h_in) (void)hipHostFree(e->h_in);
-  if (e->h_out) (void)hipHostFree(e->h_out);
+  for (gr_engine::Buf* b : {&e->d_in, &e->d_out, &e->d_msgs, &e->d_locals, &e->d_mark, &e->d_lop, &e->d_keys,
+                            &e->d_idx, &e->d_skeys, &e->d_sidx, &e->d_win, &e->d_oc, &e->d_off, &e->d_tmp,
+                            &e->d_scal, &e->d_outmsgs, &e->d_results})
+    if (b->p) (void)hipFree(b->p);
+  for (uint8_t* h : {e->h_outmsgs, e->h_results, e->h_scal})
+    if (h) (void)hipHostFree(h);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -566,66 +520,139 @@ int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t position
 
 int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
   if (!e || !in || !out) return GR_EINVAL;
+  if ((in->n_msgs && !in->msgs) || (in->n_locals && !in->locals)) return GR_EINVAL;
+  if (in->n_msgs + in->n_locals >= 0x80000000ull) return GR_EINVAL;
   std::lock_guard<std::mutex> guard(e->mu);
-  const uint32_t S = e->S;
   out->msgs = nullptr;
   out->n_msgs = 0;
   out->results = nullptr;
   out->n_results = 0;
-  e->out_msgs.clear();
-  e->out_results.clear();
-  PackedInbox pk;
-  int r = pack_inbox(in, S, e->cfg.max_peers, &pk);
-  if (r) return r;
-  const uint32_t nl = (uint32_t)pk.peers.size();
-  if (nl == 0) return GR_OK;
-  const size_t in_bytes = gr_space_bytes(1, pk.in_positions, GR_C);
-  const size_t out_bytes = gr_space_bytes(1, pk.out_positions, GR_C);
-  if ((r = grow_pinned(&e->h_in, &e->h_in_bytes, in_bytes))) return r;
-  if ((r = grow_pinned(&e->h_out, &e->h_out_bytes, out_bytes))) return r;
-  if ((r = grow_device(&e->d_in, &e->d_in_bytes, in_bytes))) return r;
-  if ((r = grow_device(&e->d_out, &e->d_out_bytes, out_bytes))) return r;
-  memset(e->h_in, 0, in_bytes);
-  encode_inbox(in, pk, e->h_in);
+  const uint32_t S = e->S, cap = e->cfg.max_peers;
+  const uint32_t nm = (uint32_t)in->n_msgs, nlc = (uint32_t)in->n_locals;
+  if (nm + nlc == 0) return GR_OK;
   const hipStream_t s = e->stream;
-  if ((r = upload_locals(e, pk.locals, nl, s))) return r;
-  HIPCHK(hipMemcpyAsync(e->d_in, e->h_in, in_bytes, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(e->ln.u32(LR_LANE_PEER), pk.peers.data(), (size_t)nl * 4, hipMemcpyHostToDevice, s));
-  for (uint32_t j = 0; j < S; ++j) {
-    HIPCHK(hipMemcpyAsync(e->ln.in_pos() + (size_t)j * e->cap, pk.in_pos.data() + (size_t)j * nl,
-                          (size_t)nl * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(e->ln.out_pos() + (size_t)j * e->cap, pk.out_pos.data() + (size_t)j * nl,
-                          (size_t)nl * 4, hipMemcpyHostToDevice, s));
+  const dim3 blk(io::kIoBlock);
+  int r;
+  // ---- inbox records -> lanes (gr_io.h)
+  if ((r = grow_device(&e->d_msgs.p, &e->d_msgs.n, (size_t)nm * sizeof(gr_message) + 1))) return r;
+  if ((r = grow_device(&e->d_locals.p, &e->d_locals.n, (size_t)nlc * sizeof(gr_local_input) + 1))) return r;
+  if ((r = grow_device(&e->d_mark.p, &e->d_mark.n, (size_t)cap * 4))) return r;
+  if ((r = grow_device(&e->d_lop.p, &e->d_lop.n, (size_t)cap * 4))) return r;
+  if ((r = grow_device(&e->d_scal.p, &e->d_scal.n, 16))) return r;
+  if ((r = grow_pinned(&e->h_scal, &e->h_scal_bytes, 16))) return r;
+  uint32_t* mark = (uint32_t*)e->d_mark.p;
+  uint32_t* lop = (uint32_t*)e->d_lop.p;
+  uint32_t* scal = (uint32_t*)e->d_scal.p;
+  const gr_message* dmsgs = (const gr_message*)e->d_msgs.p;
+  const gr_local_input* dloc = (const gr_local_input*)e->d_locals.p;
+  if (nm) HIPCHK(hipMemcpyAsync(e->d_msgs.p, in->msgs, (size_t)nm * sizeof(gr_message), hipMemcpyHostToDevice, s));
+  if (nlc)
+    HIPCHK(hipMemcpyAsync(e->d_locals.p, in->locals, (size_t)nlc * sizeof(gr_local_input), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(mark, 0, (size_t)cap * 4, s));
+  HIPCHK(hipMemsetAsync(scal, 0, 16, s));
+  hipLaunchKernelGGL(io::mark_inputs, dim3(io_grid(nm + nlc)), blk, 0, s, dmsgs, nm, dloc, nlc, S, cap, mark,
+                     scal + 1);
+  HIPCHK(hipGetLastError());
+  if ((r = io_scan(e, mark, lop, cap, s))) return r;
+  hipLaunchKernelGGL(io::finish_lanes, dim3(1), dim3(64), 0, s, (const uint32_t*)mark, (const uint32_t*)lop, cap,
+                     (const uint32_t*)(scal + 1), scal);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->h_scal, scal, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const uint32_t nl = ((uint32_t*)e->h_scal)[0];
+  if (((uint32_t*)e->h_scal)[1]) return GR_EINVAL;  // nothing of the pass ran
+  if (nl == 0) return GR_OK;
+  uint32_t* peer_of_lane = e->ln.u32(LR_LANE_PEER);
+  hipLaunchKernelGGL(io::lane_peers, dim3(io_grid(cap)), blk, 0, s, (const uint32_t*)mark, (const uint32_t*)lop, cap,
+                     peer_of_lane);
+  HIPCHK(hipGetLastError());
+  // ---- mailboxes: slot-major j*nl + lane, arrival order kept by a stable sort
+  const uint32_t positions = nl * S;
+  const size_t space = gr_space_bytes(1, positions, GR_C);
+  if ((r = grow_device(&e->d_in.p, &e->d_in.n, space))) return r;
+  if ((r = grow_device(&e->d_out.p, &e->d_out.n, space))) return r;
+  const SpaceView vin = make_view(e->d_in.p, 1, positions), vout = make_view(e->d_out.p, 1, positions);
+  HIPCHK(hipMemsetAsync(e->d_in.p, 0, vin.pc, s));  // the count bytes
+  if (nm) {
+    for (gr_engine::Buf* b : {&e->d_keys, &e->d_idx, &e->d_skeys, &e->d_sidx})
+      if ((r = grow_device(&b->p, &b->n, (size_t)nm * 4))) return r;
+    hipLaunchKernelGGL(io::msg_keys, dim3(io_grid(nm)), blk, 0, s, dmsgs, nm, (const uint32_t*)lop, nl,
+                       (uint32_t*)e->d_keys.p, (uint32_t*)e->d_idx.p);
+    HIPCHK(hipGetLastError());
+    uint32_t bits = 1;
+    while (bits < 32 && (1ull << bits) < positions) ++bits;
+    size_t tb = 0;
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, (uint32_t*)e->d_keys.p, (uint32_t*)e->d_skeys.p,
+                                     (uint32_t*)e->d_idx.p, (uint32_t*)e->d_sidx.p, (size_t)nm, 0, bits, s));
+    if ((r = grow_device(&e->d_tmp.p, &e->d_tmp.n, tb))) return r;
+    tb = e->d_tmp.n;
+    HIPCHK(rocprim::radix_sort_pairs(e->d_tmp.p, tb, (uint32_t*)e->d_keys.p, (uint32_t*)e->d_skeys.p,
+                                     (uint32_t*)e->d_idx.p, (uint32_t*)e->d_sidx.p, (size_t)nm, 0, bits, s));
+    hipLaunchKernelGGL(io::encode_sorted, dim3(io_grid(nm)), blk, 0, s, dmsgs, (const uint32_t*)e->d_skeys.p,
+                       (const uint32_t*)e->d_sidx.p, nm, vin);
+    HIPCHK(hipGetLastError());
   }
+  // ---- locals -> lane rows
+  if ((r = grow_device(&e->d_win.p, &e->d_win.n, (size_t)nl * 4))) return r;
+  HIPCHK(hipMemsetAsync(e->d_win.p, 0, (size_t)nl * 4, s));
+  if (nlc) {
+    hipLaunchKernelGGL(io::local_winner, dim3(io_grid(nlc)), blk, 0, s, dloc, nlc, (const uint32_t*)lop,
+                       (uint32_t*)e->d_win.p);
+    HIPCHK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(io::fill_locals, dim3(io_grid(nl)), blk, 0, s, dloc, (const uint32_t*)e->d_win.p, nl, e->ln);
+  HIPCHK(hipGetLastError());
+  // ---- the pass
   StepParams kp = base_params(e);
   kp.has_locals = 1;
   kp.has_lane_peer = 1;
-  kp.route_mode = RT_TABLE;
-  kp.in = make_view(e->d_in, 1, pk.in_positions);
-  kp.out = make_view(e->d_out, 1, pk.out_positions);
+  kp.route_mode = RT_IDENTITY;
+  kp.in = vin;
+  kp.out = vout;
   kp.n_lanes = nl;
   HIPCHK(launch_slots(S, kp, e->bail, e->counters, e->cap, (uint32_t)e->launches++, s, next_timing(e)));
   e->passes++;
   e->locals_set = false;    // the lane rows now hold this pass's compact locals
-  e->routes_bound = false;  // and its compact routes
-  HIPCHK(hipMemcpyAsync(e->h_out, e->d_out, out_bytes, hipMemcpyDeviceToHost, s));
+  e->routes_bound = false;  // and RT_IDENTITY replaced the bound routes
+  // ---- outbox mailboxes + lane results -> records
+  if ((r = grow_device(&e->d_oc.p, &e->d_oc.n, (size_t)nl * 4))) return r;
+  if ((r = grow_device(&e->d_off.p, &e->d_off.n, (size_t)nl * 4))) return r;
+  if ((r = grow_device(&e->d_results.p, &e->d_results.n, (size_t)nl * sizeof(gr_peer_result)))) return r;
+  uint32_t* oc = (uint32_t*)e->d_oc.p;
+  uint32_t* off = (uint32_t*)e->d_off.p;
+  hipLaunchKernelGGL(io::out_counts, dim3(io_grid(nl)), blk, 0, s, vout, nl, S, oc);
+  HIPCHK(hipGetLastError());
+  if ((r = io_scan(e, oc, off, nl, s))) return r;
+  hipLaunchKernelGGL(io::finish_total, dim3(1), dim3(64), 0, s, (const uint32_t*)oc, (const uint32_t*)off, nl,
+                     scal + 2);
+  hipLaunchKernelGGL(io::pack_results, dim3(io_grid(nl)), blk, 0, s, e->ln, e->st, (const uint32_t*)peer_of_lane,
+                     0u, nl, (gr_peer_result*)e->d_results.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->h_scal + 8, scal + 2, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  if ((r = download_results(e, 0, nl, &e->out_results, pk.peers.data()))) return r;
-  decode_outbox(e->h_out, pk, S, &e->out_msgs);
-  out->msgs = e->out_msgs.data();
-  out->n_msgs = e->out_msgs.size();
-  out->results = e->out_results.data();
-  out->n_results = e->out_results.size();
+  const uint32_t total = ((uint32_t*)e->h_scal)[2];
+  const size_t mbytes = (size_t)total * sizeof(gr_message), rbytes = (size_t)nl * sizeof(gr_peer_result);
+  if ((r = grow_device(&e->d_outmsgs.p, &e->d_outmsgs.n, mbytes + 1))) return r;
+  if ((r = grow_pinned(&e->h_outmsgs, &e->h_outmsgs_bytes, mbytes + 1))) return r;
+  if ((r = grow_pinned(&e->h_results, &e->h_results_bytes, rbytes))) return r;
+  if (total) {
+    hipLaunchKernelGGL(io::pack_outbox, dim3(io_grid(nl)), blk, 0, s, vout, nl, S, (const uint32_t*)off,
+                       (const uint32_t*)peer_of_lane, (gr_message*)e->d_outmsgs.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(e->h_outmsgs, e->d_outmsgs.p, mbytes, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipMemcpyAsync(e->h_results, e->d_results.p, rbytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  out->msgs = total ? (gr_message*)e->h_outmsgs : nullptr;
+  out->n_msgs = total;
+  out->results = (gr_peer_result*)e->h_results;
+  out->n_results = nl;
   return GR_OK;
 }
 
 int gr_release_outbox(gr_engine* e, gr_outbox* out) {
   if (!e || !out) return GR_EINVAL;
-  std::lock_guard<std::mutex> guard(e->mu);
-  e->out_msgs.clear();
-  e->out_msgs.shrink_to_fit();
-  e->out_results.clear();
-  e->out_results.shrink_to_fit();
+  std::lock_guard<std::mutex> guard(e->mu);  // the pinned outbox buffers stay for the next pass
   out->msgs = nullptr;
   out->n_msgs = 0;
   out->results = nullptr;
@@ -728,16 +755,28 @@ int gr_bind_routes(gr_engine* e, const uint32_t* in_pos, const uint32_t* out_pos
 }
 
 int gr_set_locals(gr_engine* e, const gr_local_input* locals, size_t n) {
-  if (!e || (n && !locals)) return GR_EINVAL;
-  HIPCHK(hipDeviceSynchronize());
-  std::vector<gr_local_input> byPeer(e->cfg.max_peers);
-  memset(byPeer.data(), 0, byPeer.size() * sizeof(gr_local_input));
-  for (size_t k = 0; k < n; ++k) {
-    if (locals[k].peer >= e->cfg.max_peers) return GR_EINVAL;
-    byPeer[locals[k].peer] = locals[k];
+  if (!e || (n && !locals) || n >= 0x80000000ull) return GR_EINVAL;
+  const uint32_t cap = e->cfg.max_peers;
+  for (size_t k = 0; k < n; ++k)
+    if (locals[k].peer >= cap) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  HIPCHK(hipDeviceSynchronize());  // a pass in flight on another stream may read the rows
+  const hipStream_t s = e->stream;
+  int r;
+  if ((r = grow_device(&e->d_locals.p, &e->d_locals.n, n * sizeof(gr_local_input) + 1))) return r;
+  if ((r = grow_device(&e->d_win.p, &e->d_win.n, (size_t)cap * 4))) return r;
+  if (n) HIPCHK(hipMemcpyAsync(e->d_locals.p, locals, n * sizeof(gr_local_input), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(e->d_win.p, 0, (size_t)cap * 4, s));
+  const gr_local_input* dloc = (const gr_local_input*)e->d_locals.p;
+  if (n) {
+    hipLaunchKernelGGL(io::local_winner, dim3(io_grid(n)), dim3(io::kIoBlock), 0, s, dloc, (uint32_t)n,
+                       (const uint32_t*)nullptr, (uint32_t*)e->d_win.p);
+    HIPCHK(hipGetLastError());
   }
-  const int r = upload_locals(e, byPeer, e->cfg.max_peers, e->stream);
-  if (r) return r;
+  hipLaunchKernelGGL(io::fill_locals, dim3(io_grid(cap)), dim3(io::kIoBlock), 0, s, dloc,
+                     (const uint32_t*)e->d_win.p, cap, e->ln);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
   e->locals_set = n > 0;
   return GR_OK;
 }
@@ -765,11 +804,17 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
 
 int gr_collect_results(gr_engine* e, uint32_t first, gr_peer_result* out, size_t n) {
   if (!e || (n && !out) || (uint64_t)first + n > e->cfg.max_peers) return GR_EINVAL;
+  if (n == 0) return GR_OK;
+  std::lock_guard<std::mutex> guard(e->mu);
   HIPCHK(hipDeviceSynchronize());
-  std::vector<gr_peer_result> tmp;
-  const int r = download_results(e, first, (uint32_t)n, &tmp, nullptr);
-  if (r) return r;
-  memcpy(out, tmp.data(), n * sizeof(gr_peer_result));
+  const size_t bytes = n * sizeof(gr_peer_result);
+  int r;
+  if ((r = grow_device(&e->d_results.p, &e->d_results.n, bytes))) return r;
+  hipLaunchKernelGGL(io::pack_results, dim3(io_grid(n)), dim3(io::kIoBlock), 0, e->stream, e->ln, e->st,
+                     (const uint32_t*)nullptr, first, (uint32_t)n, (gr_peer_result*)e->d_results.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, e->d_results.p, bytes, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
   return GR_OK;
 }
 

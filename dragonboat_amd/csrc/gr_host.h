@@ -1,6 +1,8 @@
-// gr_host.h — host-side helpers shared by libgpuraft.so and the test-only
-// CPU harness: gr_peer <-> SoA row conversion and the message codec of the
-// mailbox spaces (gr_layout.h). No HIP runtime calls.
+// gr_host.h — helpers shared by libgpuraft.so and the test-only CPU harness:
+// gr_peer <-> SoA row conversion and the message codec of the mailbox spaces
+// (gr_layout.h). No HIP runtime calls. The codec, validation and result
+// derivation are __host__ __device__: the boundary kernels (gr_io.h) run the
+// same functions on the device.
 #pragma once
 #include <algorithm>
 #include <cstring>
@@ -111,7 +113,7 @@ inline void set_u8_row(gr_peer& g, uint32_t row, uint32_t S, uint8_t v) {
   g.read_index[r].ack_bits = v;
 }
 
-inline int validate_msg(const gr_message& m, uint32_t S, uint32_t cap) {
+__host__ __device__ inline int validate_msg(const gr_message& m, uint32_t S, uint32_t cap) {
   if (m.peer >= cap || m.slot >= S) return GR_EINVAL;
   if (m.type > GR_TIMEOUT_NOW) return GR_EINVAL;
   if (m.n_runs > 2) return GR_EINVAL;
@@ -121,7 +123,7 @@ inline int validate_msg(const gr_message& m, uint32_t S, uint32_t cap) {
   return GR_OK;
 }
 
-inline void encode_msg(const Mailbox& mb, uint32_t k, const gr_message& m) {
+__host__ __device__ inline void encode_msg(const Mailbox& mb, uint32_t k, const gr_message& m) {
   if (wide_term(m.term, m.log_term, m.run_term[0], m.run_term[1])) {  // cannot travel: receiver escalates
     mb.type(k) = MT_WIDE;
     return;
@@ -147,9 +149,8 @@ inline void encode_msg(const Mailbox& mb, uint32_t k, const gr_message& m) {
 }
 
 // Decode one message; fields a type does not carry on the device are zero.
-inline gr_message decode_msg(const Mailbox& mb, uint32_t k) {
-  gr_message m;
-  memset(&m, 0, sizeof(m));
+__host__ __device__ inline gr_message decode_msg(const Mailbox& mb, uint32_t k) {
+  gr_message m{};  // no padding in gr_message: every byte is a zeroed field
   m.type = mb.type(k);
   const uint8_t fl = mb.flags(k);
   m.reject = (fl & MFL_REJECT) ? 1 : 0;
@@ -268,7 +269,7 @@ inline int pack_inbox(const gr_inbox* in, uint32_t S, uint32_t max_peers, Packed
 // The proposal fields of a result record from the lane rows (gr_layout.h RF_*):
 // propose_first is not stored, it follows from last_index since proposals are
 // the only appends of a pass that reports them.
-inline void derive_proposals(gr_peer_result* pr, uint8_t rf, uint8_t pres, uint64_t last_index,
+__host__ __device__ inline void derive_proposals(gr_peer_result* pr, uint8_t rf, uint8_t pres, uint64_t last_index,
                              uint32_t local_n, uint8_t fwd_n, uint32_t fwd_entries) {
   uint64_t n = 0;
   if (rf & RF_PROPOSE) {
@@ -377,7 +378,7 @@ inline bool is_loopback(const uint32_t* base, uint32_t G, uint32_t R, uint32_t S
 }
 
 // Local-input rows of a lane block (host copies).
-inline void locals_to_rows(const gr_local_input& x, uint32_t* ticks, uint32_t* qticks, uint32_t* prop,
+__host__ __device__ inline void locals_to_rows(const gr_local_input& x, uint32_t* ticks, uint32_t* qticks, uint32_t* prop,
                            uint8_t* lflags, uint64_t* rlo, uint64_t* rhi, uint64_t* rnd, uint32_t* lword) {
   *ticks = x.ticks;
   *qticks = x.quiesced_ticks;
