@@ -245,6 +245,7 @@ struct gr_engine {
   Buf d_tmp;                // rocprim scratch
   Buf d_scal;               // lane count, error, outbox total
   Buf d_outmsgs, d_results; // packed outbox
+  Buf d_peers, d_slots;     // gr_peer records of a load/sync, slot list
   uint8_t* h_outmsgs = nullptr;  // pinned: returned to the caller until gr_release_outbox
   uint8_t* h_results = nullptr;
   uint8_t* h_scal = nullptr;
@@ -277,50 +278,6 @@ namespace {
     hipError_t _e = (x);                       \
     if (_e != hipSuccess) return GR_EDEVICE;   \
   } while (0)
-
-constexpr uint32_t kStageChunk = 1u << 16;
-
-int transfer_state(gr_engine* e, uint32_t first, size_t n, gr_peer* host, bool to_device) {
-  if (!e || (n && !host)) return GR_EINVAL;
-  if ((uint64_t)first + n > e->cfg.max_peers) return GR_ERANGE;
-  const uint32_t S = e->S, n64 = rows_u64(S), n8 = rows_u8(S);
-  std::vector<uint64_t> b64;
-  std::vector<uint8_t> b8;
-  for (size_t base = 0; base < n; base += kStageChunk) {
-    const uint32_t m = (uint32_t)std::min<size_t>(kStageChunk, n - base);
-    b64.assign((size_t)n64 * m, 0);
-    b8.assign((size_t)n8 * m, 0);
-    if (to_device) {
-      for (uint32_t k = 0; k < m; ++k) {
-        const gr_peer& g = host[base + k];
-        if (g.n_runs > GR_K || g.read_index_count > GR_Q) return GR_EINVAL;
-        if (g.self_slot != GR_SLOT_NONE && g.self_slot >= S) return GR_EINVAL;
-        for (uint32_t r = 0; r < n64; ++r) b64[(size_t)r * m + k] = get_u64_row(g, r, S);
-        for (uint32_t r = 0; r < n8; ++r) b8[(size_t)r * m + k] = get_u8_row(g, r, S);
-      }
-      for (uint32_t r = 0; r < n64; ++r)
-        HIPCHK(hipMemcpy(e->st.u64(r) + first + base, b64.data() + (size_t)r * m, (size_t)m * 8,
-                         hipMemcpyHostToDevice));
-      for (uint32_t r = 0; r < n8; ++r)
-        HIPCHK(hipMemcpy(e->st.u8(r) + first + base, b8.data() + (size_t)r * m, (size_t)m,
-                         hipMemcpyHostToDevice));
-    } else {
-      for (uint32_t r = 0; r < n64; ++r)
-        HIPCHK(hipMemcpy(b64.data() + (size_t)r * m, e->st.u64(r) + first + base, (size_t)m * 8,
-                         hipMemcpyDeviceToHost));
-      for (uint32_t r = 0; r < n8; ++r)
-        HIPCHK(hipMemcpy(b8.data() + (size_t)r * m, e->st.u8(r) + first + base, (size_t)m,
-                         hipMemcpyDeviceToHost));
-      for (uint32_t k = 0; k < m; ++k) {
-        gr_peer& g = host[base + k];
-        memset(&g, 0, sizeof(g));
-        for (uint32_t r = 0; r < n64; ++r) set_u64_row(g, r, S, b64[(size_t)r * m + k]);
-        for (uint32_t r = 0; r < n8; ++r) set_u8_row(g, r, S, b8[(size_t)r * m + k]);
-      }
-    }
-  }
-  return GR_OK;
-}
 
 StepParams base_params(gr_engine* e) {
   StepParams kp;
@@ -355,6 +312,59 @@ int grow_pinned(uint8_t** p, size_t* have, size_t want) {
 uint32_t io_grid(size_t n) {
   const size_t b = (n + io::kIoBlock - 1) / io::kIoBlock;
   return (uint32_t)std::max<size_t>(1, std::min<size_t>(b, 4096));
+}
+
+// gr_peer records <-> state rows for slots [first, first+n) or a slot list
+// (gr_io.h): the records cross PCIe once, the transpose runs on the device.
+int transfer(gr_engine* e, const uint32_t* slots, uint32_t first, size_t n, gr_peer* host, bool to_device) {
+  if (!e || (n && !host)) return GR_EINVAL;
+  const uint32_t cap = e->cfg.max_peers;
+  if (!slots && (uint64_t)first + n > cap) return GR_ERANGE;
+  if (n == 0) return GR_OK;
+  if (n >= 0x80000000ull) return GR_EINVAL;
+  if (slots && !to_device)
+    for (size_t x = 0; x < n; ++x)
+      if (slots[x] >= cap) return GR_ERANGE;
+  std::lock_guard<std::mutex> guard(e->mu);
+  HIPCHK(hipDeviceSynchronize());  // passes in flight on other streams own the rows
+  const hipStream_t s = e->stream;
+  const size_t bytes = n * sizeof(gr_peer);
+  int r;
+  if ((r = grow_device(&e->d_peers.p, &e->d_peers.n, bytes))) return r;
+  const uint32_t* dslots = nullptr;
+  if (slots) {
+    if ((r = grow_device(&e->d_slots.p, &e->d_slots.n, n * 4))) return r;
+    HIPCHK(hipMemcpyAsync(e->d_slots.p, slots, n * 4, hipMemcpyHostToDevice, s));
+    dslots = (const uint32_t*)e->d_slots.p;
+  }
+  gr_peer* dp = (gr_peer*)e->d_peers.p;
+  const dim3 grid(io_grid(n)), blk(io::kIoBlock);
+  if (to_device) {
+    if ((r = grow_device(&e->d_mark.p, &e->d_mark.n, (size_t)cap * 4))) return r;
+    if ((r = grow_device(&e->d_scal.p, &e->d_scal.n, 16))) return r;
+    if ((r = grow_pinned(&e->h_scal, &e->h_scal_bytes, 16))) return r;
+    HIPCHK(hipMemcpyAsync(dp, host, bytes, hipMemcpyHostToDevice, s));
+    if (slots) HIPCHK(hipMemsetAsync(e->d_mark.p, 0, (size_t)cap * 4, s));
+    HIPCHK(hipMemsetAsync(e->d_scal.p, 0, 16, s));
+    hipLaunchKernelGGL(io::check_peers, grid, blk, 0, s, (const gr_peer*)dp, dslots, (uint32_t)n, e->S, cap,
+                       (uint32_t*)e->d_mark.p, (uint32_t*)e->d_scal.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(e->h_scal, e->d_scal.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const uint32_t err = *(uint32_t*)e->h_scal;
+    if (err & io::ERR_SLOT) return GR_ERANGE;  // no row was written
+    if (err & io::ERR_PEER) return GR_EINVAL;
+    hipLaunchKernelGGL(io::peers_to_rows, grid, blk, 0, s, (const gr_peer*)dp, dslots, first, (uint32_t)n, e->st,
+                       e->S);
+    HIPCHK(hipGetLastError());
+  } else {
+    HIPCHK(hipMemsetAsync(dp, 0, bytes, s));
+    hipLaunchKernelGGL(io::rows_to_peers, grid, blk, 0, s, e->st, dslots, first, (uint32_t)n, e->S, dp);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(host, dp, bytes, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  return GR_OK;
 }
 
 // Exclusive sum of n u32 on `s` (rocprim), scratch grown on demand.
@@ -452,7 +462,7 @@ void gr_destroy(gr_engine* e) {
   free_timings(e);
   for (gr_engine::Buf* b : {&e->d_in, &e->d_out, &e->d_msgs, &e->d_locals, &e->d_mark, &e->d_lop, &e->d_keys,
                             &e->d_idx, &e->d_skeys, &e->d_sidx, &e->d_win, &e->d_oc, &e->d_off, &e->d_tmp,
-                            &e->d_scal, &e->d_outmsgs, &e->d_results})
+                            &e->d_scal, &e->d_outmsgs, &e->d_results, &e->d_peers, &e->d_slots})
     if (b->p) (void)hipFree(b->p);
   for (uint8_t* h : {e->h_outmsgs, e->h_results, e->h_scal})
     if (h) (void)hipHostFree(h);
@@ -461,13 +471,21 @@ void gr_destroy(gr_engine* e) {
 }
 
 int gr_load_groups(gr_engine* e, uint32_t first, const gr_peer* peers, size_t n) {
-  if (e) HIPCHK(hipDeviceSynchronize());
-  return transfer_state(e, first, n, const_cast<gr_peer*>(peers), true);
+  return transfer(e, nullptr, first, n, const_cast<gr_peer*>(peers), true);
 }
 
 int gr_sync_groups_to_host(gr_engine* e, uint32_t first, gr_peer* out, size_t n) {
-  if (e) HIPCHK(hipDeviceSynchronize());
-  return transfer_state(e, first, n, out, false);
+  return transfer(e, nullptr, first, n, out, false);
+}
+
+int gr_load_peers(gr_engine* e, const uint32_t* slots, const gr_peer* peers, size_t n) {
+  if (n && !slots) return GR_EINVAL;
+  return transfer(e, slots, 0, n, const_cast<gr_peer*>(peers), true);
+}
+
+int gr_sync_peers_to_host(gr_engine* e, const uint32_t* slots, gr_peer* out, size_t n) {
+  if (n && !slots) return GR_EINVAL;
+  return transfer(e, slots, 0, n, out, false);
 }
 
 uint64_t gr_space_chunk_bytes(uint32_t positions, uint32_t depth) {

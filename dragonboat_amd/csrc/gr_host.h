@@ -13,8 +13,9 @@
 namespace gr {
 namespace host {
 
-// Row accessors between gr_peer and the SoA state rows (host side).
-inline uint64_t get_u64_row(const gr_peer& g, uint32_t row, uint32_t S) {
+// Row accessors between gr_peer and the SoA state rows (also run by the
+// load/sync passes of gr_io.h on the device).
+__host__ __device__ inline uint64_t get_u64_row(const gr_peer& g, uint32_t row, uint32_t S) {
   if (row < SR_RUN_START) {
     const uint64_t v[] = {g.term, g.vote, g.committed, g.applied, g.last_index, g.first_index_m1,
                           g.leader_id, g.leader_transfer_target, g.node_id, g.election_tick,
@@ -39,7 +40,7 @@ inline uint64_t get_u64_row(const gr_peer& g, uint32_t row, uint32_t S) {
   r -= GR_Q;
   return g.read_index[r].ctx_high;
 }
-inline void set_u64_row(gr_peer& g, uint32_t row, uint32_t S, uint64_t v) {
+__host__ __device__ inline void set_u64_row(gr_peer& g, uint32_t row, uint32_t S, uint64_t v) {
   if (row < SR_RUN_START) {
     uint64_t* f[] = {&g.term, &g.vote, &g.committed, &g.applied, &g.last_index, &g.first_index_m1,
                      &g.leader_id, &g.leader_transfer_target, &g.node_id, &g.election_tick,
@@ -66,7 +67,7 @@ inline void set_u64_row(gr_peer& g, uint32_t row, uint32_t S, uint64_t v) {
   g.read_index[r].ctx_high = v;
 }
 // u8 rows: state flags self n_runs ri_count, rstate[S], ractive[S], rkind[S], rifrom[Q], riack[Q]
-inline uint8_t get_u8_row(const gr_peer& g, uint32_t row, uint32_t S) {
+__host__ __device__ inline uint8_t get_u8_row(const gr_peer& g, uint32_t row, uint32_t S) {
   switch (row) {
     case 0: return g.state;
     case 1: {
@@ -93,7 +94,7 @@ inline uint8_t get_u8_row(const gr_peer& g, uint32_t row, uint32_t S) {
   r -= GR_Q;
   return g.read_index[r].ack_bits;
 }
-inline void set_u8_row(gr_peer& g, uint32_t row, uint32_t S, uint8_t v) {
+__host__ __device__ inline void set_u8_row(gr_peer& g, uint32_t row, uint32_t S, uint8_t v) {
   switch (row) {
     case 0: g.state = v; return;
     case 1: g.flags = (uint8_t)(v & F_PUBLIC); return;

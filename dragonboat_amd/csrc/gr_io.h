@@ -178,5 +178,45 @@ __global__ void pack_results(LaneBase L, StateBase st, const uint32_t* peer_of_l
   }
 }
 
+// ---- gr_peer records <-> SoA state rows: gr_load_groups/gr_sync_groups_to_host
+// (slot range) and gr_load_peers/gr_sync_peers_to_host (slot list, the
+// escalation hand-off of scattered groups). slots == nullptr: slot first + x.
+constexpr uint32_t ERR_PEER = 1, ERR_SLOT = 2;
+
+__global__ void check_peers(const gr_peer* in, const uint32_t* slots, uint32_t n, uint32_t S, uint32_t cap,
+                            uint32_t* mark, uint32_t* err) {
+  for (uint32_t x = io_tid(); x < n; x += io_stride()) {
+    const gr_peer& g = in[x];
+    if (g.n_runs > GR_K || g.read_index_count > GR_Q || (g.self_slot != GR_SLOT_NONE && g.self_slot >= S))
+      atomicOr(err, ERR_PEER);
+    if (slots) {  // in range and listed once, so the load is order-free
+      if (slots[x] >= cap || atomicAdd(mark + slots[x], 1u) != 0) atomicOr(err, ERR_SLOT);
+    }
+  }
+}
+
+__global__ void peers_to_rows(const gr_peer* in, const uint32_t* slots, uint32_t first, uint32_t n, StateBase st,
+                              uint32_t S) {
+  const uint32_t n64 = rows_u64(S), n8 = rows_u8(S);
+  for (uint32_t x = io_tid(); x < n; x += io_stride()) {
+    const uint32_t p = slots ? slots[x] : first + x;
+    const gr_peer& g = in[x];
+    for (uint32_t r = 0; r < n64; ++r) st.u64(r)[p] = host::get_u64_row(g, r, S);
+    for (uint32_t r = 0; r < n8; ++r) st.u8(r)[p] = host::get_u8_row(g, r, S);
+  }
+}
+
+// `out` is zeroed first: fields with no row (padding, unused slots) read 0.
+__global__ void rows_to_peers(StateBase st, const uint32_t* slots, uint32_t first, uint32_t n, uint32_t S,
+                              gr_peer* out) {
+  const uint32_t n64 = rows_u64(S), n8 = rows_u8(S);
+  for (uint32_t x = io_tid(); x < n; x += io_stride()) {
+    const uint32_t p = slots ? slots[x] : first + x;
+    gr_peer& g = out[x];
+    for (uint32_t r = 0; r < n64; ++r) host::set_u64_row(g, r, S, st.u64(r)[p]);
+    for (uint32_t r = 0; r < n8; ++r) host::set_u8_row(g, r, S, st.u8(r)[p]);
+  }
+}
+
 }  // namespace io
 }  // namespace gr

@@ -41,6 +41,8 @@ def load_library(path=LIB_PATH):
     lib.gr_escalation_name.argtypes = [c.c_int]
     lib.gr_load_groups.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p, c.c_size_t]
     lib.gr_sync_groups_to_host.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p, c.c_size_t]
+    lib.gr_load_peers.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
+    lib.gr_sync_peers_to_host.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_step.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.POINTER(abi.Outbox)]
     lib.gr_release_outbox.argtypes = [c.c_void_p, c.POINTER(abi.Outbox)]
     lib.gr_stats_get.argtypes = [c.c_void_p, c.POINTER(abi.Stats)]
@@ -103,6 +105,23 @@ class Engine:
         n = self.max_peers - first if n is None else n
         out = np.zeros(n, dtype=abi.PEER)
         _check(self.lib.gr_sync_groups_to_host(self._h, first, out.ctypes.data, n), "gr_sync")
+        return out
+
+    def load_peers(self, slots, peers):
+        """Load records into a list of engine slots (gr_load_peers)."""
+        slots = np.ascontiguousarray(slots, np.uint32)
+        peers = np.ascontiguousarray(peers, dtype=abi.PEER)
+        assert len(slots) == len(peers)
+        _check(self.lib.gr_load_peers(self._h, slots.ctypes.data if len(slots) else None,
+                                      peers.ctypes.data if len(peers) else None, len(peers)), "gr_load_peers")
+
+    def sync_peers(self, slots):
+        """Records of a list of engine slots (gr_sync_peers_to_host)."""
+        slots = np.ascontiguousarray(slots, np.uint32)
+        out = np.zeros(len(slots), dtype=abi.PEER)
+        _check(self.lib.gr_sync_peers_to_host(self._h, slots.ctypes.data if len(slots) else None,
+                                              out.ctypes.data if len(out) else None, len(slots)),
+               "gr_sync_peers_to_host")
         return out
 
     def step(self, msgs=None, locals_=None):

@@ -248,6 +248,12 @@ const char* gr_escalation_name(int esc);
  * loadBucketNodes hook, execengine.go:403-430, and the escalation hand-off). */
 int gr_load_groups(gr_engine* e, uint32_t first, const gr_peer* peers, size_t n);
 int gr_sync_groups_to_host(gr_engine* e, uint32_t first, gr_peer* out, size_t n);
+/* The same for a list of engine slots (each listed once; GR_ERANGE for a slot
+ * out of range or listed twice, before anything is written): the escalation
+ * hand-off of scattered groups in one call, SURVEY.md §8b's
+ * gr_sync_groups_to_host(cluster_ids) with ids already mapped to slots. */
+int gr_load_peers(gr_engine* e, const uint32_t* slots, const gr_peer* peers, size_t n);
+int gr_sync_peers_to_host(gr_engine* e, const uint32_t* slots, gr_peer* out, size_t n);
 
 /* One synchronous pass over host buffers (what a cgo caller uses). */
 int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out);

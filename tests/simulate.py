@@ -49,8 +49,7 @@ class GpuBackend:
         return self.eng.sync(self.n)
 
     def load(self, idx, recs):
-        for p, rec in zip(idx, recs):
-            self.eng.load(np.array([rec], abi.PEER), first=int(p))
+        self.eng.load_peers(np.asarray(idx, np.uint32), np.asarray(recs, abi.PEER))  # one call, scattered slots
 
 
 def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, check=True,

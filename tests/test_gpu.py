@@ -140,3 +140,40 @@ def test_full_size_properties(gpu):
         msgs = topo.route_messages(o["msgs"])
     bad = parity.compare_states(final[idx], pop.export(), S)
     assert not bad, bad[:3]
+
+
+def test_load_sync_round_trip(gpu):
+    """gr_load_groups/gr_sync_groups_to_host and the slot-list variants
+    (gr_load_peers/gr_sync_peers_to_host) transpose records <-> state rows on the
+    device: every field comes back; bad input is refused before any row changes."""
+    from dragonboat_amd import abi
+    from dragonboat_amd.engine import Engine, GpuRaftError
+    import parity
+    G, R = 3000, 5
+    peers, _ = P.config3(G, R)
+    topo = P.Topology(G, R)
+    P.inject_leader_change(peers, topo, 0.2, np.random.default_rng(1))
+    n = len(peers)
+    eng = Engine(n, R)
+    eng.load(peers)
+    assert not parity.compare_states(eng.sync(n), peers, R)
+    # scattered slots, shuffled order
+    rng = np.random.default_rng(2)
+    slots = rng.permutation(n)[: n // 3].astype(np.uint32)
+    fresh = P.make_groups(G, R, seed=9)[: len(slots)]
+    eng.load_peers(slots, fresh)
+    got = eng.sync_peers(slots)
+    assert not parity.compare_states(got, fresh, R)
+    whole = eng.sync(n)
+    keep = np.setdiff1d(np.arange(n), slots)
+    assert not parity.compare_states(whole[keep], peers[keep], R)
+    before = eng.sync(n)
+    for bad_slots in (np.array([1, 2, 1], np.uint32), np.array([0, n], np.uint32)):
+        with pytest.raises(GpuRaftError):
+            eng.load_peers(bad_slots, fresh[: len(bad_slots)])
+    broken = fresh[:2].copy()
+    broken["n_runs"][1] = abi.GR_K + 1
+    with pytest.raises(GpuRaftError):
+        eng.load_peers(np.array([5, 6], np.uint32), broken)
+    assert not parity.compare_states(eng.sync(n), before, R)  # nothing written
+    eng.close()
