@@ -14,7 +14,7 @@ ARCH = "gfx950"
 
 ENGINE_SRC = [os.path.join(ROOT, "dragonboat_amd", "csrc", "gr_engine.hip")]
 ENGINE_DEPS = ENGINE_SRC + [os.path.join(ROOT, "dragonboat_amd", "csrc", f)
-                            for f in ("gr_lane.h", "gr_layout.h", "gr_host.h", "gr_fast.h", "gr_tick.h")] + \
+                            for f in ("gr_lane.h", "gr_layout.h", "gr_host.h", "gr_fast.h", "gr_tick.h", "gr_io.h")] + \
     [os.path.join(ROOT, "include", "gpuraft.h")]
 ENGINE_LIB = os.path.join(ROOT, "dragonboat_amd", "_build", "libgpuraft.so")
 ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
