@@ -1252,8 +1252,8 @@ struct Lane {
     }
     OutMsg o;
     o.type = GR_PROPOSE;
-    o.n = n;
-    if (has_cc) o.flags = MFL_REJECT;  // a Propose record's reject bit: the batch holds a ConfigChangeEntry
+    o.n = n;  // one run of n entries at term 0: appendEntries has not stamped them (raft.go:643-650)
+    o.flags = (uint8_t)((1u << MFL_RUNS_SHIFT) | (has_cc ? MFL_REJECT : 0u));  // reject bit: holds a ConfigChangeEntry
     bool dropped;
     GR_TRY(forward_to_leader(o, &dropped));
     prop_result = dropped ? GR_PROP_DROPPED : GR_PROP_FORWARDED;

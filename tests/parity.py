@@ -92,10 +92,6 @@ def compare_states(eng, orc, S, peers=None, limit=20):
 
 def _norm(m):
     row = [int(m[f]) for f in MSG_FIELDS]
-    if m["type"] == abi.PROPOSE:  # forwarded proposals: payload and terms stay host-side
-        row[MSG_FIELDS.index("n_runs")] = 0
-        row[MSG_FIELDS.index("run2_offset")] = 0
-        return tuple(row) + (0, 0)
     nr = int(m["n_runs"])
     return tuple(row) + (int(m["run_term"][0]) if nr >= 1 else 0, int(m["run_term"][1]) if nr == 2 else 0)
 

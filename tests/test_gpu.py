@@ -177,3 +177,66 @@ def test_load_sync_round_trip(gpu):
         eng.load_peers(np.array([5, 6], np.uint32), broken)
     assert not parity.compare_states(eng.sync(n), before, R)  # nothing written
     eng.close()
+
+
+def _interleave(msgs, rng):
+    """A random arrival order that keeps each mailbox's (peer, slot) own order."""
+    n = len(msgs)
+    perm = rng.permutation(n)
+    key = msgs["peer"].astype(np.int64) * 256 + msgs["slot"]
+    order = np.empty(n, np.int64)
+    for k in np.unique(key):
+        idx = np.nonzero(key == k)[0]          # original order within the mailbox
+        order[np.sort(perm[idx])] = idx        # the shuffled slots this mailbox got
+    return msgs[order]
+
+
+def test_gr_step_boundary_order_and_edges(gpu):
+    """gr_step's device boundary (gr_io.h): lanes, mailbox order and records do not
+    depend on how mailboxes interleave in the inbox; a mailbox given more than GR_C
+    messages escalates CAPACITY at the first that did not travel; the last local
+    record of a peer wins; a bad record fails the call before any state changes."""
+    from dragonboat_amd import abi
+    from dragonboat_amd.engine import Engine, GpuRaftError
+    import parity
+    G, R = 400, 3
+    peers = P.make_groups(G, R, seed=4)
+    topo = P.Topology(G, R)
+    P.inject_leader_change(peers, topo, 0.3, np.random.default_rng(4))
+    a, b = Engine(R * G, R), Engine(R * G, R)
+    a.load(peers)
+    b.load(peers)
+    rng = np.random.default_rng(5)
+    msgs = np.zeros(0, abi.MESSAGE)
+    for k in range(6):
+        loc = P.propose_locals(R * G, P.current_leaders(a.sync(R * G), topo), pass_index=k)
+        oa, ra = a.step(msgs, loc)
+        ob, rb = b.step(_interleave(msgs, rng), loc[rng.permutation(len(loc))])
+        assert np.array_equal(oa, ob) and np.array_equal(ra, rb)
+        assert not parity.compare_states(a.sync(R * G), b.sync(R * G), R)
+        msgs = topo.route_messages(oa)
+    # more than GR_C messages in one mailbox
+    st = a.sync(R * G)
+    f = int(np.nonzero(st["state"] == abi.FOLLOWER)[0][0])
+    hb = np.zeros(abi.GR_C + 2, abi.MESSAGE)
+    hb["peer"], hb["type"], hb["term"] = f, abi.HEARTBEAT, st["term"][f]
+    hb["slot"] = next(j for j in range(R) if j != st["self_slot"][f])
+    _, res = a.step(hb, None)
+    r = res[res["peer"] == f][0]
+    assert abi.ESC_NAMES[r["escalation"]] == "capacity" and r["esc_item"] == abi.GR_C
+    # the last local record of a peer wins
+    loc = np.zeros(2, abi.LOCAL)
+    loc["peer"] = f
+    loc["ticks"] = [3, 1]
+    before = a.sync(R * G)[f]["election_tick"]
+    a.step(None, loc)
+    assert a.sync(R * G)[f]["election_tick"] == before + 1
+    # bad records: nothing runs
+    snap = a.sync(R * G)
+    bad = hb[:2].copy()
+    bad["slot"][1] = R  # out of range
+    with pytest.raises(GpuRaftError):
+        a.step(bad, None)
+    assert not parity.compare_states(a.sync(R * G), snap, R)
+    a.close()
+    b.close()
