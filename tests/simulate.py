@@ -73,6 +73,10 @@ def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, c
         emsgs = msgs[~parked[msgs["peer"]]] if len(msgs) else msgs
         eloc = loc[~parked[loc["peer"]]]
         out, res = eng.step(emsgs, eloc)
+        if len(out):  # the engine's outbox is valid gr_step input (gr_host.h validate_msg)
+            nr, ne = out["n_runs"], out["n_entries"]
+            assert np.all(nr <= 2) and np.all((ne == 0) == (nr == 0)), "invalid outbox record"
+            assert np.all(out["type"] <= abi.TIMEOUT_NOW)
         lim = parity.limits_from(res, n)
         o = pop.step(msgs, loc, lim)
         esc = res[res["escalation"] != 0]
