@@ -495,6 +495,29 @@ uint64_t gr_space_chunk_bytes(uint32_t positions, uint32_t depth) {
 uint64_t gr_space_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth) {
   return (uint64_t)n_chunks * gr_space_chunk_bytes(positions, depth);
 }
+uint64_t gr_space_hot_chunk_bytes(uint32_t positions, uint32_t depth) {
+  if (depth == 0 || depth > GR_C) return 0;
+  return space_hot_chunk_bytes_pc(space_pad_positions(positions), depth);
+}
+
+int gr_space_cold_used(gr_engine* e, const void* space, uint32_t n_chunks, uint32_t positions, uint32_t depth,
+                       void* stream, uint32_t* out) {
+  if (!e || !space || !out || depth == 0 || depth > GR_C) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  int r;
+  if ((r = grow_device(&e->d_scal.p, &e->d_scal.n, 16))) return r;
+  if ((r = grow_pinned(&e->h_scal, &e->h_scal_bytes, 16))) return r;
+  const hipStream_t s = (hipStream_t)stream;
+  const SpaceView v = make_view(space, n_chunks, positions, depth);
+  uint32_t* flag = (uint32_t*)e->d_scal.p + 3;
+  HIPCHK(hipMemsetAsync(flag, 0, 4, s));
+  hipLaunchKernelGGL(io::cold_used, dim3(io_grid((size_t)n_chunks * v.pc)), dim3(io::kIoBlock), 0, s, v, flag);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->h_scal + 12, flag, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *out = *(uint32_t*)(e->h_scal + 12);
+  return GR_OK;
+}
 
 int gr_space_encode(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
                     const gr_message* msgs, size_t n, const uint32_t* pos_of_msg) {

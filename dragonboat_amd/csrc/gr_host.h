@@ -294,7 +294,8 @@ inline SpaceView make_view(const void* base, uint32_t n_chunks, uint32_t positio
   v.base = (uint8_t*)base;
   v.n_chunks = n_chunks;
   v.pc = space_pad_positions(positions);
-  v.chunk_bytes = space_chunk_bytes_pc(v.pc, depth);
+  v.hot_bytes = space_hot_chunk_bytes_pc(v.pc, depth);
+  v.cold_bytes = space_cold_chunk_bytes_pc(v.pc, depth);
   v.depth = depth;
   return v;
 }

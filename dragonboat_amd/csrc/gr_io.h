@@ -178,6 +178,17 @@ __global__ void pack_results(LaneBase L, StateBase st, const uint32_t* peer_of_l
   }
 }
 
+// Does any mailbox of the space hold a message with cold fields (nonempty and
+// without MB_ALLCOMPACT)? One store per wave that finds one.
+__global__ void cold_used(SpaceView v, uint32_t* flag) {
+  const uint64_t n = (uint64_t)v.n_chunks * v.pc;
+  for (uint64_t g = io_tid(); g < n; g += io_stride()) {
+    const uint8_t c = v.base[(g / v.pc) * v.hot_bytes + g % v.pc];
+    const bool cold = (c & MB_COUNT) && !(c & MB_ALLCOMPACT);
+    if (__ballot(cold) && (threadIdx.x & 63) == 0) *flag = 1;
+  }
+}
+
 // ---- gr_peer records <-> SoA state rows: gr_load_groups/gr_sync_groups_to_host
 // (slot range) and gr_load_peers/gr_sync_peers_to_host (slot list, the
 // escalation hand-off of scattered groups). slots == nullptr: slot first + x.

@@ -14,9 +14,17 @@
 // Messages live in "spaces" of mailboxes. A mailbox holds up to GR_C messages
 // sent by one remote to one peer in one pass; message fields are SoA inside a
 // chunk so a wave of lanes reading "message k of its mailbox" is coalesced.
-// Chunk layout (pc = positions per chunk, a multiple of 64):
-//   [cnt u8 x pc] then for k < GR_C: [type u8 x pc][flags u8 x pc]
-//   [n u32 x pc][run2 u32 x pc][4 x (u32 x pc) terms][4 x (u64 x pc) indexes]
+// A space is n_chunks hot chunks followed by n_chunks cold chunks
+// (pc = positions per chunk, a multiple of 64; depth = messages per mailbox):
+//   hot chunk:  [cnt u8 x pc] then for k < depth:
+//               [type u8 x pc][flags u8 x pc][term u32 x pc][commit offset u32 x pc][LogIndex u64 x pc]
+//   cold chunk: for k < depth: [n u32][run2 u32][log term u32][run term 0 u32][run term 1 u32]
+//               [Commit u64][Hint u64][HintHigh u64] (each x pc)
+// Compact Replicates and non-reject ReplicateResps -- every steady-state message --
+// live in the hot chunk alone (18 B), and a mailbox whose messages all do carries
+// MB_ALLCOMPACT, so its readers never touch the cold chunk. An exchange between
+// GPUs moves the hot region always and the cold region only when some mailbox
+// lacks the bit (gr_space_cold_used).
 // Terms travel as 32 bits: a message whose term, log term or entry-run terms
 // reach 2^32 never enters a mailbox (the sender escalates GR_ESC_WIDE_TERM;
 // a host-encoded inbox marks it MT_WIDE and the receiver escalates there), so
@@ -182,37 +190,45 @@ __host__ __device__ inline bool wide_term(uint64_t a, uint64_t b, uint64_t c, ui
 __host__ __device__ inline uint32_t space_pad_positions(uint32_t positions) {
   return (positions + 63u) & ~63u;
 }
-__host__ __device__ inline uint64_t space_k_bytes(uint32_t pc) {
-  return (uint64_t)pc * (2 + 8 + 4 * MT_NUM + 8 * MF_NUM_U64);
+constexpr uint32_t kHotK = 18;   // bytes per position per message, hot chunk
+constexpr uint32_t kColdK = 44;  // ... cold chunk
+__host__ __device__ inline uint64_t round256(uint64_t b) { return (b + 255u) & ~(uint64_t)255u; }
+// A space's mailbox depth (1..GR_C) fixes its chunk sizes: spaces that cross
+// xGMI use the depth the steady state needs (2).
+__host__ __device__ inline uint64_t space_hot_chunk_bytes_pc(uint32_t pc, uint32_t depth = GR_C) {
+  return round256((uint64_t)pc * (1 + kHotK * depth));
 }
-// A space's mailbox depth (1..GR_C) fixes its chunk size: spaces that cross
-// xGMI use the depth the steady state needs (2) and move half the bytes.
+__host__ __device__ inline uint64_t space_cold_chunk_bytes_pc(uint32_t pc, uint32_t depth = GR_C) {
+  return round256((uint64_t)pc * kColdK * depth);
+}
 __host__ __device__ inline uint64_t space_chunk_bytes_pc(uint32_t pc, uint32_t depth = GR_C) {
-  uint64_t b = (uint64_t)pc + depth * space_k_bytes(pc);
-  return (b + 255u) & ~(uint64_t)255u;
+  return space_hot_chunk_bytes_pc(pc, depth) + space_cold_chunk_bytes_pc(pc, depth);
 }
 
 struct Mailbox {
-  uint8_t* chunk;
+  uint8_t* hot;   // the chunk's hot part
+  uint8_t* cold;  // ... and its cold part
   uint32_t local;
   uint32_t pc;
-  __host__ __device__ inline uint8_t* kblock(uint32_t k) const {
-    return chunk + pc + (uint64_t)k * space_k_bytes(pc);
-  }
-  __host__ __device__ inline uint8_t& cnt() const { return chunk[local]; }
-  __host__ __device__ inline uint8_t& type(uint32_t k) const { return kblock(k)[local]; }
-  __host__ __device__ inline uint8_t& flags(uint32_t k) const { return kblock(k)[pc + local]; }
-  __host__ __device__ inline uint32_t& n(uint32_t k) const {
-    return reinterpret_cast<uint32_t*>(kblock(k) + 2ull * pc)[local];
-  }
+  __host__ __device__ inline uint8_t* hk(uint32_t k) const { return hot + pc + (uint64_t)k * kHotK * pc; }
+  __host__ __device__ inline uint8_t* ck(uint32_t k) const { return cold + (uint64_t)k * kColdK * pc; }
+  __host__ __device__ inline uint8_t& cnt() const { return hot[local]; }
+  __host__ __device__ inline uint8_t& type(uint32_t k) const { return hk(k)[local]; }
+  __host__ __device__ inline uint8_t& flags(uint32_t k) const { return hk(k)[pc + local]; }
+  __host__ __device__ inline uint32_t& n(uint32_t k) const { return reinterpret_cast<uint32_t*>(ck(k))[local]; }
   __host__ __device__ inline uint32_t& run2(uint32_t k) const {
-    return reinterpret_cast<uint32_t*>(kblock(k) + 6ull * pc)[local];
+    return reinterpret_cast<uint32_t*>(ck(k) + 4ull * pc)[local];
   }
   __host__ __device__ inline uint32_t& t32(uint32_t k, uint32_t f) const {
-    return reinterpret_cast<uint32_t*>(kblock(k) + 10ull * pc + (uint64_t)f * 4ull * pc)[local];
+    if (f == MT_TERM) return reinterpret_cast<uint32_t*>(hk(k) + 2ull * pc)[local];
+    if (f == MT_CDELTA) return reinterpret_cast<uint32_t*>(hk(k) + 6ull * pc)[local];
+    // MT_LOG_TERM, MT_RT0, MT_RT1: cold words 2..4
+    return reinterpret_cast<uint32_t*>(ck(k) + (8ull + 4ull * (f - MT_LOG_TERM)) * pc)[local];
   }
   __host__ __device__ inline uint64_t& u64(uint32_t k, uint32_t f) const {
-    return reinterpret_cast<uint64_t*>(kblock(k) + (10ull + 4 * MT_NUM) * pc + (uint64_t)f * 8ull * pc)[local];
+    if (f == MF_LOG_INDEX) return reinterpret_cast<uint64_t*>(hk(k) + 10ull * pc)[local];
+    // MF_COMMIT, MF_HINT, MF_HINT_HIGH
+    return reinterpret_cast<uint64_t*>(ck(k) + (20ull + 8ull * (f - MF_COMMIT)) * pc)[local];
   }
 };
 
@@ -220,12 +236,14 @@ struct SpaceView {
   uint8_t* base;
   uint32_t n_chunks;
   uint32_t pc;
-  uint64_t chunk_bytes;
+  uint64_t hot_bytes;   // per chunk; the hot region is n_chunks * hot_bytes at base
+  uint64_t cold_bytes;  // per chunk; the cold region follows the hot region
   uint32_t depth;  // messages per mailbox (1..GR_C); emitting more escalates CAPACITY
   __host__ __device__ inline Mailbox at(uint32_t gpos) const {
     uint32_t c = gpos / pc;
     Mailbox m;
-    m.chunk = base + (uint64_t)c * chunk_bytes;
+    m.hot = base + (uint64_t)c * hot_bytes;
+    m.cold = base + (uint64_t)n_chunks * hot_bytes + (uint64_t)c * cold_bytes;
     m.local = gpos - c * pc;
     m.pc = pc;
     return m;

@@ -51,6 +51,10 @@ def load_library(path=LIB_PATH):
     lib.gr_space_bytes.argtypes = [c.c_uint32, c.c_uint32, c.c_uint32]
     lib.gr_space_chunk_bytes.restype = c.c_uint64
     lib.gr_space_chunk_bytes.argtypes = [c.c_uint32, c.c_uint32]
+    lib.gr_space_hot_chunk_bytes.restype = c.c_uint64
+    lib.gr_space_hot_chunk_bytes.argtypes = [c.c_uint32, c.c_uint32]
+    lib.gr_space_cold_used.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p,
+                                       c.POINTER(c.c_uint32)]
     lib.gr_bind_routes.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32]
     lib.gr_set_locals.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_step_device.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32,
@@ -163,6 +167,16 @@ class Engine:
 
     def chunk_bytes(self, positions, depth=MAILBOX_DEPTH):
         return int(self.lib.gr_space_chunk_bytes(positions, depth))
+
+    def hot_chunk_bytes(self, positions, depth=MAILBOX_DEPTH):
+        return int(self.lib.gr_space_hot_chunk_bytes(positions, depth))
+
+    def cold_used(self, space_ptr, n_chunks, positions, depth=MAILBOX_DEPTH, stream=0):
+        """True when some mailbox of the device space needs its cold fields (waits for `stream`)."""
+        v = ctypes.c_uint32()
+        _check(self.lib.gr_space_cold_used(self._h, space_ptr, n_chunks, positions, depth, stream,
+                                           ctypes.byref(v)), "gr_space_cold_used")
+        return bool(v.value)
 
     def bind_routes(self, in_pos, out_pos):
         """in_pos/out_pos: uint32 arrays [slots][n_peers] (mailbox positions, 0xFFFFFFFF = none)."""

@@ -14,9 +14,12 @@ their outgoing messages straight into mailbox "spaces" in HBM:
   some pair reaches (ordered by rank), the in space one per source rank, and
   one RCCL ``all_to_all_single`` with split sizes (0 for ranks no pair
   reaches) moves every mailbox across xGMI once per pass. At R = 3 that is
-  4 of N chunks for N ≥ 5, and the spaces hold depth-2 mailboxes (the steady
-  state's two Replicates per follower per pass; a third message escalates
-  CAPACITY): the exchange moves 125 B per mailbox instead of 249.
+  4 of N chunks for N ≥ 5, and the spaces hold depth-3 mailboxes (the steady
+  state's two Replicates per follower per pass plus a heartbeat on a tick; a
+  fourth message escalates CAPACITY). The hot region (counts + compact
+  Replicates + non-reject acks, 55 B per mailbox) crosses every pass; the cold
+  region (132 B per mailbox) only when some mailbox holds another kind of
+  message (gr_space_cold_used).
 
 Peers on a rank are laid out replica-major: peer r*G + g is replica r of the
 group (home = (rank - r) % N, index g), so a wave's accesses stay contiguous.
@@ -125,7 +128,7 @@ class Exchange:
             self.dests, self.srcs = spread_peer_ranks(R, world, rank)
             self.n_chunks = len(self.dests)
             assert len(self.srcs) == self.n_chunks
-            self.depth = 2
+            self.depth = 3  # two Replicates (or acks) + a heartbeat (or its ack) per pass
         else:
             raise ValueError(placement)
 
@@ -133,10 +136,16 @@ class Exchange:
         import torch
         nbytes = eng.space_bytes(self.n_chunks, self.positions, self.depth)
         cb = eng.chunk_bytes(self.positions, self.depth)
-        assert nbytes == self.n_chunks * cb and cb > 0
+        hb = eng.hot_chunk_bytes(self.positions, self.depth)
+        assert nbytes == self.n_chunks * cb and 0 < hb < cb
+        self.hot_region = self.n_chunks * hb  # hot chunks first, then the cold chunks
+        self.cold_exchanges = 0
         if self.placement == "spread":  # all_to_all split sizes, bytes per peer rank
-            self.out_splits = [cb if d in self.dests else 0 for d in range(self.world)]
-            self.in_splits = [cb if a in self.srcs else 0 for a in range(self.world)]
+            self.hot_splits = ([hb if d in self.dests else 0 for d in range(self.world)],
+                               [hb if a in self.srcs else 0 for a in range(self.world)])
+            cold = cb - hb
+            self.cold_splits = ([cold if d in self.dests else 0 for d in range(self.world)],
+                                [cold if a in self.srcs else 0 for a in range(self.world)])
         a = torch.zeros(nbytes, dtype=torch.uint8, device=device)
         b = torch.zeros(nbytes, dtype=torch.uint8, device=device)
         return [a, b]
@@ -155,12 +164,20 @@ class Exchange:
         if events is not None:
             events[1].record(stream)
         if self.placement == "spread":
-            import torch.distributed as dist
-            if self.world > 1:
-                dist.all_to_all_single(spaces[0], spaces[1], output_split_sizes=self.in_splits,
-                                       input_split_sizes=self.out_splits)
-            else:
-                spaces[0].copy_(spaces[1])
+            # the hot region always; the cold region only when a mailbox needs it
+            # (every steady-state message is hot-only: 37 B per depth-2 mailbox)
+            hr = self.hot_region
+            parts = [(slice(0, hr), self.hot_splits)]
+            if eng.cold_used(spaces[1].data_ptr(), self.n_chunks, self.positions, self.depth, h):
+                parts.append((slice(hr, None), self.cold_splits))
+                self.cold_exchanges += 1
+            for sl, (out_sp, in_sp) in parts:
+                if self.world > 1:
+                    import torch.distributed as dist
+                    dist.all_to_all_single(spaces[0][sl], spaces[1][sl], output_split_sizes=in_sp,
+                                           input_split_sizes=out_sp)
+                else:
+                    spaces[0][sl].copy_(spaces[1][sl])
 
 
 def build_exchange(G, R, S, world, rank, placement, seed=2):

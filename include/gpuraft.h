@@ -287,9 +287,18 @@ int gr_timing_end(gr_engine* e, gr_timing* out);
  * for remote slot j (0xFFFFFFFF = none). A chunk is one contiguous byte range,
  * so chunked spaces can be exchanged with one all-to-all.
  */
-/* 0 when depth is not in 1..GR_C. */
+/* 0 when depth is not in 1..GR_C. A space is n_chunks hot chunks then n_chunks
+ * cold chunks (gr_space_chunk_bytes = hot + cold per chunk): the hot region
+ * holds the mailbox counts and every field of compact Replicates and non-reject
+ * ReplicateResps, the cold region the rest. */
 uint64_t gr_space_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth);
 uint64_t gr_space_chunk_bytes(uint32_t positions, uint32_t depth);
+uint64_t gr_space_hot_chunk_bytes(uint32_t positions, uint32_t depth);
+/* *out = 1 when some mailbox of the (device) space holds a message with cold
+ * fields, i.e. the cold region must travel with the hot one; runs on `stream`
+ * and waits for it. */
+int gr_space_cold_used(gr_engine* e, const void* space, uint32_t n_chunks, uint32_t positions, uint32_t depth,
+                       void* stream, uint32_t* out);
 int gr_bind_routes(gr_engine* e, const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n_peers);
 int gr_set_locals(gr_engine* e, const gr_local_input* locals, size_t n);
 /* Launch one pass on `stream` (a hipStream_t, may be NULL) without syncing.

@@ -20,7 +20,9 @@ def inverse_routes(in_pos):
     return inv
 
 
-def run_device(G, R, passes, placement="local", seed=2):
+def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None):
+    """tick_every > 0: one Tick for every peer on passes k % tick_every == tick_every - 1
+    (leader heartbeats and their acks: messages with cold fields)."""
     import torch
     S = R
     ex = Exchange(G, R, S, 1, 0, placement, seed=seed)
@@ -29,7 +31,10 @@ def run_device(G, R, passes, placement="local", seed=2):
     eng.load(ex.peers)
     eng.bind_routes(ex.in_pos, ex.out_pos)
     from dragonboat_amd import populations as P
-    loc = P.propose_locals(n, ex.leader_slots, pass_index=0)
+    def locals_of(k):
+        tk = 1 if tick_every and k % tick_every == tick_every - 1 else 0
+        return P.propose_locals(n, ex.leader_slots, pass_index=0, ticks=tk)
+    loc = locals_of(0)
     eng.set_locals(loc)
     spaces = ex.allocate(eng, torch.device("cuda", 0))
     stream = torch.cuda.current_stream()
@@ -37,6 +42,9 @@ def run_device(G, R, passes, placement="local", seed=2):
     inv = inverse_routes(ex.in_pos)
     msgs = np.zeros(0, abi.MESSAGE)  # oracle's view of this pass's inbox
     for k in range(passes):
+        if tick_every:
+            loc = locals_of(k)
+            eng.set_locals(loc)
         ex.step(eng, spaces, k, stream)
         torch.cuda.synchronize()
         o = pop.step(msgs, loc)
@@ -60,6 +68,8 @@ def run_device(G, R, passes, placement="local", seed=2):
         assert not bad, f"pass {k}: results {bad[:3]}"
         msgs = want
     final = eng.sync(n)
+    if stats is not None:
+        stats["cold_exchanges"] = getattr(ex, "cold_exchanges", 0)
     eng.close()
     return final
 

@@ -67,6 +67,16 @@ def test_device_resident_path(gpu, placement):
     assert np.all(final["committed"][:777] > 2**32)
 
 
+def test_spread_cold_region_on_demand(gpu):
+    """Spread exchange: hot region every pass, cold region only on passes whose
+    mailboxes hold heartbeats/acks (ticks every third pass); parity every pass."""
+    import devsim
+    st = {}
+    final = devsim.run_device(500, 3, 9, placement="spread", tick_every=3, stats=st)
+    assert np.all(final["committed"][:500] > 2**32)
+    assert 0 < st["cold_exchanges"] < 9, st
+
+
 def test_bench_runs(gpu):
     """bench.py's contract on a small population (JSON line with roofline)."""
     import json
