@@ -183,3 +183,75 @@ def test_routes_not_affine_fall_back(built):
     in_pos = in_pos.copy()
     in_pos[1, 5], in_pos[1, 6] = in_pos[1, 6], in_pos[1, 5]
     assert hostlane_affine_routes(in_pos, out_pos, S) is None
+
+
+class _MockEngine:
+    """The C-ABI's space-size functions (CPU-callable) around a no-op pass: lets
+    Exchange.step's collective run over gloo on CPU tensors."""
+
+    def __init__(self, cold):
+        from dragonboat_amd.engine import load_library
+        self.lib = load_library()
+        self.cold = cold
+
+    def space_bytes(self, n, positions, depth):
+        return int(self.lib.gr_space_bytes(n, positions, depth))
+
+    def chunk_bytes(self, positions, depth):
+        return int(self.lib.gr_space_chunk_bytes(positions, depth))
+
+    def hot_chunk_bytes(self, positions, depth):
+        return int(self.lib.gr_space_hot_chunk_bytes(positions, depth))
+
+    def step_device(self, *a, **k):
+        pass
+
+    def cold_used(self, *a, **k):
+        return self.cold
+
+
+def _step_worker(rank, world, port, cold, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class _S:
+        cuda_stream = 0
+    G, R = 40, 3
+    ex = X.Exchange(G, R, R, world, rank, "spread")
+    eng = _MockEngine(cold)
+    spaces = ex.allocate(eng, torch.device("cpu"))
+    hr, n = ex.hot_region, ex.n_chunks
+    hb, cb = hr // n, len(spaces[1]) // n
+    out = spaces[1]
+    for c, d in enumerate(ex.dests):  # the kernel's writes: hot + cold part of chunk c (for rank d)
+        out[c * hb:(c + 1) * hb] = rank * 16 + d
+        out[hr + c * (cb - hb):hr + (c + 1) * (cb - hb)] = 128 + rank * 16 + d
+    ex.step(eng, spaces, 0, _S())
+    inp, errs = spaces[0], 0
+    for c, a in enumerate(ex.srcs):  # chunk c came from rank a
+        errs += int((inp[c * hb:(c + 1) * hb] != a * 16 + rank).sum())
+        want_cold = 128 + a * 16 + rank if cold else 0
+        errs += int((inp[hr + c * (cb - hb):hr + (c + 1) * (cb - hb)] != want_cold).sum())
+    q.put((rank, errs, ex.cold_exchanges))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cold", [(2, True), (3, False), (5, True)])
+def test_gloo_spread_step_regions(built, world, cold):
+    """Exchange.step over gloo: the hot region of every chunk reaches the rank it
+    was written for; the cold region travels only when gr_space_cold_used says so."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_step_worker, args=(r, world, port, cold, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(e == 0 for _, e, _ in res), res
+    assert all(c == int(cold) for _, _, c in res), res
