@@ -97,16 +97,16 @@ struct FastLane {
     uint32_t fl = (n ? (1u << MFL_RUNS_SHIFT) : 0u) | (narrow ? 0u : MFL_WIDE_COMMIT);
     if (compact) fl |= MFL_COMPACT | (n ? MFL_N1 : 0u);
     else outnc |= 1u << j;
-    mb.type(c) = GR_REPLICATE;
-    mb.flags(c) = (uint8_t)fl;
-    mb.t32(c, MT_TERM) = (uint32_t)(term);
-    mb.u64(c, MF_LOG_INDEX) = log_index;
-    if (narrow) mb.t32(c, MT_CDELTA) = cd;
+    ntst(mb.type(c), (uint8_t)(GR_REPLICATE));
+    ntst(mb.flags(c), (uint8_t)(fl));
+    ntst(mb.t32(c, MT_TERM), (uint32_t)((term)));
+    ntst(mb.u64(c, MF_LOG_INDEX), (uint64_t)(log_index));
+    if (narrow) ntst(mb.t32(c, MT_CDELTA), (uint32_t)(cd));
     else mb.u64(c, MF_COMMIT) = committed;
     if (!compact) {
-      mb.n(c) = n;
-      mb.t32(c, MT_LOG_TERM) = (uint32_t)(log_term);
-      if (n) mb.t32(c, MT_RT0) = (uint32_t)(rt0);
+      ntst(mb.n(c), (uint32_t)(n));
+      ntst(mb.t32(c, MT_LOG_TERM), (uint32_t)((log_term)));
+      if (n) ntst(mb.t32(c, MT_RT0), (uint32_t)((rt0)));
     }
     outc[j] = c + 1;
     nmo++;
@@ -118,12 +118,12 @@ struct FastLane {
     if (!ok) return;
     const Mailbox mb = kp.out.at(gpos);
     const uint32_t c = *cnt;
-    mb.type(c) = GR_REPLICATE_RESP;
-    mb.flags(c) = (uint8_t)(reject ? MFL_REJECT : 0u);
-    mb.t32(c, MT_TERM) = (uint32_t)(term);
-    mb.u64(c, MF_LOG_INDEX) = log_index;
+    ntst(mb.type(c), (uint8_t)(GR_REPLICATE_RESP));
+    ntst(mb.flags(c), (uint8_t)((reject ? MFL_REJECT : 0u)));
+    ntst(mb.t32(c, MT_TERM), (uint32_t)((term)));
+    ntst(mb.u64(c, MF_LOG_INDEX), (uint64_t)(log_index));
     if (reject) {
-      mb.u64(c, MF_HINT) = hint;
+      ntst(mb.u64(c, MF_HINT), (uint64_t)(hint));
       resp_nc = true;
     }
     *cnt = c + 1;
@@ -262,15 +262,15 @@ struct FastLane {
   // ------------------------------------------------------------- step
   GF_HD bool step(LaneStats* ls) {
     // ---- round 1: core, locals, routes
-    state = s8(Rw::B_STATE);
-    self = s8(Rw::B_SELF);
-    const uint32_t nbyte = s8(Rw::B_NRUNS);
+    state = ntld(s8(Rw::B_STATE));
+    self = ntld(s8(Rw::B_SELF));
+    const uint32_t nbyte = ntld(s8(Rw::B_NRUNS));
     nruns = nbyte & NR_MASK;
-    term = s64(SR_TERM);
-    committed = s64(SR_COMMITTED);
-    hi = s64(SR_LAST_INDEX);
-    const uint32_t flags = s8(Rw::B_FLAGS);
-    const uint32_t lw = kp.has_locals ? kp.ln.u32(LR_LWORD)[i] : 0u;  // packed locals (gr_layout.h)
+    term = ntld(s64(SR_TERM));
+    committed = ntld(s64(SR_COMMITTED));
+    hi = ntld(s64(SR_LAST_INDEX));
+    const uint32_t flags = ntld(s8(Rw::B_FLAGS));
+    const uint32_t lw = kp.has_locals ? ntld(kp.ln.u32(LR_LWORD)[i]) : 0u;  // packed locals (gr_layout.h)
     uint32_t gin[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
@@ -283,27 +283,27 @@ struct FastLane {
     uint32_t allc = 0;  // in mailboxes whose messages are all compact (MB_ALLCOMPACT)
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      const uint32_t b = gin[j] != NOPOS ? (uint32_t)kp.in.at(gin[j]).cnt() : 0u;
+      const uint32_t b = gin[j] != NOPOS ? (uint32_t)ntld(kp.in.at(gin[j]).cnt()) : 0u;
       cnt[j] = b & MB_COUNT;
       allc |= (b & MB_ALLCOMPACT) ? (1u << j) : 0u;
     }
     if (nruns) {
-      rsn = s64(SR_RUN_START + nruns - 1);
-      rtn = s64(SR_RUN_TERM + nruns - 1);
+      rsn = ntld(s64(SR_RUN_START + nruns - 1));
+      rtn = ntld(s64(SR_RUN_TERM + nruns - 1));
     }
     const bool leader = state == GR_LEADER;
     const uint32_t np = lw & 0xFFFFu;
     const uint32_t nq = (lw >> LW_QT_SHIFT) & LW_QT_MAX;
     uint64_t etick = 0;
-    if (nq) etick = s64(SR_ETICK);
+    if (nq) etick = ntld(s64(SR_ETICK));
     if (kLeaderPath && leader) {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        match[j] = s64(Rw::MATCH + j);
-        next[j] = s64(Rw::NEXT + j);
-        rst[j] = s8(Rw::B_RSTATE + j) & 3u;
-        ract[j] = s8(Rw::B_RACTIVE + j) & 1u;
-        rkind[j] = s8(Rw::B_RKIND + j) & 3u;
+        match[j] = ntld(s64(Rw::MATCH + j));
+        next[j] = ntld(s64(Rw::NEXT + j));
+        rst[j] = ntld(s8(Rw::B_RSTATE + j)) & 3u;
+        ract[j] = ntld(s8(Rw::B_RACTIVE + j)) & 1u;
+        rkind[j] = ntld(s8(Rw::B_RKIND + j)) & 3u;
       }
     }
     // ---- round 3: message fields
@@ -325,9 +325,9 @@ struct FastLane {
           lidx[j][k] = 0;
           if ((uint32_t)k < cnt[j]) {
             const Mailbox mb = kp.in.at(gin[j]);
-            lh[j][k] = (uint32_t)mb.type(k) | ((uint32_t)mb.flags(k) << 8);
-            lterm[j][k] = mb.t32(k, MT_TERM);
-            lidx[j][k] = mb.u64(k, MF_LOG_INDEX);
+            lh[j][k] = (uint32_t)ntld(mb.type(k)) | ((uint32_t)ntld(mb.flags(k)) << 8);
+            lterm[j][k] = ntld(mb.t32(k, MT_TERM));
+            lidx[j][k] = ntld(mb.u64(k, MF_LOG_INDEX));
           }
         }
       }
@@ -349,20 +349,20 @@ struct FastLane {
         fh[k] = 0; fn[k] = 0; fterm[k] = 0; fidx[k] = 0; flt[k] = 0; fcd[k] = 0; frt0[k] = 0;
         if ((uint32_t)k < cc) {
           const Mailbox mb = kp.in.at(gl);
-          fh[k] = (uint32_t)mb.type(k) | ((uint32_t)mb.flags(k) << 8);
-          fterm[k] = mb.t32(k, MT_TERM);
-          fidx[k] = mb.u64(k, MF_LOG_INDEX);
-          fcd[k] = mb.t32(k, MT_CDELTA);
+          fh[k] = (uint32_t)ntld(mb.type(k)) | ((uint32_t)ntld(mb.flags(k)) << 8);
+          fterm[k] = ntld(mb.t32(k, MT_TERM));
+          fidx[k] = ntld(mb.u64(k, MF_LOG_INDEX));
+          fcd[k] = ntld(mb.t32(k, MT_CDELTA));
           if (!lc) {  // a compact mailbox carries none of these
-            fn[k] = mb.n(k);
-            flt[k] = mb.t32(k, MT_LOG_TERM);
-            frt0[k] = mb.t32(k, MT_RT0);
+            fn[k] = ntld(mb.n(k));
+            flt[k] = ntld(mb.t32(k, MT_LOG_TERM));
+            frt0[k] = ntld(mb.t32(k, MT_RT0));
           }
         }
       }
       // electionTick = 0 and leaderID = remote_id(L) are usually already so
       // (F_ETZ, F_LSLOT): then neither is loaded nor rewritten
-      if (c && ((flags & F_LSLOT) >> F_LSLOT_SHIFT) != L + 1) rid = s64(Rw::RID + L);
+      if (c && ((flags & F_LSLOT) >> F_LSLOT_SHIFT) != L + 1) rid = ntld(s64(Rw::RID + L));
     }
     // ---- checks: anything outside the steady state goes to the general lane
     bool any_input = np != 0;
@@ -376,12 +376,12 @@ struct FastLane {
       GF_BAIL(any_input);
       if (!ok) return false;
       etick += nq;
-      s64(SR_ETICK) = etick;
-      if (flags & F_ETZ) s8(Rw::B_FLAGS) = (uint8_t)(flags & ~F_ETZ);
+      ntst(s64(SR_ETICK), (uint64_t)(etick));
+      if (flags & F_ETZ) ntst(s8(Rw::B_FLAGS), (uint8_t)((flags & ~F_ETZ)));
 #pragma unroll
       for (int j = 0; j < S; ++j)
-        if (gout[j] != NOPOS) kp.out.at(gout[j]).cnt() = 0;
-      kp.ln.u8(LR_RFLAGS)[i] = 0;
+        if (gout[j] != NOPOS) ntst(kp.out.at(gout[j]).cnt(), (uint8_t)(0));
+      ntst(kp.ln.u8(LR_RFLAGS)[i], (uint8_t)(0));
       return true;  // *ls stays zero
     }
     GF_BAIL(!leader && state != GR_FOLLOWER);
@@ -441,44 +441,44 @@ struct FastLane {
     }
     if (!ok) return false;
     // ---- stores (nothing above this line has written state)
-    if (committed != committed0) s64(SR_COMMITTED) = committed;
-    if (hi != hi0) s64(SR_LAST_INDEX) = hi;
+    if (committed != committed0) ntst(s64(SR_COMMITTED), (uint64_t)(committed));
+    if (hi != hi0) ntst(s64(SR_LAST_INDEX), (uint64_t)(hi));
     if (pushed) {  // the new run starts above the old newest run: NR_GE_LO still holds
-      s64(SR_RUN_START + nruns - 1) = rsn;
-      s64(SR_RUN_TERM + nruns - 1) = rtn;
-      s8(Rw::B_NRUNS) = (uint8_t)(nruns | NR_GE_LO);
+      ntst(s64(SR_RUN_START + nruns - 1), (uint64_t)(rsn));
+      ntst(s64(SR_RUN_TERM + nruns - 1), (uint64_t)(rtn));
+      ntst(s8(Rw::B_NRUNS), (uint8_t)((nruns | NR_GE_LO)));
     }
     if (kLeaderPath && leader) {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         if ((mdirty >> j) & 1u) {
-          s64(Rw::MATCH + j) = match[j];
-          s64(Rw::NEXT + j) = next[j];
+          ntst(s64(Rw::MATCH + j), (uint64_t)(match[j]));
+          ntst(s64(Rw::NEXT + j), (uint64_t)(next[j]));
         }
         if ((sdirty >> j) & 1u) {
-          s8(Rw::B_RSTATE + j) = (uint8_t)rst[j];
-          s8(Rw::B_RACTIVE + j) = (uint8_t)ract[j];
+          ntst(s8(Rw::B_RSTATE + j), (uint8_t)(rst[j]));
+          ntst(s8(Rw::B_RACTIVE + j), (uint8_t)(ract[j]));
         }
       }
 #pragma unroll
       for (int j = 0; j < S; ++j)
-        if ((snapz >> j) & 1u) s64(Rw::SNAP + j) = 0;
+        if ((snapz >> j) & 1u) ntst(s64(Rw::SNAP + j), (uint64_t)(0));
     } else if (c) {
       uint32_t nf = flags;
       if (!(flags & F_ETZ)) {
-        s64(SR_ETICK) = 0;  // electionTick = 0 (raft.go:1360)
+        ntst(s64(SR_ETICK), (uint64_t)(0));  // electionTick = 0 (raft.go:1360)
         nf |= F_ETZ;
       }
       if (((flags & F_LSLOT) >> F_LSLOT_SHIFT) != L + 1) {
-        s64(SR_LEADER_ID) = rid;  // setLeaderID(m.From)
+        ntst(s64(SR_LEADER_ID), (uint64_t)(rid));  // setLeaderID(m.From)
         nf = (nf & ~F_LSLOT) | ((L + 1) << F_LSLOT_SHIFT);
       }
-      if (nf != flags) s8(Rw::B_FLAGS) = (uint8_t)nf;
+      if (nf != flags) ntst(s8(Rw::B_FLAGS), (uint8_t)(nf));
     }
 #pragma unroll
     for (int j = 0; j < S; ++j)
       if (gout[j] != NOPOS)
-        kp.out.at(gout[j]).cnt() = (uint8_t)(outc[j] | (((outnc >> j) & 1u) ? 0u : MB_ALLCOMPACT));
+        ntst(kp.out.at(gout[j]).cnt(), (uint8_t)((outc[j] | (((outnc >> j) & 1u) ? 0u : MB_ALLCOMPACT))));
     uint8_t rf = 0;
     if (prop_result) {  // propose_first = last_index - n + 1 (gr_layout.h)
       rf |= RF_PROPOSE;
@@ -488,7 +488,7 @@ struct FastLane {
       rf |= RF_APPEND;
       kp.ln.u64(LR_APPEND_FROM)[i] = append_from;
     }
-    kp.ln.u8(LR_RFLAGS)[i] = rf;
+    ntst(kp.ln.u8(LR_RFLAGS)[i], (uint8_t)(rf));
     const bool adv = committed > committed0;
     ls->leader_commit = adv && leader;
     ls->follower_commit = adv && !leader;

@@ -205,6 +205,34 @@ __host__ __device__ inline uint64_t space_chunk_bytes_pc(uint32_t pc, uint32_t d
   return space_hot_chunk_bytes_pc(pc, depth) + space_cold_chunk_bytes_pc(pc, depth);
 }
 
+// Streaming access for the lean lane: every state and message byte of a pass
+// is touched once per pass and the working set is far above the caches, so its
+// loads carry the nontemporal hint: 0.148 vs 0.156 ms per 1M x 3 pass, A/B in
+// one call (GR_NT=0 builds without). Nontemporal stores (GR_NT_ST=1) measured
+// 0.152: the lane's stores stay default.
+#ifndef GR_NT
+#define GR_NT 1
+#endif
+template <class T>
+__host__ __device__ inline T ntld(const T& r) {
+#if GR_NT && defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_nontemporal_load(&r);
+#else
+  return r;
+#endif
+}
+#ifndef GR_NT_ST
+#define GR_NT_ST 0
+#endif
+template <class T>
+__host__ __device__ inline void ntst(T& r, T v) {
+#if GR_NT_ST && defined(__HIP_DEVICE_COMPILE__)
+  __builtin_nontemporal_store(v, &r);
+#else
+  r = v;
+#endif
+}
+
 struct Mailbox {
   uint8_t* hot;   // the chunk's hot part
   uint8_t* cold;  // ... and its cold part
