@@ -72,7 +72,7 @@ __device__ inline void block_stats(const StepParams& kp, const LaneStats& ls) {
 
 // Pass 1: every lane runs the lean steady-state lane (gr_fast.h). Lanes that
 // meet anything else store no state and are appended to one of kBailLists
-// lists (list = workgroup % kBailLists, one returning atomic per wave with a
+// lists (followers: list = workgroup % 8, leaders: 8 + workgroup % 8; one returning atomic per wave and role with a
 // bailing lane, a wave's lanes contiguous and ascending). Spreading the
 // appends over 16 counters 256 B apart keeps them from serialising when every
 // wave bails a few lanes (one shared counter: 105 us instead of 37 us on
@@ -88,19 +88,27 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   LaneStats ls;
   bool bail = false;
+  uint32_t role = 0;
   if (i < kp.n_lanes) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-    bail = !fast_step<S>(kp, i, p, &ls);  // leaves ls zero when it bails
+    bail = !fast_step<S>(kp, i, p, &ls, &role);  // leaves ls zero when it bails
   }
-  const uint64_t bm = __ballot(bail);
-  if (bm) {
-    const uint32_t list = blockIdx.x % kBailLists;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t first = (uint32_t)__ffsll((unsigned long long)bm) - 1;
-    uint32_t base = 0;
-    if (lane == first) base = atomicAdd(counters + list * kCounterStride, (uint32_t)__popcll(bm));
-    base = __shfl(base, (int)first);
-    if (bail) bail_list[(uint64_t)list * list_cap + base + (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
+  // followers into lists 0..7, leaders into 8..15: the general kernel walks the
+  // lists in order, so its waves hold one role and diverge less
+  const bool lead = role == GR_LEADER;
+#pragma unroll
+  for (uint32_t side = 0; side < 2; ++side) {
+    const bool mine = bail && (lead == (side == 1));
+    const uint64_t bm = __ballot(mine);
+    if (bm) {
+      const uint32_t list = (blockIdx.x % (kBailLists / 2)) + side * (kBailLists / 2);
+      const uint32_t lane = threadIdx.x & 63;
+      const uint32_t first = (uint32_t)__ffsll((unsigned long long)bm) - 1;
+      uint32_t base = 0;
+      if (lane == first) base = atomicAdd(counters + list * kCounterStride, (uint32_t)__popcll(bm));
+      base = __shfl(base, (int)first);
+      if (mine) bail_list[(uint64_t)list * list_cap + base + (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
+    }
   }
   if (kp.stats) block_stats(kp, ls);
 }

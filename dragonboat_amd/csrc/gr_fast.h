@@ -543,9 +543,11 @@ struct FastLane {
 
 // Kernel-side entry: the lean lane for lane i; false = hand the lane to the general kernel.
 template <int S>
-GF_HD bool fast_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls) {
+GF_HD bool fast_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, uint32_t* state = nullptr) {
   FastLane<S> L(kp, i, p);
-  return L.step(ls);
+  const bool done = L.step(ls);
+  if (state) *state = L.state;  // the role the lane entered the pass with
+  return done;
 }
 
 }  // namespace gr
