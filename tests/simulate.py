@@ -12,6 +12,8 @@ A peer whose full state no longer fits a gr_peer record (e.g. more than GR_Q
 pending ReadIndex requests) is "parked": the host steps it alone (the engine
 gets no input for it) until it fits again, then it is reloaded.
 """
+import os
+
 import numpy as np
 
 from dragonboat_amd import abi
@@ -53,7 +55,7 @@ class GpuBackend:
 
 
 def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, check=True,
-             max_report=3, drop_fn=None):
+             max_report=3, drop_fn=None, threads=None):
     """Run `passes` passes; returns a dict of counters. Raises AssertionError on divergence."""
     pop = OraclePopulation(peers, slots)
     eng = backend(peers, slots)
@@ -68,7 +70,9 @@ def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, c
             if changed is not None and len(changed):
                 pop.reload(changed, cur[changed])
                 eng.load(changed, cur[changed])
-        loc = locals_fn(k)
+        # locals_fn(k) or locals_fn(k, state): the second form sees the pass's
+        # starting state (e.g. to propose on the current leaders)
+        loc = locals_fn(k, pop.export()) if locals_fn.__code__.co_argcount == 2 else locals_fn(k)
         before = eng.sync()["committed"] if check else None
         emsgs = msgs[~parked[msgs["peer"]]] if len(msgs) else msgs
         eloc = loc[~parked[loc["peer"]]]
@@ -78,7 +82,7 @@ def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, c
             assert np.all(nr <= 2) and np.all((ne == 0) == (nr == 0)), "invalid outbox record"
             assert np.all(out["type"] <= abi.TIMEOUT_NOW)
         lim = parity.limits_from(res, n)
-        o = pop.step(msgs, loc, lim)
+        o = pop.step(msgs, loc, lim, threads=threads or min(16, os.cpu_count() or 1))
         esc = res[res["escalation"] != 0]
         stats["ready"] += int(res["n_ready"].sum())
         stats["forwarded"] += int(res["n_forwarded"].sum())

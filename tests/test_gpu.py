@@ -250,3 +250,35 @@ def test_gr_step_boundary_order_and_edges(gpu):
     assert not parity.compare_states(a.sync(R * G), snap, R)
     a.close()
     b.close()
+
+
+# ---- BASELINE.json configs 2, 3 and 5 at their full sizes, bit-exact against the
+# oracle after every pass (gr_step path; SIM.simulate compares state, messages and
+# results of every peer).
+
+def test_baseline_config2_full_size(gpu):
+    """configs[1]: 10k groups x 3 replicas, uniform proposals."""
+    st = _sim(10_000, 8, seed=2)
+    assert st["escalations"] == 0 and st["commits"] >= 10_000 * 6
+
+
+def test_baseline_config3_full_size(gpu):
+    """configs[2]: 100k groups x 5, 90% quiesced, ReadIndex on the active 10%,
+    acks dropped with p = 0.1, ticks, CheckQuorum on half."""
+    R, G = 5, 100_000
+    peers, active = P.config3(G, R)
+    topo = P.Topology(G, R)
+    rng = np.random.default_rng(3)
+    st = SIM.simulate(SIM.GpuBackend, peers, topo, 4, lambda k: P.config3_locals(G, R, active, k),
+                      slots=R, drop_fn=lambda k, m: P.drop_acks(m, 0.1, rng))
+    assert st["ready"] > 0
+
+
+def test_baseline_config5_full_size(gpu):
+    """configs[4]: 100k groups x 3 with leader changes injected at p = 0.1 per pass
+    (divergent suffixes, rejects, decreaseTo, truncation, forwarded proposals)."""
+    G, R = 100_000, 3
+    topo = P.Topology(G, R)
+    st = _sim(G, 6, seed=5, inject_p=0.1,
+              locals_fn=lambda k, cur: P.propose_locals(R * G, P.current_leaders(cur, topo), pass_index=k))
+    assert st["commits"] > 0 and st["forwarded"] > 0
