@@ -282,3 +282,10 @@ def test_baseline_config5_full_size(gpu):
     st = _sim(G, 6, seed=5, inject_p=0.1,
               locals_fn=lambda k, cur: P.propose_locals(R * G, P.current_leaders(cur, topo), pass_index=k))
     assert st["commits"] > 0 and st["forwarded"] > 0
+
+
+def test_baseline_config4_full_size_one_gpu(gpu):
+    """configs[3] at N=1: 1M groups x 3 replicas, every peer bit-exact against the
+    oracle after each of 3 passes (gr_step path; leaders commit on the third)."""
+    st = _sim(1_000_000, 3, seed=4)
+    assert st["escalations"] == 0 and st["commits"] > 0
