@@ -254,6 +254,9 @@ struct gr_engine {
   Buf d_scal;               // lane count, error, outbox total
   Buf d_outmsgs, d_results; // packed outbox
   Buf d_peers, d_slots;     // gr_peer records of a load/sync, slot list
+  uint8_t* h_inmsgs = nullptr;   // pinned inbox the caller may fill in place (gr_inbox_reserve)
+  uint8_t* h_inlocals = nullptr;
+  size_t h_inmsgs_bytes = 0, h_inlocals_bytes = 0;
   uint8_t* h_outmsgs = nullptr;  // pinned: returned to the caller until gr_release_outbox
   uint8_t* h_results = nullptr;
   uint8_t* h_scal = nullptr;
@@ -472,7 +475,7 @@ void gr_destroy(gr_engine* e) {
                             &e->d_idx, &e->d_skeys, &e->d_sidx, &e->d_win, &e->d_oc, &e->d_off, &e->d_tmp,
                             &e->d_scal, &e->d_outmsgs, &e->d_results, &e->d_peers, &e->d_slots})
     if (b->p) (void)hipFree(b->p);
-  for (uint8_t* h : {e->h_outmsgs, e->h_results, e->h_scal})
+  for (uint8_t* h : {e->h_outmsgs, e->h_results, e->h_scal, e->h_inmsgs, e->h_inlocals})
     if (h) (void)hipHostFree(h);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -696,6 +699,19 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
   out->n_msgs = total;
   out->results = (gr_peer_result*)e->h_results;
   out->n_results = nl;
+  return GR_OK;
+}
+
+int gr_inbox_reserve(gr_engine* e, size_t n_msgs, size_t n_locals, gr_inbox* in) {
+  if (!e || !in || n_msgs + n_locals >= 0x80000000ull) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  int r;
+  if ((r = grow_pinned(&e->h_inmsgs, &e->h_inmsgs_bytes, n_msgs * sizeof(gr_message) + 1))) return r;
+  if ((r = grow_pinned(&e->h_inlocals, &e->h_inlocals_bytes, n_locals * sizeof(gr_local_input) + 1))) return r;
+  in->msgs = (const gr_message*)e->h_inmsgs;
+  in->n_msgs = n_msgs;
+  in->locals = (const gr_local_input*)e->h_inlocals;
+  in->n_locals = n_locals;
   return GR_OK;
 }
 

@@ -45,6 +45,7 @@ def load_library(path=LIB_PATH):
     lib.gr_sync_peers_to_host.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_step.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.POINTER(abi.Outbox)]
     lib.gr_release_outbox.argtypes = [c.c_void_p, c.POINTER(abi.Outbox)]
+    lib.gr_inbox_reserve.argtypes = [c.c_void_p, c.c_size_t, c.c_size_t, c.POINTER(abi.Inbox)]
     lib.gr_stats_get.argtypes = [c.c_void_p, c.POINTER(abi.Stats)]
     lib.gr_stats_reset.argtypes = [c.c_void_p]
     lib.gr_space_bytes.restype = c.c_uint64
@@ -143,6 +144,17 @@ class Engine:
             ctypes.memmove(res.ctypes.data, ob.results, ob.n_results * abi.RESULT.itemsize)
         _check(self.lib.gr_release_outbox(self._h, ctypes.byref(ob)), "gr_release_outbox")
         return out, res
+
+    def reserve_inbox(self, n_msgs, n_locals):
+        """gr_inbox_reserve: (Inbox, msgs view, locals view) over engine-owned pinned
+        memory; fill the views, then step_inbox(Inbox)."""
+        ib = abi.Inbox()
+        _check(self.lib.gr_inbox_reserve(self._h, n_msgs, n_locals, ctypes.byref(ib)), "gr_inbox_reserve")
+        msgs = np.ctypeslib.as_array(ctypes.cast(ib.msgs, ctypes.POINTER(ctypes.c_uint8)),
+                                     (max(n_msgs, 1) * abi.MESSAGE.itemsize,)).view(abi.MESSAGE)[:n_msgs]
+        loc = np.ctypeslib.as_array(ctypes.cast(ib.locals, ctypes.POINTER(ctypes.c_uint8)),
+                                    (max(n_locals, 1) * abi.LOCAL.itemsize,)).view(abi.LOCAL)[:n_locals]
+        return ib, msgs, loc
 
     def stats(self):
         s = abi.Stats()

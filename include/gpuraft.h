@@ -257,6 +257,12 @@ int gr_sync_peers_to_host(gr_engine* e, const uint32_t* slots, gr_peer* out, siz
 
 /* One synchronous pass over host buffers (what a cgo caller uses). */
 int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out);
+/* Engine-owned pinned buffers for the next gr_step's inbox: sets in->msgs /
+ * in->locals to room for n_msgs / n_locals records and the counts to them. The
+ * caller writes the records in place (no staging copy; the upload runs at
+ * pinned-DMA rate) and passes `in` to gr_step. Valid until the next
+ * gr_inbox_reserve or gr_destroy; gr_step may also be given any other memory. */
+int gr_inbox_reserve(gr_engine* e, size_t n_msgs, size_t n_locals, gr_inbox* in);
 int gr_release_outbox(gr_engine* e, gr_outbox* out);
 int gr_stats_get(gr_engine* e, gr_stats* out);
 int gr_stats_reset(gr_engine* e);

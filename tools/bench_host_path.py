@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--replicas", type=int, default=3)
     ap.add_argument("--passes", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pinned", action="store_true", help="fill a gr_inbox_reserve buffer instead of passing pageable arrays")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -51,7 +52,12 @@ def main():
             eng.timing_begin()
         # the C-ABI call alone (what a Go step worker pays), then a copy out
         msgs = np.ascontiguousarray(msgs, abi.MESSAGE)  # alive across the call
-        ib = abi.inbox_of(msgs, loc)
+        if args.pinned:  # records written in place into engine-owned pinned memory (untimed)
+            ib, mv, lv = eng.reserve_inbox(len(msgs), len(loc))
+            mv[:] = msgs
+            lv[:] = loc
+        else:
+            ib = abi.inbox_of(msgs, loc)
         ob = abi.Outbox()
         t0 = time.perf_counter()
         rc = eng.lib.gr_step(eng._h, ctypes.byref(ib), ctypes.byref(ob))
@@ -74,7 +80,7 @@ def main():
     st = eng.stats()
     passes = args.passes
     line = {
-        "path": "gr_step (host arrays in/out, PCIe-inclusive)",
+        "path": "gr_step (host arrays in/out, PCIe-inclusive)" + (", pinned inbox" if args.pinned else ""),
         "groups": G, "replicas": R, "passes": passes,
         "ms_per_pass": t_step / passes * 1e3,
         "kernel_ms_per_pass": t_kern / passes * 1e3,
