@@ -20,6 +20,11 @@ ENGINE_LIB = os.path.join(ROOT, "dragonboat_amd", "_build", "libgpuraft.so")
 ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
 KAT_BIN = os.path.join(ROOT, "oracle", "_build", "kat_tests")
 HOSTLANE_LIB = os.path.join(ROOT, "tests", "_build", "libhostlane.so")
+WIRE_SRC = os.path.join(ROOT, "dragonboat_amd", "csrc", "gr_wire.hip")
+WIRE_DEPS = [WIRE_SRC, os.path.join(ROOT, "include", "gpuraft_wire.h"), os.path.join(ROOT, "include", "gpuraft.h")]
+WIRE_LIB = os.path.join(ROOT, "dragonboat_amd", "_build", "libgrwire.so")
+WIRE_ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "liboraclewire.so")
+HBM_CALIB = os.path.join(ROOT, "tools", "hbm_calib")
 
 
 def source_digest():
@@ -79,7 +84,39 @@ def build_hostlane(force=False):
     return HOSTLANE_LIB
 
 
+def build_wire(force=False):
+    """libgrwire.so: the wire codec (include/gpuraft_wire.h)."""
+    os.makedirs(os.path.dirname(WIRE_LIB), exist_ok=True)
+    if force or _stale(WIRE_LIB, WIRE_DEPS):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              "-I" + os.path.join(ROOT, "include"), WIRE_SRC, "-o", WIRE_LIB])
+    return WIRE_LIB
+
+
+def build_wire_oracle(force=False):
+    """liboraclewire.so: the codec's CPU restatement (test infrastructure)."""
+    odir = os.path.join(ROOT, "oracle")
+    os.makedirs(os.path.dirname(WIRE_ORACLE_LIB), exist_ok=True)
+    deps = [os.path.join(odir, "wire_oracle.hpp"), os.path.join(odir, "wire_capi.cpp"),
+            os.path.join(ROOT, "include", "gpuraft_wire.h")]
+    if force or _stale(WIRE_ORACLE_LIB, deps):
+        _run(["g++", "-std=c++17", "-O2", "-g", "-fPIC", "-shared", "-I" + odir, "-I" + os.path.join(ROOT, "include"),
+              os.path.join(odir, "wire_capi.cpp"), "-o", WIRE_ORACLE_LIB, "-lpthread"])
+    return WIRE_ORACLE_LIB
+
+
+def build_tools(force=False):
+    """tools/hbm_calib: known-byte-count kernels that calibrate the PMC byte counters."""
+    src = HBM_CALIB + ".hip"
+    if force or _stale(HBM_CALIB, [src]):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", src, "-o", HBM_CALIB])
+    return HBM_CALIB
+
+
 def build_all(force=False):
     build_engine(force)
+    build_wire(force)
     build_oracle(force)
+    build_wire_oracle(force)
     build_hostlane(force)
+    build_tools(force)

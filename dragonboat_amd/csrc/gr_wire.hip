@@ -1,0 +1,1076 @@
+// gr_wire.hip — libgrwire.so: the raft wire codec (MessageBatch / Message /
+// Entry marshal and unmarshal) as HIP passes for gfx950, C-ABI in
+// include/gpuraft_wire.h. SURVEY.md §8f-2.
+//
+// The work is byte parsing: varints, tag dispatch and bounds checks. It is
+// HBM/latency bound with no MFMA. Structure:
+//
+// decode (MessageBatch.Unmarshal, raft_optimized.go:1050-1202)
+//   1. walk_frames   one wave per frame walks the top-level fields through a
+//                    4 KiB LDS window loaded with coalesced 16-B reads: message
+//                    spans (into a scratch slot per 2 frame bytes, so no scan is
+//                    needed first), DeploymentId/SourceAddress/BinVer, the first
+//                    walk error and whether messageCount panics.
+//   2. scan          exclusive sum of messages per frame -> first_msg.
+//   3. decode_msgs   one lane per message: every Message field (last wins),
+//                    entries validated (colfer), entry count, Snapshot span.
+//   4. scan          exclusive sum of entries per message -> first_entry.
+//   5. decode_ents   one lane per message writes its Entry records.
+//   6. finish        one lane per frame: status = first error in wire order.
+// encode (MessageBatch.MarshalTo, raft.pb.go:1929-1958)
+//   1. size_msgs     one lane per message: Message.Size() and its field size.
+//   2. scan (u64)    message positions in the stream of message fields.
+//   3. frame_sizes   one lane per frame: MessageBatch.Size(); scan -> offsets.
+//   4. write_msgs    one lane per message writes tag, length and Message bytes.
+//   5. write_tails   one lane per frame writes DeploymentId/SourceAddress/BinVer.
+#include <hip/hip_runtime.h>
+
+#pragma clang diagnostic ignored "-Wunused-value"
+
+#include <cstring>
+#include <mutex>
+#include <new>
+
+#include <rocprim/rocprim.hpp>
+
+#include "gpuraft.h"
+#include "gpuraft_wire.h"
+
+namespace grw {
+
+using u8 = uint8_t;
+using u32 = uint32_t;
+using i32 = int32_t;
+using u64 = uint64_t;
+using i64 = int64_t;
+
+__device__ __forceinline__ i64 wrap_add(i64 a, i64 b) { return (i64)((u64)a + (u64)b); }
+
+// Snapshot{}.MarshalTo (raft.pb.go:1696-1735, empty Membership :1589-1594).
+__constant__ u8 kZeroSnap[12] = {0x12, 0x00, 0x18, 0x00, 0x20, 0x00, 0x28, 0x00, 0x32, 0x02, 0x08, 0x00};
+
+// ------------------------------------------------------------ byte readers --
+
+// Per-lane reader over buf[0, len): one aligned 16-B load per 16 bytes walked,
+// byte loads only for a chunk that crosses the buffer's ends.
+struct Rd {
+  const u8* buf;
+  u64 len;
+  u64 cbase;  // absolute offset of the cached chunk, ~0 = none
+  uint4 c;
+  __device__ Rd(const u8* b, u64 l) : buf(b), len(l), cbase(~0ull) {}
+  __device__ __forceinline__ u8 at(u64 a) {  // a < len
+    u64 base = a & ~15ull;
+    if (base != cbase) {
+      const u8* p = buf + base;
+      if ((((uintptr_t)p) & 15) == 0 && base + 16 <= len) {
+        const u32* q = (const u32*)p;
+        c.x = __builtin_nontemporal_load(q);
+        c.y = __builtin_nontemporal_load(q + 1);
+        c.z = __builtin_nontemporal_load(q + 2);
+        c.w = __builtin_nontemporal_load(q + 3);
+      } else {
+        u8 t[16];
+        for (int k = 0; k < 16; ++k) t[k] = (base + k < len) ? p[k] : 0;
+        memcpy(&c, t, 16);
+      }
+      cbase = base;
+    }
+    u32 w = (&c.x)[(a >> 2) & 3];
+    return (u8)(w >> (8 * (a & 3)));
+  }
+};
+
+// One frame's bytes through an LDS window, walked by a whole wave in lockstep
+// (every lane computes the same offsets, so branches stay uniform).
+constexpr int kWin = 4096;
+struct Win {
+  u8* lds;
+  const u8* buf;
+  u64 buf_len;
+  u64 lo, hi;
+  __device__ __forceinline__ void load(u64 at) {
+    __syncthreads();
+    lo = at & ~15ull;
+    hi = lo + kWin < buf_len ? lo + kWin : buf_len;
+    for (int k = threadIdx.x; k < kWin / 16; k += 64) {
+      u64 a = lo + (u64)k * 16;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      const u8* p = buf + a;
+      if (a + 16 <= buf_len && (((uintptr_t)p) & 15) == 0) {
+        v = *(const uint4*)p;
+      } else if (a < buf_len) {
+        u8 t[16];
+        for (int j = 0; j < 16; ++j) t[j] = (a + j < buf_len) ? p[j] : 0;
+        memcpy(&v, t, 16);
+      }
+      ((uint4*)lds)[k] = v;
+    }
+    __syncthreads();
+  }
+  __device__ __forceinline__ u8 at(u64 a) {  // a < buf_len
+    if (a < lo || a >= hi) load(a);
+    return lds[a - lo];
+  }
+};
+
+// Checked varint (raft_optimized.go:658-671) on a frame-relative cursor i over
+// [0, l); `R` maps frame offsets to bytes.
+template <class R>
+__device__ __forceinline__ int rd_varint(R& r, u64 base, i64 l, i64& i, u64& v) {
+  v = 0;
+  for (u32 shift = 0;; shift += 7) {
+    if (shift >= 64) return GRW_E_INT_OVERFLOW;
+    if (i >= l) return GRW_E_UNEXPECTED_EOF;
+    u8 b = r.at(base + (u64)i);
+    i++;
+    v |= (u64)(b & 0x7F) << shift;
+    if (b < 0x80) break;
+  }
+  return GRW_OK;
+}
+
+// messageCount / entryCount (raft_optimized.go:1014-1048 / 979-1012) over
+// [0, l): false where the reference indexes outside the slice (a panic).
+template <class R>
+__device__ bool count_chain_ok(R& r, u64 base, i64 l, i32 field) {
+  i64 i = 0;
+  while (i < l) {
+    u64 vv[2];
+    for (int k = 0; k < 2; ++k) {
+      u64 v = 0;
+      for (u64 shift = 0;; shift += 7) {
+        if (i < 0 || i >= l) return false;
+        u8 b = r.at(base + (u64)i);
+        i++;
+        if (shift < 64) v |= (u64)(b & 0x7F) << shift;
+        if (b < 0x80) break;
+      }
+      vv[k] = v;
+      if (k == 0 && (i32)(u32)(v >> 3) != field) return true;
+    }
+    i = wrap_add(i, (i64)vv[1]);
+  }
+  return true;
+}
+
+// skipRaft (raft.pb.go:5139-5236) on [0, l) relative to base; groups by depth.
+template <class R>
+__device__ int skip_raft(R& r, u64 base, i64 l, i64& n) {
+  i64 i = 0;
+  u64 depth = 0;
+  for (;;) {
+    if (i < 0) return GRW_E_PANIC;  // dAtA[-k] after a wrapped length inside a group
+    u64 wire;
+    int st = rd_varint(r, base, l, i, wire);
+    if (st) return st;
+    switch ((int)(wire & 7)) {
+      case 0:
+        for (u32 shift = 0;; shift += 7) {
+          if (shift >= 64) return GRW_E_INT_OVERFLOW;
+          if (i >= l) return GRW_E_UNEXPECTED_EOF;
+          i++;
+          if (r.at(base + (u64)(i - 1)) < 0x80) break;
+        }
+        break;
+      case 1: i = wrap_add(i, 8); break;
+      case 2: {
+        u64 len;
+        if ((st = rd_varint(r, base, l, i, len))) return st;
+        i = wrap_add(i, (i64)len);
+        if ((i64)len < 0) return GRW_E_INVALID_LENGTH;
+        break;
+      }
+      case 3: depth++; break;
+      case 4: depth--; break;
+      case 5: i = wrap_add(i, 4); break;
+      default: return GRW_E_ILLEGAL_WIRE_TYPE;
+    }
+    if (depth == 0) {
+      n = i;
+      return GRW_OK;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ decode --
+
+struct Scratch {
+  u64* spans;        // [buf_len/2 + 1] (msg start rel. frame) | (len << 32), slot frame_off/2 + k
+  u32* walked;       // [n] messages walked per frame
+  u32* first_msg;    // [n]
+  u64* walk_err;     // [n] status | level<<8 | panic<<16 | field<<32
+  u32* msg_batch;    // [msgs]
+  u32* ents_per_msg; // [msgs]
+  u32* first_ent;    // [msgs]
+  u64* msg_err;      // [msgs] status | level<<8 | field<<32
+};
+
+__device__ __forceinline__ u64 pack_err(int st, int lvl, int panic, u32 field) {
+  return (u64)(u32)st | ((u64)lvl << 8) | ((u64)panic << 16) | ((u64)field << 32);
+}
+
+// 1. One wave per frame: the MessageBatch.Unmarshal loop without decoding the
+// messages (raft_optimized.go:1050-1202).
+__global__ __launch_bounds__(64) void walk_frames(const u8* buf, u64 buf_len, grw_batch* batches, u32 n,
+                                                  Scratch s) {
+  __shared__ uint4 lds_raw[kWin / 16];
+  u32 b = blockIdx.x;
+  if (b >= n) return;
+  Win w{(u8*)lds_raw, buf, buf_len, 1, 0};
+  grw_batch bt = batches[b];
+  const u64 base = bt.frame_off;
+  const i64 l = bt.frame_len;
+  u64* spans = s.spans + (base >> 1);
+  u64 dep = 0, src_off = 0, binver = 0;
+  u32 src_len = 0;
+  u32 nm = 0;
+  int st = GRW_OK;
+  u32 efield = 0;
+  i64 first_post = -1;  // post of the first message field: messageCount's start
+  i64 i = 0;
+  while (i < l) {
+    i64 pre = i;
+    u64 wire;
+    if ((st = rd_varint(w, base, l, i, wire))) break;
+    i32 field = (i32)(u32)(wire >> 3);
+    int wt = (int)(wire & 7);
+    if (wt == 4) { st = GRW_E_END_GROUP; break; }
+    if (field <= 0) { st = GRW_E_ILLEGAL_TAG; efield = (u32)field; break; }
+    if (field == 1 || field == 3) {
+      if (wt != 2) { st = GRW_E_WRONG_WIRE_TYPE; efield = (u32)field; break; }
+      u64 len;
+      if ((st = rd_varint(w, base, l, i, len))) break;
+      if ((i64)len < 0) { st = GRW_E_INVALID_LENGTH; break; }
+      i64 post = wrap_add(i, (i64)len);
+      if (post < 0) { st = GRW_E_PANIC; break; }
+      if (post > l) { st = GRW_E_UNEXPECTED_EOF; break; }
+      if (field == 1) {
+        if (nm == 0) first_post = post;
+        if (threadIdx.x == 0) spans[nm] = (u64)(u32)i | ((u64)(u32)(post - i) << 32);
+        nm++;
+      } else {
+        src_off = base + (u64)i;
+        src_len = (u32)(post - i);
+      }
+      i = post;
+      continue;
+    }
+    if (field == 2 || field == 4) {
+      if (wt != 0) { st = GRW_E_WRONG_WIRE_TYPE; efield = (u32)field; break; }
+      u64 v;
+      if ((st = rd_varint(w, base, l, i, v))) break;
+      if (field == 2) dep = v; else binver = (u32)v;
+      continue;
+    }
+    i = pre;
+    i64 skippy;
+    if ((st = skip_raft(w, base + (u64)i, l - i, skippy))) break;
+    if (skippy < 0) { st = GRW_E_INVALID_LENGTH; break; }
+    if (wrap_add(i, skippy) > l) { st = GRW_E_UNEXPECTED_EOF; break; }
+    i += skippy;
+  }
+  // messageCount ran when the first message was reached. Where the walk went
+  // through every field it read the same chain with checked varints, so it
+  // cannot have panicked; after a walk error, run it as written.
+  int panic = 0;
+  if (st != GRW_OK && first_post >= 0) panic = count_chain_ok(w, base + (u64)first_post, l - first_post, 1) ? 0 : 1;
+  if (threadIdx.x == 0) {
+    s.walked[b] = nm;
+    s.walk_err[b] = pack_err(st, GRW_LVL_BATCH, panic, efield);
+    batches[b].deployment_id = dep;
+    batches[b].source_off = src_off;
+    batches[b].source_len = src_len;
+    batches[b].bin_ver = (u32)binver;
+  }
+}
+
+__global__ void map_msgs(const u32* walked, const u32* first_msg, u32 n, u32* msg_batch) {
+  u32 b = blockIdx.x;
+  if (b >= n) return;
+  u32 f = first_msg[b], c = walked[b];
+  for (u32 k = threadIdx.x; k < c; k += blockDim.x) msg_batch[f + k] = b;
+}
+
+struct MsgOut {
+  int st = GRW_OK;
+  int lvl = GRW_LVL_MESSAGE;
+  u32 field = 0;
+};
+
+// Entry.unmarshal (raft_optimized.go:302-650) of [0, l) at absolute `base`.
+template <bool kStore>
+__device__ int entry_unmarshal(Rd& r, u64 base, i64 l, grw_entry* o) {
+  if (l == 0) return GRW_E_ENTRY_EOF;
+  u8 header = r.at(base);
+  i64 i = 1;
+  u64 f64[7] = {0, 0, 0, 0, 0, 0, 0};
+  i32 type = 0;
+#pragma unroll
+  for (int f = 0; f < 7; ++f) {
+    if (f == 2) {
+      if (header == 2 || header == (2 | 0x80)) {
+        if (i + 1 >= l) return GRW_E_ENTRY_EOF;
+        u32 x = r.at(base + i);
+        i++;
+        if (x >= 0x80) {
+          x &= 0x7f;
+          for (u32 shift = 7;; shift += 7) {
+            u32 bb = r.at(base + i);
+            i++;
+            if (i >= l) return GRW_E_ENTRY_EOF;
+            if (bb < 0x80) {
+              if (shift < 32) x |= bb << shift;
+              break;
+            }
+            if (shift < 32) x |= (bb & 0x7f) << shift;
+          }
+        }
+        type = (header == 2) ? (i32)x : (i32)(~x + 1);
+        header = r.at(base + i);
+        i++;
+      }
+      continue;
+    }
+    if (header == (u8)f) {
+      i64 start = i;
+      i++;
+      if (i >= l) return GRW_E_ENTRY_EOF;
+      u64 x = r.at(base + start);
+      if (x >= 0x80) {
+        x &= 0x7f;
+        for (u32 shift = 7;; shift += 7) {
+          u64 bb = r.at(base + i);
+          i++;
+          if (i >= l) return GRW_E_ENTRY_EOF;
+          if (bb < 0x80 || shift == 56) {
+            x |= bb << shift;
+            break;
+          }
+          x |= (bb & 0x7f) << shift;
+        }
+      }
+      f64[f] = x;
+      header = r.at(base + i);
+      i++;
+    } else if (header == (u8)(f | 0x80)) {
+      i64 start = i;
+      i += 8;
+      if (i >= l) return GRW_E_ENTRY_EOF;
+      u64 x = 0;
+      for (int k = 0; k < 8; ++k) x = (x << 8) | r.at(base + start + k);
+      f64[f] = x;
+      header = r.at(base + i);
+      i++;
+    }
+  }
+  u64 cmd_off = 0;
+  u32 cmd_len = 0;
+  if (header == 7) {
+    if (i >= l) return GRW_E_ENTRY_EOF;
+    u64 x = r.at(base + i);
+    i++;
+    if (x >= 0x80) {
+      x &= 0x7f;
+      for (u64 shift = 7;; shift += 7) {
+        if (i >= l) return GRW_E_ENTRY_EOF;
+        u64 bb = r.at(base + i);
+        i++;
+        if (bb < 0x80) {
+          if (shift < 64) x |= bb << shift;
+          break;
+        }
+        if (shift < 64) x |= (bb & 0x7f) << shift;
+      }
+    }
+    if (x > (u64)GRW_COLFER_SIZE_MAX) return GRW_E_ENTRY_MAX;
+    i64 start = i;
+    i += (i64)x;
+    if (i >= l) return i >= (i64)GRW_COLFER_SIZE_MAX ? GRW_E_ENTRY_MAX : GRW_E_ENTRY_EOF;
+    cmd_off = base + (u64)start;
+    cmd_len = (u32)x;
+    header = r.at(base + i);
+    i++;
+  }
+  if (header != 0x7f) return GRW_E_ENTRY_HEADER;
+  if (i >= (i64)GRW_COLFER_SIZE_MAX) return GRW_E_ENTRY_MAX;
+  if (kStore) {
+    o->term = f64[0];
+    o->index = f64[1];
+    o->key = f64[3];
+    o->client_id = f64[4];
+    o->series_id = f64[5];
+    o->responded_to = f64[6];
+    o->cmd_off = cmd_off;
+    o->cmd_len = cmd_len;
+    o->type = type;
+  }
+  return GRW_OK;
+}
+
+__device__ __forceinline__ bool zero_snapshot(Rd& r, u64 a, i64 len) {
+  if (len == 0) return true;
+  if (len != 12) return false;
+  for (int k = 0; k < 12; ++k)
+    if (r.at(a + k) != kZeroSnap[k]) return false;
+  return true;
+}
+
+// Message.Unmarshal (raft_optimized.go:653-977) of [0, l) at absolute base.
+// kStore = false: fields into m, entries validated and counted (n_ents).
+// kStore = true: entries written to ents (the fields pass already succeeded).
+template <bool kStore>
+__device__ MsgOut message_unmarshal(Rd& r, u64 base, i64 l, grw_message* m, grw_entry* ents, u32& n_ents) {
+  MsgOut e;
+  i64 i = 0;
+  i64 first_ent_post = -1;  // entryCount's start (the first Entries field's post)
+  n_ents = 0;
+  while (i < l) {
+    i64 pre = i;
+    u64 wire;
+    if ((e.st = rd_varint(r, base, l, i, wire))) break;
+    i32 field = (i32)(u32)(wire >> 3);
+    int wt = (int)(wire & 7);
+    if (wt == 4) { e.st = GRW_E_END_GROUP; break; }
+    if (field <= 0) { e.st = GRW_E_ILLEGAL_TAG; e.field = (u32)field; break; }
+    if ((field >= 1 && field <= 10) || field == 13) {
+      if (wt != 0) { e.st = GRW_E_WRONG_WIRE_TYPE; e.field = (u32)field; break; }
+      u64 v;
+      if ((e.st = rd_varint(r, base, l, i, v))) break;
+      if (!kStore) {
+        switch (field) {
+          case 1: m->type = (i32)(u32)v; break;
+          case 2: m->to = v; break;
+          case 3: m->from = v; break;
+          case 4: m->cluster_id = v; break;
+          case 5: m->term = v; break;
+          case 6: m->log_term = v; break;
+          case 7: m->log_index = v; break;
+          case 8: m->commit = v; break;
+          case 9: m->reject = v != 0; break;
+          case 10: m->hint = v; break;
+          default: m->hint_high = v; break;
+        }
+      }
+      continue;
+    }
+    if (field == 11 || field == 12) {
+      if (wt != 2) { e.st = GRW_E_WRONG_WIRE_TYPE; e.field = (u32)field; break; }
+      u64 len;
+      if ((e.st = rd_varint(r, base, l, i, len))) break;
+      if ((i64)len < 0) { e.st = GRW_E_INVALID_LENGTH; break; }
+      i64 post = wrap_add(i, (i64)len);
+      if (post < 0) { e.st = GRW_E_PANIC; break; }
+      if (post > l) { e.st = GRW_E_UNEXPECTED_EOF; break; }
+      if (field == 11) {
+        if (first_ent_post < 0) first_ent_post = post;
+        int st = entry_unmarshal<kStore>(r, base + (u64)i, post - i, kStore ? ents + n_ents : nullptr);
+        if (st) { e.st = st; e.lvl = GRW_LVL_ENTRY; break; }
+        n_ents++;
+      } else if (!kStore) {
+        if (!zero_snapshot(r, base + (u64)i, post - i)) m->snapshot_host = 1;
+        m->snapshot_off = base + (u64)i;
+        m->snapshot_len = (u32)(post - i);
+      }
+      i = post;
+      continue;
+    }
+    i = pre;
+    i64 skippy;
+    if ((e.st = skip_raft(r, base + (u64)i, l - i, skippy))) break;
+    if (skippy < 0) { e.st = GRW_E_INVALID_LENGTH; break; }
+    if (wrap_add(i, skippy) > l) { e.st = GRW_E_UNEXPECTED_EOF; break; }
+    i += skippy;
+  }
+  // entryCount ran at the first Entries field; only a later error can hide a
+  // chain that runs off the message (see walk_frames).
+  if (e.st != GRW_OK && first_ent_post >= 0 &&
+      !count_chain_ok(r, base + (u64)first_ent_post, l - first_ent_post, 11)) {
+    e.st = GRW_E_PANIC;
+    e.lvl = GRW_LVL_MESSAGE;
+    e.field = 0;
+  }
+  return e;
+}
+
+__global__ void decode_msgs(const u8* buf, u64 buf_len, const grw_batch* batches, u32 total, Scratch s,
+                            grw_message* msgs) {
+  u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= total) return;
+  u32 b = s.msg_batch[j];
+  u32 k = j - s.first_msg[b];
+  u64 fo = batches[b].frame_off;
+  u64 sp = s.spans[(fo >> 1) + k];
+  u64 start = fo + (u32)sp;
+  u32 len = (u32)(sp >> 32);
+  Rd r(buf, buf_len);
+  grw_message m;
+  memset(&m, 0, sizeof(m));
+  u32 ne = 0;
+  MsgOut e = message_unmarshal<false>(r, start, len, &m, nullptr, ne);
+  m.msg_off = start;
+  m.msg_len = len;
+  m.batch = b;
+  m.n_entries = ne;
+  msgs[j] = m;
+  s.ents_per_msg[j] = e.st ? 0 : ne;
+  s.msg_err[j] = pack_err(e.st, e.lvl, 0, e.field);
+}
+
+__global__ void decode_ents(const u8* buf, u64 buf_len, u32 total, Scratch s, grw_message* msgs, grw_entry* ents) {
+  u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= total) return;
+  u32 fe = s.first_ent[j];
+  msgs[j].first_entry = fe;
+  if (s.ents_per_msg[j] == 0) return;
+  Rd r(buf, buf_len);
+  u32 ne;
+  message_unmarshal<true>(r, msgs[j].msg_off, msgs[j].msg_len, nullptr, ents + fe, ne);
+}
+
+// 6. Status = the first error in wire order: a messageCount panic (raised at
+// the first message), else the first failing message, else the walk's error.
+__global__ void finish_frames(grw_batch* batches, u32 n, Scratch s) {
+  u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  u64 we = s.walk_err[b];
+  u32 f = s.first_msg[b], c = s.walked[b];
+  grw_batch& bt = batches[b];
+  bt.first_msg = f;
+  int st = (int)(we & 0xff), lvl = (int)((we >> 8) & 0xff);
+  u32 field = (u32)(we >> 32), at = c;
+  if ((we >> 16) & 1) {
+    st = GRW_E_PANIC; lvl = GRW_LVL_BATCH; field = 0; at = 0;
+  } else {
+    for (u32 k = 0; k < c; ++k) {
+      u64 me = s.msg_err[f + k];
+      if (me & 0xff) {
+        st = (int)(me & 0xff); lvl = (int)((me >> 8) & 0xff); field = (u32)(me >> 32); at = k;
+        break;
+      }
+    }
+  }
+  bt.status = st;
+  bt.err_level = (u8)(st ? lvl : GRW_LVL_BATCH);
+  bt.err_field = st ? field : 0;
+  bt.err_msg = st ? at : 0;
+  bt.n_msgs = st ? at : c;
+}
+
+// ------------------------------------------------------------------ encode --
+
+__device__ __forceinline__ int sov(u64 x) {
+  int n = 0;
+  do { n++; x >>= 7; } while (x);
+  return n;
+}
+
+// Entry.Size (raft_optimized.go:78-153); -1 where it panics.
+__device__ i64 entry_size(const grw_entry& o) {
+  i64 l = 1;
+  const u64 f64[6] = {o.term, o.index, o.key, o.client_id, o.series_id, o.responded_to};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    u64 x = f64[k];
+    if (x >= (1ull << 49)) l += 9;
+    else if (x != 0) { for (l += 2; x >= 0x80; l++) x >>= 7; }
+    if (k == 1 && o.type != 0) {
+      u32 x32 = (u32)o.type;
+      if (o.type < 0) x32 = ~x32 + 1;
+      for (l += 2; x32 >= 0x80; l++) x32 >>= 7;
+    }
+  }
+  if (u64 x = o.cmd_len) {
+    if (x > GRW_COLFER_SIZE_MAX) return -1;
+    for (l += (i64)x + 2; x >= 0x80; l++) x >>= 7;
+  }
+  if (l > (i64)GRW_COLFER_SIZE_MAX) return -1;
+  return l;
+}
+
+__device__ __forceinline__ u64 snap_size(const grw_message& m) { return m.snapshot_len ? m.snapshot_len : 12; }
+
+// Message.Size (raft.pb.go:2219-2245); -1 where an entry's Size panics.
+__device__ i64 message_size(const grw_message& m, const grw_entry* ents) {
+  i64 n = 1 + sov((u64)(i64)m.type);
+  n += 7 + sov(m.to) + sov(m.from) + sov(m.cluster_id) + sov(m.term) + sov(m.log_term) + sov(m.log_index) +
+       sov(m.commit);
+  n += 2 + 1 + sov(m.hint);
+  for (u32 k = 0; k < m.n_entries; ++k) {
+    i64 l = entry_size(ents[m.first_entry + k]);
+    if (l < 0) return -1;
+    n += 1 + l + sov((u64)l);
+  }
+  u64 sl = snap_size(m);
+  n += 1 + (i64)sl + sov(sl) + 1 + sov(m.hint_high);
+  return n;
+}
+
+// Byte writer over out[lo, hi): dword stores for the dwords it owns whole,
+// byte stores at the two ends it may share with a neighbouring record.
+// Alignment is taken from the address, so any output pointer works.
+struct Wr {
+  u8* p;       // next byte
+  u8* lo;
+  u8* hi;
+  u32 acc;     // bytes of the dword being assembled
+  __device__ Wr(u8* out, u64 start, u64 end) : p(out + start), lo(out + start), hi(out + end), acc(0) {}
+  __device__ __forceinline__ void put(u8 v) {
+    uintptr_t a = (uintptr_t)p;
+    acc |= (u32)v << (8 * (a & 3));
+    p++;
+    if ((((uintptr_t)p) & 3) == 0 || p == hi) flush((u8*)(a & ~(uintptr_t)3));
+  }
+  __device__ __forceinline__ void flush(u8* d) {
+    if (d >= lo && d + 4 <= hi) {
+      *(u32*)d = acc;
+    } else {
+      for (u8* q = (d > lo ? d : lo); q < d + 4 && q < hi; ++q) *q = (u8)(acc >> (8 * (q - d)));
+    }
+    acc = 0;
+  }
+  __device__ __forceinline__ void varint(u64 v) {
+    while (v >= 0x80) { put((u8)(v | 0x80)); v >>= 7; }
+    put((u8)v);
+  }
+};
+
+__device__ void entry_write(Wr& w, const grw_entry& o, const u8* payload) {
+  const u64 f64[6] = {o.term, o.index, o.key, o.client_id, o.series_id, o.responded_to};
+  const u8 hdr[6] = {0, 1, 3, 4, 5, 6};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    u64 x = f64[k];
+    if (x >= (1ull << 49)) {
+      w.put(hdr[k] | 0x80);
+      for (int s = 0; s < 8; ++s) w.put((u8)(x >> (56 - 8 * s)));
+    } else if (x != 0) {
+      w.put(hdr[k]);
+      w.varint(x);
+    }
+    if (k == 1 && o.type != 0) {
+      u32 x32 = (u32)o.type;
+      if (o.type >= 0) w.put(2);
+      else { x32 = ~x32 + 1; w.put(2 | 0x80); }
+      w.varint(x32);
+    }
+  }
+  if (o.cmd_len) {
+    w.put(7);
+    w.varint(o.cmd_len);
+    const u8* p = payload + o.cmd_off;
+    for (u32 k = 0; k < o.cmd_len; ++k) w.put(p[k]);
+  }
+  w.put(0x7f);
+}
+
+struct EncScratch {
+  u64* fsz;        // [msgs] size of the message's field in the batch (0 if it panics)
+  u64* pos;        // [msgs+1] exclusive scan of fsz
+  u64* flen;       // [n] frame lengths
+  u64* foff;       // [n] frame offsets
+  u32* msg_batch;  // [msgs]
+  u32* bad;        // [1] batches not contiguous in message order
+};
+
+__global__ void size_msgs(const grw_message* msgs, u32 total, const grw_entry* ents, EncScratch s, u32* panic_flag) {
+  u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= total) return;
+  i64 l = message_size(msgs[j], ents);
+  if (l < 0) {
+    s.fsz[j] = 0;
+    atomicOr(&panic_flag[s.msg_batch[j]], 1u);
+  } else {
+    s.fsz[j] = 1 + (u64)l + (u64)sov((u64)l);
+  }
+}
+
+__global__ void enc_map(const grw_batch* batches, u32 n, u32 total, EncScratch s, u32* panic_flag) {
+  u32 b = blockIdx.x;
+  if (b >= n) return;
+  u32 f = batches[b].first_msg, c = batches[b].n_msgs;
+  if (threadIdx.x == 0) panic_flag[b] = 0;
+  for (u32 k = threadIdx.x; k < c; k += blockDim.x)
+    if (f + k < total) s.msg_batch[f + k] = b;
+}
+
+__global__ void check_contig(const grw_batch* batches, u32 n, u32 total, EncScratch s) {
+  u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  u32 f = batches[b].first_msg, c = batches[b].n_msgs;
+  u32 expect_next = (b + 1 < n) ? batches[b + 1].first_msg : total;
+  if ((u64)f + c > total || (b + 1 < n && f + c != expect_next) || (b == 0 && f != 0) ||
+      (b + 1 == n && f + c != total))
+    atomicOr(s.bad, 1u);
+}
+
+__global__ void frame_sizes(grw_batch* batches, u32 n, EncScratch s, const u32* panic_flag) {
+  u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  const grw_batch& bt = batches[b];
+  u64 body = s.pos[bt.first_msg + bt.n_msgs] - s.pos[bt.first_msg];
+  u64 tail = 1 + sov(bt.deployment_id) + 1 + (u64)bt.source_len + sov(bt.source_len) + 1 + sov(bt.bin_ver);
+  s.flen[b] = panic_flag[b] ? 0 : body + tail;
+}
+
+__global__ void frame_finish(grw_batch* batches, u32 n, EncScratch s, const u32* panic_flag) {
+  u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  batches[b].frame_off = s.foff[b];
+  batches[b].frame_len = (u32)s.flen[b];
+  batches[b].status = panic_flag[b] ? GRW_E_PANIC : GRW_OK;
+}
+
+__global__ void write_msgs(const grw_batch* batches, const grw_message* msgs, u32 total, const grw_entry* ents,
+                           const u8* payload, EncScratch s, const u32* panic_flag, u8* out) {
+  u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= total) return;
+  u32 b = s.msg_batch[j];
+  if (panic_flag[b]) return;
+  u64 at = s.foff[b] + (s.pos[j] - s.pos[batches[b].first_msg]);
+  const grw_message m = msgs[j];
+  Wr w(out, at, at + s.fsz[j]);
+  w.put(0x0a);
+  w.varint((u64)message_size(m, ents));
+  w.put(0x08); w.varint((u64)(i64)m.type);
+  w.put(0x10); w.varint(m.to);
+  w.put(0x18); w.varint(m.from);
+  w.put(0x20); w.varint(m.cluster_id);
+  w.put(0x28); w.varint(m.term);
+  w.put(0x30); w.varint(m.log_term);
+  w.put(0x38); w.varint(m.log_index);
+  w.put(0x40); w.varint(m.commit);
+  w.put(0x48); w.put(m.reject ? 1 : 0);
+  w.put(0x50); w.varint(m.hint);
+  for (u32 k = 0; k < m.n_entries; ++k) {
+    const grw_entry e = ents[m.first_entry + k];
+    w.put(0x5a);
+    w.varint((u64)entry_size(e));
+    entry_write(w, e, payload);
+  }
+  w.put(0x62);
+  w.varint(snap_size(m));
+  if (m.snapshot_len) {
+    const u8* p = payload + m.snapshot_off;
+    for (u32 k = 0; k < m.snapshot_len; ++k) w.put(p[k]);
+  } else {
+    for (int k = 0; k < 12; ++k) w.put(kZeroSnap[k]);
+  }
+  w.put(0x68); w.varint(m.hint_high);
+}
+
+__global__ void write_tails(const grw_batch* batches, u32 n, const u8* payload, EncScratch s, const u32* panic_flag,
+                            u8* out) {
+  u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n || panic_flag[b]) return;
+  const grw_batch& bt = batches[b];
+  u64 end = s.foff[b] + s.flen[b];
+  u64 tail = 1 + sov(bt.deployment_id) + 1 + (u64)bt.source_len + sov(bt.source_len) + 1 + sov(bt.bin_ver);
+  Wr w(out, end - tail, end);
+  w.put(0x10); w.varint(bt.deployment_id);
+  w.put(0x1a); w.varint(bt.source_len);
+  const u8* p = payload + bt.source_off;
+  for (u32 k = 0; k < bt.source_len; ++k) w.put(p[k]);
+  w.put(0x20); w.varint(bt.bin_ver);
+}
+
+}  // namespace grw
+
+// ------------------------------------------------------------------- C-ABI --
+
+using namespace grw;
+
+struct grw_ctx {
+  struct Buf {
+    void* p = nullptr;
+    size_t n = 0;
+  };
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[6] = {};
+  grw_timing timing{};
+  Buf spans, walked, first_msg, walk_err, msg_batch, ents_per_msg, first_ent, msg_err, tmp, scal;
+  Buf fsz, pos, flen, foff, pflag;
+  // host-path staging
+  Buf d_buf, d_batches, d_msgs, d_ents;
+  u8* h_scal = nullptr;
+  std::mutex mu;
+};
+
+#define HIPCHK(x)                            \
+  do {                                       \
+    hipError_t _e = (x);                     \
+    if (_e != hipSuccess) return GR_EDEVICE; \
+  } while (0)
+
+static int grow(grw_ctx::Buf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.n >= bytes) return GR_OK;
+  if (b.p) hipFree(b.p);
+  b.p = nullptr;
+  b.n = 0;
+  size_t want = bytes + bytes / 4;
+  if (hipMalloc(&b.p, want) != hipSuccess) return GR_ENOMEM;
+  b.n = want;
+  return GR_OK;
+}
+
+template <class T>
+static int scan_excl(grw_ctx* c, const T* in, T* out, size_t n) {
+  size_t tb = 0;
+  HIPCHK(rocprim::exclusive_scan(nullptr, tb, in, out, (T)0, n, rocprim::plus<T>(), c->stream));
+  if (int r = grow(c->tmp, tb)) return r;
+  tb = c->tmp.n;
+  HIPCHK(rocprim::exclusive_scan(c->tmp.p, tb, in, out, (T)0, n, rocprim::plus<T>(), c->stream));
+  return GR_OK;
+}
+
+static inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+extern "C" {
+
+int grw_create(uint32_t device, grw_ctx** out) {
+  if (!out) return GR_EINVAL;
+  *out = nullptr;
+  int cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess || (int)device >= cnt) return GR_EDEVICE;
+  grw_ctx* c = new (std::nothrow) grw_ctx();
+  if (!c) return GR_ENOMEM;
+  c->device = (int)device;
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return GR_EDEVICE;
+  }
+  for (auto& e : c->ev) hipEventCreate(&e);
+  if (hipHostMalloc((void**)&c->h_scal, 64) != hipSuccess) {
+    delete c;
+    return GR_ENOMEM;
+  }
+  *out = c;
+  return GR_OK;
+}
+
+void grw_destroy(grw_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  grw_ctx::Buf* bufs[] = {&c->spans, &c->walked, &c->first_msg, &c->walk_err, &c->msg_batch, &c->ents_per_msg,
+                          &c->first_ent, &c->msg_err, &c->tmp, &c->scal, &c->fsz, &c->pos, &c->flen, &c->foff,
+                          &c->pflag, &c->d_buf, &c->d_batches, &c->d_msgs, &c->d_ents};
+  for (auto* b : bufs)
+    if (b->p) hipFree(b->p);
+  for (auto& e : c->ev)
+    if (e) hipEventDestroy(e);
+  if (c->h_scal) hipHostFree(c->h_scal);
+  hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* grw_status_name(int s) {
+  static const char* names[] = {"ok", "ErrIntOverflowRaft", "io.ErrUnexpectedEOF", "ErrInvalidLengthRaft",
+                                "wiretype end group for non-group", "illegal tag", "wrong wireType",
+                                "illegal wireType", "colfer io.EOF", "ColferError", "ColferMax", "panic"};
+  return (s >= 0 && s <= GRW_E_PANIC) ? names[s] : "unknown";
+}
+
+int grw_decode_device(grw_ctx* c, const uint8_t* d_buf, size_t buf_len, grw_batch* d_batches, size_t n,
+                      grw_message* d_msgs, size_t msg_cap, grw_entry* d_ents, size_t ent_cap, size_t* n_msgs,
+                      size_t* n_ents) {
+  if (!c || !n_msgs || !n_ents || (n && (!d_buf || !d_batches)) || n > 0xFFFFFFFFull) return GR_EINVAL;
+  *n_msgs = *n_ents = 0;
+  if (n == 0) return GR_OK;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  int r;
+  if ((r = grow(c->spans, (buf_len / 2 + 2) * 8)) || (r = grow(c->walked, n * 4)) || (r = grow(c->first_msg, n * 4)) ||
+      (r = grow(c->walk_err, n * 8)) || (r = grow(c->scal, 64)))
+    return r;
+  Scratch sc{};
+  sc.spans = (u64*)c->spans.p;
+  sc.walked = (u32*)c->walked.p;
+  sc.first_msg = (u32*)c->first_msg.p;
+  sc.walk_err = (u64*)c->walk_err.p;
+  HIPCHK(hipEventRecord(c->ev[0], s));
+  walk_frames<<<(unsigned)n, 64, 0, s>>>(d_buf, buf_len, d_batches, (u32)n, sc);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev[1], s));
+  if ((r = scan_excl<u32>(c, sc.walked, sc.first_msg, n))) return r;
+  // total = first_msg[n-1] + walked[n-1]
+  HIPCHK(hipMemcpyAsync(c->h_scal, sc.first_msg + n - 1, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(c->h_scal + 4, sc.walked + n - 1, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  u32 total = ((u32*)c->h_scal)[0] + ((u32*)c->h_scal)[1];
+  if ((r = grow(c->msg_batch, (size_t)total * 4 + 4)) || (r = grow(c->ents_per_msg, (size_t)total * 4 + 4)) ||
+      (r = grow(c->first_ent, (size_t)total * 4 + 4)) || (r = grow(c->msg_err, (size_t)total * 8 + 8)))
+    return r;
+  sc.msg_batch = (u32*)c->msg_batch.p;
+  sc.ents_per_msg = (u32*)c->ents_per_msg.p;
+  sc.first_ent = (u32*)c->first_ent.p;
+  sc.msg_err = (u64*)c->msg_err.p;
+  if (total > msg_cap || (total && !d_msgs)) {
+    *n_msgs = total;
+    return GR_ECAPACITY;
+  }
+  if (total) {
+    map_msgs<<<(unsigned)n, 64, 0, s>>>(sc.walked, sc.first_msg, (u32)n, sc.msg_batch);
+    HIPCHK(hipEventRecord(c->ev[2], s));
+    decode_msgs<<<nblk(total, 256), 256, 0, s>>>(d_buf, buf_len, d_batches, total, sc, d_msgs);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[3], s));
+    if ((r = scan_excl<u32>(c, sc.ents_per_msg, sc.first_ent, total))) return r;
+    HIPCHK(hipMemcpyAsync(c->h_scal, sc.first_ent + total - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(c->h_scal + 4, sc.ents_per_msg + total - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  } else {
+    HIPCHK(hipEventRecord(c->ev[2], s));
+    HIPCHK(hipEventRecord(c->ev[3], s));
+    memset(c->h_scal, 0, 8);
+  }
+  u32 tents = ((u32*)c->h_scal)[0] + ((u32*)c->h_scal)[1];
+  *n_msgs = total;
+  *n_ents = tents;
+  if (tents > ent_cap || (tents && !d_ents)) return GR_ECAPACITY;
+  HIPCHK(hipEventRecord(c->ev[4], s));
+  if (total) {
+    decode_ents<<<nblk(total, 256), 256, 0, s>>>(d_buf, buf_len, total, sc, d_msgs, d_ents);
+    HIPCHK(hipGetLastError());
+  }
+  finish_frames<<<nblk(n, 256), 256, 0, s>>>(d_batches, (u32)n, sc);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev[5], s));
+  HIPCHK(hipStreamSynchronize(s));
+  float t01 = 0, t12 = 0, t23 = 0, t45 = 0, t05 = 0;
+  hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
+  hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
+  hipEventElapsedTime(&t23, c->ev[2], c->ev[3]);
+  hipEventElapsedTime(&t45, c->ev[4], c->ev[5]);
+  hipEventElapsedTime(&t05, c->ev[0], c->ev[5]);
+  c->timing = grw_timing{t01, t12, t23, t45, t05};
+  return GR_OK;
+}
+
+int grw_decode(grw_ctx* c, const uint8_t* buf, size_t buf_len, grw_batch* batches, size_t n, grw_message* msgs,
+               size_t msg_cap, grw_entry* ents, size_t ent_cap, size_t* n_msgs, size_t* n_ents) {
+  if (!c || !n_msgs || !n_ents || (n && (!buf || !batches))) return GR_EINVAL;
+  for (size_t b = 0; b < n; ++b)
+    if (batches[b].frame_off + (u64)batches[b].frame_len > buf_len) return GR_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  int r;
+  if ((r = grow(c->d_buf, buf_len + 16)) || (r = grow(c->d_batches, n * sizeof(grw_batch)))) return r;
+  HIPCHK(hipMemcpyAsync(c->d_buf.p, buf, buf_len, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_batches.p, batches, n * sizeof(grw_batch), hipMemcpyHostToDevice, c->stream));
+  size_t nm = 0, ne = 0;
+  if ((r = grow(c->d_msgs, msg_cap * sizeof(grw_message))) || (r = grow(c->d_ents, ent_cap * sizeof(grw_entry))))
+    return r;
+  r = grw_decode_device(c, (const u8*)c->d_buf.p, buf_len, (grw_batch*)c->d_batches.p, n, (grw_message*)c->d_msgs.p,
+                        msg_cap, (grw_entry*)c->d_ents.p, ent_cap, &nm, &ne);
+  *n_msgs = nm;
+  *n_ents = ne;
+  if (r) return r;
+  HIPCHK(hipMemcpyAsync(batches, c->d_batches.p, n * sizeof(grw_batch), hipMemcpyDeviceToHost, c->stream));
+  if (nm) HIPCHK(hipMemcpyAsync(msgs, c->d_msgs.p, nm * sizeof(grw_message), hipMemcpyDeviceToHost, c->stream));
+  if (ne) HIPCHK(hipMemcpyAsync(ents, c->d_ents.p, ne * sizeof(grw_entry), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return GR_OK;
+}
+
+int grw_encode_device(grw_ctx* c, const uint8_t* d_payload, size_t payload_len, grw_batch* d_batches, size_t n,
+                      const grw_message* d_msgs, size_t n_msgs, const grw_entry* d_ents, size_t n_ents, uint8_t* d_out,
+                      size_t out_cap, size_t* out_len) {
+  (void)payload_len;
+  (void)n_ents;
+  if (!c || !out_len || (n && !d_batches) || n > 0xFFFFFFFFull || n_msgs > 0xFFFFFFFFull) return GR_EINVAL;
+  *out_len = 0;
+  if (n == 0) return GR_OK;
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  int r;
+  if ((r = grow(c->fsz, n_msgs * 8 + 8)) || (r = grow(c->pos, n_msgs * 8 + 16)) || (r = grow(c->flen, n * 8)) ||
+      (r = grow(c->foff, n * 8 + 8)) || (r = grow(c->msg_batch, n_msgs * 4 + 4)) || (r = grow(c->pflag, n * 4)) ||
+      (r = grow(c->scal, 64)))
+    return r;
+  EncScratch es{(u64*)c->fsz.p, (u64*)c->pos.p, (u64*)c->flen.p, (u64*)c->foff.p, (u32*)c->msg_batch.p,
+                (u32*)c->scal.p};
+  u32* pflag = (u32*)c->pflag.p;
+  u32 total = (u32)n_msgs;
+  HIPCHK(hipEventRecord(c->ev[0], s));
+  HIPCHK(hipMemsetAsync(es.bad, 0, 4, s));
+  check_contig<<<nblk(n, 256), 256, 0, s>>>(d_batches, (u32)n, total, es);
+  enc_map<<<(unsigned)n, 64, 0, s>>>(d_batches, (u32)n, total, es, pflag);
+  HIPCHK(hipMemcpyAsync(c->h_scal, es.bad, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (((u32*)c->h_scal)[0]) return GR_EINVAL;
+  HIPCHK(hipEventRecord(c->ev[1], s));
+  if (total) {
+    size_msgs<<<nblk(total, 256), 256, 0, s>>>(d_msgs, total, d_ents, es, pflag);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipMemsetAsync(es.fsz + total, 0, 8, s));
+  if ((r = scan_excl<u64>(c, es.fsz, es.pos, (size_t)total + 1))) return r;
+  frame_sizes<<<nblk(n, 256), 256, 0, s>>>(d_batches, (u32)n, es, pflag);
+  if ((r = scan_excl<u64>(c, es.flen, es.foff, n))) return r;
+  frame_finish<<<nblk(n, 256), 256, 0, s>>>(d_batches, (u32)n, es, pflag);
+  HIPCHK(hipMemcpyAsync(c->h_scal, es.foff + n - 1, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(c->h_scal + 8, es.flen + n - 1, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(c->ev[2], s));
+  HIPCHK(hipStreamSynchronize(s));
+  u64 need = ((u64*)c->h_scal)[0] + ((u64*)c->h_scal)[1];
+  *out_len = need;
+  if (need > out_cap || (need && !d_out)) return GR_ECAPACITY;
+  HIPCHK(hipEventRecord(c->ev[3], s));
+  if (total) write_msgs<<<nblk(total, 256), 256, 0, s>>>(d_batches, d_msgs, total, d_ents, d_payload, es, pflag, d_out);
+  write_tails<<<nblk(n, 256), 256, 0, s>>>(d_batches, (u32)n, d_payload, es, pflag, d_out);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev[4], s));
+  HIPCHK(hipStreamSynchronize(s));
+  float t01 = 0, t12 = 0, t34 = 0, t04 = 0;
+  hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
+  hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
+  hipEventElapsedTime(&t34, c->ev[3], c->ev[4]);
+  hipEventElapsedTime(&t04, c->ev[0], c->ev[4]);
+  c->timing = grw_timing{t01, 0.f, t12, t34, t04};
+  return GR_OK;
+}
+
+int grw_encode(grw_ctx* c, const uint8_t* payload, size_t payload_len, grw_batch* batches, size_t n,
+               const grw_message* msgs, size_t n_msgs, const grw_entry* ents, size_t n_ents, uint8_t* out,
+               size_t out_cap, size_t* out_len) {
+  if (!c || !out_len || (n && !batches)) return GR_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  int r;
+  if ((r = grow(c->d_buf, payload_len + 16)) || (r = grow(c->d_batches, n * sizeof(grw_batch))) ||
+      (r = grow(c->d_msgs, n_msgs * sizeof(grw_message))) || (r = grow(c->d_ents, n_ents * sizeof(grw_entry))))
+    return r;
+  if (payload_len) HIPCHK(hipMemcpyAsync(c->d_buf.p, payload, payload_len, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_batches.p, batches, n * sizeof(grw_batch), hipMemcpyHostToDevice, c->stream));
+  if (n_msgs) HIPCHK(hipMemcpyAsync(c->d_msgs.p, msgs, n_msgs * sizeof(grw_message), hipMemcpyHostToDevice, c->stream));
+  if (n_ents) HIPCHK(hipMemcpyAsync(c->d_ents.p, ents, n_ents * sizeof(grw_entry), hipMemcpyHostToDevice, c->stream));
+  // size first (no output buffer), then the device output, then one DMA back
+  size_t need = 0;
+  r = grw_encode_device(c, (const u8*)c->d_buf.p, payload_len, (grw_batch*)c->d_batches.p, n,
+                        (const grw_message*)c->d_msgs.p, n_msgs, (const grw_entry*)c->d_ents.p, n_ents, nullptr, 0,
+                        &need);
+  *out_len = need;
+  if (r && r != GR_ECAPACITY) return r;
+  if (need > out_cap) return GR_ECAPACITY;
+  grw_ctx::Buf& dout = c->spans;  // reuse: decode scratch is idle during an encode
+  if ((r = grow(dout, need + 16))) return r;
+  r = grw_encode_device(c, (const u8*)c->d_buf.p, payload_len, (grw_batch*)c->d_batches.p, n,
+                        (const grw_message*)c->d_msgs.p, n_msgs, (const grw_entry*)c->d_ents.p, n_ents, (u8*)dout.p,
+                        need, &need);
+  if (r) return r;
+  HIPCHK(hipMemcpyAsync(batches, c->d_batches.p, n * sizeof(grw_batch), hipMemcpyDeviceToHost, c->stream));
+  if (need) HIPCHK(hipMemcpyAsync(out, dout.p, need, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return GR_OK;
+}
+
+int grw_last_timing(grw_ctx* c, grw_timing* out) {
+  if (!c || !out) return GR_EINVAL;
+  *out = c->timing;
+  return GR_OK;
+}
+
+}  // extern "C"
