@@ -59,24 +59,26 @@ struct Rd {
   u64 cbase;  // absolute offset of the cached chunk, ~0 = none
   uint4 c;
   __device__ Rd(const u8* b, u64 l) : buf(b), len(l), cbase(~0ull) {}
+  // A chunk crossing the buffer's ends (rare): byte loads, out of line.
+  __device__ __noinline__ uint4 edge_chunk(u64 base) const {
+    const u8* p = buf + base;
+    u32 v[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 16; ++k)
+      if (base + k < len) v[k >> 2] |= (u32)p[k] << (8 * (k & 3));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
   __device__ __forceinline__ u8 at(u64 a) {  // a < len
     u64 base = a & ~15ull;
     if (base != cbase) {
       const u8* p = buf + base;
-      if ((((uintptr_t)p) & 15) == 0 && base + 16 <= len) {
-        const u32* q = (const u32*)p;
-        c.x = __builtin_nontemporal_load(q);
-        c.y = __builtin_nontemporal_load(q + 1);
-        c.z = __builtin_nontemporal_load(q + 2);
-        c.w = __builtin_nontemporal_load(q + 3);
-      } else {
-        u8 t[16];
-        for (int k = 0; k < 16; ++k) t[k] = (base + k < len) ? p[k] : 0;
-        memcpy(&c, t, 16);
-      }
+      // Cached load: the next chunk of the same message is in the same line
+      // (a nontemporal load refetched each line once per 16 B: 2.5x slower).
+      if ((((uintptr_t)p) & 15) == 0 && base + 16 <= len) c = *(const uint4*)p;
+      else c = edge_chunk(base);
       cbase = base;
     }
-    u32 w = (&c.x)[(a >> 2) & 3];
+    u32 k = (u32)(a >> 2) & 3;  // select, not an indexed load: keeps c in registers
+    u32 w = k == 0 ? c.x : k == 1 ? c.y : k == 2 ? c.z : c.w;
     return (u8)(w >> (8 * (a & 3)));
   }
 };
@@ -106,11 +108,24 @@ struct Win {
       }
       ((uint4*)lds)[k] = v;
     }
+    if (threadIdx.x == 0) ((uint4*)lds)[kWin / 16] = make_uint4(0, 0, 0, 0);
     __syncthreads();
   }
   __device__ __forceinline__ u8 at(u64 a) {  // a < buf_len
     if (a < lo || a >= hi) load(a);
     return lds[a - lo];
+  }
+  // Bytes a..a+3 (zeros past the buffer) as one wave-uniform scalar: two
+  // aligned LDS dword reads and a funnel shift, then readfirstlane, so the
+  // walk's branches are scalar.
+  __device__ __forceinline__ u32 peek4(u64 a) {
+    if (a < lo || a + 4 > hi) {
+      if (a < lo || hi < buf_len || a >= hi) load(a);
+    }
+    u32 o = (u32)(a - lo);
+    const u32* d = (const u32*)lds;
+    u64 pair = (u64)d[o >> 2] | ((u64)d[(o >> 2) + 1] << 32);
+    return __builtin_amdgcn_readfirstlane((u32)(pair >> (8 * (o & 3))));
   }
 };
 
@@ -204,6 +219,7 @@ struct Scratch {
   u32* ents_per_msg; // [msgs]
   u32* first_ent;    // [msgs]
   u64* msg_err;      // [msgs] status | level<<8 | field<<32
+  u32* ent_pos;      // [msgs] offset of the first Entries field of a canonical message, ~0 = general
 };
 
 __device__ __forceinline__ u64 pack_err(int st, int lvl, int panic, u32 field) {
@@ -214,7 +230,7 @@ __device__ __forceinline__ u64 pack_err(int st, int lvl, int panic, u32 field) {
 // messages (raft_optimized.go:1050-1202).
 __global__ __launch_bounds__(64) void walk_frames(const u8* buf, u64 buf_len, grw_batch* batches, u32 n,
                                                   Scratch s) {
-  __shared__ uint4 lds_raw[kWin / 16];
+  __shared__ uint4 lds_raw[kWin / 16 + 1];  // +16 B: peek4 past the window end
   u32 b = blockIdx.x;
   if (b >= n) return;
   Win w{(u8*)lds_raw, buf, buf_len, 1, 0};
@@ -229,6 +245,24 @@ __global__ __launch_bounds__(64) void walk_frames(const u8* buf, u64 buf_len, gr
   u32 efield = 0;
   i64 first_post = -1;  // post of the first message field: messageCount's start
   i64 i = 0;
+  // Fast loop: Requests fields back to back, as MessageBatch.MarshalTo writes
+  // them (raft.pb.go:1935-1945), with 1- or 2-byte lengths. It consumes only
+  // fields the general loop below would accept unchanged, then hands over.
+  while (i + 3 <= l) {
+    u32 q = w.peek4(base + (u64)i);
+    if ((q & 0xff) != 0x0a) break;
+    u32 b1 = (q >> 8) & 0xff, b2 = (q >> 16) & 0xff;
+    i64 len, hdr;
+    if (b1 < 0x80) { len = b1; hdr = 2; }
+    else if (b2 < 0x80) { len = (b1 & 0x7f) | (b2 << 7); hdr = 3; }
+    else break;
+    i64 post = i + hdr + len;
+    if (post > l) break;
+    if (nm == 0) first_post = post;
+    if (threadIdx.x == 0) spans[nm] = (u64)(u32)(i + hdr) | ((u64)(u32)len << 32);
+    nm++;
+    i = post;
+  }
   while (i < l) {
     i64 pre = i;
     u64 wire;
@@ -300,15 +334,15 @@ struct MsgOut {
 
 // Entry.unmarshal (raft_optimized.go:302-650) of [0, l) at absolute `base`.
 template <bool kStore>
-__device__ int entry_unmarshal(Rd& r, u64 base, i64 l, grw_entry* o) {
+__device__ __forceinline__ int entry_unmarshal(Rd& r, u64 base, i64 l, grw_entry* o) {
   if (l == 0) return GRW_E_ENTRY_EOF;
   u8 header = r.at(base);
   i64 i = 1;
-  u64 f64[7] = {0, 0, 0, 0, 0, 0, 0};
+  u64 term = 0, index = 0, key = 0, client = 0, series = 0, resp = 0;
   i32 type = 0;
-#pragma unroll
+#pragma unroll 1
   for (int f = 0; f < 7; ++f) {
-    if (f == 2) {
+    if (f == 2) {  // Type (raft_optimized.go:379-436): u32, no shift cap
       if (header == 2 || header == (2 | 0x80)) {
         if (i + 1 >= l) return GRW_E_ENTRY_EOF;
         u32 x = r.at(base + i);
@@ -332,11 +366,12 @@ __device__ int entry_unmarshal(Rd& r, u64 base, i64 l, grw_entry* o) {
       }
       continue;
     }
-    if (header == (u8)f) {
+    u64 x;
+    if (header == (u8)f) {  // varint form, e.g. raft_optimized.go:310-335
       i64 start = i;
       i++;
       if (i >= l) return GRW_E_ENTRY_EOF;
-      u64 x = r.at(base + start);
+      x = r.at(base + start);
       if (x >= 0x80) {
         x &= 0x7f;
         for (u32 shift = 7;; shift += 7) {
@@ -350,23 +385,29 @@ __device__ int entry_unmarshal(Rd& r, u64 base, i64 l, grw_entry* o) {
           x |= (bb & 0x7f) << shift;
         }
       }
-      f64[f] = x;
-      header = r.at(base + i);
-      i++;
-    } else if (header == (u8)(f | 0x80)) {
+    } else if (header == (u8)(f | 0x80)) {  // big-endian fixed form, :336-345
       i64 start = i;
       i += 8;
       if (i >= l) return GRW_E_ENTRY_EOF;
-      u64 x = 0;
+      x = 0;
       for (int k = 0; k < 8; ++k) x = (x << 8) | r.at(base + start + k);
-      f64[f] = x;
-      header = r.at(base + i);
-      i++;
+    } else {
+      continue;
     }
+    switch (f) {
+      case 0: term = x; break;
+      case 1: index = x; break;
+      case 3: key = x; break;
+      case 4: client = x; break;
+      case 5: series = x; break;
+      default: resp = x; break;
+    }
+    header = r.at(base + i);
+    i++;
   }
   u64 cmd_off = 0;
   u32 cmd_len = 0;
-  if (header == 7) {
+  if (header == 7) {  // Cmd, raft_optimized.go:600-637
     if (i >= l) return GRW_E_ENTRY_EOF;
     u64 x = r.at(base + i);
     i++;
@@ -395,12 +436,12 @@ __device__ int entry_unmarshal(Rd& r, u64 base, i64 l, grw_entry* o) {
   if (header != 0x7f) return GRW_E_ENTRY_HEADER;
   if (i >= (i64)GRW_COLFER_SIZE_MAX) return GRW_E_ENTRY_MAX;
   if (kStore) {
-    o->term = f64[0];
-    o->index = f64[1];
-    o->key = f64[3];
-    o->client_id = f64[4];
-    o->series_id = f64[5];
-    o->responded_to = f64[6];
+    o->term = term;
+    o->index = index;
+    o->key = key;
+    o->client_id = client;
+    o->series_id = series;
+    o->responded_to = resp;
     o->cmd_off = cmd_off;
     o->cmd_len = cmd_len;
     o->type = type;
@@ -493,8 +534,83 @@ __device__ MsgOut message_unmarshal(Rd& r, u64 base, i64 l, grw_message* m, grw_
   return e;
 }
 
-__global__ void decode_msgs(const u8* buf, u64 buf_len, const grw_batch* batches, u32 total, Scratch s,
-                            grw_message* msgs) {
+// Varint that only succeeds where rd_varint would (no error paths to report).
+__device__ __forceinline__ bool fast_varint(Rd& r, u64 base, i64 l, i64& i, u64& v) {
+  v = 0;
+#pragma unroll 1
+  for (u32 shift = 0; shift < 64; shift += 7) {
+    if (i >= l) return false;
+    u8 b = r.at(base + (u64)i);
+    i++;
+    v |= (u64)(b & 0x7F) << shift;
+    if (b < 0x80) return true;
+  }
+  return false;
+}
+
+struct Fast {
+  u64 f[11];  // Type To From ClusterId Term LogTerm LogIndex Commit Reject Hint HintHigh
+  u64 snap_off;
+  u32 snap_len, n_ents, ent_pos;
+  u8 snap_host;
+};
+
+// The canonical layout Message.MarshalTo writes (raft.pb.go:1747-1809): fields
+// 1..10 in order, Entries, Snapshot, HintHigh, nothing else. Returns true only
+// for such a message whose entries are all valid, with the values the general
+// decoder would produce; anything else goes to message_unmarshal.
+__device__ __forceinline__ bool fast_message(Rd& r, u64 base, i64 l, Fast& o) {
+  i64 i = 0;
+#pragma unroll 1
+  for (int k = 0; k < 10; ++k) {
+    if (i >= l || r.at(base + (u64)i) != (u8)((k + 1) << 3)) return false;
+    i++;
+    if (!fast_varint(r, base, l, i, o.f[k])) return false;
+  }
+  o.n_ents = 0;
+  o.ent_pos = (u32)i;
+  while (i < l && r.at(base + (u64)i) == 0x5a) {
+    i++;
+    u64 len;
+    if (!fast_varint(r, base, l, i, len) || len > (u64)l) return false;
+    i64 post = i + (i64)len;
+    if (post > l) return false;
+    if (entry_unmarshal<false>(r, base + (u64)i, post - i, nullptr)) return false;
+    o.n_ents++;
+    i = post;
+  }
+  if (i >= l || r.at(base + (u64)i) != 0x62) return false;
+  i++;
+  u64 len;
+  if (!fast_varint(r, base, l, i, len) || len > (u64)l) return false;
+  i64 post = i + (i64)len;
+  if (post > l) return false;
+  o.snap_off = base + (u64)i;
+  o.snap_len = (u32)len;
+  o.snap_host = zero_snapshot(r, base + (u64)i, (i64)len) ? 0 : 1;
+  i = post;
+  if (i >= l || r.at(base + (u64)i) != 0x68) return false;
+  i++;
+  if (!fast_varint(r, base, l, i, o.f[10])) return false;
+  return i == l;
+}
+
+// The general decoder, kept out of line: only non-canonical or failing
+// messages take it.
+__device__ __noinline__ MsgOut general_message(const u8* buf, u64 buf_len, u64 base, i64 l, grw_message* m,
+                                               u32* ne) {
+  Rd r(buf, buf_len);
+  return message_unmarshal<false>(r, base, l, m, nullptr, *ne);
+}
+
+__device__ __noinline__ void general_entries(const u8* buf, u64 buf_len, u64 base, i64 l, grw_entry* ents) {
+  Rd r(buf, buf_len);
+  u32 ne;
+  message_unmarshal<true>(r, base, l, nullptr, ents, ne);
+}
+
+__global__ __launch_bounds__(256) void decode_msgs(const u8* buf, u64 buf_len, const grw_batch* batches, u32 total,
+                                                   Scratch s, grw_message* msgs) {
   u32 j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= total) return;
   u32 b = s.msg_batch[j];
@@ -503,29 +619,72 @@ __global__ void decode_msgs(const u8* buf, u64 buf_len, const grw_batch* batches
   u64 sp = s.spans[(fo >> 1) + k];
   u64 start = fo + (u32)sp;
   u32 len = (u32)(sp >> 32);
+  grw_message* mo = msgs + j;
   Rd r(buf, buf_len);
+  Fast f;
+  if (fast_message(r, start, len, f)) {
+    mo->type = (i32)(u32)f.f[0];
+    mo->to = f.f[1];
+    mo->from = f.f[2];
+    mo->cluster_id = f.f[3];
+    mo->term = f.f[4];
+    mo->log_term = f.f[5];
+    mo->log_index = f.f[6];
+    mo->commit = f.f[7];
+    mo->reject = f.f[8] != 0;
+    mo->hint = f.f[9];
+    mo->hint_high = f.f[10];
+    mo->snapshot_off = f.snap_off;
+    mo->snapshot_len = f.snap_len;
+    mo->snapshot_host = f.snap_host;
+    mo->msg_off = start;
+    mo->msg_len = len;
+    mo->batch = b;
+    mo->n_entries = f.n_ents;
+    s.ents_per_msg[j] = f.n_ents;
+    s.ent_pos[j] = f.ent_pos;
+    s.msg_err[j] = 0;
+    return;
+  }
   grw_message m;
   memset(&m, 0, sizeof(m));
   u32 ne = 0;
-  MsgOut e = message_unmarshal<false>(r, start, len, &m, nullptr, ne);
+  MsgOut e = general_message(buf, buf_len, start, len, &m, &ne);
   m.msg_off = start;
   m.msg_len = len;
   m.batch = b;
   m.n_entries = ne;
-  msgs[j] = m;
+  *mo = m;
   s.ents_per_msg[j] = e.st ? 0 : ne;
+  s.ent_pos[j] = 0xFFFFFFFFu;
   s.msg_err[j] = pack_err(e.st, e.lvl, 0, e.field);
 }
 
-__global__ void decode_ents(const u8* buf, u64 buf_len, u32 total, Scratch s, grw_message* msgs, grw_entry* ents) {
+__global__ __launch_bounds__(256) void decode_ents(const u8* buf, u64 buf_len, u32 total, Scratch s,
+                                                   grw_message* msgs, grw_entry* ents) {
   u32 j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= total) return;
   u32 fe = s.first_ent[j];
   msgs[j].first_entry = fe;
-  if (s.ents_per_msg[j] == 0) return;
+  u32 n = s.ents_per_msg[j];
+  if (n == 0) return;
+  u64 base = msgs[j].msg_off;
+  u32 l = msgs[j].msg_len;
+  u32 pos = s.ent_pos[j];
+  if (pos == 0xFFFFFFFFu) {
+    general_entries(buf, buf_len, base, l, ents + fe);
+    return;
+  }
+  // Canonical message: its n Entries fields start at pos, back to back.
   Rd r(buf, buf_len);
-  u32 ne;
-  message_unmarshal<true>(r, msgs[j].msg_off, msgs[j].msg_len, nullptr, ents + fe, ne);
+  i64 i = pos;
+  for (u32 k = 0; k < n; ++k) {
+    i++;  // 0x5a
+    u64 len;
+    fast_varint(r, base, l, i, len);
+    entry_unmarshal<true>(r, base + (u64)i, (i64)len, ents + fe + k);
+    i += (i64)len;
+  }
 }
 
 // 6. Status = the first error in wire order: a messageCount panic (raised at
@@ -789,7 +948,7 @@ struct grw_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev[6] = {};
   grw_timing timing{};
-  Buf spans, walked, first_msg, walk_err, msg_batch, ents_per_msg, first_ent, msg_err, tmp, scal;
+  Buf spans, walked, first_msg, walk_err, msg_batch, ents_per_msg, first_ent, msg_err, ent_pos, tmp, scal;
   Buf fsz, pos, flen, foff, pflag;
   // host-path staging
   Buf d_buf, d_batches, d_msgs, d_ents;
@@ -855,7 +1014,7 @@ void grw_destroy(grw_ctx* c) {
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   grw_ctx::Buf* bufs[] = {&c->spans, &c->walked, &c->first_msg, &c->walk_err, &c->msg_batch, &c->ents_per_msg,
-                          &c->first_ent, &c->msg_err, &c->tmp, &c->scal, &c->fsz, &c->pos, &c->flen, &c->foff,
+                          &c->first_ent, &c->msg_err, &c->ent_pos, &c->tmp, &c->scal, &c->fsz, &c->pos, &c->flen, &c->foff,
                           &c->pflag, &c->d_buf, &c->d_batches, &c->d_msgs, &c->d_ents};
   for (auto* b : bufs)
     if (b->p) hipFree(b->p);
@@ -901,8 +1060,10 @@ int grw_decode_device(grw_ctx* c, const uint8_t* d_buf, size_t buf_len, grw_batc
   HIPCHK(hipStreamSynchronize(s));
   u32 total = ((u32*)c->h_scal)[0] + ((u32*)c->h_scal)[1];
   if ((r = grow(c->msg_batch, (size_t)total * 4 + 4)) || (r = grow(c->ents_per_msg, (size_t)total * 4 + 4)) ||
-      (r = grow(c->first_ent, (size_t)total * 4 + 4)) || (r = grow(c->msg_err, (size_t)total * 8 + 8)))
+      (r = grow(c->first_ent, (size_t)total * 4 + 4)) || (r = grow(c->msg_err, (size_t)total * 8 + 8)) ||
+      (r = grow(c->ent_pos, (size_t)total * 4 + 4)))
     return r;
+  sc.ent_pos = (u32*)c->ent_pos.p;
   sc.msg_batch = (u32*)c->msg_batch.p;
   sc.ents_per_msg = (u32*)c->ents_per_msg.p;
   sc.first_ent = (u32*)c->first_ent.p;
