@@ -56,30 +56,39 @@ __constant__ u8 kZeroSnap[12] = {0x12, 0x00, 0x18, 0x00, 0x20, 0x00, 0x28, 0x00,
 struct Rd {
   const u8* buf;
   u64 len;
-  u64 cbase;  // absolute offset of the cached chunk, ~0 = none
-  uint4 c;
-  __device__ Rd(const u8* b, u64 l) : buf(b), len(l), cbase(~0ull) {}
-  // A chunk crossing the buffer's ends (rare): byte loads, out of line.
-  __device__ __noinline__ uint4 edge_chunk(u64 base) const {
-    const u8* p = buf + base;
-    u32 v[4] = {0, 0, 0, 0};
-    for (int k = 0; k < 16; ++k)
-      if (base + k < len) v[k >> 2] |= (u32)p[k] << (8 * (k & 3));
-    return make_uint4(v[0], v[1], v[2], v[3]);
-  }
+  u64 cbase;   // absolute offset of the cached 16-B chunk, ~0 = none
+  u64 lo, hi;  // the chunk, as two words: bytes are taken by shifts (an indexed
+               // read of a vector would put the chunk in scratch memory)
+  const uint4* lds = nullptr;  // optional block-staged copy of buf[llo, lhi), 16-B aligned
+  u64 llo = 0, lhi = 0;
+  __device__ Rd(const u8* b, u64 l) : buf(b), len(l), cbase(~0ull), lo(0), hi(0) {}
   __device__ __forceinline__ u8 at(u64 a) {  // a < len
     u64 base = a & ~15ull;
     if (base != cbase) {
+      uint4 c;
       const u8* p = buf + base;
-      // Cached load: the next chunk of the same message is in the same line
-      // (a nontemporal load refetched each line once per 16 B: 2.5x slower).
-      if ((((uintptr_t)p) & 15) == 0 && base + 16 <= len) c = *(const uint4*)p;
-      else c = edge_chunk(base);
+      if (base >= llo && base < lhi) {
+        c = lds[(base - llo) >> 4];
+      } else if ((((uintptr_t)p) & 15) == 0 && base + 16 <= len) {
+        // Cached load: the next chunk of the same message is in the same line
+        // (a nontemporal load refetched each line once per 16 B: 2.5x slower).
+        c = *(const uint4*)p;
+      } else {  // a chunk crossing the buffer's ends: a rolled byte loop, no call
+        u64 x = 0, y = 0;
+#pragma unroll 1
+        for (u32 k = 0; k < 16 && base + k < len; ++k) {
+          u64 v = p[k];
+          if (k < 8) x |= v << (8 * k); else y |= v << (8 * (k - 8));
+        }
+        c = make_uint4((u32)x, (u32)(x >> 32), (u32)y, (u32)(y >> 32));
+      }
+      lo = (u64)c.y << 32 | c.x;
+      hi = (u64)c.w << 32 | c.z;
       cbase = base;
     }
-    u32 k = (u32)(a >> 2) & 3;  // select, not an indexed load: keeps c in registers
-    u32 w = k == 0 ? c.x : k == 1 ? c.y : k == 2 ? c.z : c.w;
-    return (u8)(w >> (8 * (a & 3)));
+    u32 o = (u32)a & 15;
+    u64 m = 0ull - (u64)(o >> 3);  // all ones for the high word: arithmetic, not a select
+    return (u8)((lo ^ ((lo ^ hi) & m)) >> ((o & 7) * 8));
   }
 };
 
@@ -561,8 +570,8 @@ struct Fast {
 // decoder would produce; anything else goes to message_unmarshal.
 __device__ __forceinline__ bool fast_message(Rd& r, u64 base, i64 l, Fast& o) {
   i64 i = 0;
-#pragma unroll 1
-  for (int k = 0; k < 10; ++k) {
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {  // unrolled: o.f[k] stays in registers
     if (i >= l || r.at(base + (u64)i) != (u8)((k + 1) << 3)) return false;
     i++;
     if (!fast_varint(r, base, l, i, o.f[k])) return false;
@@ -609,18 +618,51 @@ __device__ __noinline__ void general_entries(const u8* buf, u64 buf_len, u64 bas
   message_unmarshal<true>(r, base, l, nullptr, ents, ne);
 }
 
+// Stage the bytes a block's messages cover, [lo, hi) capped at kStage, into
+// LDS with coalesced 16-B loads; lanes then read their messages from LDS
+// (Rd falls back to global loads outside the window).
+constexpr int kStage = 16384;
+__device__ __forceinline__ void stage_block(Rd& r, uint4* lds, u64 lo, u64 hi, bool active) {
+  __shared__ unsigned long long s_lo, s_hi;
+  if (threadIdx.x == 0) { s_lo = ~0ull; s_hi = 0; }
+  __syncthreads();
+  if (active) {
+    atomicMin(&s_lo, (unsigned long long)lo);
+    atomicMax(&s_hi, (unsigned long long)hi);
+  }
+  __syncthreads();
+  u64 a = s_lo & ~15ull, b = s_hi;
+  u64 cap_end = r.len & ~15ull;  // whole chunks inside the buffer only
+  if (b > a + kStage) b = a + kStage;
+  if (b > cap_end) b = cap_end;
+  b &= ~15ull;
+  if ((((uintptr_t)r.buf) & 15) != 0 || s_lo == ~0ull || b <= a) { a = b = 0; }
+  for (u64 k = threadIdx.x; k < (b - a) >> 4; k += blockDim.x) lds[k] = *(const uint4*)(r.buf + a + (k << 4));
+  __syncthreads();
+  r.lds = lds;
+  r.llo = a;
+  r.lhi = b;
+}
+
 __global__ __launch_bounds__(256) void decode_msgs(const u8* buf, u64 buf_len, const grw_batch* batches, u32 total,
                                                    Scratch s, grw_message* msgs) {
+  __shared__ uint4 lds[kStage / 16];
   u32 j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= total) return;
-  u32 b = s.msg_batch[j];
-  u32 k = j - s.first_msg[b];
-  u64 fo = batches[b].frame_off;
-  u64 sp = s.spans[(fo >> 1) + k];
-  u64 start = fo + (u32)sp;
-  u32 len = (u32)(sp >> 32);
-  grw_message* mo = msgs + j;
+  bool act = j < total;
+  u64 start = 0;
+  u32 len = 0, b = 0;
+  if (act) {
+    b = s.msg_batch[j];
+    u32 k = j - s.first_msg[b];
+    u64 fo = batches[b].frame_off;
+    u64 sp = s.spans[(fo >> 1) + k];
+    start = fo + (u32)sp;
+    len = (u32)(sp >> 32);
+  }
   Rd r(buf, buf_len);
+  stage_block(r, lds, start, start + len, act);
+  if (!act) return;
+  grw_message* mo = msgs + j;
   Fast f;
   if (fast_message(r, start, len, f)) {
     mo->type = (i32)(u32)f.f[0];
@@ -662,21 +704,28 @@ __global__ __launch_bounds__(256) void decode_msgs(const u8* buf, u64 buf_len, c
 
 __global__ __launch_bounds__(256) void decode_ents(const u8* buf, u64 buf_len, u32 total, Scratch s,
                                                    grw_message* msgs, grw_entry* ents) {
+  __shared__ uint4 lds[kStage / 16];
   u32 j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= total) return;
-  u32 fe = s.first_ent[j];
-  msgs[j].first_entry = fe;
-  u32 n = s.ents_per_msg[j];
-  if (n == 0) return;
-  u64 base = msgs[j].msg_off;
-  u32 l = msgs[j].msg_len;
-  u32 pos = s.ent_pos[j];
+  bool act = j < total;
+  u32 n = 0, l = 0, pos = 0, fe = 0;
+  u64 base = 0;
+  if (act) {
+    fe = s.first_ent[j];
+    msgs[j].first_entry = fe;
+    n = s.ents_per_msg[j];
+    base = msgs[j].msg_off;
+    l = msgs[j].msg_len;
+    pos = s.ent_pos[j];
+  }
+  act = act && n != 0;
+  Rd r(buf, buf_len);
+  stage_block(r, lds, base, base + l, act);
+  if (!act) return;
   if (pos == 0xFFFFFFFFu) {
     general_entries(buf, buf_len, base, l, ents + fe);
     return;
   }
   // Canonical message: its n Entries fields start at pos, back to back.
-  Rd r(buf, buf_len);
   i64 i = pos;
   for (u32 k = 0; k < n; ++k) {
     i++;  // 0x5a
