@@ -229,6 +229,8 @@ struct Scratch {
   u32* first_ent;    // [msgs]
   u64* msg_err;      // [msgs] status | level<<8 | field<<32
   u32* ent_pos;      // [msgs] offset of the first Entries field of a canonical message, ~0 = general
+  u64* msg_start;    // [msgs] absolute start and length of each message: decode_ents reads
+  u32* msg_len;      //        12 B here, not the 120-B record
 };
 
 __device__ __forceinline__ u64 pack_err(int st, int lvl, int panic, u32 field) {
@@ -685,6 +687,8 @@ __global__ __launch_bounds__(256) void decode_msgs(const u8* buf, u64 buf_len, c
     mo->n_entries = f.n_ents;
     s.ents_per_msg[j] = f.n_ents;
     s.ent_pos[j] = f.ent_pos;
+    s.msg_start[j] = start;
+    s.msg_len[j] = len;
     s.msg_err[j] = 0;
     return;
   }
@@ -699,6 +703,8 @@ __global__ __launch_bounds__(256) void decode_msgs(const u8* buf, u64 buf_len, c
   *mo = m;
   s.ents_per_msg[j] = e.st ? 0 : ne;
   s.ent_pos[j] = 0xFFFFFFFFu;
+  s.msg_start[j] = start;
+    s.msg_len[j] = len;
   s.msg_err[j] = pack_err(e.st, e.lvl, 0, e.field);
 }
 
@@ -713,8 +719,8 @@ __global__ __launch_bounds__(256) void decode_ents(const u8* buf, u64 buf_len, u
     fe = s.first_ent[j];
     msgs[j].first_entry = fe;
     n = s.ents_per_msg[j];
-    base = msgs[j].msg_off;
-    l = msgs[j].msg_len;
+    base = s.msg_start[j];
+    l = s.msg_len[j];
     pos = s.ent_pos[j];
   }
   act = act && n != 0;
@@ -997,7 +1003,7 @@ struct grw_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev[6] = {};
   grw_timing timing{};
-  Buf spans, walked, first_msg, walk_err, msg_batch, ents_per_msg, first_ent, msg_err, ent_pos, tmp, scal;
+  Buf spans, walked, first_msg, walk_err, msg_batch, ents_per_msg, first_ent, msg_err, ent_pos, msg_start, msg_len, tmp, scal;
   Buf fsz, pos, flen, foff, pflag;
   // host-path staging
   Buf d_buf, d_batches, d_msgs, d_ents;
@@ -1063,7 +1069,7 @@ void grw_destroy(grw_ctx* c) {
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   grw_ctx::Buf* bufs[] = {&c->spans, &c->walked, &c->first_msg, &c->walk_err, &c->msg_batch, &c->ents_per_msg,
-                          &c->first_ent, &c->msg_err, &c->ent_pos, &c->tmp, &c->scal, &c->fsz, &c->pos, &c->flen, &c->foff,
+                          &c->first_ent, &c->msg_err, &c->ent_pos, &c->msg_start, &c->msg_len, &c->tmp, &c->scal, &c->fsz, &c->pos, &c->flen, &c->foff,
                           &c->pflag, &c->d_buf, &c->d_batches, &c->d_msgs, &c->d_ents};
   for (auto* b : bufs)
     if (b->p) hipFree(b->p);
@@ -1110,9 +1116,12 @@ int grw_decode_device(grw_ctx* c, const uint8_t* d_buf, size_t buf_len, grw_batc
   u32 total = ((u32*)c->h_scal)[0] + ((u32*)c->h_scal)[1];
   if ((r = grow(c->msg_batch, (size_t)total * 4 + 4)) || (r = grow(c->ents_per_msg, (size_t)total * 4 + 4)) ||
       (r = grow(c->first_ent, (size_t)total * 4 + 4)) || (r = grow(c->msg_err, (size_t)total * 8 + 8)) ||
-      (r = grow(c->ent_pos, (size_t)total * 4 + 4)))
+      (r = grow(c->ent_pos, (size_t)total * 4 + 4)) || (r = grow(c->msg_start, (size_t)total * 8 + 8)) ||
+      (r = grow(c->msg_len, (size_t)total * 4 + 4)))
     return r;
   sc.ent_pos = (u32*)c->ent_pos.p;
+  sc.msg_start = (u64*)c->msg_start.p;
+  sc.msg_len = (u32*)c->msg_len.p;
   sc.msg_batch = (u32*)c->msg_batch.p;
   sc.ents_per_msg = (u32*)c->ents_per_msg.p;
   sc.first_ent = (u32*)c->first_ent.p;
