@@ -499,6 +499,35 @@ int gr_sync_peers_to_host(gr_engine* e, const uint32_t* slots, gr_peer* out, siz
   return transfer(e, slots, 0, n, out, false);
 }
 
+// Peer.NotifyRaftLastApplied (peer.go:282-284) for a slot list: raft.applied =
+// the RSM's batched last applied index, as node.handleEvents does first in
+// every step (node.go:632-635,653). No other field changes.
+int gr_notify_applied(gr_engine* e, const uint32_t* slots, const uint64_t* applied, size_t n) {
+  if (!e || (n && (!slots || !applied))) return GR_EINVAL;
+  if (n == 0) return GR_OK;
+  if (n >= 0x80000000ull) return GR_EINVAL;
+  const uint32_t cap = e->cfg.max_peers;
+  std::vector<uint64_t> seen((cap + 63) / 64, 0);
+  for (size_t x = 0; x < n; ++x) {
+    const uint32_t p = slots[x];
+    if (p >= cap || (seen[p >> 6] >> (p & 63)) & 1) return GR_ERANGE;  // nothing written
+    seen[p >> 6] |= 1ull << (p & 63);
+  }
+  std::lock_guard<std::mutex> guard(e->mu);
+  HIPCHK(hipDeviceSynchronize());  // passes in flight on other streams own the rows
+  const hipStream_t s = e->stream;
+  int r;
+  if ((r = grow_device(&e->d_slots.p, &e->d_slots.n, n * 4))) return r;
+  if ((r = grow_device(&e->d_peers.p, &e->d_peers.n, n * 8))) return r;
+  HIPCHK(hipMemcpyAsync(e->d_slots.p, slots, n * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(e->d_peers.p, applied, n * 8, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(io::set_row_u64, dim3(io_grid(n)), dim3(io::kIoBlock), 0, s, e->st, (uint32_t)SR_APPLIED,
+                     (const uint32_t*)e->d_slots.p, (const uint64_t*)e->d_peers.p, (uint32_t)n);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  return GR_OK;
+}
+
 uint64_t gr_space_chunk_bytes(uint32_t positions, uint32_t depth) {
   if (depth == 0 || depth > GR_C) return 0;
   return space_chunk_bytes_pc(space_pad_positions(positions), depth);

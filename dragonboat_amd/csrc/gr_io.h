@@ -229,5 +229,11 @@ __global__ void rows_to_peers(StateBase st, const uint32_t* slots, uint32_t firs
   }
 }
 
+// gr_notify_applied: one u64 row scattered over a slot list (slots checked on
+// the host: in range, each listed once).
+__global__ void set_row_u64(StateBase st, uint32_t row, const uint32_t* slots, const uint64_t* vals, uint32_t n) {
+  for (uint32_t x = io_tid(); x < n; x += io_stride()) st.u64(row)[slots[x]] = vals[x];
+}
+
 }  // namespace io
 }  // namespace gr

@@ -43,6 +43,7 @@ def load_library(path=LIB_PATH):
     lib.gr_sync_groups_to_host.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p, c.c_size_t]
     lib.gr_load_peers.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_sync_peers_to_host.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
+    lib.gr_notify_applied.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_step.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.POINTER(abi.Outbox)]
     lib.gr_release_outbox.argtypes = [c.c_void_p, c.POINTER(abi.Outbox)]
     lib.gr_inbox_reserve.argtypes = [c.c_void_p, c.c_size_t, c.c_size_t, c.POINTER(abi.Inbox)]
@@ -128,6 +129,15 @@ class Engine:
                                               out.ctypes.data if len(out) else None, len(slots)),
                "gr_sync_peers_to_host")
         return out
+
+    def notify_applied(self, slots, applied):
+        """Peer.NotifyRaftLastApplied for a list of engine slots (gr_notify_applied)."""
+        slots = np.ascontiguousarray(slots, np.uint32)
+        applied = np.ascontiguousarray(applied, np.uint64)
+        assert len(slots) == len(applied)
+        _check(self.lib.gr_notify_applied(self._h, slots.ctypes.data if len(slots) else None,
+                                          applied.ctypes.data if len(applied) else None, len(slots)),
+               "gr_notify_applied")
 
     def step(self, msgs=None, locals_=None):
         """One synchronous pass (gr_step). Returns (messages, results) record arrays."""

@@ -255,6 +255,13 @@ int gr_sync_groups_to_host(gr_engine* e, uint32_t first, gr_peer* out, size_t n)
 int gr_load_peers(gr_engine* e, const uint32_t* slots, const gr_peer* peers, size_t n);
 int gr_sync_peers_to_host(gr_engine* e, const uint32_t* slots, gr_peer* out, size_t n);
 
+/* Peer.NotifyRaftLastApplied (peer.go:282-284) for a list of engine slots
+ * (each listed once; GR_ERANGE before anything is written otherwise): sets
+ * raft.applied, which handleNodeElection reads (raft.go:1055-1079). Call it
+ * before each gr_step with the RSM's batched last applied index, as
+ * node.handleEvents does first in every step (node.go:632-635,653). */
+int gr_notify_applied(gr_engine* e, const uint32_t* slots, const uint64_t* applied, size_t n);
+
 /* One synchronous pass over host buffers (what a cgo caller uses). */
 int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out);
 /* Engine-owned pinned buffers for the next gr_step's inbox: sets in->msgs /

@@ -289,3 +289,52 @@ def test_baseline_config4_full_size_one_gpu(gpu):
     oracle after each of 3 passes (gr_step path; leaders commit on the third)."""
     st = _sim(1_000_000, 3, seed=4)
     assert st["escalations"] == 0 and st["commits"] > 0
+
+
+@pytest.mark.gpu
+def test_notify_applied_gates_elections(built, gpu):
+    """gr_notify_applied = Peer.NotifyRaftLastApplied (peer.go:282) before a pass.
+    Followers whose election timeout fires this pass start an election only when
+    committed <= applied (handleNodeElection, raft.go:1055-1079): behind applied
+    they skip it; after the notify they escalate GR_ESC_ELECTION. Same as the
+    oracle given the same applied indexes; other groups untouched."""
+    from dragonboat_amd import abi, populations as P
+    from dragonboat_amd.engine import Engine
+    from oracle.pyoracle import OraclePopulation
+    import parity
+
+    G, R, S = 512, 3, 3
+    peers = P.make_groups(G, R, seed=17)
+    fol = np.nonzero(peers["state"] == abi.FOLLOWER)[0]
+    peers["election_tick"][fol] = peers["randomized_election_timeout"][fol] - 1
+    peers["applied"][fol] = peers["committed"][fol] - 1
+    eng = Engine(R * G, S)
+    eng.load(peers)
+    slots = fol[::2].astype(np.uint32)
+    new_applied = peers["committed"][slots]
+    eng.notify_applied(slots, new_applied)
+    dev0 = eng.sync(R * G)
+    assert (dev0["applied"][slots] == new_applied).all()
+    rest = np.setdiff1d(np.arange(R * G), slots)
+    assert (dev0["applied"][rest] == peers["applied"][rest]).all()
+
+    want = peers.copy()
+    want["applied"][slots] = new_applied
+    pop = OraclePopulation(want, S)
+    loc = P.propose_locals(R * G, [], ticks=1)
+    msgs = np.zeros(0, abi.MESSAGE)
+    out, res = eng.step(msgs, loc)
+    lim = parity.limits_from(res, R * G)
+    o = pop.step(msgs, loc, lim)
+    bad = parity.compare_states(eng.sync(R * G), o["mid"], S)
+    bad += parity.compare_msgs(out, parity.prefix_msgs(o, lim))
+    bad += parity.compare_results(res, o["results"])
+    assert bad == [], bad[:3]
+    esc = {int(r["peer"]) for r in res if r["escalation"] == 4}  # GR_ESC_ELECTION
+    assert esc == set(int(x) for x in slots)
+    # refused: a slot out of range or listed twice writes nothing
+    with pytest.raises(Exception):
+        eng.notify_applied(np.array([0, 0], np.uint32), np.array([1, 2], np.uint64))
+    with pytest.raises(Exception):
+        eng.notify_applied(np.array([R * G], np.uint32), np.array([1], np.uint64))
+    eng.close()
