@@ -499,6 +499,55 @@ int gr_sync_peers_to_host(gr_engine* e, const uint32_t* slots, gr_peer* out, siz
   return transfer(e, slots, 0, n, out, false);
 }
 
+// LogReader.Compact(index) (logreader.go:251-269) for a slot list, mirrored
+// into the device's firstIndex-1 (entryLog.firstIndex, logentry.go:97-104):
+// after compaction term() answers 0 below it and Replicate sends below it take
+// the snapshot path, as in the reference.
+int gr_compact_log(gr_engine* e, const uint32_t* slots, const uint64_t* index, size_t n, int32_t* status) {
+  if (!e || (n && (!slots || !index))) return GR_EINVAL;
+  if (n == 0) return GR_OK;
+  if (n >= 0x80000000ull) return GR_EINVAL;
+  const uint32_t cap = e->cfg.max_peers;
+  std::vector<uint64_t> seen((cap + 63) / 64, 0);
+  for (size_t x = 0; x < n; ++x) {
+    const uint32_t p = slots[x];
+    if (p >= cap || (seen[p >> 6] >> (p & 63)) & 1) return GR_ERANGE;  // nothing written
+    seen[p >> 6] |= 1ull << (p & 63);
+  }
+  std::lock_guard<std::mutex> guard(e->mu);
+  HIPCHK(hipDeviceSynchronize());  // passes in flight on other streams own the rows
+  const hipStream_t s = e->stream;
+  int r;
+  if ((r = grow_device(&e->d_slots.p, &e->d_slots.n, n * 4))) return r;
+  if ((r = grow_device(&e->d_peers.p, &e->d_peers.n, n * 12 + 16))) return r;
+  if ((r = grow_device(&e->d_scal.p, &e->d_scal.n, 16))) return r;
+  if ((r = grow_pinned(&e->h_scal, &e->h_scal_bytes, 16))) return r;
+  uint64_t* didx = (uint64_t*)e->d_peers.p;
+  int32_t* dst = (int32_t*)(didx + n);
+  HIPCHK(hipMemcpyAsync(e->d_slots.p, slots, n * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(didx, index, n * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(e->d_scal.p, 0, 16, s));
+  const dim3 grid(io_grid(n)), blk(io::kIoBlock);
+  const uint32_t* ds = (const uint32_t*)e->d_slots.p;
+  uint32_t* refused = (uint32_t*)e->d_scal.p;
+  switch (e->S) {
+#define GR_COMPACT_CASE(SS)                                                                                 \
+  case SS:                                                                                                  \
+    hipLaunchKernelGGL(io::compact_rows<SS>, grid, blk, 0, s, e->st, ds, (const uint64_t*)didx, (uint32_t)n, \
+                       dst, refused);                                                                       \
+    break;
+    GR_COMPACT_CASE(1) GR_COMPACT_CASE(2) GR_COMPACT_CASE(3) GR_COMPACT_CASE(4)
+    GR_COMPACT_CASE(5) GR_COMPACT_CASE(6) GR_COMPACT_CASE(7) GR_COMPACT_CASE(8)
+#undef GR_COMPACT_CASE
+    default: return GR_EINVAL;
+  }
+  HIPCHK(hipGetLastError());
+  if (status) HIPCHK(hipMemcpyAsync(status, dst, n * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(e->h_scal, refused, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return *(uint32_t*)e->h_scal ? GR_ESTATE : GR_OK;
+}
+
 // Peer.NotifyRaftLastApplied (peer.go:282-284) for a slot list: raft.applied =
 // the RSM's batched last applied index, as node.handleEvents does first in
 // every step (node.go:632-635,653). No other field changes.

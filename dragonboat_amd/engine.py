@@ -44,6 +44,7 @@ def load_library(path=LIB_PATH):
     lib.gr_load_peers.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_sync_peers_to_host.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_notify_applied.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
+    lib.gr_compact_log.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p]
     lib.gr_step.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.POINTER(abi.Outbox)]
     lib.gr_release_outbox.argtypes = [c.c_void_p, c.POINTER(abi.Outbox)]
     lib.gr_inbox_reserve.argtypes = [c.c_void_p, c.c_size_t, c.c_size_t, c.POINTER(abi.Inbox)]
@@ -138,6 +139,20 @@ class Engine:
         _check(self.lib.gr_notify_applied(self._h, slots.ctypes.data if len(slots) else None,
                                           applied.ctypes.data if len(applied) else None, len(slots)),
                "gr_notify_applied")
+
+    def compact_log(self, slots, index):
+        """LogReader.Compact mirrored on the device (gr_compact_log); returns
+        (rc, per-slot status: 0 ok, 1 ErrCompacted, 2 ErrUnavailable)."""
+        slots = np.ascontiguousarray(slots, np.uint32)
+        index = np.ascontiguousarray(index, np.uint64)
+        assert len(slots) == len(index)
+        st = np.zeros(len(slots), np.int32)
+        rc = self.lib.gr_compact_log(self._h, slots.ctypes.data if len(slots) else None,
+                                     index.ctypes.data if len(index) else None, len(slots),
+                                     st.ctypes.data if len(st) else None)
+        if rc not in (0, -6):
+            _check(rc, "gr_compact_log")
+        return rc, st
 
     def step(self, msgs=None, locals_=None):
         """One synchronous pass (gr_step). Returns (messages, results) record arrays."""

@@ -262,6 +262,15 @@ int gr_sync_peers_to_host(gr_engine* e, const uint32_t* slots, gr_peer* out, siz
  * node.handleEvents does first in every step (node.go:632-635,653). */
 int gr_notify_applied(gr_engine* e, const uint32_t* slots, const uint64_t* applied, size_t n);
 
+/* LogReader.Compact(index) (logreader.go:251-269) for a list of engine slots,
+ * mirrored into entryLog.firstIndex()-1 (logentry.go:97-104): call it when the
+ * host compacts a loaded group's LogDB range (node.compactLog). Per slot,
+ * status (may be NULL) gets 0, 1 = ErrCompacted (index below firstIndex-1) or
+ * 2 = ErrUnavailable (index past lastIndex); only status-0 slots are written
+ * and the call returns GR_ESTATE if any slot was refused. Slots out of range or
+ * listed twice: GR_ERANGE before anything is written. */
+int gr_compact_log(gr_engine* e, const uint32_t* slots, const uint64_t* index, size_t n, int32_t* status);
+
 /* One synchronous pass over host buffers (what a cgo caller uses). */
 int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out);
 /* Engine-owned pinned buffers for the next gr_step's inbox: sets in->msgs /

@@ -338,3 +338,65 @@ def test_notify_applied_gates_elections(built, gpu):
     with pytest.raises(Exception):
         eng.notify_applied(np.array([R * G], np.uint32), np.array([1], np.uint64))
     eng.close()
+
+
+@pytest.mark.gpu
+def test_compact_log_moves_first_index(built, gpu):
+    """gr_compact_log = LogReader.Compact (logreader.go:251-269) mirrored into
+    entryLog.firstIndex. A leader whose lagging follower needs entries below the
+    new firstIndex takes the snapshot path (makeReplicateMessage, raft.go:474-498)
+    exactly as the oracle with the same firstIndex; uncompacted groups replicate.
+    Refusals follow Compact: below firstIndex-1 -> ErrCompacted, past lastIndex ->
+    ErrUnavailable, nothing written for those slots."""
+    from dragonboat_amd import abi, populations as P
+    from dragonboat_amd.engine import Engine
+    from oracle.pyoracle import OraclePopulation
+    import parity
+
+    G, R, S = 256, 3, 3
+    peers = P.make_groups(G, R, seed=23)
+    leaders = np.arange(G)  # replica-major: slot g is group g's leader
+    hi = peers["last_index"][leaders]
+    rem = peers["remotes"]  # field views first: fancy indexing would copy
+    rem["match"][leaders, 1] = hi - np.uint64(10)
+    rem["next"][leaders, 1] = hi - np.uint64(9)
+    eng = Engine(R * G, S)
+    eng.load(peers)
+    comp = leaders[::2].astype(np.uint32)
+    new_lo = peers["last_index"][comp] - np.uint64(5)
+    rc, st = eng.compact_log(comp, new_lo)
+    assert rc == 0 and (st == 0).all()
+    dev0 = eng.sync(R * G)
+    assert (dev0["first_index_m1"][comp] == new_lo).all()
+
+    want = peers.copy()
+    want["first_index_m1"][comp] = new_lo
+    pop = OraclePopulation(want, S)
+    loc = P.propose_locals(R * G, leaders, pass_index=0)
+    msgs = np.zeros(0, abi.MESSAGE)
+    out, res = eng.step(msgs, loc)
+    lim = parity.limits_from(res, R * G)
+    # The oracle runs the host suffix too: in the reference the escalated item
+    # reaches makeInstallSnapshotMessage, whose log has no snapshot here (a Go
+    # panic, "got an empty snapshot"); the device prefix is compared.
+    o = pop.step(msgs, loc, lim, allow_error=True)
+    assert o["error"] == "" or "empty snapshot" in o["error"], o["error"]
+    bad = parity.compare_states(eng.sync(R * G), o["mid"], S)
+    bad += parity.compare_msgs(out, parity.prefix_msgs(o, lim))
+    bad += parity.compare_results(res, o["results"])
+    assert bad == [], bad[:3]
+    snap = {int(r["peer"]) for r in res if r["escalation"] == 7}  # GR_ESC_SNAPSHOT
+    assert snap == set(int(x) for x in comp)
+
+    # Compact's refusals: index below firstIndex-1, index past lastIndex
+    dev1 = eng.sync(R * G)
+    probe = np.array([G + 1, G + 2, G + 3], np.uint32)
+    idx = np.array([dev1["first_index_m1"][G + 1] - 1, dev1["last_index"][G + 2] + 1,
+                    dev1["first_index_m1"][G + 3] + 1], np.uint64)
+    rc, st = eng.compact_log(probe, idx)
+    assert rc == -6 and list(st) == [1, 2, 0]
+    dev2 = eng.sync(R * G)
+    assert dev2["first_index_m1"][G + 1] == dev1["first_index_m1"][G + 1]
+    assert dev2["first_index_m1"][G + 2] == dev1["first_index_m1"][G + 2]
+    assert dev2["first_index_m1"][G + 3] == idx[2]
+    eng.close()
