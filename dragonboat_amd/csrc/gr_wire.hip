@@ -231,6 +231,7 @@ struct Scratch {
   u32* ent_pos;      // [msgs] offset of the first Entries field of a canonical message, ~0 = general
   u64* msg_start;    // [msgs] absolute start and length of each message: decode_ents reads
   u32* msg_len;      //        12 B here, not the 120-B record
+  u32* first_bad;    // [n] lowest failing message ordinal per frame (atomicMin), ~0 = none
 };
 
 __device__ __forceinline__ u64 pack_err(int st, int lvl, int panic, u32 field) {
@@ -706,6 +707,7 @@ __global__ __launch_bounds__(256) void decode_msgs(const u8* buf, u64 buf_len, c
   s.msg_start[j] = start;
     s.msg_len[j] = len;
   s.msg_err[j] = pack_err(e.st, e.lvl, 0, e.field);
+  if (e.st) atomicMin(&s.first_bad[b], j - s.first_msg[b]);
 }
 
 __global__ __launch_bounds__(256) void decode_ents(const u8* buf, u64 buf_len, u32 total, Scratch s,
@@ -755,14 +757,10 @@ __global__ void finish_frames(grw_batch* batches, u32 n, Scratch s) {
   u32 field = (u32)(we >> 32), at = c;
   if ((we >> 16) & 1) {
     st = GRW_E_PANIC; lvl = GRW_LVL_BATCH; field = 0; at = 0;
-  } else {
-    for (u32 k = 0; k < c; ++k) {
-      u64 me = s.msg_err[f + k];
-      if (me & 0xff) {
-        st = (int)(me & 0xff); lvl = (int)((me >> 8) & 0xff); field = (u32)(me >> 32); at = k;
-        break;
-      }
-    }
+  } else if (s.first_bad[b] < c) {  // the first failing message, found by decode_msgs' atomicMin
+    const u32 k = s.first_bad[b];
+    const u64 me = s.msg_err[f + k];
+    st = (int)(me & 0xff); lvl = (int)((me >> 8) & 0xff); field = (u32)(me >> 32); at = k;
   }
   bt.status = st;
   bt.err_level = (u8)(st ? lvl : GRW_LVL_BATCH);
@@ -1003,7 +1001,7 @@ struct grw_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev[6] = {};
   grw_timing timing{};
-  Buf spans, walked, first_msg, walk_err, msg_batch, ents_per_msg, first_ent, msg_err, ent_pos, msg_start, msg_len, tmp, scal;
+  Buf spans, walked, first_msg, walk_err, msg_batch, ents_per_msg, first_ent, msg_err, ent_pos, msg_start, msg_len, first_bad, tmp, scal;
   Buf fsz, pos, flen, foff, pflag;
   // host-path staging
   Buf d_buf, d_batches, d_msgs, d_ents;
@@ -1069,7 +1067,7 @@ void grw_destroy(grw_ctx* c) {
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   grw_ctx::Buf* bufs[] = {&c->spans, &c->walked, &c->first_msg, &c->walk_err, &c->msg_batch, &c->ents_per_msg,
-                          &c->first_ent, &c->msg_err, &c->ent_pos, &c->msg_start, &c->msg_len, &c->tmp, &c->scal, &c->fsz, &c->pos, &c->flen, &c->foff,
+                          &c->first_ent, &c->msg_err, &c->ent_pos, &c->msg_start, &c->msg_len, &c->first_bad, &c->tmp, &c->scal, &c->fsz, &c->pos, &c->flen, &c->foff,
                           &c->pflag, &c->d_buf, &c->d_batches, &c->d_msgs, &c->d_ents};
   for (auto* b : bufs)
     if (b->p) hipFree(b->p);
@@ -1097,13 +1095,15 @@ int grw_decode_device(grw_ctx* c, const uint8_t* d_buf, size_t buf_len, grw_batc
   hipStream_t s = c->stream;
   int r;
   if ((r = grow(c->spans, (buf_len / 2 + 2) * 8)) || (r = grow(c->walked, n * 4)) || (r = grow(c->first_msg, n * 4)) ||
-      (r = grow(c->walk_err, n * 8)) || (r = grow(c->scal, 64)))
+      (r = grow(c->walk_err, n * 8)) || (r = grow(c->scal, 64)) || (r = grow(c->first_bad, n * 4)))
     return r;
   Scratch sc{};
   sc.spans = (u64*)c->spans.p;
   sc.walked = (u32*)c->walked.p;
   sc.first_msg = (u32*)c->first_msg.p;
   sc.walk_err = (u64*)c->walk_err.p;
+  sc.first_bad = (u32*)c->first_bad.p;
+  HIPCHK(hipMemsetAsync(sc.first_bad, 0xFF, n * 4, s));
   HIPCHK(hipEventRecord(c->ev[0], s));
   walk_frames<<<(unsigned)n, 64, 0, s>>>(d_buf, buf_len, d_batches, (u32)n, sc);
   HIPCHK(hipGetLastError());
