@@ -11,6 +11,8 @@
 //                    spans (into a scratch slot per 2 frame bytes, so no scan is
 //                    needed first), DeploymentId/SourceAddress/BinVer, the first
 //                    walk error and whether messageCount panics.
+//      (frames of >= 4 segments on average first run spec_segments: one wave
+//      per 8 KiB segment walks a speculative chain that walk_frames adopts)
 //   2. scan          exclusive sum of messages per frame -> first_msg.
 //   3. decode_msgs   one lane per message: every Message field (last wins),
 //                    entries validated (colfer), entry count, Snapshot span.
@@ -27,6 +29,7 @@
 
 #pragma clang diagnostic ignored "-Wunused-value"
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -232,7 +235,82 @@ struct Scratch {
   u64* msg_start;    // [msgs] absolute start and length of each message: decode_ents reads
   u32* msg_len;      //        12 B here, not the 120-B record
   u32* first_bad;    // [n] lowest failing message ordinal per frame (atomicMin), ~0 = none
+  // Large frames only (null otherwise): speculative segment chains, see spec_segments.
+  u64* stage;        // [buf_len/2 + 2] chain heads of segment g at slot (g << seg_shift)/2 + k
+  const struct SegRec* segs;  // [ceil(buf_len/segment)]
+  u32 seg_shift;
 };
+
+// 1a. Speculative segment walks, launched when frames average >= 4 segments
+// of bytes (the transport's large batches, SendQueueLength 8,192 at soft.go:254).
+// The walk's fast rule (a Requests field `0a len` with a 1- or 2-byte length)
+// is a function of the position alone, so two chains that share one head
+// coincide from there on. One wave per segment of the buffer starts
+// at the first plausible message head in the segment (`0a len 08`, 08 being
+// Message.Type's tag, raft.pb.go Message.MarshalTo) and follows the rule until
+// it leaves the segment. walk_frames adopts a segment's chain as soon as its
+// own serial walk lands on one of the chain's first kSegProbe heads, and copies
+// the staged spans instead of walking them. The chain is frame-agnostic; the
+// adopting walk accepts it only when every head and end lies inside its frame.
+// Segment size is 1 << seg_shift bytes (kSegShift by default, GRW_SEG_SHIFT in
+// the environment overrides it for tuning, 10..16: a head's offset in its
+// segment is staged in 16 bits).
+constexpr u32 kSegShift = 13;  // A/B on 512 x 8,192 messages: 12..16 -> walk 0.48/0.45/0.52/0.58/0.85 ms
+constexpr u32 kSegProbe = 64;
+struct SegRec {
+  u64 exit;  // absolute: first position >= the segment end, or the head the rule refused
+  u32 k;     // chain heads staged (0: no plausible head in the segment)
+  u32 pad;
+};
+// Staged head: head offset in the segment | header bytes << 16 (low word), length (high word).
+__device__ __forceinline__ u64 stage_head(u64 s0, u64 st) { return s0 + (st & 0xffff); }
+
+__global__ __launch_bounds__(64) void spec_segments(const u8* buf, u64 buf_len, u64* stage, SegRec* segs, u32 nseg,
+                                                    u32 seg_shift) {
+  __shared__ uint4 lds_raw[kWin / 16 + 1];
+  const u32 g = blockIdx.x;
+  if (g >= nseg) return;
+  Win w{(u8*)lds_raw, buf, buf_len, 1, 0};
+  const u64 s0 = (u64)g << seg_shift;
+  const u64 s1 = s0 + (1ull << seg_shift) < buf_len ? s0 + (1ull << seg_shift) : buf_len;
+  const u32* d = (const u32*)w.lds;
+  // First plausible head, 64 positions per round.
+  u64 c = ~0ull;
+  for (u64 p = s0; p < s1; p += 64) {
+    if (p < w.lo || p >= w.hi || p + 72 > w.lo + kWin) w.load(p);  // uniform; zeros past the buffer
+    u32 o = (u32)(p - w.lo) + threadIdx.x;
+    u64 pair = (u64)d[o >> 2] | ((u64)d[(o >> 2) + 1] << 32);
+    u32 q = (u32)(pair >> (8 * (o & 3)));
+    u32 b1 = (q >> 8) & 0xff, b2 = (q >> 16) & 0xff, b3 = q >> 24;
+    bool hit = (q & 0xff) == 0x0a && p + threadIdx.x < s1 &&
+               ((b1 < 0x80 && b2 == 0x08) || (b1 >= 0x80 && b2 < 0x80 && b3 == 0x08));
+    u64 m = __ballot(hit);
+    if (m) {
+      c = p + (u64)(__ffsll((long long)m) - 1);
+      break;
+    }
+  }
+  u32 k = 0;
+  u64 i = c;
+  if (c != ~0ull) {
+    u64* st = stage + (s0 >> 1);
+    while (i < s1) {
+      u32 q = w.peek4(i);
+      if ((q & 0xff) != 0x0a) break;
+      u32 b1 = (q >> 8) & 0xff, b2 = (q >> 16) & 0xff;
+      u64 len, hdr;
+      if (b1 < 0x80) { len = b1; hdr = 2; }
+      else if (b2 < 0x80) { len = (b1 & 0x7f) | (b2 << 7); hdr = 3; }
+      else break;
+      u64 post = i + hdr + len;
+      if (post > buf_len) break;
+      if (threadIdx.x == 0) st[k] = (u64)((u32)(i - s0) | ((u32)hdr << 16)) | (len << 32);
+      k++;
+      i = post;
+    }
+  }
+  if (threadIdx.x == 0) segs[g] = SegRec{i, k, 0};
+}
 
 __device__ __forceinline__ u64 pack_err(int st, int lvl, int panic, u32 field) {
   return (u64)(u32)st | ((u64)lvl << 8) | ((u64)panic << 16) | ((u64)field << 32);
@@ -240,6 +318,7 @@ __device__ __forceinline__ u64 pack_err(int st, int lvl, int panic, u32 field) {
 
 // 1. One wave per frame: the MessageBatch.Unmarshal loop without decoding the
 // messages (raft_optimized.go:1050-1202).
+template <bool kSpec>
 __global__ __launch_bounds__(64) void walk_frames(const u8* buf, u64 buf_len, grw_batch* batches, u32 n,
                                                   Scratch s) {
   __shared__ uint4 lds_raw[kWin / 16 + 1];  // +16 B: peek4 past the window end
@@ -257,10 +336,52 @@ __global__ __launch_bounds__(64) void walk_frames(const u8* buf, u64 buf_len, gr
   u32 efield = 0;
   i64 first_post = -1;  // post of the first message field: messageCount's start
   i64 i = 0;
+  // Segment chain adoption state (large frames, see spec_segments).
+  u32 cur_seg = ~0u;
+  SegRec rec{0, 0, 0};
+  u64 probe = ~0ull;  // this lane's staged head (absolute) in segment cur_seg
   // Fast loop: Requests fields back to back, as MessageBatch.MarshalTo writes
   // them (raft.pb.go:1935-1945), with 1- or 2-byte lengths. It consumes only
   // fields the general loop below would accept unchanged, then hands over.
   while (i + 3 <= l) {
+    if (kSpec && nm > 0) {
+      const u64 a = base + (u64)i;
+      const u32 g = (u32)(a >> s.seg_shift);
+      const u64 s0 = (u64)g << s.seg_shift;
+      if (g != cur_seg) {
+        cur_seg = g;
+        rec = s.segs[g];
+        u64 st = s.stage[(s0 >> 1) + threadIdx.x];
+        probe = threadIdx.x < rec.k && threadIdx.x < kSegProbe ? stage_head(s0, st) : ~0ull;
+      }
+      const u64 m = __ballot(probe == a);
+      // Adopt: heads o..k-1 of the segment's chain are the heads this walk
+      // would take from a, provided the chain's end lies inside the frame
+      // (then every head h has h + 3 <= l and every end <= l).
+      if (m && rec.exit < base + (u64)l) {
+        const u32 o = (u32)(__ffsll((long long)m) - 1);
+        const u64* st = s.stage + (s0 >> 1) + o;
+        const u32 cnt = rec.k - o;
+        for (u32 q0 = 0; q0 < cnt; q0 += 8 * 64) {
+          u64 v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            u32 t = q0 + (u32)j * 64 + threadIdx.x;
+            v[j] = t < cnt ? st[t] : 0;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            u32 t = q0 + (u32)j * 64 + threadIdx.x;
+            if (t < cnt)
+              spans[nm + t] = (u64)(u32)(stage_head(s0, v[j]) + ((v[j] >> 16) & 3) - base) |
+                              (v[j] & 0xffffffff00000000ull);
+          }
+        }
+        nm += cnt;
+        i = (i64)(rec.exit - base);
+        continue;
+      }
+    }
     u32 q = w.peek4(base + (u64)i);
     if ((q & 0xff) != 0x0a) break;
     u32 b1 = (q >> 8) & 0xff, b2 = (q >> 16) & 0xff;
@@ -1002,6 +1123,7 @@ struct grw_ctx {
   hipEvent_t ev[6] = {};
   grw_timing timing{};
   Buf spans, walked, first_msg, walk_err, msg_batch, ents_per_msg, first_ent, msg_err, ent_pos, msg_start, msg_len, first_bad, tmp, scal;
+  Buf stage, segs;  // large-frame segment chains (spec_segments)
   Buf fsz, pos, flen, foff, pflag;
   // host-path staging
   Buf d_buf, d_batches, d_msgs, d_ents;
@@ -1067,7 +1189,7 @@ void grw_destroy(grw_ctx* c) {
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   grw_ctx::Buf* bufs[] = {&c->spans, &c->walked, &c->first_msg, &c->walk_err, &c->msg_batch, &c->ents_per_msg,
-                          &c->first_ent, &c->msg_err, &c->ent_pos, &c->msg_start, &c->msg_len, &c->first_bad, &c->tmp, &c->scal, &c->fsz, &c->pos, &c->flen, &c->foff,
+                          &c->first_ent, &c->msg_err, &c->ent_pos, &c->msg_start, &c->msg_len, &c->first_bad, &c->stage, &c->segs, &c->tmp, &c->scal, &c->fsz, &c->pos, &c->flen, &c->foff,
                           &c->pflag, &c->d_buf, &c->d_batches, &c->d_msgs, &c->d_ents};
   for (auto* b : bufs)
     if (b->p) hipFree(b->p);
@@ -1104,8 +1226,28 @@ int grw_decode_device(grw_ctx* c, const uint8_t* d_buf, size_t buf_len, grw_batc
   sc.walk_err = (u64*)c->walk_err.p;
   sc.first_bad = (u32*)c->first_bad.p;
   HIPCHK(hipMemsetAsync(sc.first_bad, 0xFF, n * 4, s));
+  u32 seg_shift = kSegShift;
+  if (const char* e = getenv("GRW_SEG_SHIFT")) {
+    int v = atoi(e);
+    if (v >= 10 && v <= 16) seg_shift = (u32)v;
+  }
+  const bool spec = buf_len / n >= (4ull << seg_shift);  // >= 4 segments per frame on average
+  const u64 nseg = (buf_len + (1ull << seg_shift) - 1) >> seg_shift;
+  sc.seg_shift = seg_shift;
+  if (spec) {
+    if ((r = grow(c->stage, (buf_len / 2 + 2 + kSegProbe) * 8)) || (r = grow(c->segs, nseg * sizeof(SegRec)))) return r;
+    sc.stage = (u64*)c->stage.p;
+    sc.segs = (const SegRec*)c->segs.p;
+  }
   HIPCHK(hipEventRecord(c->ev[0], s));
-  walk_frames<<<(unsigned)n, 64, 0, s>>>(d_buf, buf_len, d_batches, (u32)n, sc);
+  if (spec) {
+    spec_segments<<<(unsigned)nseg, 64, 0, s>>>(d_buf, buf_len, sc.stage, (SegRec*)c->segs.p, (u32)nseg, seg_shift);
+    HIPCHK(hipGetLastError());
+  }
+  if (spec)
+    walk_frames<true><<<(unsigned)n, 64, 0, s>>>(d_buf, buf_len, d_batches, (u32)n, sc);
+  else
+    walk_frames<false><<<(unsigned)n, 64, 0, s>>>(d_buf, buf_len, d_batches, (u32)n, sc);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[1], s));
   if ((r = scan_excl<u32>(c, sc.walked, sc.first_msg, n))) return r;

@@ -385,3 +385,37 @@ def test_gpu_large_pass(wbuilt, gpu):
     b2, m2, e2 = PW.decode(out, fr.copy())
     assert compare(out, b1, m1, e1, b2, m2, e2) == []
     assert len(m1) == len(m) == 4096 * 256
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seg_shift", [None, "10", "16"])
+def test_gpu_large_frame_segment_walk(wbuilt, gpu, seg_shift, monkeypatch):
+    """Frames that average >= 64 KiB take the speculative segment walk (spec_segments +
+    chain adoption in walk_frames): records, statuses and fields equal the oracle on
+    steady and mixed large frames, and on seeded corruptions of them (flips,
+    truncations and insertions anywhere in the frame shift or break the chains).
+    GRW_SEG_SHIFT sweeps the segment size (1 KiB, the default 8 KiB, 64 KiB)."""
+    if seg_shift:
+        monkeypatch.setenv("GRW_SEG_SHIFT", seg_shift)
+    codec = W.WireCodec(0)
+    rng = np.random.default_rng(33)
+    frames = []
+    for seed, n_frames, mpb, steady in ((31, 5, 3000, True), (32, 4, 1500, False)):
+        payload, b, m, e = PW.make_records(n_frames, mpb, seed=seed, steady=steady, snap_frac=0.02)
+        out = PW.encode(payload, b, m, e)
+        fr = W.frames_table(b["frame_off"], b["frame_len"])
+        assert out.size // len(fr) >= 65536
+        b1, m1, e1 = codec.unmarshal(out, fr.copy())
+        b2, m2, e2 = PW.decode(out, fr.copy())
+        assert compare(out, b1, m1, e1, b2, m2, e2) == [], seed
+        assert (b1["status"] == 0).all() and len(m1) == len(m) and len(e1) == len(e)
+        frames += [out[int(o):int(o) + int(l)].tobytes() for o, l in zip(b["frame_off"], b["frame_len"])]
+    corpus = list(frames)
+    for f in frames:
+        corpus += mutate(f, rng, 3)
+    buf, b = PW.frames(*corpus)
+    assert buf.size // len(b) >= 65536
+    bd, md, ed = codec.unmarshal(buf, b.copy())
+    bo, mo, eo = PW.decode(buf, b.copy())
+    assert compare(buf, bd, md, ed, bo, mo, eo) == []
+    assert (bo["status"] != 0).any() and (bo["status"] == 0).any()
