@@ -10,7 +10,7 @@ rc=$?; tail -4 $OUT/wire_tests.log; [ $rc -eq 0 ] || exit $rc
 for sh in 13; do
   GRW_SEG_SHIFT=$sh timeout -k 10 120 python -u tools/bench_wire.py --frames 512 --per-frame 8192 --cpu-baseline off > $OUT/wire_8192_s$sh.json 2>$OUT/wire_8192_s$sh.err || exit $?
 done
-for sh in 10 11 12 13; do GRW_SEG_SHIFT=$sh timeout -k 10 120 python -u tools/bench_wire.py --cpu-baseline off > $OUT/wire_default_s$sh.json 2>$OUT/wire_default_s$sh.err || exit $?; done
+for sh in; do GRW_SEG_SHIFT=$sh timeout -k 10 120 python -u tools/bench_wire.py --cpu-baseline off > $OUT/wire_default_s$sh.json 2>$OUT/wire_default_s$sh.err || exit $?; done
 timeout -k 10 120 python -u tools/bench_wire.py --cpu-baseline off > $OUT/wire_default.json 2>$OUT/wire_default.err || exit $?
 python3 - <<'PY'
 import json, glob
