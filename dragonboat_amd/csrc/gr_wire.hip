@@ -904,11 +904,8 @@ __global__ void finish_frames(grw_batch* batches, u32 n, Scratch s) {
 
 // ------------------------------------------------------------------ encode --
 
-__device__ __forceinline__ int sov(u64 x) {
-  int n = 0;
-  do { n++; x >>= 7; } while (x);
-  return n;
-}
+// Varint length of x, branch-free: ceil(bits / 7) with bits(0) taken as 1.
+__device__ __forceinline__ int sov(u64 x) { return (70 - __clzll((long long)(x | 1))) / 7; }
 
 // Entry.Size (raft_optimized.go:78-153); -1 where it panics.
 __device__ i64 entry_size(const grw_entry& o) {
@@ -918,16 +915,16 @@ __device__ i64 entry_size(const grw_entry& o) {
   for (int k = 0; k < 6; ++k) {
     u64 x = f64[k];
     if (x >= (1ull << 49)) l += 9;
-    else if (x != 0) { for (l += 2; x >= 0x80; l++) x >>= 7; }
+    else if (x != 0) l += 1 + sov(x);
     if (k == 1 && o.type != 0) {
       u32 x32 = (u32)o.type;
       if (o.type < 0) x32 = ~x32 + 1;
-      for (l += 2; x32 >= 0x80; l++) x32 >>= 7;
+      l += 1 + sov(x32);
     }
   }
   if (u64 x = o.cmd_len) {
     if (x > GRW_COLFER_SIZE_MAX) return -1;
-    for (l += (i64)x + 2; x >= 0x80; l++) x >>= 7;
+    l += (i64)x + 1 + sov(x);
   }
   if (l > (i64)GRW_COLFER_SIZE_MAX) return -1;
   return l;
