@@ -1071,9 +1071,15 @@ __global__ void write_msgs(const grw_batch* batches, const grw_message* msgs, u3
   if (panic_flag[b]) return;
   u64 at = s.foff[b] + (s.pos[j] - s.pos[batches[b].first_msg]);
   const grw_message m = msgs[j];
-  Wr w(out, at, at + s.fsz[j]);
+  // fsz = 1 + l + sov(l) with l = Message.Size(); l + sov(l) rises strictly
+  // with l, so l is found from fsz in a few steps instead of re-reading the
+  // entries (the batch did not panic, so size_msgs stored a real size).
+  const u64 fsz = s.fsz[j];
+  u64 l = fsz - 2;
+  while (1 + l + (u64)sov(l) != fsz) --l;
+  Wr w(out, at, at + fsz);
   w.put(0x0a);
-  w.varint((u64)message_size(m, ents));
+  w.varint(l);
   w.put(0x08); w.varint((u64)(i64)m.type);
   w.put(0x10); w.varint(m.to);
   w.put(0x18); w.varint(m.from);
