@@ -1063,13 +1063,8 @@ __global__ void frame_finish(grw_batch* batches, u32 n, EncScratch s, const u32*
   batches[b].status = panic_flag[b] ? GRW_E_PANIC : GRW_OK;
 }
 
-__global__ void write_msgs(const grw_batch* batches, const grw_message* msgs, u32 total, const grw_entry* ents,
-                           const u8* payload, EncScratch s, const u32* panic_flag, u8* out) {
-  u32 j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= total) return;
-  u32 b = s.msg_batch[j];
-  if (panic_flag[b]) return;
-  u64 at = s.foff[b] + (s.pos[j] - s.pos[batches[b].first_msg]);
+__device__ __forceinline__ void write_msg(u32 j, u64 at, const grw_message* msgs, const grw_entry* ents,
+                                          const u8* payload, EncScratch s, u8* out) {
   const grw_message m = msgs[j];
   // fsz = 1 + l + sov(l) with l = Message.Size(); l + sov(l) rises strictly
   // with l, so l is found from fsz in a few steps instead of re-reading the
@@ -1105,6 +1100,60 @@ __global__ void write_msgs(const grw_batch* batches, const grw_message* msgs, u3
     for (int k = 0; k < 12; ++k) w.put(kZeroSnap[k]);
   }
   w.put(0x68); w.varint(m.hint_high);
+}
+
+// One lane per message. A block whose messages span at most kOutStage bytes
+// (and whose batches did not panic) assembles them in LDS and stores the span
+// with coalesced 16-B writes; bytes between frames (tails) are written by
+// write_tails afterwards. Writing the records straight to HBM, each wave's
+// dword stores touched ~60 lines at once and partial lines were evicted:
+// WRITE_SIZE was ~5x the output (profiles/r01_wire_h/pmc).
+constexpr u32 kOutStage = 24576;
+__global__ __launch_bounds__(256) void write_msgs(const grw_batch* batches, const grw_message* msgs, u32 total,
+                                                  const grw_entry* ents, const u8* payload, EncScratch s,
+                                                  const u32* panic_flag, u8* out) {
+  __shared__ uint4 img[kOutStage / 16];
+  __shared__ unsigned long long s_lo, s_hi;
+  __shared__ int s_bad;
+  u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+  bool act = j < total;
+  u32 b = 0;
+  bool bad = false;
+  u64 at = 0, end = 0;
+  if (threadIdx.x == 0) { s_lo = ~0ull; s_hi = 0; s_bad = 0; }
+  __syncthreads();
+  if (act) {
+    b = s.msg_batch[j];
+    bad = panic_flag[b] != 0;
+    at = s.foff[b] + (s.pos[j] - s.pos[batches[b].first_msg]);
+    end = at + s.fsz[j];
+    if (bad) atomicOr(&s_bad, 1);
+    else {
+      atomicMin(&s_lo, (unsigned long long)at);
+      atomicMax(&s_hi, (unsigned long long)end);
+    }
+  }
+  __syncthreads();
+  const u64 lo = s_lo, hi = s_hi, alo = lo & ~15ull;
+  const bool staged = s_bad == 0 && hi > lo && hi - alo <= kOutStage;
+  if (!staged) {
+    if (act && !bad) write_msg(j, at, msgs, ents, payload, s, out);
+    return;
+  }
+  if (act) write_msg(j, at - alo, msgs, ents, payload, s, (u8*)img);
+  __syncthreads();
+  for (u64 off = (u64)threadIdx.x * 16; alo + off < hi; off += (u64)blockDim.x * 16) {
+    const u64 g = alo + off;
+    const uint4 v = img[off >> 4];
+    u8* q = out + g;
+    if (g >= lo && g + 16 <= hi && (((uintptr_t)q) & 15) == 0) {
+      *(uint4*)q = v;
+    } else {
+      const u8* vb = (const u8*)&v;
+      for (int k = 0; k < 16; ++k)
+        if (g + k >= lo && g + k < hi) q[k] = vb[k];
+    }
+  }
 }
 
 __global__ void write_tails(const grw_batch* batches, u32 n, const u8* payload, EncScratch s, const u32* panic_flag,
