@@ -16,15 +16,20 @@ replica r of a group homed on rank h lives on rank (h + r) % N and the
 Replicate/ReplicateResp mailboxes cross GPUs with one RCCL all_to_all_single
 per pass (dragonboat_amd/exchange.py).
 
-Roofline accounting: algorithmic bytes are SURVEY.md §8d's
-per-unit figures times the units the launch processed, counted on the device:
-69 B per message a leader ingests (B_resp), 65 B per message a leader emits
-(B_emit), 122 + 16 n B per Replicate of n entries a follower matches
-(B_match with ov + ap = n), and 8R + 48 B per group for the quorum commit
-(B_commit). In steady state each follower gets two Replicates per pass (the
-commit-carrying broadcast of raft.go:1214 and the proposal's), so one
-group-round is 1,128 B at R = 3; SURVEY's B_round (616 B) assumes one, and is
-reported beside it as "canonical_round_bytes".
+Roofline accounting: `achieved` = SURVEY.md §8d's algorithmic
+bytes per unit times the units one launch processed, over the fast kernel's
+HIP-event duration. The unit is one group-round, B_round(R) = (R-1)(69+65+138)
++ 8R + 48 = 616 B at R = 3, and a launch processes one group-round per leader
+commit. `traffic` is the calibrated FETCH_SIZE + WRITE_SIZE of the same kernel
+(profiles/pmc_latest.json, used only when its source digest matches this
+build) and `traffic_frac` the physical rate over the 8 TB/s peak. The
+reference-width per-message count (two Replicates and two acks per follower per
+round, 1,128 B/group) is reported as `reference_width_bytes_per_launch` only.
+`copy_f4_GBs` is tools/hbm_calib's float4 copy on the same box (achievable HBM).
+
+Beside the headline (rank 0, N = 1): `host_path` times gr_step with host records
+(the C-ABI call a Go step worker makes, PCIe-inclusive), and `cpu_baseline`
+follows BASELINE.md's CPU protocol on bounded samples.
 """
 import argparse
 import json
@@ -44,35 +49,15 @@ def b_round(R):
 B_RESP, B_EMIT, B_MATCH0, B_ENTRY = 69, 65, 122, 16
 
 
-def algorithmic_bytes(st, groups, R, passes):
-    """SURVEY.md §8d per-unit bytes x the units counted by the device stats over `passes` passes."""
+def reference_width_bytes(st, groups, R, passes):
+    """SURVEY.md §8d per-message bytes x the messages counted by the device over `passes`
+    passes (two Replicates and two acks per follower per round: 1,128 B/group at R = 3)."""
     follower_in = st["msgs_in"] - st["leader_msgs_in"]
     return (B_RESP * st["leader_msgs_in"] + B_EMIT * st["leader_msgs_out"] + B_MATCH0 * follower_in
             + B_ENTRY * st["replicate_entries"] + (8 * R + 48) * groups * passes)
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, spec
-
-
-def stream_copy_gbs(torch, dev, nbytes=1 << 30, reps=5):
-    """Achievable HBM bandwidth on this box: a device-to-device copy of 1 GiB
-    (read + write = 2 GiB moved per copy, past the 256 MiB Infinity Cache),
-    best of `reps`, HIP events. Reported beside the spec peak, never instead of it."""
-    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    b = torch.empty_like(a)
-    a.fill_(1)
-    b.copy_(a)
-    best = None
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        b.copy_(a)
-        e1.record()
-        e1.synchronize()
-        ms = e0.elapsed_time(e1)
-        best = ms if best is None else min(best, ms)
-    del a, b
-    return 2 * nbytes / (best * 1e-3) / 1e9
 
 
 def parse():
@@ -85,47 +70,187 @@ def parse():
     ap.add_argument("--placement", choices=["local", "spread"], default=None)
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
     ap.add_argument("--cpu-groups", type=int, default=20000)
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(affinity CPUs, GR_CPU_SHARE=16)")
+    ap.add_argument("--cpu-seconds", type=float, default=24.0, help="CPU baseline time budget (all legs)")
+    ap.add_argument("--host-path", choices=["on", "off"], default="on",
+                    help="also time gr_step with host records (N=1, rank 0)")
+    ap.add_argument("--host-passes", type=int, default=4)
     ap.add_argument("--check", action="store_true", help="verify the final state against a host replay")
     return ap.parse_args()
 
 
-def cpu_baseline(args, R):
-    """The oracle (C++ restatement of the reference Go step, faithful data
-    structures) on a bounded sample of the same workload, host cores only."""
+def cpu_info():
+    """Host CPU description for the baseline (nproc + lscpu model)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "lscpu_model": model}
+
+
+# The GPU box allots 16 host CPUs per GPU (its process guard sizes pools to that
+# share even though nproc shows the whole machine), so T = min(affinity, 16).
+CPU_SHARE = int(os.environ.get("GR_CPU_SHARE", "16"))
+
+
+def _oracle_rate(peers, topo, R, locals_fn, threads, seconds, inject=None, drop=None):
+    """Oracle raft step (C++ restatement of internal/raft, faithful data structures)
+    over a population for about `seconds`: returns (leader commits/s, groups
+    stepped/s, passes). Message routing, persistence and injection are untimed."""
     import numpy as np
-    from dragonboat_amd import abi, populations as P
+    from dragonboat_amd import abi
     from oracle.pyoracle import OraclePopulation
-    G = args.cpu_groups
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    peers = P.make_groups(G, R, seed=2)
-    topo = P.Topology(G, R)
     pop = OraclePopulation(peers, R)
+    G = topo.G
     msgs = np.zeros(0, abi.MESSAGE)
-    # warm to steady state (2 passes), then time
-    for k in range(2):
-        loc = P.propose_locals(R * G, np.arange(G), pass_index=k)
-        o = pop.step(msgs, loc, threads=threads)
+    for k in range(2):  # to steady state
+        o = pop.step(msgs, locals_fn(k, pop), threads=threads)
         msgs = topo.route_messages(o["msgs"])
+        pop.commit_all()
     passes, t_step, commits = 0, 0.0, 0
-    before = pop.export()["committed"][:G].copy()
-    t_end = time.time() + 10.0
+    t_end = time.time() + seconds
     k = 2
     while time.time() < t_end or passes < 2:
-        loc = P.propose_locals(R * G, np.arange(G), pass_index=k)
+        if inject is not None:
+            inject(k, pop)
+        loc = locals_fn(k, pop)
+        before = pop.export()["committed"]
         t0 = time.perf_counter()
         o = pop.step(msgs, loc, threads=threads)
         t_step += time.perf_counter() - t0
+        end = o["mid"]  # no limits: the state after the whole pass
+        commits += int(np.sum((end["committed"] > before) & (end["state"] == abi.LEADER)))
         msgs = topo.route_messages(o["msgs"])
+        if drop is not None:
+            msgs = drop(k, msgs)
         pop.commit_all()
         passes += 1
         k += 1
-    after = pop.export()["committed"][:G]
-    commits = int(np.sum(after - before))
-    return {"value": commits / t_step, "unit": "commit-index updates/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{G} groups x {R} replicas, {passes} passes, oracle raft step timed "
-                      f"(message routing and persistence excluded), {threads} threads"}
+    return commits / t_step, G * passes / t_step, passes
+
+
+def cpu_baseline(args, R):
+    """BASELINE.md's CPU protocol on bounded samples, host cores only: the oracle
+    (C++ restatement of the reference Go step, kind "port") at T threads and at 1
+    thread on BASELINE config 4's shape (the headline's twin), plus configs 2, 3
+    and 5 on the same generators and seeds as the GPU runs."""
+    import numpy as np
+    from dragonboat_amd import abi, populations as P
+    info = cpu_info()
+    T = args.cpu_threads or max(1, min(info["affinity_cpus"], CPU_SHARE))
+    G = args.cpu_groups
+    budget = args.cpu_seconds
+    steady = lambda G_: (lambda k, pop: P.propose_locals(R * G_, np.arange(G_), pass_index=k))
+    # config 4's shape (1M x 3 on the GPU): a G-group sample, T threads and 1 thread
+    peers = P.make_groups(G, R, seed=2)
+    topo = P.Topology(G, R)
+    c4, _, n4 = _oracle_rate(peers, topo, R, steady(G), T, 0.35 * budget)
+    c4_1, _, n4_1 = _oracle_rate(peers, topo, R, steady(G), 1, 0.2 * budget)
+    out = {"value": c4, "unit": "commit-index updates/s", "cores": T, "kind": "port",
+           "sample": f"config 4 shape: {G} groups x {R} replicas, {n4} passes, oracle raft step "
+                     f"timed (message routing and persistence excluded), {T} threads",
+           "one_thread": {"value": c4_1, "passes": n4_1},
+           "label": "C++ restatement of reference Go step (oracle/raft_oracle.hpp), not Go",
+           **info}
+    cfg = {}
+    # config 2: 10k x 3 at full size
+    G2 = 10_000
+    c2, _, n2 = _oracle_rate(P.make_groups(G2, 3, seed=2), P.Topology(G2, 3), 3, steady(G2), T, 0.15 * budget)
+    cfg["2"] = {"commits_per_s": c2, "groups": G2, "passes": n2, "threads": T}
+    # config 3: 100k x 5, 90% quiesced, ReadIndex + ticks (sample of the same generator)
+    G3 = min(20_000, 100_000)
+    p3, act3 = P.config3(G3, 5)
+    rng3 = np.random.default_rng(3)
+    _, g3, n3 = _oracle_rate(p3, P.Topology(G3, 5), 5, lambda k, pop: P.config3_locals(G3, 5, act3, k), T,
+                             0.15 * budget, drop=lambda k, m: P.drop_acks(m, 0.1, rng3))
+    cfg["3"] = {"groups_per_s": g3, "groups": G3, "passes": n3, "threads": T,
+                "sample": f"{G3} of 100k groups x 5 (same generator)"}
+    # config 5: leader churn p = 0.1, 100k x 3 (sample)
+    G5 = min(20_000, 100_000)
+    t5 = P.Topology(G5, 3)
+    rng5 = np.random.default_rng(5)
+
+    def inject5(k, pop):
+        cur = pop.export()
+        ch = P.inject_leader_change(cur, t5, 0.1, rng5)
+        if len(ch):
+            pop.reload(ch, cur[ch])
+    c5, g5, n5 = _oracle_rate(P.make_groups(G5, 3, seed=5), t5, 3,
+                              lambda k, pop: P.propose_locals(3 * G5, P.current_leaders(pop.export(), t5),
+                                                              pass_index=k),
+                              T, 0.15 * budget, inject=inject5)
+    cfg["5"] = {"commits_per_s": c5, "groups_per_s": g5, "groups": G5, "passes": n5, "threads": T,
+                "sample": f"{G5} of 100k groups x 3 (same generator)"}
+    out["configs"] = cfg
+    return out
+
+
+def host_path(args, R, ordinal):
+    """The C-ABI path a Go step worker calls (gr_step: host records in, device
+    passes, host records out), PCIe-inclusive, at the headline shape. Routing of
+    the previous outbox to the receivers (the transport's role) is untimed."""
+    import ctypes
+    import numpy as np
+    from dragonboat_amd import abi, populations as P
+    from dragonboat_amd.engine import Engine
+    G = args.groups
+    peers = P.make_groups(G, R, seed=2)
+    topo = P.Topology(G, R)
+    eng = Engine(R * G, R, device=ordinal)
+    eng.load(peers)
+    msgs = np.zeros(0, abi.MESSAGE)
+    t_step = 0.0
+    n_in = n_out = 0
+    warm, passes = 2, args.host_passes
+    for k in range(warm + passes):
+        loc = P.propose_locals(R * G, np.arange(G), pass_index=k)
+        if k == warm:
+            eng.reset_stats()
+        ib = abi.inbox_of(msgs, loc)
+        ob = abi.Outbox()
+        t0 = time.perf_counter()
+        rc = eng.lib.gr_step(eng._h, ctypes.byref(ib), ctypes.byref(ob))
+        t1 = time.perf_counter()
+        assert rc == 0, rc
+        out = np.zeros(ob.n_msgs, abi.MESSAGE)
+        if ob.n_msgs:
+            ctypes.memmove(out.ctypes.data, ob.msgs, ob.n_msgs * abi.MESSAGE.itemsize)
+        eng.lib.gr_release_outbox(eng._h, ctypes.byref(ob))
+        if k >= warm:
+            t_step += t1 - t0
+            n_in += len(msgs)
+            n_out += len(out)
+        msgs = topo.route_unsorted(out)
+    st = eng.stats()
+    eng.close()
+    return {"path": "gr_step: host gr_message/gr_local_input records in, gr_message/gr_peer_result records "
+                    "out (PCIe-inclusive)",
+            "groups": G, "replicas": R, "passes": passes, "ms_per_pass": t_step / passes * 1e3,
+            "commits_per_s": st["leader_commits"] / t_step, "escalations": st["escalations"],
+            "msgs_in_per_pass": n_in / passes, "msgs_out_per_pass": n_out / passes,
+            "record_bytes_per_pass": (n_in + n_out) / passes * abi.MESSAGE.itemsize
+            + R * G * abi.RESULT.itemsize}
+
+
+def copy_peak_gbs():
+    """Achievable HBM bandwidth on this box: tools/hbm_calib's float4 copy
+    (MI355X_MICROARCH.md's 6.29 TB/s method), run as a child process."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "hbm_calib")
+    try:
+        p = subprocess.run([exe, "copy"], capture_output=True, text=True, timeout=120)
+        return json.loads(p.stdout.strip().splitlines()[-1])["copy_f4_GBs"]
+    except Exception:
+        return None
 
 
 def main():
@@ -201,7 +326,6 @@ def main():
     for k in range(args.steps):
         ex.step(eng, spaces, args.warmup + args.steps + k, stream)
     tm = eng.timing_end()
-    copy_gbs = stream_copy_gbs(torch, dev)
     commits = st["leader_commits"]
     esc = st["escalations"]
     if world > 1:
@@ -210,12 +334,16 @@ def main():
         commits, esc = int(t[0].item()), int(t[1].item())
     value = commits / elapsed
     passes = max(1, tm["passes"])
-    kavg = tm["fast_ms"] / passes  # the dominant kernel
+    kavg = tm["fast_ms"] / passes  # the dominant kernel, HIP events on the pass's stream
     gavg = tm["general_ms"] / passes
     groups_total = G * world
-    alg = algorithmic_bytes(st, G, R, args.steps) / args.steps  # per launch (this rank)
-    achieved = alg / (kavg * 1e-3) / 1e9  # GB/s: algorithmic bytes of the launch / its time
-    canon = b_round(R) * G
+    # SURVEY.md §8d's unit: one group-round (R-1 acks in, quorum commit, R-1
+    # Replicates out, R-1 follower matches) = B_round(R) bytes at reference field
+    # widths; a launch processes one group-round per leader commit.
+    rounds = st["leader_commits"] / args.steps
+    alg = b_round(R) * rounds  # algorithmic bytes per launch (this rank)
+    achieved = alg / (kavg * 1e-3) / 1e9
+    refw = reference_width_bytes(st, G, R, args.steps) / args.steps
     if rank == 0:
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
@@ -228,6 +356,8 @@ def main():
                     traffic = rec.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
+        copy_gbs = copy_peak_gbs()
+        traffic_gbs = traffic / (kavg * 1e-3) / 1e9 if traffic else None
         line = {
             "metric": "commit-index updates/sec (1M groups x 3 replicas) + achieved HBM GB/s",
             "value": value,
@@ -249,18 +379,23 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"gr_fast_kernel<{S}>", "kernel_ms": kavg,
                          "algorithmic_bytes_per_launch": alg,
-                         "units_per_launch": {k: st[k] / args.steps for k in
-                                              ("leader_msgs_in", "leader_msgs_out", "msgs_in",
-                                               "replicate_entries")},
-                         "canonical_round_bytes": canon,
-                         "canonical_frac": canon / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "hbm_traffic_GBs": (traffic / (kavg * 1e-3) / 1e9) if traffic else None,
-                         "stream_copy_GBs": copy_gbs,
-                         "hbm_traffic_frac_of_stream_copy": ((traffic / (kavg * 1e-3) / 1e9) / copy_gbs)
-                         if traffic else None,
+                         "algorithmic_unit": f"group-round, B_round({R}) = {b_round(R)} B (SURVEY.md 8d)",
+                         "group_rounds_per_launch": rounds,
+                         "traffic_GBs": traffic_gbs,
+                         "traffic_frac": traffic_gbs / HBM_PEAK_GBS if traffic else None,
+                         "copy_f4_GBs": copy_gbs,
+                         "traffic_frac_of_copy": traffic_gbs / copy_gbs if traffic and copy_gbs else None,
+                         "reference_width_bytes_per_launch": refw,
+                         "reference_width_note": "two Replicates + two acks per follower per round at "
+                                                 "reference field widths (1,128 B/group): never used as frac",
                          "general_kernel_ms": gavg,
                          "bailed_lanes_per_pass": tm["bailed_lanes"] / passes},
         }
+        if args.host_path == "on" and world == 1:
+            try:
+                line["host_path"] = host_path(args, R, ordinal)
+            except Exception as e:  # reported beside the headline, never as `value`
+                line["host_path"] = {"error": str(e)}
         if args.cpu_baseline == "on" and world == 1:
             try:
                 line["cpu_baseline"] = cpu_baseline(args, R)

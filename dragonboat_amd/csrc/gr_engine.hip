@@ -201,6 +201,7 @@ static hipError_t launch_slots(uint32_t S, const StepParams& kp, uint32_t* bail_
     case 1: return launch<1>(kp, bail_list, counters, list_cap, parity, s, t);
     case 3: return launch<3>(kp, bail_list, counters, list_cap, parity, s, t);
     case 5: return launch<5>(kp, bail_list, counters, list_cap, parity, s, t);
+    case 8: return launch<8>(kp, bail_list, counters, list_cap, parity, s, t);
   }
   return hipErrorInvalidValue;
 }
@@ -209,6 +210,7 @@ static uint32_t instantiated_slots(uint32_t want) {
   if (want <= 1) return 1;
   if (want <= 3) return 3;
   if (want <= 5) return 5;
+  if (want <= GR_SMAX) return GR_SMAX;  // wide groups (e.g. 5 voters + 2 observers): leaders take the general lane
   return 0;
 }
 

@@ -15,21 +15,25 @@ NOPOS = 0xFFFFFFFF
 
 def make_groups(G, R=3, seed=2, term_lo=1, term_hi=5, base_index=2**32, spread=2**20,
                 election=10, heartbeat=1, check_quorum=False, payload=16, slots=None,
-                log_span=1024):
+                log_span=1024, observers=0):
     """Steady-state groups: leader at term T, followers caught up, all committed.
 
     BASELINE config 2/4: T ~ U[term_lo, term_hi] and lastIndex = 2^32 + U[0, 2^20)
-    (exercises the upper 32 bits of every index)."""
-    S = slots or R
+    (exercises the upper 32 bits of every index). A group has R voters (node ids
+    1..R, replica 0 leads) and `observers` observers (node ids R+1..R+observers,
+    raft.observers): M = R + observers members in slots 0..M-1 of every member."""
+    M = R + observers
+    S = slots or M
+    assert S >= M
     rng = np.random.default_rng(seed)
     T = rng.integers(term_lo, term_hi + 1, G).astype(np.uint64)
     hi = (np.uint64(base_index) + rng.integers(0, spread, G).astype(np.uint64))
     lo = hi - np.uint64(log_span)
-    peers = np.zeros(R * G, abi.PEER)
-    for r in range(R):
+    peers = np.zeros(M * G, abi.PEER)
+    for r in range(M):
         v = peers[r * G:(r + 1) * G]
         v["term"] = T
-        v["vote"] = 1
+        v["vote"] = 1 if r < R else 0
         v["committed"] = hi
         v["applied"] = hi
         v["last_index"] = hi
@@ -47,22 +51,22 @@ def make_groups(G, R=3, seed=2, term_lo=1, term_hi=5, base_index=2**32, spread=2
         v["run_term"][:, 0] = np.where(two, T - np.uint64(1), T)
         v["run_start"][:, 1] = np.where(two, hi, 0)
         v["run_term"][:, 1] = np.where(two, T, 0)
-        for j in range(R):
+        for j in range(M):
             v["remote_id"][:, j] = j + 1
-            v["remotes"][:, j]["kind"] = abi.SLOT_VOTER
+            v["remotes"][:, j]["kind"] = abi.SLOT_VOTER if j < R else abi.SLOT_OBSERVER
             if r == 0:  # leader: followers in Replicate state, caught up
                 v["remotes"][:, j]["match"] = hi
                 v["remotes"][:, j]["next"] = hi + np.uint64(1)
                 v["remotes"][:, j]["state"] = abi.RETRY if j == 0 else abi.REPLICATE_ST
                 v["remotes"][:, j]["active"] = 0 if j == 0 else 1
-            else:  # follower: remotes as reset() leaves them
+            else:  # follower / observer: remotes as reset() leaves them
                 v["remotes"][:, j]["match"] = hi if j == r else 0
                 v["remotes"][:, j]["next"] = hi + np.uint64(1)
                 v["remotes"][:, j]["state"] = abi.RETRY
-        v["state"] = abi.LEADER if r == 0 else abi.FOLLOWER
+        v["state"] = abi.LEADER if r == 0 else (abi.FOLLOWER if r < R else abi.OBSERVER)
         v["self_slot"] = r
         v["flags"] = abi.F_CHECK_QUORUM if check_quorum else 0
-    for j in range(R, S):
+    for j in range(M, S):
         peers["remotes"][:, j]["kind"] = abi.SLOT_EMPTY
     return peers
 
@@ -91,6 +95,16 @@ class Topology:
         # stable order: by receiver, then sender slot, then arrival
         order = np.lexsort((np.arange(len(nxt)), nxt["slot"], nxt["peer"]))
         return nxt[order]
+
+    def route_unsorted(self, out):
+        """route_messages without the sort: gr_step groups the records by mailbox on
+        the device (stable), so only the relative order of one sender's records to
+        one target matters, and it is kept."""
+        nxt = out.copy()
+        dp, ds = self.dest(out["peer"], out["slot"])
+        nxt["peer"] = dp.astype(np.uint32)
+        nxt["slot"] = ds.astype(np.uint8)
+        return nxt
 
     def loopback_routes(self, S):
         """in_pos/out_pos tables [S][n] for a one-space loopback.
@@ -157,12 +171,15 @@ def inject_leader_change(state, topo, p, rng, max_div=8, max_extra=4):
     terms = st["term"]
     leaders = st["state"] == abi.LEADER
     settled = (leaders.sum(0) == 1) & np.all(terms == terms[0], axis=0) & \
-        np.all((st["state"] == abi.LEADER) | (st["state"] == abi.FOLLOWER), axis=0)
+        np.all((st["state"] == abi.LEADER) | (st["state"] == abi.FOLLOWER) | (st["state"] == abi.OBSERVER), axis=0)
     cand = np.nonzero(settled & (rng.random(G) < p))[0]
     changed = []
     for g in cand:
         a = int(np.argmax(leaders[:, g]))
-        b = int(rng.choice([r for r in range(R) if r != a]))
+        voters = [r for r in range(R) if r != a and st["state"][r, g] == abi.FOLLOWER]
+        if not voters:
+            continue
+        b = int(rng.choice(voters))
         L = state[a * G + g]
         F = state[b * G + g]
         T = int(L["term"])
@@ -248,3 +265,62 @@ def drop_acks(msgs, p, rng):
         return msgs
     keep = ~((msgs["type"] == abi.HEARTBEAT_RESP) & (rng.random(len(msgs)) < p))
     return msgs[keep]
+
+
+def inject_leader_transfer(state, topo, p, rng, lag_frac=0.5):
+    """Leader transfer in flight (raft.go:1242-1262 handleLeaderLeaderTransfer):
+    with probability p a settled group's leader gets leaderTransferTarget = a
+    follower's node id, the target is flagged isLeaderTransferTarget, and for
+    `lag_frac` of them the target lags (its match one below the leader's log, so
+    the next ack that catches it up sends TimeoutNow, raft.go:1216-1219; a
+    caught-up target gets TimeoutNow on its next ack). electionTick is reset as
+    the handler does. Returns the changed slots."""
+    G, M = topo.G, topo.R
+    st = state.reshape(M, G)
+    changed = []
+    for g in np.nonzero(rng.random(G) < p)[0]:
+        lead = np.nonzero(st["state"][:, g] == abi.LEADER)[0]
+        if len(lead) != 1:
+            continue
+        a = int(lead[0])
+        L = state[a * G + g]
+        if int(L["leader_transfer_target"]):
+            continue
+        cands = [r for r in range(M) if r != a and int(L["remotes"][r]["kind"]) == abi.SLOT_VOTER]
+        if not cands:
+            continue
+        b = int(rng.choice(cands))
+        L["leader_transfer_target"] = int(L["remote_id"][b])
+        L["election_tick"] = 0
+        if rng.random() < lag_frac and int(L["remotes"][b]["match"]) > 0:
+            L["remotes"][b]["match"] = int(L["remotes"][b]["match"]) - 1
+        F = state[b * G + g]
+        F["flags"] = int(F["flags"]) | abi.F_IS_LEADER_TRANSFER_TARGET
+        changed += [a * G + g, b * G + g]
+    return np.array(sorted(changed), np.int64)
+
+
+def inject_snapshot_state(state, topo, p, rng):
+    """Leader remotes in Snapshot state (remote.go:98-106 becomeSnapshot) with a
+    Replicate already in flight to them: with probability p per group one of the
+    leader's remotes gets state Snapshot and snapshotIndex at or below its match
+    (the next accepted ack runs respondedTo -> becomeRetry, remote.go:130-138) or
+    above it (the remote stays paused). Returns the changed slots."""
+    G, M = topo.G, topo.R
+    st = state.reshape(M, G)
+    changed = []
+    for g in np.nonzero(rng.random(G) < p)[0]:
+        lead = np.nonzero(st["state"][:, g] == abi.LEADER)[0]
+        if len(lead) != 1:
+            continue
+        a = int(lead[0])
+        L = state[a * G + g]
+        js = [j for j in range(M) if j != int(L["self_slot"]) and int(L["remotes"][j]["kind"]) != abi.SLOT_EMPTY]
+        if not js:
+            continue
+        j = int(rng.choice(js))
+        m = int(L["remotes"][j]["match"])
+        L["remotes"][j]["state"] = abi.SNAPSHOT_ST
+        L["remotes"][j]["snapshot_index"] = max(1, m - int(rng.integers(0, 3))) if rng.random() < 0.7 else m + 3
+        changed.append(a * G + g)
+    return np.array(sorted(changed), np.int64)

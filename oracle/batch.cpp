@@ -358,6 +358,87 @@ Message from_record(const OPeer& op, const gr_message& g) {
   return m;
 }
 
+// ---- escalation predicate -------------------------------------------------
+// The device escalates an item (hands it to the host) for a reason (gr_escalation).
+// The harness re-derives, from the oracle's own execution of that item, every
+// reason that applies to it, so a test can fail any escalation the reference
+// behaviour does not justify (too early, or for the wrong reason). The device's
+// term-run window is modelled here (same truncate/push rules as gr_lane.h) from
+// the device state at the start of the pass.
+struct ItemProbe : Probe {
+  std::vector<std::pair<u64, u64>> runs;  // device window model: (start, term), <= GR_K
+  bool active = false;
+  bool termWindow = false, replErr = false, riCap = false;
+  int resetsPass = 0, resetsItem = 0, campaigns = 0;
+  u64 replMaxCnt = 0;
+  void begin_item() {
+    termWindow = replErr = riCap = false;
+    resetsItem = campaigns = 0;
+    replMaxCnt = 0;
+  }
+  void lookup(u64 i) override {
+    if (active && (runs.empty() || i < runs[0].first)) termWindow = true;
+  }
+  void merged(const std::vector<Entry>& es) override {
+    if (es.empty()) return;
+    const u64 ci = es[0].Index;
+    while (!runs.empty() && runs.back().first >= ci) runs.pop_back();  // win_truncate
+    for (const Entry& e : es) {                                          // win_push per term change
+      if (!runs.empty() && runs.back().second == e.Term) continue;
+      if (runs.size() == GR_K) runs.erase(runs.begin());
+      runs.push_back({e.Index, e.Term});
+    }
+  }
+  void resetCalled() override {
+    resetsPass++;
+    if (active) resetsItem++;
+  }
+  void campaignCalled() override {
+    if (active) campaigns++;
+  }
+  void replicateError() override {
+    if (active) replErr = true;
+  }
+  void replicateRange(u64 next, u64 last) override {
+    if (active && next <= last) replMaxCnt = std::max<u64>(replMaxCnt, last - next + 1);
+  }
+  void readIndexAdd(size_t queued, bool dup) override {
+    if (active && !dup && queued >= GR_Q) riCap = true;
+  }
+};
+
+inline bool wide64(u64 a) { return (a >> 32) != 0; }
+
+// UNSUPPORTED: (state, message) pairs the device hands to the host
+// (gr_lane.h Lane::handle and its handlers), from the oracle's state at the item.
+bool unsupported_msg(const raft& r, const Message& m, bool fwd_before) {
+  const MessageType t = m.Type;
+  RaftState st = r.state;
+  if (m.Term != 0 && m.Term != r.term) {
+    if (m.Term < r.term) return false;  // dropped or answered with NoOP
+    if (t == RequestVote) return true;
+    if (st != observer) {
+      if (fwd_before) return true;      // step-down after forwarded proposals were appended
+      st = follower;
+    }
+  }
+  if (st == leader) {
+    if (t == RequestVote) return true;
+    if (t == Propose) {
+      bool transferring = r.leaderTransferTarget != NoNode;
+      return m.Entries.empty() || r.selfRemoved() || transferring;
+    }
+    return false;
+  }
+  if (st == follower || st == observer) {
+    if (t == InstallSnapshot) return true;
+    if ((t == RequestVote || t == TimeoutNow) && st != observer) return true;
+    return false;
+  }
+  return t == Heartbeat || t == Replicate || t == InstallSnapshot || t == RequestVoteResp || t == Election ||
+         t == RequestVote;  // candidate
+}
+
 }  // namespace
 
 extern "C" {
@@ -443,19 +524,36 @@ int ob_commit_all(ob_pop* p) {
 // If limits != NULL, mid[p] receives the state after items < limits[p] and
 // results/ready reflect only that prefix; messages carry the emitting item
 // index in out_item so callers can split device-prefix and host-suffix output.
+// esc_mask (may be NULL) receives, for every peer with a limit, the set of
+// gr_escalation reasons (bit r) the item at limits[p] justifies; dev_before
+// (may be NULL: the oracle's own export is used) is the device state at the
+// start of the pass, whose term-run window the predicate models; in_depth /
+// out_depth are the mailbox depths of the device spaces; has_locals = 0 models
+// a device pass without local-input rows (every reset() needs the host).
 // n_threads > 1 steps disjoint peer ranges concurrently (clusterID % T, the
 // FixedPartitioner rule of internal/server/partition.go:34-36).
-int ob_step(ob_pop* p, const gr_inbox* in, const uint32_t* limits, gr_peer* mid, gr_message* out,
-            uint32_t* out_item, size_t cap, size_t* n_out, gr_peer_result* results, uint32_t n_threads,
-            char* err, size_t errcap) {
+int ob_step2(ob_pop* p, const gr_inbox* in, const uint32_t* limits, const gr_peer* dev_before, uint32_t in_depth,
+             uint32_t out_depth, uint32_t has_locals, uint32_t* esc_mask, gr_peer* mid, gr_message* out,
+             uint32_t* out_item, size_t cap, size_t* n_out, gr_peer_result* results, uint32_t n_threads, char* err,
+             size_t errcap) {
   if (!p || !in || !n_out) return GR_EINVAL;
   const uint32_t n = (uint32_t)p->peers.size(), S = p->S;
-  // bucket messages per peer, slot-major then arrival order
-  std::vector<std::vector<std::vector<const gr_message*>>> box(n, std::vector<std::vector<const gr_message*>>(S));
+  if (in_depth == 0) in_depth = GR_C;
+  if (out_depth == 0) out_depth = GR_C;
+  // bucket messages per (peer, slot), arrival order kept: a counting sort
+  std::vector<uint32_t> start((size_t)n * S + 1, 0), order(in->n_msgs);
   for (size_t k = 0; k < in->n_msgs; ++k) {
     const gr_message& m = in->msgs[k];
     if (m.peer >= n || m.slot >= S) return GR_EINVAL;
-    box[m.peer][m.slot].push_back(&m);
+    start[(size_t)m.peer * S + m.slot + 1]++;
+  }
+  for (size_t x = 1; x < start.size(); ++x) start[x] += start[x - 1];
+  {
+    std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+    for (size_t k = 0; k < in->n_msgs; ++k) {
+      const gr_message& m = in->msgs[k];
+      order[fill[(size_t)m.peer * S + m.slot]++] = (uint32_t)k;
+    }
   }
   std::vector<const gr_local_input*> loc(n, nullptr);
   for (size_t k = 0; k < in->n_locals; ++k) {
@@ -471,17 +569,32 @@ int ob_step(ob_pop* p, const gr_inbox* in, const uint32_t* limits, gr_peer* mid,
   std::vector<std::vector<Out>> outs(n_threads);
   std::vector<std::string> errs(n_threads);
   auto work = [&](uint32_t t) {
+    ItemProbe probe;
+    g_probe = &probe;
     for (uint32_t pi = t; pi < n; pi += n_threads) {
       OPeer& op = p->peers[pi];
       raft& r = *op.r;
       const uint32_t limit = limits ? limits[pi] : 0xFFFFFFFFu;
+      const bool want_mask = esc_mask && limit != 0xFFFFFFFFu;
       r.msgs.clear();
       r.readyToRead.clear();
       op.appendFrom = 0;
       op.rand.clear();
       op.randNext = 0;
-      if (loc[pi]) op.rand.push_back(loc[pi]->rand);
+      // the draw is an input: a peer without a local record gets the device's zero row
+      if (has_locals) op.rand.push_back(loc[pi] ? loc[pi]->rand : 0);
+      probe.runs.clear();
+      probe.active = false;
+      probe.resetsPass = 0;
+      if (want_mask) {
+        gr_peer w;
+        if (dev_before) w = dev_before[pi];
+        else export_peer(op, S, &w);
+        for (int k = 0; k < w.n_runs && k < GR_K; ++k) probe.runs.push_back({w.run_start[k], w.run_term[k]});
+      }
       uint32_t item = 0;
+      uint32_t mask = 0;
+      std::vector<uint32_t> sent(S, 0);  // messages this peer emitted per target slot
       gr_peer_result res;
       memset(&res, 0, sizeof(res));
       res.peer = pi;
@@ -498,25 +611,72 @@ int ob_step(ob_pop* p, const gr_inbox* in, const uint32_t* limits, gr_peer* mid,
         }
         res.append_from = op.appendFrom;
       };
+      // called before item `it` runs: arms the probe for the escalated item
+      auto pre = [&](uint32_t it) {
+        if (it == limit) take_mid();
+        probe.active = want_mask && it == limit;
+        if (probe.active) probe.begin_item();
+      };
+      // after item `it`: its messages; for the escalated item, the reasons
       auto flush = [&](uint32_t it) {
+        const bool judged = probe.active;
         for (auto& m : r.msgs) {
           Out o;
           o.peer = pi;
           o.item = it;
           o.ok = to_record(op, pi, m, &o.rec);
+          if (o.rec.slot < S) sent[o.rec.slot]++;
+          if (judged) {
+            if (op.slotOf(m.To) == GR_SLOT_NONE) mask |= 1u << GR_ESC_NONMEMBER;
+            else if (sent[o.rec.slot] > out_depth) mask |= 1u << GR_ESC_CAPACITY;
+            u64 rt1 = 0;
+            int runs = m.Entries.empty() ? 0 : 1;
+            for (size_t k = 1; k < m.Entries.size(); ++k)
+              if (m.Entries[k].Term != m.Entries[k - 1].Term) { runs++; rt1 = std::max<u64>(rt1, m.Entries[k].Term); }
+            if (runs > 2) mask |= 1u << GR_ESC_MSG_RUNS;
+            const u64 mterm = isRequestMessage(m.Type) ? m.Term : r.term;
+            if (wide64(mterm) || wide64(m.LogTerm) || (!m.Entries.empty() && wide64(m.Entries[0].Term)) || wide64(rt1))
+              mask |= 1u << GR_ESC_WIDE_TERM;
+          }
           outs[t].push_back(o);
         }
         r.msgs.clear();
+        if (judged) {
+          if (probe.termWindow) mask |= 1u << GR_ESC_TERM_WINDOW;
+          if (probe.resetsItem && (probe.resetsPass > probe.resetsItem || !has_locals)) mask |= 1u << GR_ESC_RANDOM;
+          if (probe.campaigns) mask |= 1u << GR_ESC_ELECTION;
+          if (probe.replErr) mask |= 1u << GR_ESC_SNAPSHOT;
+          if (probe.replMaxCnt > 1 &&
+              (op.entryUB == 0 || probe.replMaxCnt > p->maxEntrySize / op.entryUB))
+            mask |= 1u << GR_ESC_ENTRY_SIZE;
+          if (probe.replMaxCnt > 0xFFFFFFFFull || probe.riCap || r.readyToRead.size() > GR_Q)
+            mask |= 1u << GR_ESC_CAPACITY;
+          probe.active = false;
+        }
       };
       try {
         for (uint32_t j = 0; j < S; ++j) {
-          for (const gr_message* gm : box[pi][j]) {
-            if (item == limit) take_mid();
+          const size_t b0 = start[(size_t)pi * S + j], b1 = start[(size_t)pi * S + j + 1];
+          for (size_t x = b0; x < b1; ++x) {
+            const gr_message* gm = &in->msgs[order[x]];
+            pre(item);
             Message m = from_record(op, *gm);
+            if (probe.active) {
+              if (x - b0 >= in_depth) mask |= 1u << GR_ESC_CAPACITY;  // did not fit the mailbox
+              if (wide64(m.Term) || wide64(m.LogTerm) || (gm->n_runs && wide64(gm->run_term[0])) ||
+                  (gm->n_runs == 2 && wide64(gm->run_term[1])))
+                mask |= 1u << GR_ESC_WIDE_TERM;
+              bool member = op.kinds[j] != GR_SLOT_EMPTY;
+              if ((member || !isResponseMessageType(m.Type)) && unsupported_msg(r, m, res.n_forwarded != 0))
+                mask |= 1u << GR_ESC_UNSUPPORTED;
+              if (m.Type == Propose && gm->reject && r.state == leader) mask |= 1u << GR_ESC_CONFIG_CHANGE;
+            }
             const u64 before = r.log->lastIndex();
+            const RaftState st0 = r.state;
             // Peer.Handle (peer.go:199-209)
             bool member = op.kinds[j] != GR_SLOT_EMPTY;
             if (member || !isResponseMessageType(m.Type)) r.Handle(m);
+            if (probe.active && st0 == leader && r.state != leader && res.n_forwarded) mask |= 1u << GR_ESC_UNSUPPORTED;
             if (m.Type == Propose && !midTaken && r.log->lastIndex() > before) {  // forwarded batch appended
               if (!res.propose_first) res.propose_first = before + 1;
               res.n_forwarded++;
@@ -529,7 +689,7 @@ int ob_step(ob_pop* p, const gr_inbox* in, const uint32_t* limits, gr_peer* mid,
         const gr_local_input* L = loc[pi];
         if (L) {
           if (L->read_index) {
-            if (item == limit) take_mid();
+            pre(item);
             SystemCtx ctx{L->read_ctx_low, L->read_ctx_high};
             Message m;
             m.Type = ReadIndex;
@@ -540,33 +700,37 @@ int ob_step(ob_pop* p, const gr_inbox* in, const uint32_t* limits, gr_peer* mid,
             item++;
           }
           for (uint32_t k = 0; k < L->ticks; ++k) {
-            if (item == limit) take_mid();
+            pre(item);
+            const RaftState st0 = r.state;
             r.tick();
+            if (probe.active && st0 == leader && r.state != leader && res.n_forwarded) mask |= 1u << GR_ESC_UNSUPPORTED;
             flush(item);
             item++;
           }
           if (L->quiesced_ticks) {
-            if (item == limit) take_mid();
+            pre(item);
             for (uint32_t k = 0; k < L->quiesced_ticks; ++k) r.quiescedTick();
+            flush(item);
             item++;
           }
           if (L->propose_entries) {
-            if (item == limit) take_mid();
+            pre(item);
             const u64 before = r.log->lastIndex();
             std::vector<Entry> es(L->propose_entries);
             const size_t payload = op.entryUB >= 128 ? (size_t)(op.entryUB - 128) : 0;
             for (auto& e : es) e.Cmd.assign(payload, 0);
             if (L->propose_has_config_change) es[0].Type = ConfigChangeEntry;
+            if (probe.active && L->propose_has_config_change && r.state == leader && !r.selfRemoved() &&
+                r.leaderTransferTarget == NoNode)
+              mask |= 1u << GR_ESC_CONFIG_CHANGE;
             Message m;
             m.Type = Propose;
             m.From = r.nodeID;
             m.Entries = es;
-            const size_t outBefore = outs[t].size();
             r.Handle(m);  // Peer.ProposeEntries (peer.go:126-134)
             bool fwd = false;
             for (auto& x : r.msgs) fwd = fwd || x.Type == Propose;
             flush(item);
-            (void)outBefore;
             if (!midTaken) {
               if (r.log->lastIndex() > before) {
                 res.propose_result = GR_PROP_APPENDED;
@@ -581,12 +745,22 @@ int ob_step(ob_pop* p, const gr_inbox* in, const uint32_t* limits, gr_peer* mid,
         take_mid();
       } catch (const std::exception& ex) {
         if (errs[t].empty()) errs[t] = "peer " + std::to_string(pi) + " item " + std::to_string(item) + ": " + ex.what();
+        if (probe.active) {
+          mask |= 1u << GR_ESC_PANIC;
+          if (probe.replErr) mask |= 1u << GR_ESC_SNAPSHOT;  // the snapshot path itself panicked
+          if (probe.termWindow) mask |= 1u << GR_ESC_TERM_WINDOW;
+          if (probe.campaigns) mask |= 1u << GR_ESC_ELECTION;
+          probe.active = false;
+        }
+        r.msgs.clear();
         take_mid();
         res.escalation = GR_ESC_PANIC;
         res.esc_item = item;
       }
       if (results) results[pi] = res;
+      if (esc_mask) esc_mask[pi] = want_mask ? mask : 0;
     }
+    g_probe = nullptr;
   };
   if (n_threads == 1) {
     work(0);
@@ -618,6 +792,13 @@ int ob_step(ob_pop* p, const gr_inbox* in, const uint32_t* limits, gr_peer* mid,
   }
   if (k > cap && out) return GR_ECAPACITY;
   return e.empty() ? GR_OK : GR_ESTATE;
+}
+
+int ob_step(ob_pop* p, const gr_inbox* in, const uint32_t* limits, gr_peer* mid, gr_message* out,
+            uint32_t* out_item, size_t cap, size_t* n_out, gr_peer_result* results, uint32_t n_threads,
+            char* err, size_t errcap) {
+  return ob_step2(p, in, limits, nullptr, GR_C, GR_C, 1, nullptr, mid, out, out_item, cap, n_out, results, n_threads,
+                  err, errcap);
 }
 
 }  // extern "C"

@@ -35,6 +35,9 @@ def oracle_lib():
         lib.ob_step.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.c_void_p, c.c_void_p, c.c_void_p,
                                 c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t), c.c_void_p, c.c_uint32,
                                 c.c_char_p, c.c_size_t]
+        lib.ob_step2.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32,
+                                 c.c_uint32, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t,
+                                 c.POINTER(c.c_size_t), c.c_void_p, c.c_uint32, c.c_char_p, c.c_size_t]
         _olib = lib
     return _olib
 
@@ -102,29 +105,41 @@ class OraclePopulation:
     def commit_all(self):
         self.lib.ob_commit_all(self._h)
 
-    def step(self, msgs=None, locals_=None, limits=None, threads=1, allow_error=False):
-        """Returns dict(msgs, items, results, mid, error)."""
+    def step(self, msgs=None, locals_=None, limits=None, threads=1, allow_error=False, dev_before=None,
+             in_depth=abi.GR_C, out_depth=abi.GR_C, has_locals=True):
+        """Returns dict(msgs, items, results, mid, error, esc_mask).
+
+        esc_mask[p] (when limits are given) is the set of gr_escalation reasons,
+        bit r, that the oracle's own execution of item limits[p] justifies: the
+        escalation predicate (batch.cpp). dev_before = device state at the start
+        of the pass (its term-run window is modelled); None uses the oracle's."""
         msgs = np.zeros(0, abi.MESSAGE) if msgs is None else np.ascontiguousarray(msgs, abi.MESSAGE)
         locals_ = np.zeros(0, abi.LOCAL) if locals_ is None else np.ascontiguousarray(locals_, abi.LOCAL)
         ib = abi.inbox_of(msgs, locals_)
         lim = None
         if limits is not None:
             lim = np.ascontiguousarray(limits, np.uint32)
+        db = None
+        if dev_before is not None:
+            db = np.ascontiguousarray(dev_before, abi.PEER)
+            assert len(db) == self.n
         mid = np.zeros(self.n, abi.PEER)
         res = np.zeros(self.n, abi.RESULT)
+        mask = np.zeros(self.n, np.uint32)
         cap = max(16, 4 * len(msgs) + 8 * self.n * self.slots)
         out = np.zeros(cap, abi.MESSAGE)
         items = np.zeros(cap, np.uint32)
         n_out = ctypes.c_size_t()
         err = ctypes.create_string_buffer(512)
-        rc = self.lib.ob_step(self._h, ctypes.byref(ib), lim.ctypes.data if lim is not None else None,
-                              mid.ctypes.data, out.ctypes.data, items.ctypes.data, cap, ctypes.byref(n_out),
-                              res.ctypes.data, threads, err, 512)
+        rc = self.lib.ob_step2(self._h, ctypes.byref(ib), lim.ctypes.data if lim is not None else None,
+                               db.ctypes.data if db is not None else None, in_depth, out_depth,
+                               1 if has_locals else 0, mask.ctypes.data, mid.ctypes.data, out.ctypes.data,
+                               items.ctypes.data, cap, ctypes.byref(n_out), res.ctypes.data, threads, err, 512)
         if rc and not (allow_error and rc == -6):
             raise OracleError(f"ob_step rc={rc}: {err.value.decode()}")
         n = n_out.value
         return {"msgs": out[:n], "items": items[:n], "results": res, "mid": mid,
-                "error": err.value.decode() if rc else ""}
+                "error": err.value.decode() if rc else "", "esc_mask": mask}
 
 
 def hostlane_step(peers, msgs=None, locals_=None, slots=3, max_entry_size=abi.MAX_ENTRY_SIZE):

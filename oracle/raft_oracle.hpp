@@ -34,6 +34,22 @@
 namespace oracle {
 
 using u64 = uint64_t;
+struct Entry;
+
+// Observation hooks for the batch harness's escalation predicate (batch.cpp):
+// they record what an item did (term lookups, resets, campaigns, snapshot
+// paths, appends) and never change behaviour. One probe per harness thread.
+struct Probe {
+  virtual ~Probe() {}
+  virtual void lookup(u64 index) = 0;                          // a term()/entries() read inside [firstIndex-1, lastIndex]
+  virtual void merged(const std::vector<Entry>& es) = 0;      // inMemory.merge
+  virtual void resetCalled() = 0;                              // raft.reset
+  virtual void campaignCalled() = 0;                           // raft.campaign
+  virtual void replicateError() = 0;                           // makeReplicateMessage failed (InstallSnapshot path)
+  virtual void replicateRange(u64 next, u64 last) = 0;         // makeReplicateMessage(next) with lastIndex last
+  virtual void readIndexAdd(size_t queued, bool dup) = 0;      // readIndex.addRequest
+};
+inline thread_local Probe* g_probe = nullptr;
 
 struct Panic : std::runtime_error {
   explicit Panic(const std::string& s) : std::runtime_error(s) {}
@@ -365,6 +381,7 @@ struct inMemory {
     if (ok && idx == index) snapshot.reset();
   }
   void merge(const std::vector<Entry>& ents) {  // :157-177
+    if (g_probe) g_probe->merged(ents);
     u64 firstNewIndex = ents[0].Index;
     if (firstNewIndex == markerIndex + (u64)entries.size()) {
       checkEntriesToAppend(entries, ents);
@@ -437,6 +454,7 @@ struct entryLog {
     *err = Err::None;
     auto r = termEntryRange();
     if (index < r.first || index > r.second) return 0;
+    if (g_probe) g_probe->lookup(index);
     u64 t;
     if (inmem.getTerm(index, &t)) return t;
     Err e;
@@ -487,6 +505,7 @@ struct entryLog {
     *err = checkBound(low, high);
     if (*err != Err::None) return {};
     if (low == high) return {};
+    if (g_probe) g_probe->lookup(low);
     bool checkInMem;
     auto ents = getEntriesFromLogDB(low, high, maxSize, &checkInMem, err);
     if (*err != Err::None) return {};
@@ -668,6 +687,7 @@ struct readIndex {
   std::vector<SystemCtx> queue;
 
   void addRequest(u64 index, SystemCtx ctx, u64 from) {  // :43-67
+    if (g_probe) g_probe->readIndexAdd(queue.size(), pending.count(ctx) != 0);
     if (pending.count(ctx)) return;
     if (!queue.empty()) {
       auto it = pending.find(peepCtx());
@@ -920,6 +940,7 @@ struct raft {
   }
   void quiescedTick() { electionTick++; }  // :431-433
   void setRandomizedElectionTimeout() {  // :435-438
+    if (electionTimeout == 0) panicf("runtime error: integer divide by zero");  // Go's % by zero
     u64 randTime = rng() % electionTimeout;
     randomizedElectionTimeout = electionTimeout + randTime;
   }
@@ -945,6 +966,7 @@ struct raft {
     return s.Index;
   }
   Message makeReplicateMessage(u64 to, u64 next, u64 maxSize, Err* err) {  // :474-498
+    if (g_probe) g_probe->replicateRange(next, log->lastIndex());
     u64 t = log->term(next - 1, err);
     if (*err != Err::None) return Message{};
     auto ents = log->entries(next, maxSize, err);
@@ -975,6 +997,7 @@ struct raft {
     Err err;
     Message m = makeReplicateMessage(to, rp->next, maxEntrySize, &err);
     if (err != Err::None) {
+      if (g_probe) g_probe->replicateError();
       if (!rp->isActive()) return;
       u64 index = makeInstallSnapshotMessage(to, &m);
       rp->becomeSnapshot(index);
@@ -1078,6 +1101,7 @@ struct raft {
     appendEntries(es);
   }
   void reset(u64 t) {  // :704-720
+    if (g_probe) g_probe->resetCalled();
     if (term != t) {
       term = t;
       vote = NoLeader;
@@ -1125,6 +1149,7 @@ struct raft {
     return votedFor;
   }
   void campaign() {  // :779-807
+    if (g_probe) g_probe->campaignCalled();
     becomeCandidate();
     u64 t = term;
     handleVoteResp(nodeID, false);

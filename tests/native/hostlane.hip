@@ -45,7 +45,7 @@ void run_lanes(const StepParams& kp) {
   g_bailed_lanes += bailed.size();
 }
 
-uint32_t inst(uint32_t want) { return want <= 1 ? 1 : want <= 3 ? 3 : want <= 5 ? 5 : 0; }
+uint32_t inst(uint32_t want) { return want <= 1 ? 1 : want <= 3 ? 3 : want <= 5 ? 5 : want <= GR_SMAX ? GR_SMAX : 0; }
 
 }  // namespace
 
@@ -99,7 +99,8 @@ extern "C" int hl_step(uint32_t slots, uint64_t max_entry_size, gr_peer* peers, 
   kp.route_mode = RT_TABLE;
   if (S == 1) run_lanes<1>(kp);
   else if (S == 3) run_lanes<3>(kp);
-  else run_lanes<5>(kp);
+  else if (S == 5) run_lanes<5>(kp);
+  else run_lanes<GR_SMAX>(kp);
   std::vector<gr_message> msgs;
   decode_outbox(obuf.data(), pk, S, &msgs);
   *n_out = msgs.size();

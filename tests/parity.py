@@ -194,3 +194,20 @@ def prefix_msgs(orc, limits):
         return m
     keep = it < limits[m["peer"].astype(np.int64)]
     return m[keep]
+
+
+def check_escalations(results, esc_mask, limit=20):
+    """Every escalation the engine reported must be one the oracle's own execution
+    of that item justifies (oracle.pyoracle step(..)["esc_mask"], bit = reason):
+    an item handed to the host too early, or for a reason the reference behaviour
+    does not show, fails. Returns [(peer, item, reason, justified reasons)]."""
+    bad = []
+    for r in results[results["escalation"] != 0]:
+        p, why = int(r["peer"]), int(r["escalation"])
+        m = int(esc_mask[p])
+        if not (m >> why) & 1:
+            bad.append((p, int(r["esc_item"]), abi.ESC_NAMES[why],
+                        [abi.ESC_NAMES[b] for b in range(len(abi.ESC_NAMES)) if (m >> b) & 1]))
+            if len(bad) >= limit:
+                break
+    return bad

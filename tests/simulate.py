@@ -55,8 +55,12 @@ class GpuBackend:
 
 
 def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, check=True,
-             max_report=3, drop_fn=None, threads=None):
-    """Run `passes` passes; returns a dict of counters. Raises AssertionError on divergence."""
+             max_report=3, drop_fn=None, threads=None, extra_fn=None):
+    """Run `passes` passes; returns a dict of counters. Raises AssertionError on divergence.
+
+    inject_fn(k, state) -> changed slots (state edited in place, reloaded on both sides);
+    extra_fn(k, state) -> gr_message records appended to pass k's inbox (local
+    messages such as LeaderTransfer, or messages from outside the population)."""
     pop = OraclePopulation(peers, slots)
     eng = backend(peers, slots)
     n = len(peers)
@@ -73,7 +77,12 @@ def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, c
         # locals_fn(k) or locals_fn(k, state): the second form sees the pass's
         # starting state (e.g. to propose on the current leaders)
         loc = locals_fn(k, pop.export()) if locals_fn.__code__.co_argcount == 2 else locals_fn(k)
-        before = eng.sync()["committed"] if check else None
+        if extra_fn is not None:
+            ext = extra_fn(k, pop.export())
+            if ext is not None and len(ext):
+                msgs = np.concatenate([msgs, np.asarray(ext, abi.MESSAGE)])
+        dev0 = eng.sync() if check else None
+        before = dev0["committed"] if check else None
         emsgs = msgs[~parked[msgs["peer"]]] if len(msgs) else msgs
         eloc = loc[~parked[loc["peer"]]]
         out, res = eng.step(emsgs, eloc)
@@ -82,7 +91,7 @@ def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, c
             assert np.all(nr <= 2) and np.all((ne == 0) == (nr == 0)), "invalid outbox record"
             assert np.all(out["type"] <= abi.TIMEOUT_NOW)
         lim = parity.limits_from(res, n)
-        o = pop.step(msgs, loc, lim, threads=threads or min(16, os.cpu_count() or 1))
+        o = pop.step(msgs, loc, lim, threads=threads or min(16, os.cpu_count() or 1), dev_before=dev0)
         esc = res[res["escalation"] != 0]
         stats["ready"] += int(res["n_ready"].sum())
         stats["forwarded"] += int(res["n_forwarded"].sum())
@@ -98,9 +107,11 @@ def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, c
             om = parity.prefix_msgs(o, lim)
             bad_m = parity.compare_msgs(out, om[~parked[om["peer"]]])
             bad_r = parity.compare_results(res, o["results"])
-            if bad_s or bad_m or bad_r:
+            bad_e = parity.check_escalations(res, o["esc_mask"])
+            if bad_s or bad_m or bad_r or bad_e:
                 raise AssertionError(
-                    f"pass {k}: state {bad_s[:max_report]} msgs {bad_m[:max_report]} results {bad_r[:max_report]}")
+                    f"pass {k}: state {bad_s[:max_report]} msgs {bad_m[:max_report]} results {bad_r[:max_report]}"
+                    f" unjustified escalations {bad_e[:max_report]}")
             stats["commits"] += int(np.sum(dev["committed"] > before))
         full = pop.export()
         fits = pop.representable()
@@ -115,4 +126,5 @@ def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, c
         msgs = topo.route_messages(o["msgs"])
         if drop_fn is not None:
             msgs = drop_fn(k, msgs)
+    stats["final"] = pop.export()
     return stats

@@ -36,3 +36,50 @@ def test_result_field_change_is_reported():
     o["n_ready"][3] = 1
     o["ready"][3][0]["index"] = 9
     assert [p for p, _ in parity.compare_results(r, o)] == [3]
+
+
+def test_escalation_predicate(built):
+    """The oracle's escalation predicate (batch.cpp) justifies an escalation only
+    when the item needs the host: a steady leader's ReplicateResp does not, a
+    follower whose election timeout fires with committed <= applied does
+    (ELECTION), a second reset in one pass does (RANDOM), a sixth message into
+    a depth-4 mailbox does (CAPACITY)."""
+    import numpy as np
+    from dragonboat_amd import abi, populations as P
+    from oracle.pyoracle import OraclePopulation
+    import parity
+    G, R = 4, 3
+    peers = P.make_groups(G, R, seed=3)
+    topo = P.Topology(G, R)
+    pop = OraclePopulation(peers, R)
+    o = pop.step(None, P.propose_locals(R * G, np.arange(G), pass_index=0))
+    msgs = topo.route_messages(o["msgs"])
+    pop = OraclePopulation(peers, R)
+    o = pop.step(None, P.propose_locals(R * G, np.arange(G), pass_index=0))
+    # pass 2: claim the leader of group 0 escalated its first ack (item 0)
+    loc = P.propose_locals(R * G, np.arange(G), pass_index=1)
+    lim = np.full(R * G, 0xFFFFFFFF, np.uint32)
+    lim[0] = 0
+    o = pop.step(msgs, loc, lim, dev_before=pop.export())
+    res = np.zeros(1, abi.RESULT)
+    res["peer"], res["escalation"], res["esc_item"] = 0, abi.ESC_NAMES.index("capacity"), 0
+    bad = parity.check_escalations(res, o["esc_mask"])
+    assert bad and bad[0][2] == "capacity" and bad[0][3] == [], bad
+    # a follower's election timeout with committed <= applied: ELECTION is justified
+    p2 = peers.copy()
+    f = G  # replica 1 of group 0
+    p2["election_tick"][f] = p2["randomized_election_timeout"][f] - 1
+    pop = OraclePopulation(p2, R)
+    loc = P.propose_locals(R * G, [], pass_index=0, ticks=1)
+    lim = np.full(R * G, 0xFFFFFFFF, np.uint32)
+    lim[f] = 0
+    o = pop.step(None, loc, lim, dev_before=p2)
+    assert (int(o["esc_mask"][f]) >> abi.ESC_NAMES.index("election")) & 1
+    assert not (int(o["esc_mask"][f]) >> abi.ESC_NAMES.index("capacity")) & 1
+    # six Heartbeats into one depth-4 mailbox: the fifth is a CAPACITY item
+    hb = np.zeros(6, abi.MESSAGE)
+    hb["peer"], hb["type"], hb["slot"], hb["term"] = f, abi.HEARTBEAT, 0, p2["term"][f]
+    pop = OraclePopulation(peers, R)
+    lim[f] = 4
+    o = pop.step(hb, None, lim, dev_before=peers)
+    assert (int(o["esc_mask"][f]) >> abi.ESC_NAMES.index("capacity")) & 1

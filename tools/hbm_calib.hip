@@ -28,9 +28,45 @@ __global__ void write_u8(uint8_t* __restrict__ a, size_t n) {
   for (; i < n; i += (size_t)gridDim.x * blockDim.x) a[i] = (uint8_t)i;
 }
 
+// Achievable HBM bandwidth (MI355X_MICROARCH.md: float4 copy): read + write of
+// a 4 GiB buffer, 16 B per lane per access, grid-stride over 2048 x 256 lanes.
+__global__ void copy_f4(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  for (; i < n; i += (size_t)gridDim.x * blockDim.x) b[i] = a[i];
+}
+
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s\n", hipGetErrorString(e_)); return 1; } } while (0)
 
-int main() {
+// `hbm_calib copy`: best of 5 float4 copies of 2 GiB -> 2 GiB, one JSON line.
+static int copy_mode() {
+  const size_t bytes = 2ull << 30;
+  void *a, *b;
+  CK(hipMalloc(&a, bytes));
+  CK(hipMalloc(&b, bytes));
+  CK(hipMemset(a, 1, bytes));
+  CK(hipMemset(b, 0, bytes));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const size_t n = bytes / 16;
+  float best = 1e30f;
+  for (int rep = 0; rep < 6; ++rep) {
+    CK(hipEventRecord(e0));
+    copy_f4<<<256 * 32, 256>>>((const float4*)a, (float4*)b, n);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (rep > 0 && ms < best) best = ms;  // rep 0 warms up
+  }
+  printf("{\"copy_bytes_moved\": %zu, \"copy_f4_GBs\": %.1f}\n", 2 * bytes, 2.0 * bytes / best / 1e6);
+  CK(hipFree(a));
+  CK(hipFree(b));
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && argv[1][0] == 'c') return copy_mode();
   const size_t bytes = 2ull << 30;
   void* buf;
   uint64_t* out;
