@@ -7,16 +7,22 @@ Outputs stay in-tree (git-ignored) so they travel to the GPU box.
 """
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-ENGINE_SRC = [os.path.join(ROOT, "dragonboat_amd", "csrc", "gr_engine.hip")]
-ENGINE_DEPS = ENGINE_SRC + [os.path.join(ROOT, "dragonboat_amd", "csrc", f)
-                            for f in ("gr_lane.h", "gr_layout.h", "gr_host.h", "gr_fast.h", "gr_tick.h", "gr_io.h")] + \
+CSRC = os.path.join(ROOT, "dragonboat_amd", "csrc")
+# the C-ABI + boundary passes, and one translation unit per slot count (compiled in parallel)
+ENGINE_SRC = [os.path.join(CSRC, "gr_engine.hip")] + [os.path.join(CSRC, f"gr_kernels_s{s}.hip") for s in (1, 3, 5, 8)]
+ENGINE_DEPS = ENGINE_SRC + [os.path.join(CSRC, f)
+                            for f in ("gr_lane.h", "gr_layout.h", "gr_host.h", "gr_fast.h", "gr_tick.h", "gr_io.h",
+                                      "gr_cover.h", "gr_kernels.h")] + \
     [os.path.join(ROOT, "include", "gpuraft.h")]
+JOBS = max(1, min(8, os.cpu_count() or 1))
 ENGINE_LIB = os.path.join(ROOT, "dragonboat_amd", "_build", "libgpuraft.so")
+COVER_LIB = os.path.join(ROOT, "dragonboat_amd", "_build", "libgpuraft_cover.so")
 ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
 KAT_BIN = os.path.join(ROOT, "oracle", "_build", "kat_tests")
 HOSTLANE_LIB = os.path.join(ROOT, "tests", "_build", "libhostlane.so")
@@ -50,13 +56,31 @@ def _run(cmd):
         raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
+def _hip_lib(out, srcs, deps, extra=(), force=False):
+    """Compile every source to an object in parallel (hipcc, gfx950), then link `out`."""
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    if not (force or _stale(out, deps)):
+        return out
+    odir = out + ".o.d"
+    os.makedirs(odir, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *extra,
+             "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
+    objs = [os.path.join(odir, os.path.basename(s) + ".o") for s in srcs]
+    with ThreadPoolExecutor(JOBS) as ex:
+        for f in [ex.submit(_run, [HIPCC, *flags, "-c", s, "-o", o]) for s, o in zip(srcs, objs)]:
+            f.result()
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out])
+    return out
+
+
 def build_engine(force=False):
-    os.makedirs(os.path.dirname(ENGINE_LIB), exist_ok=True)
-    if force or _stale(ENGINE_LIB, ENGINE_DEPS):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "dragonboat_amd", "csrc"),
-              *ENGINE_SRC, "-o", ENGINE_LIB])
-    return ENGINE_LIB
+    return _hip_lib(ENGINE_LIB, ENGINE_SRC, ENGINE_DEPS, force=force)
+
+
+def build_engine_cover(force=False):
+    """libgpuraft_cover.so: the same engine with per-branch hit counters
+    (-DGR_COVERAGE, gr_cover.h), for tests/test_coverage.py only."""
+    return _hip_lib(COVER_LIB, ENGINE_SRC, ENGINE_DEPS, extra=("-DGR_COVERAGE",), force=force)
 
 
 def build_oracle(force=False):
@@ -78,7 +102,7 @@ def build_hostlane(force=False):
     os.makedirs(os.path.dirname(HOSTLANE_LIB), exist_ok=True)
     src = os.path.join(ROOT, "tests", "native", "hostlane.hip")
     if force or _stale(HOSTLANE_LIB, ENGINE_DEPS + [src]):
-        _run([HIPCC, "--cuda-host-only", "-O2", "-g", "-std=c++17", "-fPIC", "-shared",
+        _run([HIPCC, "--cuda-host-only", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-DGR_COVERAGE",
               "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "dragonboat_amd", "csrc"),
               src, "-o", HOSTLANE_LIB])
     return HOSTLANE_LIB
@@ -114,9 +138,11 @@ def build_tools(force=False):
 
 
 def build_all(force=False):
-    build_engine(force)
-    build_wire(force)
-    build_oracle(force)
-    build_wire_oracle(force)
-    build_hostlane(force)
-    build_tools(force)
+    # independent targets side by side (each engine build also compiles its units in parallel)
+    with ThreadPoolExecutor(4) as ex:
+        fs = [ex.submit(f, force) for f in (build_engine, build_engine_cover, build_hostlane, build_wire)]
+        build_oracle(force)
+        build_wire_oracle(force)
+        build_tools(force)
+        for f in fs:
+            f.result()

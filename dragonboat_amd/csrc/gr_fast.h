@@ -18,6 +18,7 @@
 // from its untouched state (message bodies this lane may have written to its
 // out mailboxes are overwritten there, and their counts were never written).
 #pragma once
+#include "gr_cover.h"
 #include "gr_layout.h"
 
 namespace gr {
@@ -382,6 +383,7 @@ struct FastLane {
       for (int j = 0; j < S; ++j)
         if (gout[j] != NOPOS) ntst(kp.out.at(gout[j]).cnt(), (uint8_t)(0));
       ntst(kp.ln.u8(LR_RFLAGS)[i], (uint8_t)(0));
+      GR_COVER(FAST_QUIESCED);
       return true;  // *ls stays zero
     }
     GF_BAIL(!leader && state != GR_FOLLOWER);
@@ -498,6 +500,8 @@ struct FastLane {
     ls->leader_in = leader ? nmi : 0;
     ls->leader_out = leader ? nmo : 0;
     ls->entries = nent;
+    if (leader) GR_COVER(FAST_LEADER);
+    else GR_COVER(FAST_FOLLOWER);
     return true;
   }
 

@@ -1,0 +1,216 @@
+// gr_kernels.h — the two step kernels of a pass and their launcher, templated
+// on the remote-slot count S. Each instantiation lives in its own translation
+// unit (gr_kernels_s<S>.hip) so the four builds compile in parallel; the
+// C-ABI in gr_engine.hip calls launch<S> through launch_slots.
+//
+// One lane per Raft group (peer). Work is integer compares, min/max, a
+// sorting network and gathers over structure-of-arrays state: HBM-bandwidth
+// bound, no MFMA. 256-lane workgroups, one lane per slot,
+// consecutive lanes on consecutive slots so every SoA field access of a wave
+// is one contiguous 512-byte (u64) or 64-byte (u8) segment.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "gr_fast.h"
+#include "gr_lane.h"
+#include "gr_tick.h"
+
+namespace gr {
+
+constexpr int kBlock = 256;
+
+// Per-workgroup partial counters (no atomics on global memory): row b of the
+// stats block belongs to workgroup b of whichever kernel runs.
+__device__ inline uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ inline void block_stats(const StepParams& kp, const LaneStats& ls) {
+  constexpr int N = 9;
+  __shared__ uint32_t red[N];
+  if (threadIdx.x < N) red[threadIdx.x] = 0;
+  __syncthreads();
+  // one named field at a time: a register array indexed in a loop was put in scratch
+  const uint32_t f0 = wave_sum(ls.leader_commit), f1 = wave_sum(ls.follower_commit),
+                 f2 = wave_sum(ls.escalated), f3 = wave_sum(ls.msgs_in), f4 = wave_sum(ls.msgs_out),
+                 f5 = wave_sum(ls.leader_in), f6 = wave_sum(ls.leader_out), f7 = wave_sum(ls.entries),
+                 f8 = wave_sum(ls.bailed);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&red[0], f0);
+    atomicAdd(&red[1], f1);
+    atomicAdd(&red[2], f2);
+    atomicAdd(&red[3], f3);
+    atomicAdd(&red[4], f4);
+    atomicAdd(&red[5], f5);
+    atomicAdd(&red[6], f6);
+    atomicAdd(&red[7], f7);
+    atomicAdd(&red[8], f8);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t* row = kp.stats + (uint64_t)blockIdx.x * NSTAT;
+    row[ST_LEADER_COMMITS] += red[0];
+    row[ST_FOLLOWER_COMMITS] += red[1];
+    row[ST_ESCALATIONS] += red[2];
+    row[ST_MSGS_IN] += red[3];
+    row[ST_MSGS_OUT] += red[4];
+    row[ST_LEADER_MSGS_IN] += red[5];
+    row[ST_LEADER_MSGS_OUT] += red[6];
+    row[ST_REPLICATE_ENTRIES] += red[7];
+    row[ST_BAILED] += red[8];
+  }
+}
+
+// Pass 1: every lane runs the lean steady-state lane (gr_fast.h). Lanes that
+// meet anything else store no state and are appended to one of kBailLists
+// lists (followers: list = workgroup % 8, leaders: 8 + workgroup % 8; one returning atomic per wave and role with a
+// bailing lane, a wave's lanes contiguous and ascending). Spreading the
+// appends over 16 counters 256 B apart keeps them from serialising when every
+// wave bails a few lanes (one shared counter: 105 us instead of 37 us on
+// config 3); no barrier, so waves of steady-state populations retire freely.
+constexpr uint32_t kBailLists = 16, kCounterStride = 64;  // counters 256 B apart
+
+template <int S>
+#ifndef GR_FAST_MIN_WAVES
+#define GR_FAST_MIN_WAVES 1  // waves per SIMD the register allocation must allow (A/B builds)
+#endif
+__global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
+                                                                             uint32_t* counters, uint32_t list_cap) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  LaneStats ls;
+  bool bail = false;
+  uint32_t role = 0;
+  if (i < kp.n_lanes) {
+    const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+    bail = !fast_step<S>(kp, i, p, &ls, &role);  // leaves ls zero when it bails
+  }
+  // followers into lists 0..7, leaders into 8..15: the general kernel walks the
+  // lists in order, so its waves hold one role and diverge less
+  const bool lead = role == GR_LEADER;
+#pragma unroll
+  for (uint32_t side = 0; side < 2; ++side) {
+    const bool mine = bail && (lead == (side == 1));
+    const uint64_t bm = __ballot(mine);
+    if (bm) {
+      const uint32_t list = (blockIdx.x % (kBailLists / 2)) + side * (kBailLists / 2);
+      const uint32_t lane = threadIdx.x & 63;
+      const uint32_t first = (uint32_t)__ffsll((unsigned long long)bm) - 1;
+      uint32_t base = 0;
+      if (lane == first) base = atomicAdd(counters + list * kCounterStride, (uint32_t)__popcll(bm));
+      base = __shfl(base, (int)first);
+      if (mine) bail_list[(uint64_t)list * list_cap + base + (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
+    }
+  }
+  if (kp.stats) block_stats(kp, ls);
+}
+
+// Pass 2: the general lane (every handler, escalation with prefix re-run)
+// over the bailed lanes only, grid-stride over the concatenated lists; also
+// clears the counters the next pass's fast kernel will use.
+#ifndef GR_GENERAL_MIN_WAVES
+#define GR_GENERAL_MIN_WAVES 1  // A/B builds: waves per SIMD for the general kernel
+#endif
+template <int S>
+__global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(StepParams kp, const uint32_t* bail_list,
+                                                         const uint32_t* counters, uint32_t* next_counters,
+                                                         uint32_t list_cap) {
+  uint32_t start[kBailLists + 1];
+  start[0] = 0;
+#pragma unroll
+  for (uint32_t l = 0; l < kBailLists; ++l) start[l + 1] = start[l] + counters[l * kCounterStride];
+  const uint32_t n = start[kBailLists];
+  if (blockIdx.x == 0 && threadIdx.x < kBailLists) next_counters[threadIdx.x * kCounterStride] = 0;
+  if (blockIdx.x * kBlock >= n) return;  // uniform per block: nothing to do, no stats row touched
+  LaneStats acc;
+  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    const uint32_t x = base + threadIdx.x;
+    if (x < n) {
+      uint32_t l = 0;
+#pragma unroll
+      for (uint32_t k = 1; k < kBailLists; ++k) l = x >= start[k] ? k : l;
+      uint32_t off = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kBailLists; ++k) off = (k == l) ? x - start[k] : off;
+      const uint32_t i = bail_list[(uint64_t)l * list_cap + off];
+      const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+      LaneStats ls;
+      // lanes with ticks or a ReadIndex (LW_OTHER) try the heartbeat/ReadIndex/tick
+      // lane first; the rest (and its hand-overs) take the general lane
+      const bool tickish = kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
+      if (!tickish || !tick_step<S>(kp, i, p, &ls)) {
+        Lane<S> L(kp, i, p);
+        L.step(&ls);
+      }
+      acc.leader_commit += ls.leader_commit;
+      acc.follower_commit += ls.follower_commit;
+      acc.escalated += ls.escalated;
+      acc.msgs_in += ls.msgs_in;
+      acc.msgs_out += ls.msgs_out;
+      acc.leader_in += ls.leader_in;
+      acc.leader_out += ls.leader_out;
+      acc.entries += ls.entries;
+      acc.bailed += 1;
+    }
+  }
+  if (kp.stats) block_stats(kp, acc);
+}
+
+// The general kernel's grid: one 256-lane workgroup per CU fills the chip at
+// its occupancy (1 wave per SIMD); never more than the stats block has rows for.
+// Kept small because with no bailed lanes the launch is pure overhead.
+constexpr uint32_t kGeneralBlocks = 256;
+
+// Optional per-pass timing: events around the two kernels, recorded on the
+// pass's stream.
+struct PassTiming {
+  hipEvent_t ev[3];
+};
+
+template <int S>
+hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters, uint32_t list_cap,
+                         uint32_t parity, hipStream_t s, const PassTiming* t) {
+  if (kp.n_lanes == 0) return hipSuccess;
+  const uint32_t blocks = (kp.n_lanes + kBlock - 1) / kBlock;
+  uint32_t* cur = counters + (parity & 1) * kBailLists * kCounterStride;
+  uint32_t* nxt = counters + ((parity + 1) & 1) * kBailLists * kCounterStride;
+  hipError_t err;
+  if (t && (err = hipEventRecord(t->ev[0], s)) != hipSuccess) return err;
+  hipLaunchKernelGGL(gr_fast_kernel<S>, dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
+  if ((err = hipGetLastError()) != hipSuccess) return err;
+  if (t && (err = hipEventRecord(t->ev[1], s)) != hipSuccess) return err;
+  const uint32_t gblocks = blocks < kGeneralBlocks ? blocks : kGeneralBlocks;
+  hipLaunchKernelGGL(gr_step_kernel<S>, dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list,
+                     (const uint32_t*)cur, nxt, list_cap);
+  if ((err = hipGetLastError()) != hipSuccess) return err;
+  if (t && (err = hipEventRecord(t->ev[2], s)) != hipSuccess) return err;
+  return hipSuccess;
+}
+
+
+#ifdef GR_COVERAGE
+// This translation unit's hit counters (gr_cover.h: one static array per code object).
+template <int S>
+hipError_t cover_read(uint64_t* out) {
+  unsigned long long h[CV_N];
+  const hipError_t e = hipMemcpyFromSymbol(h, HIP_SYMBOL(gr_cover_dev), sizeof(h), 0, hipMemcpyDeviceToHost);
+  if (e == hipSuccess)
+    for (uint32_t k = 0; k < CV_N; ++k) out[k] += h[k];
+  return e;
+}
+#endif
+
+}  // namespace gr
+
+// one explicit instantiation per translation unit
+#define GR_INSTANTIATE_SLOTS(SS)                                                                               \
+  namespace gr {                                                                                              \
+  template hipError_t launch<SS>(const StepParams&, uint32_t*, uint32_t*, uint32_t, uint32_t, hipStream_t,      \
+                                 const PassTiming*);                                                          \
+  GR_INSTANTIATE_COVER(SS)                                                                                    \
+  }
+#ifdef GR_COVERAGE
+#define GR_INSTANTIATE_COVER(SS) template hipError_t cover_read<SS>(uint64_t*);
+#else
+#define GR_INSTANTIATE_COVER(SS)
+#endif

@@ -13,6 +13,7 @@
 //
 // Function-level citations are to /root/reference/internal/raft/*.go.
 #pragma once
+#include "gr_cover.h"
 #include "gr_layout.h"
 
 namespace gr {
@@ -400,10 +401,16 @@ struct Lane {
   GR_HD void responded_to(uint32_t j) {  // :130-138
     const uint32_t s = rstate(j);
     if (s == GR_RETRY) {
+      GR_COVER(RESPONDED_RETRY);
       become_replicate(j);
     } else if (s == GR_SNAPSHOT_ST) {
       need(G_SNAP);
-      if (sel(match, j) >= sel(snap, j)) become_retry(j);
+      if (sel(match, j) >= sel(snap, j)) {
+        GR_COVER(RESPONDED_SNAPSHOT_RETRY);
+        become_retry(j);
+      } else {
+        GR_COVER(RESPONDED_SNAPSHOT_STAY);
+      }
     }
   }
   GR_HD bool try_update(uint32_t j, uint64_t index) {  // :108-118
@@ -417,11 +424,19 @@ struct Lane {
   }
   GR_HD bool decrease_to(uint32_t j, uint64_t rejected, uint64_t last) {  // :140-156
     if (rstate(j) == GR_REPLICATE_ST) {
-      if (rejected <= sel(match, j)) return false;
+      if (rejected <= sel(match, j)) {
+        GR_COVER(DECREASE_IGNORED);
+        return false;
+      }
+      GR_COVER(DECREASE_REPLICATE);
       put(next, j, sel(match, j) + 1);
       return true;
     }
-    if (sel(next, j) - 1 != rejected) return false;
+    if (sel(next, j) - 1 != rejected) {
+      GR_COVER(DECREASE_IGNORED);
+      return false;
+    }
+    GR_COVER(DECREASE_PROBE);
     wait_to_retry(j);
     put(next, j, umax(1, umin(rejected, last + 1)));
     return true;
@@ -614,7 +629,10 @@ struct Lane {
   // raft.sendReplicateMessage + makeReplicateMessage (raft.go:474-532).
   GR_HD int send_replicate(uint32_t j) {
     need(G_CORE | G_REM | G_WIN);
-    if (is_paused(rstate(j))) return 0;
+    if (is_paused(rstate(j))) {
+      GR_COVER(SEND_PAUSED);
+      return 0;
+    }
     const uint64_t nx = sel(next, j);
     uint64_t lt;
     GR_TRY(term_of(nx - 1, &lt));
@@ -629,6 +647,7 @@ struct Lane {
       const uint64_t cnt = hi - nx + 1;
       if (cnt > 0xFFFFFFFFull) return GR_ESC_CAPACITY;
       if (cnt > 1) {  // limitSize (entryutils.go:50-63) keeps all iff sum <= max
+        GR_COVER(SEND_MULTI_ENTRY);
         need(G_EUB);
         if (eub == 0 || cnt > kp.max_entry_size / eub) return GR_ESC_ENTRY_SIZE;
       }
@@ -647,6 +666,7 @@ struct Lane {
       m.n = (uint32_t)cnt;
       m.rt0 = t0;
       if (nr == 2) {
+        GR_COVER(SEND_TWO_RUNS);
         m.rt1 = t1;
         m.run2 = (uint32_t)(s1 - nx);
         m.flags = (uint8_t)(2 << MFL_RUNS_SHIFT);
@@ -658,6 +678,8 @@ struct Lane {
       else if (s == GR_RETRY) set_rstate(j, GR_WAIT);
       else return GR_ESC_PANIC;
       dirty |= D_REM;
+    } else {
+      GR_COVER(SEND_EMPTY);
     }
     return emit(j, m);
   }
@@ -670,6 +692,7 @@ struct Lane {
     for (uint32_t j = 0; j < (uint32_t)S; ++j) {
       if (rkind(j) == GR_SLOT_OBSERVER) {
         if (j == self) return GR_ESC_PANIC;
+        GR_COVER(BCAST_OBSERVER);
         GR_TRY(send_replicate(j));
       }
     }
@@ -691,7 +714,10 @@ struct Lane {
     if (clo == 0 && chi == 0) {
 #pragma unroll 1
       for (uint32_t j = 0; j < (uint32_t)S; ++j)
-        if (rkind(j) == GR_SLOT_OBSERVER) GR_TRY(send_heartbeat(j, 0, 0));
+        if (rkind(j) == GR_SLOT_OBSERVER) {
+          GR_COVER(HEARTBEAT_OBSERVER);
+          GR_TRY(send_heartbeat(j, 0, 0));
+        }
     }
     return 0;
   }
@@ -707,6 +733,7 @@ struct Lane {
   GR_HD int send_timeout_now(uint64_t target) {  // raft.go:589-594
     const uint32_t j = find_slot(target);
     if (j == GR_SLOT_NONE) return GR_ESC_NONMEMBER;
+    GR_COVER(TIMEOUT_NOW_SENT);
     OutMsg m;
     m.type = GR_TIMEOUT_NOW;
     return emit(j, m);
@@ -722,9 +749,13 @@ struct Lane {
     bool dup = false;
 #pragma unroll
     for (int q = 0; q < GR_Q; ++q) dup = dup || ((uint32_t)q < ric && rilo[q] == clo && rihi[q] == chi);
-    if (dup) return 0;
+    if (dup) {
+      GR_COVER(RI_DUP);
+      return 0;
+    }
     if (ric > 0 && index < sel(rii, ric - 1)) return GR_ESC_PANIC;
     if (ric >= GR_Q) return GR_ESC_CAPACITY;
+    GR_COVER(RI_ADD);
 #pragma unroll
     for (int q = 0; q < GR_Q; ++q) {
       const bool hit = (uint32_t)q == ric;
@@ -750,7 +781,11 @@ struct Lane {
     riack |= (1u << from) << (8 * pos);
     dirty |= D_RI;
     const uint32_t ack = (riack >> (8 * pos)) & 0xFFu;
-    if (popc8(ack) + 1 < quorum()) return 0;
+    if (popc8(ack) + 1 < quorum()) {
+      GR_COVER(RI_ACK_PENDING);
+      return 0;
+    }
+    GR_COVER(RI_CONFIRM_RELEASE);
     const uint64_t sidx = sel(rii, (uint32_t)pos);
     bool bad = false;
 #pragma unroll
@@ -762,6 +797,7 @@ struct Lane {
       if (f == GR_SLOT_NONE || f == self) {
         GR_TRY(add_ready(sidx, sel(rilo, (uint32_t)q), sel(rihi, (uint32_t)q)));
       } else {
+        GR_COVER(RI_RESP_REMOTE);
         OutMsg m;
         m.type = GR_READ_INDEX_RESP;
         m.log_index = sidx;
@@ -798,12 +834,17 @@ struct Lane {
       if (term == 0) return GR_ESC_PANIC;  // hasCommittedEntryAtCurrentTerm :1148-1157
       uint64_t t;
       GR_TRY(term_of(committed, &t));
-      if (t != term) return 0;
+      if (t != term) {
+        GR_COVER(RI_NOT_AT_TERM);
+        return 0;
+      }
       GR_TRY(ri_add(committed, clo, chi, from));
       return broadcast_heartbeat_with_hint(clo, chi);
     }
+    GR_COVER(RI_SINGLE_READY);
     GR_TRY(add_ready(committed, clo, chi));
     if (from != GR_SLOT_NONE && from != self && rkind(from) == GR_SLOT_OBSERVER) {
+      GR_COVER(RI_SINGLE_OBSERVER_RESP);
       OutMsg m;
       m.type = GR_READ_INDEX_RESP;
       m.log_index = committed;
@@ -878,6 +919,7 @@ struct Lane {
     OutMsg r;
     r.type = GR_REPLICATE_RESP;
     if (m.log_index < committed) {
+      GR_COVER(REP_EARLY_ACK);
       r.log_index = committed;
       return emit(from, r);
     }
@@ -886,6 +928,9 @@ struct Lane {
     if (lt == m.log_term) {
       uint64_t ci;
       GR_TRY(conflict_index(m, &ci));
+      if (ci == 0) GR_COVER(REP_MATCH_NO_APPEND);
+      else if (ci <= hi) GR_COVER(REP_TRUNCATE);
+      else GR_COVER(REP_APPEND_TAIL);
       if (ci != 0) {
         if (ci <= committed) return GR_ESC_PANIC;  // logentry.go:284-287
         if (ci > hi + 1) return GR_ESC_PANIC;      // merge would hit a hole
@@ -894,6 +939,7 @@ struct Lane {
         win_truncate(ci);
         const uint32_t nr = (m.flags >> MFL_RUNS_SHIFT) & 3u;
         if (nr == 2) {
+          GR_COVER(REP_TWO_RUNS);
           const uint64_t b2 = m.log_index + 1 + m.run2;
           if (ci < b2) win_push(ci, m.rt0);
           win_push(umax(ci, b2), m.rt1);
@@ -913,6 +959,7 @@ struct Lane {
       }
       r.log_index = last_idx;
     } else {
+      GR_COVER(REP_REJECT);
       r.flags = MFL_REJECT;
       r.log_index = m.log_index;
       r.hint = hi;
@@ -926,6 +973,7 @@ struct Lane {
     set_ractive(j, 1);
     dirty |= D_REM;
     if (!(m.flags & MFL_REJECT)) {
+      GR_COVER(L_REPLICATE_RESP_ACCEPT);
       const bool paused = is_paused(rstate(j));
       if (try_update(j, m.log_index)) {
         responded_to(j);
@@ -937,6 +985,7 @@ struct Lane {
           GR_TRY(send_timeout_now(ltt));
       }
     } else {
+      GR_COVER(L_REPLICATE_RESP_REJECT);
       if (decrease_to(j, m.log_index, m.hint)) {
         enter_retry(j);
         GR_TRY(send_replicate(j));
@@ -976,7 +1025,11 @@ struct Lane {
       }
     }
     dirty |= D_REM;
-    if (c < quorum()) return become_follower(term, 0);
+    if (c < quorum()) {
+      GR_COVER(TICK_STEP_DOWN);
+      return become_follower(term, 0);
+    }
+    GR_COVER(TICK_CHECK_QUORUM_OK);
     return 0;
   }
 
@@ -984,12 +1037,16 @@ struct Lane {
   GR_HD int handle_election() {  // handleNodeElection, raft.go:1073-1086
     need(G_CORE | G_LEAD);
     if (state == GR_LEADER) return 0;
-    if (committed > applied) return 0;  // hasConfigChangeToApply :1055-1061
+    if (committed > applied) {  // hasConfigChangeToApply :1055-1061
+      GR_COVER(TICK_ELECTION_SKIPPED);
+      return 0;
+    }
     return GR_ESC_ELECTION;
   }
   GR_HD int tick() {  // raft.go:377-429
     need(G_CORE | G_TICK);
     if (state == GR_LEADER) {
+      GR_COVER(TICK_LEADER);
       etick++;
       dirty |= D_ETICK;
       const bool abort = leader_transfering() && etick >= etimeout;
@@ -997,18 +1054,29 @@ struct Lane {
         etick = 0;
         if (flags & GR_F_CHECK_QUORUM) GR_TRY(check_quorum());
       }
-      if (abort) { ltt = 0; dirty |= D_LTT; }
+      if (abort) {
+        GR_COVER(TICK_TRANSFER_ABORT);
+        ltt = 0;
+        dirty |= D_LTT;
+      }
       htick++;
       dirty |= D_HTICK;
       if (htick >= htimeout) {
         htick = 0;
-        if (state == GR_LEADER) GR_TRY(broadcast_heartbeat());  // only the leader has a handler
+        if (state == GR_LEADER) {  // only the leader has a handler
+          GR_COVER(TICK_HEARTBEAT);
+          GR_TRY(broadcast_heartbeat());
+        }
       }
       return 0;
     }
     etick++;
     dirty |= D_ETICK;
-    if (state == GR_OBSERVER) return 0;
+    if (state == GR_OBSERVER) {
+      GR_COVER(TICK_OBSERVER);
+      return 0;
+    }
+    GR_COVER(TICK_FOLLOWER);
     if (etick >= retimeout && !self_removed()) {
       etick = 0;
       return handle_election();
@@ -1095,14 +1163,21 @@ struct Lane {
       if (m.term > term) {
         if (t == GR_REQUEST_VOTE) return GR_ESC_UNSUPPORTED;  // dropRequestVoteFromHighTermNode + vote
         const uint64_t lid = is_leader_message(t) ? remote_id(from) : 0;
-        if (state == GR_OBSERVER) GR_TRY(become_observer(m.term, lid));
-        else GR_TRY(become_follower(m.term, lid));
+        if (state == GR_OBSERVER) {
+          GR_COVER(TERM_HIGHER_OBSERVER);
+          GR_TRY(become_observer(m.term, lid));
+        } else {
+          GR_COVER(TERM_HIGHER);
+          GR_TRY(become_follower(m.term, lid));
+        }
       } else {
         if (is_leader_message(t) && (flags & GR_F_CHECK_QUORUM)) {
+          GR_COVER(TERM_LOWER_NOOP);
           OutMsg o;
           o.type = GR_NOOP;
           return emit(from, o);
         }
+        GR_COVER(TERM_LOWER_DROP);
         return 0;
       }
     }
@@ -1114,15 +1189,26 @@ struct Lane {
         case GR_UNREACHABLE:
         case GR_LEADER_TRANSFER: {
           need(G_REM);
-          if (rkind(from) == GR_SLOT_EMPTY) return 0;  // lw: no remote (raft.go:1466-1479)
+          if (rkind(from) == GR_SLOT_EMPTY) {  // lw: no remote (raft.go:1466-1479)
+            GR_COVER(L_RESP_NONMEMBER);
+            return 0;
+          }
           if (t == GR_REPLICATE_RESP) return leader_replicate_resp(m, from);
-          if (t == GR_HEARTBEAT_RESP) return leader_heartbeat_resp(m, from);
-          if (t == GR_LEADER_TRANSFER) return leader_leader_transfer(m, from);
+          if (t == GR_HEARTBEAT_RESP) {
+            GR_COVER(L_HEARTBEAT_RESP);
+            return leader_heartbeat_resp(m, from);
+          }
+          if (t == GR_LEADER_TRANSFER) {
+            GR_COVER(L_LEADER_TRANSFER);
+            return leader_leader_transfer(m, from);
+          }
           if (t == GR_UNREACHABLE) {
+            GR_COVER(L_UNREACHABLE);
             enter_retry(from);
             dirty |= D_REM;
             return 0;
           }
+          GR_COVER(L_SNAPSHOT_STATUS);
           if (rstate(from) != GR_SNAPSHOT_ST) return 0;  // SnapshotStatus :1286-1299
           need(G_SNAP);
           if (m.flags & MFL_REJECT) {
@@ -1134,23 +1220,27 @@ struct Lane {
           dirty |= D_REM;
           return 0;
         }
-        case GR_READ_INDEX: return leader_read_index(from, m.hint, m.hint_high, m.commit);
-        case GR_LEADER_HEARTBEAT: return broadcast_heartbeat();
-        case GR_CHECK_QUORUM: return check_quorum();
-        case GR_ELECTION: return 0;
-        case GR_PROPOSE: return leader_forwarded_propose(m);
+        case GR_READ_INDEX: GR_COVER(L_READ_INDEX_MSG); return leader_read_index(from, m.hint, m.hint_high, m.commit);
+        case GR_LEADER_HEARTBEAT: GR_COVER(L_LEADER_HEARTBEAT); return broadcast_heartbeat();
+        case GR_CHECK_QUORUM: GR_COVER(L_CHECK_QUORUM_MSG); return check_quorum();
+        case GR_ELECTION: GR_COVER(L_ELECTION); return 0;
+        case GR_PROPOSE: GR_COVER(L_PROPOSE_FWD); return leader_forwarded_propose(m);
         case GR_REQUEST_VOTE: return GR_ESC_UNSUPPORTED;
-        default: return 0;  // nil handler
+        default: GR_COVER(L_NIL); return 0;  // nil handler
       }
     }
     if (state == GR_FOLLOWER || state == GR_OBSERVER) {
       const bool obs = state == GR_OBSERVER;
       switch (t) {
         case GR_REPLICATE:  // raft.go:1359-1363
+          if (obs) GR_COVER(O_REPLICATE);
+          else GR_COVER(F_REPLICATE);
           zero_etick();
           set_leader_from(from);
           return handle_replicate(m, from);
         case GR_HEARTBEAT: {  // raft.go:1365-1369, 923-931
+          if (obs) GR_COVER(O_HEARTBEAT);
+          else GR_COVER(F_HEARTBEAT);
           zero_etick();
           set_leader_from(from);
           if (m.commit > committed) {
@@ -1165,42 +1255,50 @@ struct Lane {
           return emit(from, o);
         }
         case GR_READ_INDEX_RESP:  // raft.go:1391-1399
+          if (obs) GR_COVER(O_READ_INDEX_RESP);
+          else GR_COVER(F_READ_INDEX_RESP);
           zero_etick();
           set_leader_from(from);
           return add_ready(m.log_index, m.hint, m.hint_high);
         case GR_READ_INDEX: {
+          if (obs) GR_COVER(O_READ_INDEX_FWD);
+          else GR_COVER(F_READ_INDEX_FWD);
           bool d;
           return forward_to_leader(as_out(m), &d);
         }
         case GR_LEADER_TRANSFER: {
-          if (obs) return 0;
+          if (obs) { GR_COVER(O_DROPPED); return 0; }
+          GR_COVER(F_LEADER_TRANSFER_FWD);
           bool d;
           return forward_to_leader(as_out(m), &d);
         }
         case GR_ELECTION:
-          if (obs) return 0;
+          if (obs) { GR_COVER(O_DROPPED); return 0; }
+          GR_COVER(F_ELECTION);
           return handle_election();
         case GR_PROPOSE: {  // handleFollowerPropose / handleObserverPropose (raft.go:1346-1357, 1322)
+          if (obs) GR_COVER(O_PROPOSE_FWD);
+          else GR_COVER(F_PROPOSE_FWD);
           bool d;
           return forward_to_leader(as_out(m), &d);
         }
         case GR_INSTALL_SNAPSHOT: return GR_ESC_UNSUPPORTED;
         case GR_REQUEST_VOTE:
         case GR_TIMEOUT_NOW:
-          if (obs) return 0;
+          if (obs) { GR_COVER(O_DROPPED); return 0; }
           return GR_ESC_UNSUPPORTED;
-        default: return 0;
+        default: GR_COVER(F_NIL); return 0;
       }
     }
     switch (t) {  // candidate: every non-nil handler changes role or votes
-      case GR_PROPOSE: return 0;  // handleCandidatePropose only logs
+      case GR_PROPOSE: GR_COVER(C_PROPOSE); return 0;  // handleCandidatePropose only logs
       case GR_HEARTBEAT:
       case GR_REPLICATE:
       case GR_INSTALL_SNAPSHOT:
       case GR_REQUEST_VOTE_RESP:
       case GR_ELECTION:
       case GR_REQUEST_VOTE: return GR_ESC_UNSUPPORTED;
-      default: return 0;
+      default: GR_COVER(C_NIL); return 0;
     }
   }
 
@@ -1239,14 +1337,16 @@ struct Lane {
   GR_HD int propose(uint32_t n, bool has_cc) {
     need(G_CORE);
     if (state == GR_LEADER) {
-      if (self_removed()) { prop_result = GR_PROP_DROPPED; return 0; }
-      if (leader_transfering()) { prop_result = GR_PROP_DROPPED; return 0; }
+      if (self_removed()) { GR_COVER(PROP_DROP_SELF_REMOVED); prop_result = GR_PROP_DROPPED; return 0; }
+      if (leader_transfering()) { GR_COVER(PROP_DROP_TRANSFER); prop_result = GR_PROP_DROPPED; return 0; }
       if (has_cc) return GR_ESC_CONFIG_CHANGE;
+      GR_COVER(PROP_APPEND);
       GR_TRY(append_proposal(n));
       prop_result = GR_PROP_APPENDED;
       return 0;
     }
     if (state == GR_CANDIDATE) {
+      GR_COVER(PROP_CANDIDATE);
       prop_result = GR_PROP_DROPPED;
       return 0;
     }
@@ -1256,6 +1356,8 @@ struct Lane {
     o.flags = (uint8_t)((1u << MFL_RUNS_SHIFT) | (has_cc ? MFL_REJECT : 0u));  // reject bit: holds a ConfigChangeEntry
     bool dropped;
     GR_TRY(forward_to_leader(o, &dropped));
+    if (dropped) GR_COVER(PROP_DROP_NO_LEADER);
+    else GR_COVER(PROP_FORWARD);
     prop_result = dropped ? GR_PROP_DROPPED : GR_PROP_FORWARDED;
     return 0;
   }
@@ -1312,6 +1414,7 @@ struct Lane {
         if (state == GR_LEADER) {
           e = leader_read_index(GR_SLOT_NONE, clo, chi, 0);
         } else if (state != GR_CANDIDATE) {
+          GR_COVER(RI_LOCAL_FORWARD);
           OutMsg o;
           o.type = GR_READ_INDEX;
           o.hint = clo;
@@ -1331,6 +1434,7 @@ struct Lane {
       }
       if (nq) {  // quiescedTick x nq: electionTick++ only (raft.go:431-433); one item
         if (item == limit) { *at = item; return 0; }
+        GR_COVER(QTICK);
         need(G_ETICK);
         etick += nq;
         dirty |= D_ETICK;
@@ -1350,6 +1454,7 @@ struct Lane {
   // Kernel body for one lane: run, and on escalation re-run the prefix on the
   // pristine state so the escalating item is left entirely to the host.
   GR_HD bool step(LaneStats* ls) {
+    GR_COVER(GENERAL_LANE);
     uint32_t at = 0, limit = 0xFFFFFFFFu;
     int esc = 0;
 #pragma unroll 1
@@ -1368,6 +1473,7 @@ struct Lane {
     }
     uint8_t rf = 0;
     if (esc) {
+      GR_COVER_ESC(esc);
       rf |= RF_ESCALATED;
       kp.ln.u8(LR_ESC_REASON)[i] = (uint8_t)esc;
       kp.ln.u32(LR_ESC_ITEM)[i] = at;

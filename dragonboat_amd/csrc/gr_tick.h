@@ -21,6 +21,7 @@
 // the general kernel, in front of the general lane, on the lanes pass 1 handed
 // over, so it costs the steady-state kernel nothing.
 #pragma once
+#include "gr_cover.h"
 #include "gr_layout.h"
 
 namespace gr {
@@ -421,6 +422,8 @@ struct TickLane {
     ls->msgs_out = nmo;
     ls->leader_in = leader ? nmi : 0;
     ls->leader_out = leader ? nmo : 0;
+    if (leader) GR_COVER(TICKLANE_LEADER);
+    else GR_COVER(TICKLANE_FOLLOWER);
     return true;
   }
 };

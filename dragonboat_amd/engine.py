@@ -16,6 +16,7 @@ from . import abi
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GPURAFT_LIB") or os.path.join(_HERE, "_build", "libgpuraft.so")  # env: A/B builds
 _lib = None
+_libs = {}  # other builds by path (e.g. the coverage build), loaded beside the default
 MAILBOX_DEPTH = abi.GR_C  # full-depth spaces; exchange.py uses 2 for spaces that cross GPUs
 
 
@@ -26,8 +27,10 @@ class GpuRaftError(RuntimeError):
 def load_library(path=LIB_PATH):
     """Load the HIP engine library (import torch first so one HIP runtime is shared)."""
     global _lib
-    if _lib is not None:
+    if path == LIB_PATH and _lib is not None:
         return _lib
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise GpuRaftError(f"libgpuraft.so not built at {path}; run __graft_entry__.build()")
     lib = ctypes.CDLL(path)
@@ -69,7 +72,12 @@ def load_library(path=LIB_PATH):
                                     c.c_void_p]
     lib.gr_timing_begin.argtypes = [c.c_void_p]
     lib.gr_timing_end.argtypes = [c.c_void_p, c.POINTER(abi.Timing)]
-    _lib = lib
+    if hasattr(lib, "gr_coverage_read"):  # coverage build only (GR_COVERAGE)
+        lib.gr_coverage_read.argtypes = [c.c_void_p, c.c_uint32]
+        lib.gr_coverage_names.restype = c.c_char_p
+    if path == LIB_PATH:
+        _lib = lib
+    _libs[path] = lib
     return lib
 
 
@@ -81,8 +89,8 @@ def _check(rc, what):
 class Engine:
     """One engine = one device's slab of group slots (engine slots 0..max_peers-1)."""
 
-    def __init__(self, max_peers, slots=3, device=0, max_entry_size=abi.MAX_ENTRY_SIZE):
-        lib = load_library()
+    def __init__(self, max_peers, slots=3, device=0, max_entry_size=abi.MAX_ENTRY_SIZE, lib_path=None):
+        lib = load_library(lib_path or LIB_PATH)
         cfg = abi.Config(max_peers=max_peers, slots=slots, window_runs=abi.GR_K,
                          read_index_depth=abi.GR_Q, mailbox_depth=abi.GR_C, device=device,
                          max_entry_size=max_entry_size)

@@ -87,7 +87,10 @@ class Topology:
         return slot * self.G + peer % self.G, peer // self.G
 
     def route_messages(self, out):
-        """Outbox records (peer = sender, slot = target) -> inbox records of the next pass."""
+        """Outbox records (peer = sender, slot = target) -> inbox records of the next pass.
+        Records addressed outside the group (no remote slot) are dropped, as a
+        transport drops messages to an unknown node."""
+        out = out[out["slot"] < self.R]
         nxt = out.copy()
         dp, ds = self.dest(out["peer"], out["slot"])
         nxt["peer"] = dp.astype(np.uint32)

@@ -157,3 +157,15 @@ extern "C" int hl_detect_affine(const uint32_t* in_pos, const uint32_t* out_pos,
   if (!detect_affine_routes(in_pos, out_pos, n, S, base, g, &r)) return 0;
   return is_loopback(base, *g, r, S) ? 2 : 1;
 }
+
+// per-branch hit counts of the lane code run here (built with GR_COVERAGE; gr_cover.h)
+extern "C" int hl_coverage(uint64_t* out, uint32_t n) {
+  if (!out || n < CV_N) return -1;
+  for (uint32_t k = 0; k < CV_N; ++k) out[k] = gr_cover_host[k];
+  return (int)CV_N;
+}
+extern "C" const char* hl_coverage_names() {
+#define GR_COVER_NAME(x) #x ","
+  return GR_COVER_IDS(GR_COVER_NAME);
+#undef GR_COVER_NAME
+}

@@ -6,7 +6,9 @@ Escalation protocol (what the Go host does in production): a group that
 escalates at item i keeps the device's state after items < i; the host runs
 items >= i with the reference code and reloads the group. Here the oracle plays
 the host: its prefix snapshot is compared with the device, its full-pass state
-is what both sides continue from, and its full message list is routed.
+is what both sides continue from, and its full message list is routed. Every
+escalation must be one the oracle's own execution of that item justifies
+(parity.check_escalations).
 
 A peer whose full state no longer fits a gr_peer record (e.g. more than GR_Q
 pending ReadIndex requests) is "parked": the host steps it alone (the engine
@@ -22,12 +24,13 @@ import parity
 
 
 class HostlaneBackend:
-    def __init__(self, peers, slots):
+    def __init__(self, peers, slots, max_entry_size=abi.MAX_ENTRY_SIZE):
         self.state = np.array(peers, abi.PEER, copy=True)
         self.slots = slots
+        self.max_entry_size = max_entry_size
 
     def step(self, msgs, loc):
-        self.state, out, res = hostlane_step(self.state, msgs, loc, self.slots)
+        self.state, out, res = hostlane_step(self.state, msgs, loc, self.slots, self.max_entry_size)
         return out, res
 
     def sync(self):
@@ -36,11 +39,19 @@ class HostlaneBackend:
     def load(self, idx, recs):
         self.state[idx] = recs
 
+    def notify_applied(self, idx, applied):
+        self.state["applied"][idx] = applied
+
+    def close(self):
+        pass
+
 
 class GpuBackend:
-    def __init__(self, peers, slots):
+    lib_path = None  # a different build of libgpuraft (e.g. the coverage build)
+
+    def __init__(self, peers, slots, max_entry_size=abi.MAX_ENTRY_SIZE):
         from dragonboat_amd.engine import Engine
-        self.eng = Engine(len(peers), slots)
+        self.eng = Engine(len(peers), slots, max_entry_size=max_entry_size, lib_path=self.lib_path)
         self.eng.load(peers)
         self.n = len(peers)
 
@@ -53,78 +64,154 @@ class GpuBackend:
     def load(self, idx, recs):
         self.eng.load_peers(np.asarray(idx, np.uint32), np.asarray(recs, abi.PEER))  # one call, scattered slots
 
+    def notify_applied(self, idx, applied):
+        self.eng.notify_applied(np.asarray(idx, np.uint32), np.asarray(applied, np.uint64))
 
-def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, check=True,
-             max_report=3, drop_fn=None, threads=None, extra_fn=None):
-    """Run `passes` passes; returns a dict of counters. Raises AssertionError on divergence.
+    def close(self):
+        self.eng.close()
 
-    inject_fn(k, state) -> changed slots (state edited in place, reloaded on both sides);
-    extra_fn(k, state) -> gr_message records appended to pass k's inbox (local
-    messages such as LeaderTransfer, or messages from outside the population)."""
-    pop = OraclePopulation(peers, slots)
-    eng = backend(peers, slots)
-    n = len(peers)
-    msgs = np.zeros(0, abi.MESSAGE)
-    stats = {"msgs": 0, "escalations": 0, "esc_reasons": {}, "commits": 0, "ready": 0, "forwarded": 0}
-    parked = np.zeros(n, bool)
-    for k in range(passes):
-        if inject_fn is not None:
-            cur = pop.export()
-            changed = inject_fn(k, cur)
-            if changed is not None and len(changed):
-                pop.reload(changed, cur[changed])
-                eng.load(changed, cur[changed])
-        # locals_fn(k) or locals_fn(k, state): the second form sees the pass's
-        # starting state (e.g. to propose on the current leaders)
-        loc = locals_fn(k, pop.export()) if locals_fn.__code__.co_argcount == 2 else locals_fn(k)
-        if extra_fn is not None:
-            ext = extra_fn(k, pop.export())
-            if ext is not None and len(ext):
-                msgs = np.concatenate([msgs, np.asarray(ext, abi.MESSAGE)])
-        dev0 = eng.sync() if check else None
-        before = dev0["committed"] if check else None
+
+def _threads():
+    return min(16, os.cpu_count() or 1)
+
+
+class Lockstep:
+    """The engine and the oracle stepped pass by pass on identical inputs.
+
+    step(msgs, loc) runs one pass over inbox records `msgs` (receiver peer,
+    sender slot) and local inputs `loc` on both sides, checks state, messages,
+    results and escalations, reloads escalated peers from the oracle (the host's
+    role) and returns (oracle outbox records, engine results). The oracle's full
+    outbox is what the network delivers next."""
+
+    def __init__(self, backend, peers, slots, max_entry_size=abi.MAX_ENTRY_SIZE, check=True, max_report=3,
+                 allow_error=False):
+        self.pop = OraclePopulation(peers, slots, max_entry_size=max_entry_size)
+        self.eng = backend(peers, slots, max_entry_size=max_entry_size)
+        self.n = len(peers)
+        self.slots = slots
+        self.check = check
+        self.max_report = max_report
+        self.allow_error = allow_error  # reference panics (and records the network cannot carry) tolerated
+        self.errors = 0
+        self.parked = np.zeros(self.n, bool)
+        self.k = 0
+        self.stats = {"msgs": 0, "escalations": 0, "esc_reasons": {}, "commits": 0, "ready": 0, "forwarded": 0,
+                      "parked": 0}
+        self.last_out = np.zeros(0, abi.MESSAGE)  # the engine's outbox of the last pass (device prefix)
+        self.last_ready = {}                      # peer -> [(index, ctx_low, ctx_high)] of the last pass
+
+    def export(self):
+        return self.pop.export()
+
+    def reload(self, idx, recs):
+        """Host-side state edits (fault injection): both sides."""
+        idx = np.asarray(idx, np.int64)
+        if len(idx):
+            self.pop.reload(idx, recs)
+            self.eng.load(idx, recs)
+
+    def apply_all(self):
+        """The host applies what is committed (node.handleEvents ->
+        Peer.NotifyRaftLastApplied, peer.go:282-284): raft.applied = committed."""
+        self.pop.commit_all()
+        cur = self.pop.export()
+        keep = np.nonzero(~self.parked)[0]
+        self.eng.notify_applied(keep, cur["committed"][keep])
+
+    def step(self, msgs, loc):
+        msgs = np.zeros(0, abi.MESSAGE) if msgs is None else np.asarray(msgs, abi.MESSAGE)
+        loc = np.zeros(0, abi.LOCAL) if loc is None else np.asarray(loc, abi.LOCAL)
+        st, parked = self.stats, self.parked
+        dev0 = self.eng.sync() if self.check else None
+        before = dev0["committed"] if self.check else None
         emsgs = msgs[~parked[msgs["peer"]]] if len(msgs) else msgs
-        eloc = loc[~parked[loc["peer"]]]
-        out, res = eng.step(emsgs, eloc)
+        eloc = loc[~parked[loc["peer"]]] if len(loc) else loc
+        out, res = self.eng.step(emsgs, eloc)
         if len(out):  # the engine's outbox is valid gr_step input (gr_host.h validate_msg)
             nr, ne = out["n_runs"], out["n_entries"]
             assert np.all(nr <= 2) and np.all((ne == 0) == (nr == 0)), "invalid outbox record"
             assert np.all(out["type"] <= abi.TIMEOUT_NOW)
-        lim = parity.limits_from(res, n)
-        o = pop.step(msgs, loc, lim, threads=threads or min(16, os.cpu_count() or 1), dev_before=dev0)
+        lim = parity.limits_from(res, self.n)
+        o = self.pop.step(msgs, loc, lim, threads=_threads(), dev_before=dev0, allow_error=self.allow_error)
+        self.errors += bool(o["error"])
         esc = res[res["escalation"] != 0]
-        stats["ready"] += int(res["n_ready"].sum())
-        stats["forwarded"] += int(res["n_forwarded"].sum())
-        stats["escalations"] += len(esc)
+        st["ready"] += int(res["n_ready"].sum())
+        st["forwarded"] += int(res["n_forwarded"].sum())
+        st["escalations"] += len(esc)
         for r in esc:
             nm = abi.ESC_NAMES[r["escalation"]]
-            stats["esc_reasons"][nm] = stats["esc_reasons"].get(nm, 0) + 1
-        stats["msgs"] += len(msgs)
-        if check:
-            dev = eng.sync()
+            st["esc_reasons"][nm] = st["esc_reasons"].get(nm, 0) + 1
+        st["msgs"] += len(msgs)
+        if self.check:
+            dev = self.eng.sync()
             keep = np.nonzero(~parked)[0]
-            bad_s = parity.compare_states(dev, o["mid"], slots, peers=keep)
+            bad_s = parity.compare_states(dev, o["mid"], self.slots, peers=keep)
             om = parity.prefix_msgs(o, lim)
             bad_m = parity.compare_msgs(out, om[~parked[om["peer"]]])
             bad_r = parity.compare_results(res, o["results"])
             bad_e = parity.check_escalations(res, o["esc_mask"])
             if bad_s or bad_m or bad_r or bad_e:
+                mr = self.max_report
                 raise AssertionError(
-                    f"pass {k}: state {bad_s[:max_report]} msgs {bad_m[:max_report]} results {bad_r[:max_report]}"
-                    f" unjustified escalations {bad_e[:max_report]}")
-            stats["commits"] += int(np.sum(dev["committed"] > before))
-        full = pop.export()
-        fits = pop.representable()
-        reload = np.zeros(n, bool)
+                    f"pass {self.k}: state {bad_s[:mr]} msgs {bad_m[:mr]} results {bad_r[:mr]}"
+                    f" unjustified escalations {bad_e[:mr]}")
+            st["commits"] += int(np.sum(dev["committed"] > before))
+        self.last_out = out
+        # ReadyToRead of the whole pass (device prefix + host suffix): the oracle's
+        self.last_ready = {}
+        for p in np.nonzero(o["results"]["n_ready"])[0]:
+            r = o["results"][p]
+            self.last_ready[int(p)] = [tuple(int(x) for x in r["ready"][q]) for q in range(min(int(r["n_ready"]),
+                                                                                                abi.GR_Q))]
+        full = self.pop.export()
+        fits = self.pop.representable()
+        reload = np.zeros(self.n, bool)
         reload[esc["peer"].astype(np.int64)] = True
         reload |= parked & fits  # back on the device
-        parked = ~fits
-        stats["parked"] = stats.get("parked", 0) + int(parked.sum())
+        self.parked = ~fits
+        st["parked"] += int(self.parked.sum())
         idx = np.nonzero(reload & fits)[0]
         if len(idx):
-            eng.load(idx, full[idx])
-        msgs = topo.route_messages(o["msgs"])
-        if drop_fn is not None:
-            msgs = drop_fn(k, msgs)
-    stats["final"] = pop.export()
-    return stats
+            self.eng.load(idx, full[idx])
+        self.k += 1
+        return o["msgs"], res
+
+    def close(self):
+        self.eng.close()
+
+
+def simulate(backend, peers, topo, passes, locals_fn, slots=3, inject_fn=None, check=True,
+             max_report=3, drop_fn=None, threads=None, extra_fn=None, max_entry_size=abi.MAX_ENTRY_SIZE,
+             allow_error=False):
+    """Run `passes` passes; returns a dict of counters. Raises AssertionError on divergence.
+
+    inject_fn(k, state) -> changed slots (state edited in place, reloaded on both sides);
+    extra_fn(k, state) -> gr_message records appended to pass k's inbox (local
+    messages such as LeaderTransfer, or messages from outside the population)."""
+    ls = Lockstep(backend, peers, slots, max_entry_size=max_entry_size, check=check, max_report=max_report,
+                  allow_error=allow_error)
+    msgs = np.zeros(0, abi.MESSAGE)
+    try:
+        for k in range(passes):
+            if inject_fn is not None:
+                cur = ls.export()
+                changed = inject_fn(k, cur)
+                if changed is not None and len(changed):
+                    ls.reload(changed, cur[changed])
+            # locals_fn(k) or locals_fn(k, state): the second form sees the pass's
+            # starting state (e.g. to propose on the current leaders)
+            loc = locals_fn(k, ls.export()) if locals_fn.__code__.co_argcount == 2 else locals_fn(k)
+            if extra_fn is not None:
+                ext = extra_fn(k, ls.export())
+                if ext is not None and len(ext):
+                    msgs = np.concatenate([msgs, np.asarray(ext, abi.MESSAGE)])
+            out, _ = ls.step(msgs, loc)
+            msgs = topo.route_messages(out)
+            if drop_fn is not None:
+                msgs = drop_fn(k, msgs)
+        ls.stats["final"] = ls.export()
+        ls.stats["oracle_errors"] = ls.errors
+        return ls.stats
+    finally:
+        ls.close()
