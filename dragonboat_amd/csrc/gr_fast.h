@@ -41,9 +41,11 @@ struct FastLane {
   const StepParams& kp;
   const uint32_t i, p;
   // core
+  uint64_t hdr = 0;  // the header word as loaded (gr_layout.h)
   uint32_t state = 0, self = 0, nruns = 0;
   uint64_t term = 0, committed = 0, committed0 = 0, hi = 0, hi0 = 0;
   uint64_t rsn = 0, rtn = 0;  // newest term run (start, term)
+  uint64_t rsn0 = 0, rtn0 = 0;  // ... as loaded (moves one row down when a run is pushed)
   bool pushed = false;        // a run was appended this pass (row nruns-1)
   bool ok = true;             // still on the steady-state path
   // leader remotes
@@ -68,7 +70,7 @@ struct FastLane {
   GF_HD uint8_t& s8(uint32_t row) const { return kp.st.u8(row)[p]; }
 
   // entryLog.term (logentry.go:141-157) when the answer is in the newest run.
-  // The lane only runs with NR_GE_LO (newest run start >= firstIndex-1), so
+  // The lane only runs with H_GE_LO (newest run start >= firstIndex-1), so
   // x >= rsn is inside [firstIndex-1, lastIndex]; anything below the newest
   // run (an older run, or below firstIndex-1) hands the lane over.
   GF_HD uint64_t term_of(uint64_t x) {
@@ -76,10 +78,12 @@ struct FastLane {
     GF_BAIL(nruns == 0 || x < rsn);
     return rtn;
   }
-  // win_push (gr_lane.h) for one new run per pass, no window shift.
+  // win_push (gr_lane.h) for one new run per pass onto a window of at most one
+  // run: the right-aligned rows then move only the old newest run down one row
+  // (a longer window would shift every run: the general lane does that).
   GF_HD void win_push(uint64_t start, uint64_t t) {
     if (nruns > 0 && rtn == t) return;
-    GF_BAIL(pushed || nruns >= (uint32_t)GR_K);
+    GF_BAIL(pushed || nruns >= 2);
     rsn = start;
     rtn = t;
     nruns++;
@@ -173,7 +177,7 @@ struct FastLane {
     uint32_t n = 0;
     if (nx <= hi) {
       // nx <= rsn covers entries in an older run and nx <= firstIndex-1
-      // (InstallSnapshot path): with NR_GE_LO, nx > rsn implies nx > firstIndex-1
+      // (InstallSnapshot path): with H_GE_LO, nx > rsn implies nx > firstIndex-1
       GF_BAIL(nruns == 0 || nx <= rsn);
       GF_BAIL(hi - nx + 1 > 1);         // several entries: MaxEntrySize check
       GF_BAIL(rst[j] != GR_REPLICATE_ST && rst[j] != GR_RETRY);
@@ -262,15 +266,18 @@ struct FastLane {
 
   // ------------------------------------------------------------- step
   GF_HD bool step(LaneStats* ls) {
-    // ---- round 1: core, locals, routes
-    state = ntld(s8(Rw::B_STATE));
-    self = ntld(s8(Rw::B_SELF));
-    const uint32_t nbyte = ntld(s8(Rw::B_NRUNS));
-    nruns = nbyte & NR_MASK;
+    // ---- round 1: core (one header word), the newest run (a fixed row), locals, routes
+    hdr = ntld(s64(SR_HDR));
+    state = h_state(hdr);
+    self = h_self(hdr);
+    nruns = h_nruns(hdr);
+    const bool gelo = h_gelo(hdr);
     term = ntld(s64(SR_TERM));
     committed = ntld(s64(SR_COMMITTED));
     hi = ntld(s64(SR_LAST_INDEX));
-    const uint32_t flags = ntld(s8(Rw::B_FLAGS));
+    rsn0 = ntld(s64(SR_RUN_START + GR_K - 1));  // meaningful when nruns > 0
+    rtn0 = ntld(s64(SR_RUN_TERM + GR_K - 1));
+    const uint32_t flags = h_flags(hdr);
     const uint32_t lw = kp.has_locals ? ntld(kp.ln.u32(LR_LWORD)[i]) : 0u;  // packed locals (gr_layout.h)
     uint32_t gin[S];
 #pragma unroll
@@ -289,8 +296,8 @@ struct FastLane {
       allc |= (b & MB_ALLCOMPACT) ? (1u << j) : 0u;
     }
     if (nruns) {
-      rsn = ntld(s64(SR_RUN_START + nruns - 1));
-      rtn = ntld(s64(SR_RUN_TERM + nruns - 1));
+      rsn = rsn0;
+      rtn = rtn0;
     }
     const bool leader = state == GR_LEADER;
     const uint32_t np = lw & 0xFFFFu;
@@ -298,13 +305,14 @@ struct FastLane {
     uint64_t etick = 0;
     if (nq) etick = ntld(s64(SR_ETICK));
     if (kLeaderPath && leader) {
+      const uint64_t rb = h_rb(hdr);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         match[j] = ntld(s64(Rw::MATCH + j));
         next[j] = ntld(s64(Rw::NEXT + j));
-        rst[j] = ntld(s8(Rw::B_RSTATE + j)) & 3u;
-        ract[j] = ntld(s8(Rw::B_RACTIVE + j)) & 1u;
-        rkind[j] = ntld(s8(Rw::B_RKIND + j)) & 3u;
+        rst[j] = rb_state(rb, j);
+        ract[j] = rb_active(rb, j);
+        rkind[j] = rb_kind(rb, j);
       }
     }
     // ---- round 3: message fields
@@ -378,7 +386,7 @@ struct FastLane {
       if (!ok) return false;
       etick += nq;
       ntst(s64(SR_ETICK), (uint64_t)(etick));
-      if (flags & F_ETZ) ntst(s8(Rw::B_FLAGS), (uint8_t)((flags & ~F_ETZ)));
+      if (flags & F_ETZ) ntst(s64(SR_HDR), hdr & ~((uint64_t)F_ETZ << H_FLAGS_SHIFT));
 #pragma unroll
       for (int j = 0; j < S; ++j)
         if (gout[j] != NOPOS) ntst(kp.out.at(gout[j]).cnt(), (uint8_t)(0));
@@ -389,7 +397,7 @@ struct FastLane {
     GF_BAIL(!leader && state != GR_FOLLOWER);
     GF_BAIL(np && !leader);
     GF_BAIL(!kLeaderPath && leader && any_input);
-    GF_BAIL(any_input && !(nbyte & NR_GE_LO));  // the window test needs firstIndex-1
+    GF_BAIL(any_input && !gelo);  // the window test needs firstIndex-1
     committed0 = committed;
     hi0 = hi;
     if (kLeaderPath && leader) {
@@ -445,12 +453,20 @@ struct FastLane {
     // ---- stores (nothing above this line has written state)
     if (committed != committed0) ntst(s64(SR_COMMITTED), (uint64_t)(committed));
     if (hi != hi0) ntst(s64(SR_LAST_INDEX), (uint64_t)(hi));
-    if (pushed) {  // the new run starts above the old newest run: NR_GE_LO still holds
-      ntst(s64(SR_RUN_START + nruns - 1), (uint64_t)(rsn));
-      ntst(s64(SR_RUN_TERM + nruns - 1), (uint64_t)(rtn));
-      ntst(s8(Rw::B_NRUNS), (uint8_t)((nruns | NR_GE_LO)));
+    uint64_t nh = hdr;  // the header word, rewritten once if anything in it changed
+    if (pushed) {
+      // right-aligned window: the old newest run moves one row down, the new one
+      // takes the last row; it starts above the old newest run, so H_GE_LO holds
+      if (nruns > 1) {
+        ntst(s64(SR_RUN_START + GR_K - 2), rsn0);
+        ntst(s64(SR_RUN_TERM + GR_K - 2), rtn0);
+      }
+      ntst(s64(SR_RUN_START + GR_K - 1), (uint64_t)(rsn));
+      ntst(s64(SR_RUN_TERM + GR_K - 1), (uint64_t)(rtn));
+      nh = (nh & ~(7ull << H_NRUNS_SHIFT)) | ((uint64_t)nruns << H_NRUNS_SHIFT) | (1ull << H_GE_LO_BIT);
     }
     if (kLeaderPath && leader) {
+      uint64_t rb = h_rb(nh);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         if ((mdirty >> j) & 1u) {
@@ -458,10 +474,11 @@ struct FastLane {
           ntst(s64(Rw::NEXT + j), (uint64_t)(next[j]));
         }
         if ((sdirty >> j) & 1u) {
-          ntst(s8(Rw::B_RSTATE + j), (uint8_t)(rst[j]));
-          ntst(s8(Rw::B_RACTIVE + j), (uint8_t)(ract[j]));
+          rb = rb_with(rb, j, 0, 2, rst[j]);
+          rb = rb_with(rb, j, 2, 1, ract[j]);
         }
       }
+      nh = (nh & ((1ull << H_REM_SHIFT) - 1)) | (rb << H_REM_SHIFT);
 #pragma unroll
       for (int j = 0; j < S; ++j)
         if ((snapz >> j) & 1u) ntst(s64(Rw::SNAP + j), (uint64_t)(0));
@@ -475,8 +492,9 @@ struct FastLane {
         ntst(s64(SR_LEADER_ID), (uint64_t)(rid));  // setLeaderID(m.From)
         nf = (nf & ~F_LSLOT) | ((L + 1) << F_LSLOT_SHIFT);
       }
-      if (nf != flags) ntst(s8(Rw::B_FLAGS), (uint8_t)(nf));
+      nh = (nh & ~(0xFFull << H_FLAGS_SHIFT)) | ((uint64_t)nf << H_FLAGS_SHIFT);
     }
+    if (nh != hdr) ntst(s64(SR_HDR), nh);
 #pragma unroll
     for (int j = 0; j < S; ++j)
       if (gout[j] != NOPOS)
@@ -519,7 +537,7 @@ struct FastLane {
     }
     uint64_t ci = 0;
     if (n) {  // getConflictIndex over the newest run (logentry.go:305-312)
-      const uint64_t a = li + 1, b = li + n;  // a >= rsn >= firstIndex-1 below (NR_GE_LO)
+      const uint64_t a = li + 1, b = li + n;  // a >= rsn >= firstIndex-1 below (H_GE_LO)
       if (a <= hi) {
         GF_BAIL(nruns == 0 || a < rsn);
         if (rtn != rt0) ci = a;

@@ -15,16 +15,55 @@ namespace host {
 
 // Row accessors between gr_peer and the SoA state rows (also run by the
 // load/sync passes of gr_io.h on the device).
+// The header word of a record (gr_layout.h): small fields plus the device bits.
+__host__ __device__ inline uint64_t header_of(const gr_peer& g, uint32_t S) {
+  uint32_t sl = 0;
+  for (uint32_t j = 0; j < S && j < 7 && g.leader_id; ++j)
+    if (!sl && g.remote_id[j] == g.leader_id) sl = j + 1;
+  const uint32_t flags = (g.flags & F_PUBLIC) | (g.leader_transfer_target ? F_LTT : 0u) |
+                         (g.election_tick == 0 ? F_ETZ : 0u) | (sl << F_LSLOT_SHIFT);
+  const uint32_t n = g.n_runs <= GR_K ? g.n_runs : GR_K;
+  const bool gelo = n && g.run_start[n - 1] >= g.first_index_m1;
+  uint64_t rb = 0;
+  for (uint32_t j = 0; j < S; ++j)
+    rb |= (uint64_t)((g.remotes[j].state & 3u) | ((g.remotes[j].active & 1u) << 2) | ((g.remotes[j].kind & 3u) << 3))
+          << (5 * j);
+  return h_make(g.state, g.self_slot, n, gelo, flags, g.read_index_count, rb);
+}
+__host__ __device__ inline void set_header(gr_peer& g, uint32_t S, uint64_t h) {
+  g.state = (uint8_t)h_state(h);
+  g.self_slot = (uint8_t)h_self(h);
+  g.n_runs = (uint8_t)h_nruns(h);
+  g.flags = (uint8_t)(h_flags(h) & F_PUBLIC);
+  g.read_index_count = (uint8_t)h_ric(h);
+  const uint64_t rb = h_rb(h);
+  for (uint32_t j = 0; j < S; ++j) {
+    g.remotes[j].state = (uint8_t)rb_state(rb, j);
+    g.remotes[j].active = (uint8_t)rb_active(rb, j);
+    g.remotes[j].kind = (uint8_t)rb_kind(rb, j);
+  }
+}
+
+// Rows are converted in ascending order: SR_HDR (which carries n_runs) comes
+// before the right-aligned run rows that need it.
 __host__ __device__ inline uint64_t get_u64_row(const gr_peer& g, uint32_t row, uint32_t S) {
-  if (row < SR_RUN_START) {
+  if (row < SR_HDR) {
     const uint64_t v[] = {g.term, g.vote, g.committed, g.applied, g.last_index, g.first_index_m1,
                           g.leader_id, g.leader_transfer_target, g.node_id, g.election_tick,
                           g.heartbeat_tick, g.randomized_election_timeout, g.election_timeout,
                           g.heartbeat_timeout, g.entry_size_ub};
     return v[row];
   }
-  if (row < SR_RUN_TERM) return g.run_start[row - SR_RUN_START];
-  if (row < SR_REMOTE) return g.run_term[row - SR_RUN_TERM];
+  if (row == SR_HDR) return header_of(g, S);
+  const uint32_t n = g.n_runs <= GR_K ? g.n_runs : GR_K;
+  if (row < SR_RUN_TERM) {
+    const int k = (int)(row - SR_RUN_START) - (int)(GR_K - n);
+    return k >= 0 ? g.run_start[k] : 0;
+  }
+  if (row < SR_REMOTE) {
+    const int k = (int)(row - SR_RUN_TERM) - (int)(GR_K - n);
+    return k >= 0 ? g.run_term[k] : 0;
+  }
   uint32_t r = row - SR_REMOTE;
   if (r < S) return g.remotes[r].match;
   r -= S;
@@ -41,7 +80,7 @@ __host__ __device__ inline uint64_t get_u64_row(const gr_peer& g, uint32_t row, 
   return g.read_index[r].ctx_high;
 }
 __host__ __device__ inline void set_u64_row(gr_peer& g, uint32_t row, uint32_t S, uint64_t v) {
-  if (row < SR_RUN_START) {
+  if (row < SR_HDR) {
     uint64_t* f[] = {&g.term, &g.vote, &g.committed, &g.applied, &g.last_index, &g.first_index_m1,
                      &g.leader_id, &g.leader_transfer_target, &g.node_id, &g.election_tick,
                      &g.heartbeat_tick, &g.randomized_election_timeout, &g.election_timeout,
@@ -49,8 +88,18 @@ __host__ __device__ inline void set_u64_row(gr_peer& g, uint32_t row, uint32_t S
     *f[row] = v;
     return;
   }
-  if (row < SR_RUN_TERM) { g.run_start[row - SR_RUN_START] = v; return; }
-  if (row < SR_REMOTE) { g.run_term[row - SR_RUN_TERM] = v; return; }
+  if (row == SR_HDR) { set_header(g, S, v); return; }
+  const uint32_t n = g.n_runs <= GR_K ? g.n_runs : GR_K;  // set by the SR_HDR row before
+  if (row < SR_RUN_TERM) {
+    const int k = (int)(row - SR_RUN_START) - (int)(GR_K - n);
+    if (k >= 0) g.run_start[k] = v;
+    return;
+  }
+  if (row < SR_REMOTE) {
+    const int k = (int)(row - SR_RUN_TERM) - (int)(GR_K - n);
+    if (k >= 0) g.run_term[k] = v;
+    return;
+  }
   uint32_t r = row - SR_REMOTE;
   if (r < S) { g.remotes[r].match = v; return; }
   r -= S;
@@ -66,52 +115,14 @@ __host__ __device__ inline void set_u64_row(gr_peer& g, uint32_t row, uint32_t S
   r -= GR_Q;
   g.read_index[r].ctx_high = v;
 }
-// u8 rows: state flags self n_runs ri_count, rstate[S], ractive[S], rkind[S], rifrom[Q], riack[Q]
-__host__ __device__ inline uint8_t get_u8_row(const gr_peer& g, uint32_t row, uint32_t S) {
-  switch (row) {
-    case 0: return g.state;
-    case 1: {
-      uint32_t sl = 0;
-      for (uint32_t j = 0; j < S && j < 7 && g.leader_id; ++j)
-        if (!sl && g.remote_id[j] == g.leader_id) sl = j + 1;
-      return (uint8_t)((g.flags & F_PUBLIC) | (g.leader_transfer_target ? F_LTT : 0u) |
-                       (g.election_tick == 0 ? F_ETZ : 0u) | (sl << F_LSLOT_SHIFT));
-    }
-    case 2: return g.self_slot;
-    case 3:
-      return (uint8_t)(g.n_runs | (g.n_runs && g.n_runs <= GR_K && g.run_start[g.n_runs - 1] >= g.first_index_m1
-                                       ? NR_GE_LO : 0u));
-    case 4: return g.read_index_count;
-  }
-  uint32_t r = row - 5;
-  if (r < S) return g.remotes[r].state;
-  r -= S;
-  if (r < S) return g.remotes[r].active;
-  r -= S;
-  if (r < S) return g.remotes[r].kind;
-  r -= S;
-  if (r < GR_Q) return g.read_index[r].from_slot;
-  r -= GR_Q;
-  return g.read_index[r].ack_bits;
+// u8 rows: rifrom[Q], riack[Q]
+__host__ __device__ inline uint8_t get_u8_row(const gr_peer& g, uint32_t row, uint32_t) {
+  if (row < GR_Q) return g.read_index[row].from_slot;
+  return g.read_index[row - GR_Q].ack_bits;
 }
-__host__ __device__ inline void set_u8_row(gr_peer& g, uint32_t row, uint32_t S, uint8_t v) {
-  switch (row) {
-    case 0: g.state = v; return;
-    case 1: g.flags = (uint8_t)(v & F_PUBLIC); return;
-    case 2: g.self_slot = v; return;
-    case 3: g.n_runs = (uint8_t)(v & NR_MASK); return;
-    case 4: g.read_index_count = v; return;
-  }
-  uint32_t r = row - 5;
-  if (r < S) { g.remotes[r].state = v; return; }
-  r -= S;
-  if (r < S) { g.remotes[r].active = v; return; }
-  r -= S;
-  if (r < S) { g.remotes[r].kind = v; return; }
-  r -= S;
-  if (r < GR_Q) { g.read_index[r].from_slot = v; return; }
-  r -= GR_Q;
-  g.read_index[r].ack_bits = v;
+__host__ __device__ inline void set_u8_row(gr_peer& g, uint32_t row, uint32_t, uint8_t v) {
+  if (row < GR_Q) g.read_index[row].from_slot = v;
+  else g.read_index[row - GR_Q].ack_bits = v;
 }
 
 __host__ __device__ inline int validate_msg(const gr_message& m, uint32_t S, uint32_t cap) {

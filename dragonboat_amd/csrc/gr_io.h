@@ -238,11 +238,10 @@ __global__ void set_row_u64(StateBase st, uint32_t row, const uint32_t* slots, c
 // gr_compact_log: LogReader.Compact(index) (logreader.go:251-269) mirrored into
 // entryLog.firstIndex()-1 (logentry.go:97-104). status: 0 ok, 1 ErrCompacted
 // (index below firstIndex-1), 2 ErrUnavailable (index past lastIndex); only ok
-// slots are written. NR_GE_LO follows the new firstIndex-1.
+// slots are written. H_GE_LO follows the new firstIndex-1.
 template <int S>
 __global__ void compact_rows(StateBase st, const uint32_t* slots, const uint64_t* idx, uint32_t n, int32_t* status,
                              uint32_t* refused) {
-  using R = Rows<S>;
   for (uint32_t x = io_tid(); x < n; x += io_stride()) {
     const uint32_t p = slots[x];
     const uint64_t i = idx[x], lo = st.u64(SR_LO)[p], last = st.u64(SR_LAST_INDEX)[p];
@@ -256,30 +255,52 @@ __global__ void compact_rows(StateBase st, const uint32_t* slots, const uint64_t
     // The window forgets what the reference compacted away: runs wholly below
     // firstIndex-1 drop out and the run covering it starts there (term(i) is
     // LogReader's markerTerm), so the window never claims a term below it.
-    uint32_t nr = st.u8(R::B_NRUNS)[p] & NR_MASK;
+    const uint64_t h = st.u64(SR_HDR)[p];
+    uint32_t nr = h_nruns(h);
     if (nr > GR_K) nr = GR_K;
-    uint64_t rs[GR_K], rt[GR_K];
+    uint64_t rs[GR_K], rt[GR_K];  // oldest first
 #pragma unroll
     for (int k = 0; k < GR_K; ++k) {
-      rs[k] = st.u64(SR_RUN_START + k)[p];
-      rt[k] = st.u64(SR_RUN_TERM + k)[p];
+      const bool v = (uint32_t)k < nr;
+      rs[k] = v ? st.u64(SR_RUN_START + run_row(nr, k))[p] : 0;
+      rt[k] = v ? st.u64(SR_RUN_TERM + run_row(nr, k))[p] : 0;
     }
     uint32_t first = 0;  // last run starting at or below i
 #pragma unroll
     for (int k = 1; k < GR_K; ++k)
       if ((uint32_t)k < nr && rs[k] <= i) first = k;
-    if (nr && rs[first] <= i) {
+    uint32_t nn = nr;
+    uint64_t ns[GR_K], nt[GR_K];
+#pragma unroll
+    for (int k = 0; k < GR_K; ++k) {
+      ns[k] = rs[k];
+      nt[k] = rt[k];
+    }
+    if (nr && rs[first] <= i) {  // drop runs [0, first), the covering run starts at i
+      nn = nr - first;
 #pragma unroll
       for (int k = 0; k < GR_K; ++k) {
-        const uint32_t from = k + first;
-        const bool keep = from < nr;
-        st.u64(SR_RUN_START + k)[p] = keep ? (k == 0 ? i : rs[from < GR_K ? from : 0]) : 0;
-        st.u64(SR_RUN_TERM + k)[p] = keep ? rt[from < GR_K ? from : 0] : 0;
+        uint64_t a = 0, b = 0;
+#pragma unroll
+        for (int d = 0; d < GR_K; ++d)
+          if ((uint32_t)d == (uint32_t)k + first) { a = rs[d]; b = rt[d]; }
+        ns[k] = k == 0 ? i : a;
+        nt[k] = b;
       }
-      nr -= first;
+#pragma unroll
+      for (int k = 0; k < GR_K; ++k) {
+        if ((uint32_t)k < nn) {
+          st.u64(SR_RUN_START + run_row(nn, k))[p] = ns[k];
+          st.u64(SR_RUN_TERM + run_row(nn, k))[p] = nt[k];
+        }
+      }
     }
-    const bool ge = nr && st.u64(SR_RUN_START + nr - 1)[p] >= i;
-    st.u8(R::B_NRUNS)[p] = (uint8_t)(nr | (ge ? NR_GE_LO : 0u));
+    uint64_t newest = 0;
+#pragma unroll
+    for (int k = 0; k < GR_K; ++k)
+      if ((uint32_t)k + 1 == nn) newest = ns[k];
+    const bool ge = nn && newest >= i;
+    st.u64(SR_HDR)[p] = h_make(h_state(h), h_self(h), nn, ge, h_flags(h), h_ric(h), h_rb(h));
   }
 }
 

@@ -74,14 +74,7 @@ struct InMsg {
   uint64_t term, log_index, log_term, commit, hint, hint_high, rt0, rt1;
 };
 
-// Per-slot small fields packed 5 bits per slot: state(2) active(1) kind(2).
-GR_HD uint32_t rb_state(uint64_t rb, uint32_t j) { return (uint32_t)(rb >> (5 * j)) & 3u; }
-GR_HD uint32_t rb_active(uint64_t rb, uint32_t j) { return (uint32_t)(rb >> (5 * j + 2)) & 1u; }
-GR_HD uint32_t rb_kind(uint64_t rb, uint32_t j) { return (uint32_t)(rb >> (5 * j + 3)) & 3u; }
-GR_HD uint64_t rb_with(uint64_t rb, uint32_t j, uint32_t off, uint32_t width, uint32_t v) {
-  const uint64_t m = ((1ull << width) - 1) << (5 * j + off);
-  return (rb & ~m) | (((uint64_t)v << (5 * j + off)) & m);
-}
+// Per-slot small fields packed 5 bits per slot (state, active, kind): rb_* in gr_layout.h.
 
 // The general lane: every handler of the device path. The steady-state
 // subset runs first in the lean lane of gr_fast.h; this lane steps the lanes
@@ -95,6 +88,7 @@ struct Lane {
   uint32_t loaded = 0, dirty = 0;
 
   // G_CORE
+  uint64_t hdr0 = 0;  // the header word as loaded
   uint32_t state = 0, flags = 0, self = GR_SLOT_NONE;
   uint64_t term = 0, committed = 0, hi = 0;
   // G_ETICK / G_TICKS
@@ -132,12 +126,14 @@ struct Lane {
 
   // ---------------------------------------------------------------- loading
   GR_HD void need(uint32_t g) {
+    if (g & (G_WIN | G_REM | G_RI)) g |= G_CORE;  // their small fields live in the header word
     const uint32_t miss = g & ~loaded;
     if (!miss) return;
     if (miss & G_CORE) {
-      state = s8(R::B_STATE);
-      flags = s8(R::B_FLAGS);
-      self = s8(R::B_SELF);
+      hdr0 = s64(SR_HDR);
+      state = h_state(hdr0);
+      flags = h_flags(hdr0);
+      self = h_self(hdr0);
       term = s64(SR_TERM);
       committed = s64(SR_COMMITTED);
       committed0 = committed;
@@ -158,22 +154,21 @@ struct Lane {
     }
     if (miss & G_WIN) {
       lo = s64(SR_LO);
-      nruns = s8(R::B_NRUNS) & NR_MASK;
+      nruns = h_nruns(hdr0);
+      if (nruns > GR_K) nruns = GR_K;
 #pragma unroll
-      for (int r = 0; r < GR_K; ++r) {
-        rs[r] = s64(SR_RUN_START + r);
-        rt[r] = s64(SR_RUN_TERM + r);
+      for (int r = 0; r < GR_K; ++r) {  // right-aligned rows -> oldest-first registers
+        const bool v = (uint32_t)r < nruns;
+        rs[r] = v ? s64(SR_RUN_START + run_row(nruns, r)) : 0;
+        rt[r] = v ? s64(SR_RUN_TERM + run_row(nruns, r)) : 0;
       }
     }
     if (miss & G_REM) {
-      rb = 0;
+      rb = h_rb(hdr0) & ((1ull << (5 * S)) - 1);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         match[j] = s64(R::MATCH + j);
         next[j] = s64(R::NEXT + j);
-        rb |= (uint64_t)((s8(R::B_RSTATE + j) & 3u) | ((s8(R::B_RACTIVE + j) & 1u) << 2) |
-                         ((s8(R::B_RKIND + j) & 3u) << 3))
-              << (5 * j);
       }
     }
     if (miss & G_SNAP) {
@@ -181,7 +176,7 @@ struct Lane {
       for (int j = 0; j < S; ++j) snap[j] = ((snapz >> j) & 1u) ? 0 : s64(R::SNAP + j);
     }
     if (miss & G_RI) {
-      ric = s8(R::B_RIC);
+      ric = h_ric(hdr0);
       rifrom = 0;
       riack = 0;
 #pragma unroll
@@ -196,6 +191,7 @@ struct Lane {
     if (miss & G_EUB) eub = s64(SR_ENTRY_UB);
     loaded |= miss;
   }
+
 
   GR_HD void store() {
     if (dirty & (D_LTT | D_ETICK | D_LEADER)) {  // device-internal flag bits (gr_layout.h)
@@ -224,17 +220,13 @@ struct Lane {
     if (dirty & D_ETICK) s64(SR_ETICK) = etick;
     if (dirty & D_HTICK) s64(SR_HTICK) = htick;
     if (dirty & D_RETIMEOUT) s64(SR_RETIMEOUT) = retimeout;
-    if (dirty & D_STATE) s8(R::B_STATE) = (uint8_t)state;
-    if (dirty & D_FLAGS) s8(R::B_FLAGS) = (uint8_t)flags;
     if (dirty & D_WIN) {
-      uint64_t last_start = 0;
 #pragma unroll
-      for (int r = 0; r < GR_K; ++r) last_start = ((uint32_t)r + 1 == nruns) ? rs[r] : last_start;
-      s8(R::B_NRUNS) = (uint8_t)(nruns | (nruns && last_start >= lo ? NR_GE_LO : 0u));
-#pragma unroll
-      for (int r = 0; r < GR_K; ++r) {
-        s64(SR_RUN_START + r) = rs[r];
-        s64(SR_RUN_TERM + r) = rt[r];
+      for (int r = 0; r < GR_K; ++r) {  // oldest-first registers -> right-aligned rows
+        if ((uint32_t)r < nruns) {
+          s64(SR_RUN_START + run_row(nruns, r)) = rs[r];
+          s64(SR_RUN_TERM + run_row(nruns, r)) = rt[r];
+        }
       }
     }
     if (dirty & D_REM) {
@@ -242,8 +234,6 @@ struct Lane {
       for (int j = 0; j < S; ++j) {
         s64(R::MATCH + j) = match[j];
         s64(R::NEXT + j) = next[j];
-        s8(R::B_RSTATE + j) = (uint8_t)rb_state(rb, j);
-        s8(R::B_RACTIVE + j) = (uint8_t)rb_active(rb, j);
       }
     }
     if (dirty & D_SNAP) {
@@ -255,7 +245,6 @@ struct Lane {
         if ((snapz >> j) & 1u) s64(R::SNAP + j) = 0;
     }
     if (dirty & D_RI) {
-      s8(R::B_RIC) = (uint8_t)ric;
 #pragma unroll
       for (int q = 0; q < GR_Q; ++q) {
         s64(R::RI_INDEX + q) = rii[q];
@@ -264,6 +253,24 @@ struct Lane {
         s8(R::B_RIFROM + q) = (uint8_t)(rifrom >> (8 * q));
         s8(R::B_RIACK + q) = (uint8_t)(riack >> (8 * q));
       }
+    }
+    if (dirty & (D_STATE | D_FLAGS | D_WIN | D_REM | D_RI)) {  // one header word for the small fields
+      uint64_t h = hdr0;
+      const uint64_t remmask = ((1ull << (5 * S)) - 1) << H_REM_SHIFT;
+      const uint64_t keep_rem = h & (~0ull << H_REM_SHIFT) & ~remmask;  // bits above this S (none in practice)
+      uint32_t nr = h_nruns(h);
+      bool gelo = h_gelo(h);
+      if (dirty & D_WIN) {
+        uint64_t last_start = 0;
+#pragma unroll
+        for (int r = 0; r < GR_K; ++r) last_start = ((uint32_t)r + 1 == nruns) ? rs[r] : last_start;
+        nr = nruns;
+        gelo = nruns && last_start >= lo;
+      }
+      const uint64_t rbits = (dirty & D_REM) ? rb : (h_rb(h) & ((1ull << (5 * S)) - 1));
+      h = h_make(state, self, nr, gelo, flags, (dirty & D_RI) ? ric : h_ric(h), 0) | keep_rem |
+          (rbits << H_REM_SHIFT);
+      if (h != hdr0) s64(SR_HDR) = h;
     }
   }
 

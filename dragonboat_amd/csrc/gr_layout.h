@@ -5,9 +5,15 @@
 // address is base + r*8*cap + 8*p, with r a compile-time constant. The kernel
 // therefore takes one base pointer and one row stride instead of ~70 array
 // pointers (keeps the kernel argument small and in SGPRs).
-//   u64 rows: scalar fields, term-run window [GR_K] x2, remotes [S] x4,
-//             ReadIndex FIFO [GR_Q] x3
-//   u8 rows:  scalar fields, remotes [S] x3, ReadIndex FIFO [GR_Q] x2
+//   u64 rows: scalar fields, the header word, term-run window [GR_K] x2,
+//             remotes [S] x4, ReadIndex FIFO [GR_Q] x3
+//   u8 rows:  ReadIndex FIFO [GR_Q] x2 (requester slot, ack bitmap)
+// The header word packs every small field a lane tests (state, self slot,
+// window run count, flags, FIFO count, and per remote slot state/active/kind):
+// one 8-byte load instead of 5 + 3S byte loads.
+// The term-run window is right-aligned: run r (0 = oldest) of n lives in row
+// GR_K - n + r, so the newest run is always row GR_K - 1 and a lane reads it
+// without first knowing n.
 // Per-remote fields are [slot j][peer p], so a wave reading "match of slot j"
 // for 64 consecutive peers reads 512 contiguous bytes.
 //
@@ -17,7 +23,7 @@
 // A space is n_chunks hot chunks followed by n_chunks cold chunks
 // (pc = positions per chunk, a multiple of 64; depth = messages per mailbox):
 //   hot chunk:  [cnt u8 x pc] then for k < depth:
-//               [type u8 x pc][flags u8 x pc][term u32 x pc][commit offset u32 x pc][LogIndex u64 x pc]
+//               [tag u16 x pc = type | flags << 8][term u32 x pc][commit offset u32 x pc][LogIndex u64 x pc]
 //   cold chunk: for k < depth: [n u32][run2 u32][log term u32][run term 0 u32][run term 1 u32]
 //               [Commit u64][Hint u64][HintHigh u64] (each x pc)
 // Compact Replicates and non-reject ReplicateResps -- every steady-state message --
@@ -43,7 +49,8 @@ constexpr uint32_t NOPOS = 0xFFFFFFFFu;
 enum U64Row : uint32_t {
   SR_TERM = 0, SR_VOTE, SR_COMMITTED, SR_APPLIED, SR_LAST_INDEX, SR_LO, SR_LEADER_ID, SR_LTT,
   SR_NODE_ID, SR_ETICK, SR_HTICK, SR_RETIMEOUT, SR_ETIMEOUT, SR_HTIMEOUT, SR_ENTRY_UB,
-  SR_RUN_START,                    // + r, r < GR_K
+  SR_HDR,                          // the header word (below)
+  SR_RUN_START,                    // + row, right-aligned (run_row)
   SR_RUN_TERM = SR_RUN_START + GR_K,  // + r
   SR_REMOTE = SR_RUN_TERM + GR_K,     // remote rows start; see below
 };
@@ -58,17 +65,49 @@ struct Rows {
   static constexpr uint32_t RI_HI = RI_LO + GR_Q;     // + q
   static constexpr uint32_t NU64 = RI_HI + GR_Q;
   // u8 rows (after the u64 region)
-  static constexpr uint32_t B_STATE = 0, B_FLAGS = 1, B_SELF = 2, B_NRUNS = 3, B_RIC = 4;
-  static constexpr uint32_t B_RSTATE = 5;             // + j
-  static constexpr uint32_t B_RACTIVE = B_RSTATE + S; // + j
-  static constexpr uint32_t B_RKIND = B_RACTIVE + S;  // + j
-  static constexpr uint32_t B_RIFROM = B_RKIND + S;   // + q
+  static constexpr uint32_t B_RIFROM = 0;             // + q
   static constexpr uint32_t B_RIACK = B_RIFROM + GR_Q;// + q
   static constexpr uint32_t NU8 = B_RIACK + GR_Q;
 };
 __host__ __device__ inline uint32_t pad_cap(uint32_t n) { return (n + 63u) & ~63u; }
 __host__ __device__ inline uint32_t rows_u64(uint32_t S) { return SR_REMOTE + 4 * S + 3 * GR_Q; }
-__host__ __device__ inline uint32_t rows_u8(uint32_t S) { return 5 + 3 * S + 2 * GR_Q; }
+__host__ __device__ inline uint32_t rows_u8(uint32_t) { return 2 * GR_Q; }
+// row of run r (0 = oldest) of a window of n runs (right-aligned)
+__host__ __device__ inline uint32_t run_row(uint32_t n, uint32_t r) { return GR_K - n + r; }
+
+// ---------------------------------------------------------------- header word
+//   bits 0-1 state, 2-5 self slot (15 = none), 6-8 n_runs, 9 H_GE_LO (the newest
+//   run starts at or above firstIndex-1), 10-17 flags (GR_F_* and the device
+//   bits below), 18-20 ReadIndex FIFO count, 24 + 5j remote slot j:
+//   state (2 bits), active (1), kind (2) -- the `rb` word of gr_lane.h.
+constexpr uint32_t H_SELF_SHIFT = 2, H_NRUNS_SHIFT = 6, H_GE_LO_BIT = 9, H_FLAGS_SHIFT = 10, H_RIC_SHIFT = 18,
+                   H_REM_SHIFT = 24;
+constexpr uint32_t H_SELF_NONE = 15;
+__host__ __device__ inline uint32_t h_state(uint64_t h) { return (uint32_t)h & 3u; }
+__host__ __device__ inline uint32_t h_self(uint64_t h) {
+  const uint32_t s = (uint32_t)(h >> H_SELF_SHIFT) & 15u;
+  return s == H_SELF_NONE ? GR_SLOT_NONE : s;
+}
+__host__ __device__ inline uint32_t h_nruns(uint64_t h) { return (uint32_t)(h >> H_NRUNS_SHIFT) & 7u; }
+__host__ __device__ inline bool h_gelo(uint64_t h) { return (h >> H_GE_LO_BIT) & 1u; }
+__host__ __device__ inline uint32_t h_flags(uint64_t h) { return (uint32_t)(h >> H_FLAGS_SHIFT) & 0xFFu; }
+__host__ __device__ inline uint32_t h_ric(uint64_t h) { return (uint32_t)(h >> H_RIC_SHIFT) & 7u; }
+__host__ __device__ inline uint64_t h_rb(uint64_t h) { return h >> H_REM_SHIFT; }
+__host__ __device__ inline uint64_t h_make(uint32_t state, uint32_t self, uint32_t nruns, bool gelo, uint32_t flags,
+                                           uint32_t ric, uint64_t rb) {
+  const uint32_t s4 = self >= 15u ? H_SELF_NONE : self;
+  return (uint64_t)(state & 3u) | ((uint64_t)s4 << H_SELF_SHIFT) | ((uint64_t)(nruns & 7u) << H_NRUNS_SHIFT) |
+         ((uint64_t)(gelo ? 1u : 0u) << H_GE_LO_BIT) | ((uint64_t)(flags & 0xFFu) << H_FLAGS_SHIFT) |
+         ((uint64_t)(ric & 7u) << H_RIC_SHIFT) | (rb << H_REM_SHIFT);
+}
+// per-slot fields of rb (5 bits per slot: state(2) active(1) kind(2))
+__host__ __device__ inline uint32_t rb_state(uint64_t rb, uint32_t j) { return (uint32_t)(rb >> (5 * j)) & 3u; }
+__host__ __device__ inline uint32_t rb_active(uint64_t rb, uint32_t j) { return (uint32_t)(rb >> (5 * j + 2)) & 1u; }
+__host__ __device__ inline uint32_t rb_kind(uint64_t rb, uint32_t j) { return (uint32_t)(rb >> (5 * j + 3)) & 3u; }
+__host__ __device__ inline uint64_t rb_with(uint64_t rb, uint32_t j, uint32_t off, uint32_t width, uint32_t v) {
+  const uint64_t m = ((1ull << width) - 1) << (5 * j + off);
+  return (rb & ~m) | (((uint64_t)v << (5 * j + off)) & m);
+}
 __host__ __device__ inline uint64_t state_bytes(uint32_t S, uint32_t cap) {
   return (uint64_t)cap * (8ull * rows_u64(S) + rows_u8(S));
 }
@@ -132,9 +171,9 @@ __host__ __device__ inline uint32_t local_word(uint32_t ticks, uint32_t qticks, 
   const bool other = ticks || lflags || propose > 0xFFFFu || qticks > LW_QT_MAX;
   return other ? LW_OTHER : (propose | (qticks << LW_QT_SHIFT));
 }
-// Device-internal bits of the state flags row (never visible in gr_peer.flags:
+// Device-internal bits of the header's flags byte (never visible in gr_peer.flags:
 // gr_host.h masks them; GR_F_* use bits 0-2). They let the lean lane test one
-// byte instead of loading or rewriting 8-byte fields:
+// bit instead of loading or rewriting 8-byte fields:
 //   F_LTT    leaderTransferTarget != 0
 //   F_ETZ    electionTick == 0
 //   F_LSLOT  0, or s + 1 for a remote slot s < 7 with remote_id[s] == leaderID
@@ -143,10 +182,9 @@ constexpr uint32_t F_PUBLIC = 0x07u;
 constexpr uint32_t F_LTT = 0x80u;
 constexpr uint32_t F_ETZ = 0x40u;
 constexpr uint32_t F_LSLOT_SHIFT = 3, F_LSLOT = 0x38u;
-// Device-internal bit of the n_runs row: the newest run starts at or above
-// firstIndex-1, so every index at or above it is inside the log window and
-// the lean lane never needs firstIndex-1 (lo). n_runs itself is bits 0-2.
-constexpr uint32_t NR_MASK = 0x07u, NR_GE_LO = 0x80u;
+// H_GE_LO: the newest run starts at or above firstIndex-1, so every index at
+// or above it is inside the log window and the lean lane never needs
+// firstIndex-1 (lo).
 // The result record's propose_first is not stored: ProposeEntries is the last
 // item of a pass, so it is last_index - propose_entries + 1 after the pass.
 constexpr uint8_t RF_ESCALATED = 0x01;
@@ -241,8 +279,10 @@ struct Mailbox {
   __host__ __device__ inline uint8_t* hk(uint32_t k) const { return hot + pc + (uint64_t)k * kHotK * pc; }
   __host__ __device__ inline uint8_t* ck(uint32_t k) const { return cold + (uint64_t)k * kColdK * pc; }
   __host__ __device__ inline uint8_t& cnt() const { return hot[local]; }
-  __host__ __device__ inline uint8_t& type(uint32_t k) const { return hk(k)[local]; }
-  __host__ __device__ inline uint8_t& flags(uint32_t k) const { return hk(k)[pc + local]; }
+  __host__ __device__ inline uint8_t& type(uint32_t k) const { return hk(k)[2 * local]; }
+  __host__ __device__ inline uint8_t& flags(uint32_t k) const { return hk(k)[2 * local + 1]; }
+  // type | flags << 8 in one access (little-endian)
+  __host__ __device__ inline uint16_t& tag(uint32_t k) const { return reinterpret_cast<uint16_t*>(hk(k))[local]; }
   __host__ __device__ inline uint32_t& n(uint32_t k) const { return reinterpret_cast<uint32_t*>(ck(k))[local]; }
   __host__ __device__ inline uint32_t& run2(uint32_t k) const {
     return reinterpret_cast<uint32_t*>(ck(k) + 4ull * pc)[local];

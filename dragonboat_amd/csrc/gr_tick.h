@@ -44,7 +44,9 @@ struct TickLane {
   const StepParams& kp;
   const uint32_t i, p;
   bool ok = true;
-  uint32_t state = 0, self = 0, flags = 0, nruns = 0, nbyte = 0;
+  uint64_t hdr = 0;
+  uint32_t state = 0, self = 0, flags = 0, nruns = 0;
+  bool gelo = false;
   uint64_t term = 0, committed = 0, committed0 = 0, hi = 0, rsn = 0, rtn = 0;
   uint64_t etick = 0, etick0 = 0;
   // leader
@@ -171,8 +173,8 @@ struct TickLane {
     }
     GT_BAIL(term == 0);
     // hasCommittedEntryAtCurrentTerm: term(committed) from the newest run; with
-    // NR_GE_LO every index at or above it lies in [firstIndex-1, lastIndex]
-    GT_BAIL(!(nbyte & NR_GE_LO) || committed > hi || nruns == 0 || committed < rsn);
+    // H_GE_LO every index at or above it lies in [firstIndex-1, lastIndex]
+    GT_BAIL(!gelo || committed > hi || nruns == 0 || committed < rsn);
     if (rtn != term) return;
     bool dup = false;
 #pragma unroll
@@ -201,11 +203,12 @@ struct TickLane {
 
   GT_HD bool step(LaneStats* ls) {
     // ---- round 1
-    state = s8(Rw::B_STATE);
-    self = s8(Rw::B_SELF);
-    flags = s8(Rw::B_FLAGS);
-    nbyte = s8(Rw::B_NRUNS);
-    nruns = nbyte & NR_MASK;
+    hdr = s64(SR_HDR);
+    state = h_state(hdr);
+    self = h_self(hdr);
+    flags = h_flags(hdr);
+    nruns = h_nruns(hdr);
+    gelo = h_gelo(hdr);
     term = s64(SR_TERM);
     committed = s64(SR_COMMITTED);
     hi = s64(SR_LAST_INDEX);
@@ -233,9 +236,9 @@ struct TickLane {
     // ---- round 2
     etick = s64(SR_ETICK);
     uint64_t retimeout = 0;
-    if (nruns) {
-      rsn = s64(SR_RUN_START + nruns - 1);
-      rtn = s64(SR_RUN_TERM + nruns - 1);
+    if (nruns) {  // the newest run: always the last row (right-aligned window)
+      rsn = s64(SR_RUN_START + GR_K - 1);
+      rtn = s64(SR_RUN_TERM + GR_K - 1);
     }
     uint32_t mh[S][MK];
     uint64_t mterm[S][MK], mcom[S][MK], mlo[S][MK], mhi[S][MK];
@@ -258,13 +261,14 @@ struct TickLane {
       htick = s64(SR_HTICK);
       etimeout = s64(SR_ETIMEOUT);
       htimeout = s64(SR_HTIMEOUT);
-      ric = s8(Rw::B_RIC);
+      ric = h_ric(hdr);
+      const uint64_t rb = h_rb(hdr);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         match[j] = s64(Rw::MATCH + j);
-        rst[j] = s8(Rw::B_RSTATE + j) & 3u;
-        ract[j] = s8(Rw::B_RACTIVE + j) & 1u;
-        rkind[j] = s8(Rw::B_RKIND + j) & 3u;
+        rst[j] = rb_state(rb, j);
+        ract[j] = rb_active(rb, j);
+        rkind[j] = rb_kind(rb, j);
       }
 #pragma unroll
       for (int q = 0; q < GR_Q; ++q) {
@@ -376,18 +380,19 @@ struct TickLane {
       s64(SR_LEADER_ID) = s64(Rw::RID + L);  // setLeaderID(m.From)
       nf = (nf & ~F_LSLOT) | ((L + 1) << F_LSLOT_SHIFT);
     }
-    if (nf != flags) s8(Rw::B_FLAGS) = (uint8_t)nf;
+    uint64_t nh = (hdr & ~(0xFFull << H_FLAGS_SHIFT)) | ((uint64_t)nf << H_FLAGS_SHIFT);
     if (leader) {
       if (htick != htick0) s64(SR_HTICK) = htick;
+      uint64_t rb = h_rb(nh);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         if ((sdirty >> j) & 1u) {
-          s8(Rw::B_RSTATE + j) = (uint8_t)rst[j];
-          s8(Rw::B_RACTIVE + j) = (uint8_t)ract[j];
+          rb = rb_with(rb, j, 0, 2, rst[j]);
+          rb = rb_with(rb, j, 2, 1, ract[j]);
         }
       }
+      nh = h_make(state, self, nruns, gelo, nf, fifo_dirty ? ric : h_ric(hdr), rb);
       if (fifo_dirty) {
-        s8(Rw::B_RIC) = (uint8_t)ric;
 #pragma unroll
         for (int q = 0; q < GR_Q; ++q) {
           s64(Rw::RI_INDEX + q) = rii[q];
@@ -398,6 +403,7 @@ struct TickLane {
         }
       }
     }
+    if (nh != hdr) s64(SR_HDR) = nh;
 #pragma unroll
     for (int j = 0; j < S; ++j)
       if (gout[j] != NOPOS) kp.out.at(gout[j]).cnt() = (uint8_t)outc[j];
