@@ -125,9 +125,9 @@ def _oracle_rate(peers, topo, R, locals_fn, threads, seconds, inject=None, drop=
         loc = locals_fn(k, pop)
         before = pop.export()["committed"]
         t0 = time.perf_counter()
-        o = pop.step(msgs, loc, threads=threads)
+        o = pop.step(msgs, loc, threads=threads, want_mid=False)  # the raft step only, no record export
         t_step += time.perf_counter() - t0
-        end = o["mid"]  # no limits: the state after the whole pass
+        end = pop.export()
         commits += int(np.sum((end["committed"] > before) & (end["state"] == abi.LEADER)))
         msgs = topo.route_messages(o["msgs"])
         if drop is not None:

@@ -68,6 +68,7 @@ struct gr_engine {
   uint32_t stats_rows = 0;
   uint32_t* bail = nullptr;      // kBailLists lists of cap lanes each
   uint32_t* counters = nullptr;  // [2 (pass parity)][kBailLists][kCounterStride]
+  uint8_t* hints = nullptr;      // [cap / 64] wave hints of the device-resident path (gr_layout.h WH_*)
   uint64_t launches = 0;         // never reset: selects the live counter set
   uint64_t timing_bailed0 = 0;   // ST_BAILED when timing began
   bool timing = false;
@@ -279,7 +280,8 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
       hipMalloc((void**)&e->stats, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
       hipMalloc((void**)&e->bail, (size_t)kBailLists * e->cap * 4) != hipSuccess ||
       hipMalloc((void**)&e->counters, 2 * kBailLists * kCounterStride * 4) != hipSuccess ||
-      hipMalloc((void**)&e->route_base, 2 * GR_SMAX * GR_SMAX * 4) != hipSuccess) {
+      hipMalloc((void**)&e->route_base, 2 * GR_SMAX * GR_SMAX * 4) != hipSuccess ||
+      hipMalloc((void**)&e->hints, e->cap / 64 + 1) != hipSuccess) {
     if (ds) (void)hipFree(ds);
     if (dl) (void)hipFree(dl);
     e->st.base = nullptr;
@@ -292,6 +294,7 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
   if (hipMemset(ds, 0, sb) != hipSuccess || hipMemset(dl, 0, lb) != hipSuccess ||
       hipMemset(e->stats, 0, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
       hipMemset(e->counters, 0, 2 * kBailLists * kCounterStride * 4) != hipSuccess ||
+      hipMemset(e->hints, 0, e->cap / 64 + 1) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     gr_destroy(e);
     return GR_EDEVICE;
@@ -309,6 +312,7 @@ void gr_destroy(gr_engine* e) {
   if (e->bail) (void)hipFree(e->bail);
   if (e->counters) (void)hipFree(e->counters);
   if (e->route_base) (void)hipFree(e->route_base);
+  if (e->hints) (void)hipFree(e->hints);
   free_timings(e);
   for (gr_engine::Buf* b : {&e->d_in, &e->d_out, &e->d_msgs, &e->d_locals, &e->d_mark, &e->d_lop, &e->d_keys,
                             &e->d_idx, &e->d_skeys, &e->d_sidx, &e->d_win, &e->d_oc, &e->d_off, &e->d_tmp,
@@ -778,6 +782,7 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
   kp.in = make_view(in_space, in_chunks, in_positions, depth);
   kp.out = make_view(out_space, out_chunks, out_positions, depth);
   kp.n_lanes = n_peers;
+  kp.hints = e->hints;  // lane = peer here, so a wave's hint carries over between passes
   HIPCHK(launch_slots(e->S, kp, e->bail, e->counters, e->cap, (uint32_t)e->launches++, (hipStream_t)stream,
                       next_timing(e)));
   e->passes++;

@@ -60,6 +60,8 @@ struct FastLane {
   uint32_t outnc = 0;    // out mailboxes holding a message that is not compact (MB_ALLCOMPACT)
   bool resp_nc = false;  // a reject (carries Hint) went out
   uint32_t nmo = 0, nmi = 0, nent = 0;
+  uint32_t lslot_out = 0;  // F_LSLOT after the pass (the wave hint)
+  bool had_input = false;   // messages or proposals this pass
   // results
   uint64_t append_from = 0;
   uint32_t prop_result = 0;
@@ -265,19 +267,23 @@ struct FastLane {
   }
 
   // ------------------------------------------------------------- step
-  GF_HD bool step(LaneStats* ls) {
-    // ---- round 1: core (one header word), the newest run (a fixed row), locals, routes
+  // `hint` (wave-uniform, gr_layout.h WH_*) says what the lane's wave was at the
+  // end of the previous pass: all leaders, or all followers of one leader slot.
+  // The loads that role needs are then issued with the header, in one round,
+  // before the lane knows its state; a lane whose role differs from the hint
+  // loads what it needs afterwards, so the hint never changes a result.
+  GF_HD bool step(LaneStats* ls, uint32_t hint) {
+    const bool hl = kLeaderPath && hint == WH_LEADER;
+    const bool hf = (hint & WH_ROLE) == WH_FOLLOWER;
+    const uint32_t hL = hint >> WH_SLOT_SHIFT;
+    // ---- round 1: core (one header word), the newest run (a fixed row), locals,
+    //      routes, mailbox counts, and the hinted role's loads
     hdr = ntld(s64(SR_HDR));
-    state = h_state(hdr);
-    self = h_self(hdr);
-    nruns = h_nruns(hdr);
-    const bool gelo = h_gelo(hdr);
     term = ntld(s64(SR_TERM));
     committed = ntld(s64(SR_COMMITTED));
     hi = ntld(s64(SR_LAST_INDEX));
     rsn0 = ntld(s64(SR_RUN_START + GR_K - 1));  // meaningful when nruns > 0
     rtn0 = ntld(s64(SR_RUN_TERM + GR_K - 1));
-    const uint32_t flags = h_flags(hdr);
     const uint32_t lw = kp.has_locals ? ntld(kp.ln.u32(LR_LWORD)[i]) : 0u;  // packed locals (gr_layout.h)
     uint32_t gin[S];
 #pragma unroll
@@ -286,7 +292,6 @@ struct FastLane {
       gout[j] = route_of(kp, 1, j, i);
       outc[j] = 0;
     }
-    // ---- round 2: mailbox counts, newest run, leader remotes
     uint32_t cnt[S];
     uint32_t allc = 0;  // in mailboxes whose messages are all compact (MB_ALLCOMPACT)
 #pragma unroll
@@ -295,6 +300,56 @@ struct FastLane {
       cnt[j] = b & MB_COUNT;
       allc |= (b & MB_ALLCOMPACT) ? (1u << j) : 0u;
     }
+    // leader: ReplicateResp (tag, term, LogIndex) from every slot
+    uint32_t lh[S][MK], lterm[S][MK];
+    uint64_t lidx[S][MK];
+    if (hl) {  // speculative: match/next and both messages of every in-mailbox
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        match[j] = ntld(s64(Rw::MATCH + j));
+        next[j] = ntld(s64(Rw::NEXT + j));
+#pragma unroll
+        for (int k = 0; k < MK; ++k) {
+          lh[j][k] = 0;
+          lterm[j][k] = 0;
+          lidx[j][k] = 0;
+          if (gin[j] != NOPOS) {
+            const Mailbox mb = kp.in.at(gin[j]);
+            lh[j][k] = ntld(mb.tag(k));
+            lterm[j][k] = ntld(mb.t32(k, MT_TERM));
+            lidx[j][k] = ntld(mb.u64(k, MF_LOG_INDEX));
+          }
+        }
+      }
+    }
+    // follower: Replicate fields from the one slot L that sent, + its node id
+    uint32_t fh[MK], fn[MK], fterm[MK], flt[MK], frt0[MK], fcd[MK];
+    uint64_t fidx[MK];
+#pragma unroll
+    for (int k = 0; k < MK; ++k) {
+      fh[k] = 0; fn[k] = 0; fterm[k] = 0; fidx[k] = 0; flt[k] = 0; fcd[k] = 0; frt0[k] = 0;
+    }
+    uint32_t ghL = NOPOS;
+    if (hf) {  // speculative: the hinted leader slot's two compact Replicates
+#pragma unroll
+      for (int j = 0; j < S; ++j) ghL = ((uint32_t)j == hL) ? gin[j] : ghL;
+      if (ghL != NOPOS) {
+        const Mailbox mb = kp.in.at(ghL);
+#pragma unroll
+        for (int k = 0; k < MK; ++k) {
+          fh[k] = ntld(mb.tag(k));
+          fterm[k] = ntld(mb.t32(k, MT_TERM));
+          fidx[k] = ntld(mb.u64(k, MF_LOG_INDEX));
+          fcd[k] = ntld(mb.t32(k, MT_CDELTA));
+        }
+      }
+    }
+    state = h_state(hdr);
+    self = h_self(hdr);
+    nruns = h_nruns(hdr);
+    const bool gelo = h_gelo(hdr);
+    const uint32_t flags = h_flags(hdr);
+    lslot_out = (flags & F_LSLOT) >> F_LSLOT_SHIFT;
     if (nruns) {
       rsn = rsn0;
       rtn = rtn0;
@@ -304,43 +359,38 @@ struct FastLane {
     const uint32_t nq = (lw >> LW_QT_SHIFT) & LW_QT_MAX;
     uint64_t etick = 0;
     if (nq) etick = ntld(s64(SR_ETICK));
+    // ---- round 2 (only where the hint did not match): leader remotes and messages
     if (kLeaderPath && leader) {
       const uint64_t rb = h_rb(hdr);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        match[j] = ntld(s64(Rw::MATCH + j));
-        next[j] = ntld(s64(Rw::NEXT + j));
         rst[j] = rb_state(rb, j);
         ract[j] = rb_active(rb, j);
         rkind[j] = rb_kind(rb, j);
       }
-    }
-    // ---- round 3: message fields
-    // leader: ReplicateResp (type, flags, term, LogIndex) from every slot
-    uint32_t lh[S][MK], lterm[S][MK];
-    uint64_t lidx[S][MK];
-    // follower: Replicate fields from the one slot L that sent, + its node id
-    uint32_t L = 0, nsrc = 0, c = 0, gl = 0, go = NOPOS, lc = 0;
-    uint32_t fh[MK], fn[MK], fterm[MK], flt[MK], frt0[MK], fcd[MK];
-    uint64_t fidx[MK];
-    uint64_t rid = 0;
-    if (kLeaderPath && leader) {
+      if (!hl) {
 #pragma unroll
-      for (int j = 0; j < S; ++j) {
+        for (int j = 0; j < S; ++j) {
+          match[j] = ntld(s64(Rw::MATCH + j));
+          next[j] = ntld(s64(Rw::NEXT + j));
 #pragma unroll
-        for (int k = 0; k < MK; ++k) {
-          lh[j][k] = 0;
-          lterm[j][k] = 0;
-          lidx[j][k] = 0;
-          if ((uint32_t)k < cnt[j]) {
-            const Mailbox mb = kp.in.at(gin[j]);
-            lh[j][k] = (uint32_t)ntld(mb.type(k)) | ((uint32_t)ntld(mb.flags(k)) << 8);
-            lterm[j][k] = ntld(mb.t32(k, MT_TERM));
-            lidx[j][k] = ntld(mb.u64(k, MF_LOG_INDEX));
+          for (int k = 0; k < MK; ++k) {
+            lh[j][k] = 0;
+            lterm[j][k] = 0;
+            lidx[j][k] = 0;
+            if ((uint32_t)k < cnt[j]) {
+              const Mailbox mb = kp.in.at(gin[j]);
+              lh[j][k] = ntld(mb.tag(k));
+              lterm[j][k] = ntld(mb.t32(k, MT_TERM));
+              lidx[j][k] = ntld(mb.u64(k, MF_LOG_INDEX));
+            }
           }
         }
       }
-    } else {
+    }
+    uint32_t L = 0, nsrc = 0, c = 0, gl = 0, go = NOPOS, lc = 0;
+    uint64_t rid = 0;
+    if (!(kLeaderPath && leader)) {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         if (cnt[j]) {
@@ -353,15 +403,17 @@ struct FastLane {
         }
       }
       const uint32_t cc = c < (uint32_t)MK ? c : (uint32_t)MK;
+      const bool spec = hf && L == hL;  // the hinted mailbox is the one that sent
 #pragma unroll
       for (int k = 0; k < MK; ++k) {
-        fh[k] = 0; fn[k] = 0; fterm[k] = 0; fidx[k] = 0; flt[k] = 0; fcd[k] = 0; frt0[k] = 0;
         if ((uint32_t)k < cc) {
           const Mailbox mb = kp.in.at(gl);
-          fh[k] = (uint32_t)ntld(mb.type(k)) | ((uint32_t)ntld(mb.flags(k)) << 8);
-          fterm[k] = ntld(mb.t32(k, MT_TERM));
-          fidx[k] = ntld(mb.u64(k, MF_LOG_INDEX));
-          fcd[k] = ntld(mb.t32(k, MT_CDELTA));
+          if (!spec) {
+            fh[k] = ntld(mb.tag(k));
+            fterm[k] = ntld(mb.t32(k, MT_TERM));
+            fidx[k] = ntld(mb.u64(k, MF_LOG_INDEX));
+            fcd[k] = ntld(mb.t32(k, MT_CDELTA));
+          }
           if (!lc) {  // a compact mailbox carries none of these
             fn[k] = ntld(mb.n(k));
             flt[k] = ntld(mb.t32(k, MT_LOG_TERM));
@@ -377,6 +429,7 @@ struct FastLane {
     bool any_input = np != 0;
 #pragma unroll
     for (int j = 0; j < S; ++j) any_input = any_input || cnt[j] != 0;
+    had_input = any_input;
     GF_BAIL(lw & LW_OTHER);
     if (nq) {
       // QuiescedTick x nq alone (raft.go:431-433: electionTick++ in every
@@ -494,6 +547,7 @@ struct FastLane {
       }
       nh = (nh & ~(0xFFull << H_FLAGS_SHIFT)) | ((uint64_t)nf << H_FLAGS_SHIFT);
     }
+    lslot_out = (h_flags(nh) & F_LSLOT) >> F_LSLOT_SHIFT;
     if (nh != hdr) ntst(s64(SR_HDR), nh);
 #pragma unroll
     for (int j = 0; j < S; ++j)
@@ -521,6 +575,14 @@ struct FastLane {
     if (leader) GR_COVER(FAST_LEADER);
     else GR_COVER(FAST_FOLLOWER);
     return true;
+  }
+  // The lane's role for the next pass's wave hint (WH_*): what it is after this
+  // pass when it finished here, what it was when it handed over.
+  GF_HD uint32_t role_hint() const {
+    if (!had_input) return 0;  // quiesced or idle: nothing to speculate on
+    if (state == GR_LEADER) return WH_LEADER;
+    if (state != GR_FOLLOWER || !lslot_out) return 0;
+    return WH_FOLLOWER | ((lslot_out - 1) << WH_SLOT_SHIFT);
   }
 
   // handleReplicateMessage (raft.go:953-976) for an append at the log's end.
@@ -564,11 +626,14 @@ struct FastLane {
 };
 
 // Kernel-side entry: the lean lane for lane i; false = hand the lane to the general kernel.
+// *state = the role the lane entered the pass with; *hint_out = its role hint (WH_*).
 template <int S>
-GF_HD bool fast_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, uint32_t* state = nullptr) {
+GF_HD bool fast_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, uint32_t* state = nullptr,
+                     uint32_t hint = 0, uint32_t* hint_out = nullptr) {
   FastLane<S> L(kp, i, p);
-  const bool done = L.step(ls);
-  if (state) *state = L.state;  // the role the lane entered the pass with
+  const bool done = L.step(ls, hint);
+  if (state) *state = L.state;
+  if (hint_out) *hint_out = L.role_hint();
   return done;
 }
 

@@ -78,12 +78,22 @@ template <int S>
 __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
                                                                              uint32_t* counters, uint32_t list_cap) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  // the wave's hint: one byte, the same address for every lane (a scalar load)
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
+  const uint32_t hint = kp.hints ? (uint32_t)kp.hints[wave] : 0u;
   LaneStats ls;
   bool bail = false;
-  uint32_t role = 0;
-  if (i < kp.n_lanes) {
+  uint32_t role = 0, myhint = 0;
+  const bool active = i < kp.n_lanes;
+  if (active) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-    bail = !fast_step<S>(kp, i, p, &ls, &role);  // leaves ls zero when it bails
+    bail = !fast_step<S>(kp, i, p, &ls, &role, hint, &myhint);  // leaves ls zero when it bails
+  }
+  if (kp.hints) {  // next pass's hint: this wave's role if every active lane shares it
+    const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane(myhint);
+    const uint64_t same = __ballot(active && myhint == first), act = __ballot(active);
+    const uint32_t nh = same == act ? first : 0u;
+    if ((threadIdx.x & 63) == 0 && nh != hint) kp.hints[wave] = (uint8_t)nh;
   }
   // followers into lists 0..7, leaders into 8..15: the general kernel walks the
   // lists in order, so its waves hold one role and diverge less

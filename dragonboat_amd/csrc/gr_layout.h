@@ -346,6 +346,11 @@ struct LaneStats {
 //                load, so the mailbox counts load in the first round.
 constexpr uint8_t RT_IDENTITY = 0, RT_TABLE = 1, RT_AFFINE = 2, RT_LOOPBACK = 3;
 
+// Wave hints: one byte per wave of lanes (device-resident path), what the
+// wave's lanes were at the end of the previous pass, so the lean lane can issue
+// that role's loads with its first round (gr_fast.h). 0 = mixed or idle.
+constexpr uint32_t WH_ROLE = 3, WH_LEADER = 1, WH_FOLLOWER = 2, WH_SLOT_SHIFT = 2;
+
 // Kernel argument (small, passed by value, lives in SGPRs).
 // Lane i steps peer lane_peer[i] (identity when has_lane_peer == 0).
 struct StepParams {
@@ -353,6 +358,7 @@ struct StepParams {
   LaneBase ln;
   SpaceView in, out;
   uint64_t* stats;     // [gridDim.x][NSTAT] or nullptr
+  uint8_t* hints;      // [n_lanes / 64] wave hints (WH_*) or nullptr
   const uint32_t* route_base;  // RT_AFFINE: [2][GR_SMAX][GR_SMAX]
   uint64_t max_entry_size;
   uint32_t n_lanes;

@@ -12,6 +12,9 @@
 // Peer.Handle (peer.go:199-209), then Peer.ReadIndex, Peer.Tick x n,
 // Peer.QuiescedTick x n, Peer.ProposeEntries.
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstring>
 #include <memory>
 #include <thread>
@@ -94,7 +97,9 @@ struct RunLogDB : ILogDB {
 
 using u8 = uint8_t;
 
-struct OPeer {
+// Cache-line aligned: peers are stepped clusterID % T by T threads (the
+// FixedPartitioner rule), so neighbouring records belong to different threads.
+struct alignas(128) OPeer {
   std::unique_ptr<RunLogDB> db;
   std::unique_ptr<raft> r;
   std::vector<u64> ids;   // slot -> node id
@@ -112,10 +117,65 @@ struct OPeer {
 
 }  // namespace
 
+// Long-lived workers, like dragonboat's step workers (execengine.go:122-129):
+// worker t always steps the same peers (clusterID % T), so its allocations stay
+// in its own malloc arena instead of bouncing between freshly created threads.
+struct WorkerPool {
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable go, done;
+  std::function<void(uint32_t)> job;
+  uint64_t gen = 0;
+  uint32_t pending = 0;
+  bool quit = false;
+  ~WorkerPool() { stop(); }
+  void stop() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      quit = true;
+    }
+    go.notify_all();
+    for (auto& t : th) t.join();
+    th.clear();
+    quit = false;
+  }
+  void run(uint32_t n, const std::function<void(uint32_t)>& f) {
+    if (th.size() != n) {
+      stop();
+      for (uint32_t t = 0; t < n; ++t) th.emplace_back([this, t]() { loop(t); });
+    }
+    std::unique_lock<std::mutex> g(mu);
+    job = f;
+    pending = n;
+    gen++;
+    go.notify_all();
+    done.wait(g, [this]() { return pending == 0; });
+  }
+  void loop(uint32_t t) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void(uint32_t)> f;
+      {
+        std::unique_lock<std::mutex> g(mu);
+        go.wait(g, [&]() { return quit || gen != seen; });
+        if (quit) return;
+        seen = gen;
+        f = job;
+      }
+      f(t);
+      std::lock_guard<std::mutex> g(mu);
+      if (--pending == 0) done.notify_all();
+    }
+  }
+};
+
 struct ob_pop {
   uint32_t S = 0;
+  WorkerPool pool;
   u64 maxEntrySize = MaxEntrySize;
   std::vector<OPeer> peers;
+  std::vector<gr_message> lastOut;  // the last ob_step2 with out == NULL keeps its messages here
+  std::vector<uint32_t> lastItems;
 };
 
 namespace {
@@ -566,7 +626,10 @@ int ob_step2(ob_pop* p, const gr_inbox* in, const uint32_t* limits, const gr_pee
     bool ok;
   };
   if (n_threads == 0) n_threads = 1;
-  std::vector<std::vector<Out>> outs(n_threads);
+  struct alignas(128) PerThread {  // one cache line apart: no false sharing between workers
+    std::vector<Out> v;
+  };
+  std::vector<PerThread> outv(n_threads);
   std::vector<std::string> errs(n_threads);
   auto work = [&](uint32_t t) {
     ItemProbe probe;
@@ -638,7 +701,7 @@ int ob_step2(ob_pop* p, const gr_inbox* in, const uint32_t* limits, const gr_pee
             if (wide64(mterm) || wide64(m.LogTerm) || (!m.Entries.empty() && wide64(m.Entries[0].Term)) || wide64(rt1))
               mask |= 1u << GR_ESC_WIDE_TERM;
           }
-          outs[t].push_back(o);
+          outv[t].v.push_back(o);
         }
         r.msgs.clear();
         if (judged) {
@@ -762,20 +825,24 @@ int ob_step2(ob_pop* p, const gr_inbox* in, const uint32_t* limits, const gr_pee
     }
     g_probe = nullptr;
   };
-  if (n_threads == 1) {
-    work(0);
-  } else {
-    std::vector<std::thread> th;
-    for (uint32_t t = 0; t < n_threads; ++t) th.emplace_back(work, t);
-    for (auto& x : th) x.join();
-  }
+  if (n_threads == 1) work(0);
+  else p->pool.run(n_threads, work);
   size_t k = 0;
   bool bad = false;
-  for (auto& v : outs) {
-    for (auto& o : v) {
+  if (!out) {  // kept for ob_fetch_out (the caller sizes its buffers exactly)
+    size_t tot = 0;
+    for (auto& pt : outv) tot += pt.v.size();
+    p->lastOut.resize(tot);
+    p->lastItems.resize(tot);
+  }
+  for (auto& pt : outv) {
+    for (auto& o : pt.v) {
       if (out && k < cap) {
         out[k] = o.rec;
         if (out_item) out_item[k] = o.item;
+      } else if (!out) {
+        p->lastOut[k] = o.rec;
+        p->lastItems[k] = o.item;
       }
       if (!o.ok) bad = true;
       k++;
@@ -792,6 +859,18 @@ int ob_step2(ob_pop* p, const gr_inbox* in, const uint32_t* limits, const gr_pee
   }
   if (k > cap && out) return GR_ECAPACITY;
   return e.empty() ? GR_OK : GR_ESTATE;
+}
+
+// The messages of the last ob_step2 called with out == NULL.
+int ob_fetch_out(ob_pop* p, gr_message* out, uint32_t* items, size_t cap) {
+  if (!p || (cap && (!out || !items)) || cap < p->lastOut.size()) return GR_EINVAL;
+  if (!p->lastOut.empty()) {
+    memcpy(out, p->lastOut.data(), p->lastOut.size() * sizeof(gr_message));
+    memcpy(items, p->lastItems.data(), p->lastItems.size() * sizeof(uint32_t));
+  }
+  p->lastOut.clear();
+  p->lastItems.clear();
+  return GR_OK;
 }
 
 int ob_step(ob_pop* p, const gr_inbox* in, const uint32_t* limits, gr_peer* mid, gr_message* out,

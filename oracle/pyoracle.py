@@ -38,6 +38,7 @@ def oracle_lib():
         lib.ob_step2.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32,
                                  c.c_uint32, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t,
                                  c.POINTER(c.c_size_t), c.c_void_p, c.c_uint32, c.c_char_p, c.c_size_t]
+        lib.ob_fetch_out.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
         _olib = lib
     return _olib
 
@@ -106,7 +107,7 @@ class OraclePopulation:
         self.lib.ob_commit_all(self._h)
 
     def step(self, msgs=None, locals_=None, limits=None, threads=1, allow_error=False, dev_before=None,
-             in_depth=abi.GR_C, out_depth=abi.GR_C, has_locals=True):
+             in_depth=abi.GR_C, out_depth=abi.GR_C, has_locals=True, want_mid=True):
         """Returns dict(msgs, items, results, mid, error, esc_mask).
 
         esc_mask[p] (when limits are given) is the set of gr_escalation reasons,
@@ -123,22 +124,24 @@ class OraclePopulation:
         if dev_before is not None:
             db = np.ascontiguousarray(dev_before, abi.PEER)
             assert len(db) == self.n
-        mid = np.zeros(self.n, abi.PEER)
+        mid = np.zeros(self.n, abi.PEER) if want_mid else None  # want_mid=False: no per-peer export
         res = np.zeros(self.n, abi.RESULT)
         mask = np.zeros(self.n, np.uint32)
-        cap = max(16, 4 * len(msgs) + 8 * self.n * self.slots)
-        out = np.zeros(cap, abi.MESSAGE)
-        items = np.zeros(cap, np.uint32)
         n_out = ctypes.c_size_t()
         err = ctypes.create_string_buffer(512)
         rc = self.lib.ob_step2(self._h, ctypes.byref(ib), lim.ctypes.data if lim is not None else None,
                                db.ctypes.data if db is not None else None, in_depth, out_depth,
-                               1 if has_locals else 0, mask.ctypes.data, mid.ctypes.data, out.ctypes.data,
-                               items.ctypes.data, cap, ctypes.byref(n_out), res.ctypes.data, threads, err, 512)
+                               1 if has_locals else 0, mask.ctypes.data, mid.ctypes.data if want_mid else None,
+                               None, None, 0, ctypes.byref(n_out), res.ctypes.data, threads, err, 512)
+        n = n_out.value
+        out = np.empty(n, abi.MESSAGE)  # sized exactly: the library kept the messages
+        items = np.empty(n, np.uint32)
+        rc2 = self.lib.ob_fetch_out(self._h, out.ctypes.data if n else None, items.ctypes.data if n else None, n)
+        if rc2:
+            raise OracleError(f"ob_fetch_out rc={rc2}")
         if rc and not (allow_error and rc == -6):
             raise OracleError(f"ob_step rc={rc}: {err.value.decode()}")
-        n = n_out.value
-        return {"msgs": out[:n], "items": items[:n], "results": res, "mid": mid,
+        return {"msgs": out, "items": items, "results": res, "mid": mid,
                 "error": err.value.decode() if rc else "", "esc_mask": mask}
 
 

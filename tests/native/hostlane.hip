@@ -19,6 +19,7 @@ using namespace gr::host;
 namespace {
 
 static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0, g_tick_lanes = 0;
+static uint32_t g_hint_salt = 0;  // varies the drawn wave hints from call to call
 
 template <int S>
 void run_lanes(const StepParams& kp) {
@@ -28,7 +29,12 @@ void run_lanes(const StepParams& kp) {
   for (uint32_t i = 0; i < kp.n_lanes; ++i) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     LaneStats ls;
-    if (!fast_step<S>(kp, i, p, &ls)) bailed.push_back(i);
+    // an arbitrary wave hint (gr_fast.h): it must never change a result, so
+    // the host build draws one per wave to exercise every speculative path
+    const uint32_t w = (i >> 6) * 2654435761u + g_hint_salt;
+    const uint32_t pick = (w >> 13) % (2u + S);
+    const uint32_t hint = pick == 0 ? 0u : pick == 1 ? WH_LEADER : (WH_FOLLOWER | ((pick - 2) << WH_SLOT_SHIFT));
+    if (!fast_step<S>(kp, i, p, &ls, nullptr, hint)) bailed.push_back(i);
   }
   for (uint32_t i : bailed) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
@@ -41,6 +47,7 @@ void run_lanes(const StepParams& kp) {
     Lane<S> L(kp, i, p);
     L.step(&ls);
   }
+  g_hint_salt += 0x9E3779B9u;
   g_fast_lanes += kp.n_lanes - bailed.size();
   g_bailed_lanes += bailed.size();
 }
