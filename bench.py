@@ -110,6 +110,7 @@ def _oracle_rate(peers, topo, R, locals_fn, threads, seconds, inject=None, drop=
     from dragonboat_amd import abi
     from oracle.pyoracle import OraclePopulation
     pop = OraclePopulation(peers, R)
+    pop.set_truncate_runs()  # long churn runs build >2-run Replicates; the records carry a prefix
     G = topo.G
     msgs = np.zeros(0, abi.MESSAGE)
     for k in range(2):  # to steady state

@@ -176,6 +176,10 @@ struct ob_pop {
   std::vector<OPeer> peers;
   std::vector<gr_message> lastOut;  // the last ob_step2 with out == NULL keeps its messages here
   std::vector<uint32_t> lastItems;
+  // CPU-baseline mode only (ob_set_truncate_runs): a Replicate whose entries span
+  // more than 2 term runs travels with the first two runs (a prefix of its
+  // entries, as a size-limited send would). Parity runs keep it an error.
+  bool truncateRuns = false;
 };
 
 namespace {
@@ -360,7 +364,7 @@ void export_peer(const OPeer& op, uint32_t S, gr_peer* g) {
 }
 
 // raftpb.Message -> gr_message (target slot, entries as term runs).
-bool to_record(const OPeer& op, uint32_t peer, const Message& m, gr_message* o) {
+bool to_record(const OPeer& op, uint32_t peer, const Message& m, gr_message* o, bool truncate_runs = false) {
   memset(o, 0, sizeof(*o));
   o->peer = peer;
   o->type = (uint8_t)m.Type;
@@ -381,7 +385,11 @@ bool to_record(const OPeer& op, uint32_t peer, const Message& m, gr_message* o) 
     o->run_term[0] = m.Entries[0].Term;
     for (size_t k = 1; k < m.Entries.size(); ++k) {
       if (m.Entries[k].Term != m.Entries[k - 1].Term) {
-        if (o->n_runs == 2) { ok = false; break; }
+        if (o->n_runs == 2) {
+          if (truncate_runs) o->n_entries = (uint32_t)k;
+          else ok = false;
+          break;
+        }
         o->n_runs = 2;
         o->run2_offset = (uint32_t)k;
         o->run_term[1] = m.Entries[k].Term;
@@ -548,6 +556,12 @@ int ob_representable(ob_pop* p, uint8_t* out, uint32_t n) {
   return GR_OK;
 }
 
+int ob_set_truncate_runs(ob_pop* p, int on) {
+  if (!p) return GR_EINVAL;
+  p->truncateRuns = on != 0;
+  return GR_OK;
+}
+
 int ob_export(ob_pop* p, gr_peer* out, uint32_t n) {
   if (!p || n > p->peers.size()) return GR_EINVAL;
   for (uint32_t k = 0; k < n; ++k) export_peer(p->peers[k], p->S, &out[k]);
@@ -687,7 +701,7 @@ int ob_step2(ob_pop* p, const gr_inbox* in, const uint32_t* limits, const gr_pee
           Out o;
           o.peer = pi;
           o.item = it;
-          o.ok = to_record(op, pi, m, &o.rec);
+          o.ok = to_record(op, pi, m, &o.rec, p->truncateRuns);
           if (o.rec.slot < S) sent[o.rec.slot]++;
           if (judged) {
             if (op.slotOf(m.To) == GR_SLOT_NONE) mask |= 1u << GR_ESC_NONMEMBER;

@@ -39,6 +39,7 @@ def oracle_lib():
                                  c.c_uint32, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t,
                                  c.POINTER(c.c_size_t), c.c_void_p, c.c_uint32, c.c_char_p, c.c_size_t]
         lib.ob_fetch_out.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
+        lib.ob_set_truncate_runs.argtypes = [c.c_void_p, c.c_int]
         _olib = lib
     return _olib
 
@@ -83,6 +84,12 @@ class OraclePopulation:
         if getattr(self, "_h", None):
             self.lib.ob_destroy(self._h)
             self._h = None
+
+    def set_truncate_runs(self, on=True):
+        """CPU-baseline mode: Replicates spanning more than 2 term runs travel with
+        their first two runs (a prefix of the entries, as a size-limited send);
+        parity runs leave this off and such a message is an error."""
+        self.lib.ob_set_truncate_runs(self._h, 1 if on else 0)
 
     def export(self):
         out = np.zeros(self.n, abi.PEER)
