@@ -48,6 +48,7 @@ PEER = np.dtype([
     ("first_index_m1", u64), ("leader_id", u64), ("leader_transfer_target", u64), ("node_id", u64),
     ("election_tick", u64), ("heartbeat_tick", u64), ("randomized_election_timeout", u64),
     ("election_timeout", u64), ("heartbeat_timeout", u64), ("entry_size_ub", u64),
+    ("saved_to", u64), ("marker_index", u64), ("log_applied", u64),
     ("run_start", u64, (GR_K,)), ("run_term", u64, (GR_K,)), ("remote_id", u64, (GR_SMAX,)),
     ("remotes", REMOTE, (GR_SMAX,)), ("read_index", READ_STATUS, (GR_Q,)),
     ("state", u8), ("n_runs", u8), ("self_slot", u8), ("flags", u8), ("read_index_count", u8),
@@ -68,9 +69,11 @@ READY = np.dtype([("index", u64), ("ctx_low", u64), ("ctx_high", u64)])
 RESULT = np.dtype([
     ("peer", u32), ("escalation", u8), ("propose_result", u8), ("n_ready", u8), ("n_forwarded", u8),
     ("esc_item", u32), ("forwarded_entries", u32), ("append_from", u64), ("propose_first", u64),
+    ("committed", u64), ("last_index", u64), ("save_from", u64), ("term", u64), ("vote", u64),
     ("ready", READY, (GR_Q,)),
 ])
-SIZES = {"gr_peer": 640, "gr_message": 80, "gr_local_input": 48, "gr_peer_result": 128,
+UPDATE_COMMIT = np.dtype([("stable_log_to", u64), ("stable_log_term", u64), ("applied_to", u64)])
+SIZES = {"gr_peer": 664, "gr_message": 80, "gr_local_input": 48, "gr_peer_result": 168,
          "gr_remote": 32, "gr_read_status": 32}
 assert PEER.itemsize == SIZES["gr_peer"], PEER.itemsize
 assert MESSAGE.itemsize == SIZES["gr_message"], MESSAGE.itemsize
@@ -115,7 +118,7 @@ MAX_ENTRY_SIZE = 2 * 32 * 1024 * 1024
 EXPORTS = [
     "gr_create", "gr_destroy", "gr_strerror", "gr_escalation_name", "gr_load_groups",
     "gr_sync_groups_to_host", "gr_step", "gr_inbox_reserve", "gr_release_outbox", "gr_stats_get", "gr_stats_reset",
-    "gr_load_peers", "gr_sync_peers_to_host", "gr_notify_applied", "gr_compact_log", "gr_space_bytes", "gr_space_chunk_bytes",
+    "gr_load_peers", "gr_sync_peers_to_host", "gr_notify_applied", "gr_compact_log", "gr_commit_update", "gr_space_bytes", "gr_space_chunk_bytes",
     "gr_space_hot_chunk_bytes", "gr_space_cold_used", "gr_bind_routes",
     "gr_set_locals", "gr_step_device",
     "gr_collect_results", "gr_space_decode", "gr_space_encode", "gr_timing_begin", "gr_timing_end",

@@ -391,6 +391,45 @@ int gr_compact_log(gr_engine* e, const uint32_t* slots, const uint64_t* index, s
   return *(uint32_t*)e->h_scal ? GR_ESTATE : GR_OK;
 }
 
+// entryLog.commitUpdate (logentry.go:325-335) for a slot list: the host's
+// persistence/apply acknowledgement moves inMemory.savedTo / markerIndex and
+// entryLog.applied on the device (gr_io.h commit_rows).
+int gr_commit_update(gr_engine* e, const uint32_t* slots, const gr_update_commit* uc, size_t n, int32_t* status) {
+  if (!e || (n && (!slots || !uc))) return GR_EINVAL;
+  if (n == 0) return GR_OK;
+  if (n >= 0x80000000ull) return GR_EINVAL;
+  const uint32_t cap = e->cfg.max_peers;
+  std::vector<uint64_t> seen((cap + 63) / 64, 0);
+  for (size_t x = 0; x < n; ++x) {
+    const uint32_t p = slots[x];
+    if (p >= cap || (seen[p >> 6] >> (p & 63)) & 1) return GR_ERANGE;  // nothing written
+    seen[p >> 6] |= 1ull << (p & 63);
+  }
+  std::lock_guard<std::mutex> guard(e->mu);
+  HIPCHK(hipDeviceSynchronize());  // passes in flight on other streams own the rows
+  const hipStream_t s = e->stream;
+  int r;
+  if ((r = grow_device(&e->d_slots.p, &e->d_slots.n, n * 4))) return r;
+  if ((r = grow_device(&e->d_peers.p, &e->d_peers.n, n * (sizeof(gr_update_commit) + 4) + 16))) return r;
+  if ((r = grow_device(&e->d_scal.p, &e->d_scal.n, 16))) return r;
+  if ((r = grow_pinned(&e->h_scal, &e->h_scal_bytes, 16))) return r;
+  gr_update_commit* duc = (gr_update_commit*)e->d_peers.p;
+  int32_t* dst = (int32_t*)(duc + n);
+  HIPCHK(hipMemcpyAsync(e->d_slots.p, slots, n * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(duc, uc, n * sizeof(gr_update_commit), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(e->d_scal.p, 0, 16, s));
+  const dim3 grid(io_grid(n)), blk(io::kIoBlock);
+  const uint32_t* ds = (const uint32_t*)e->d_slots.p;
+  uint32_t* refused = (uint32_t*)e->d_scal.p;
+  hipLaunchKernelGGL(io::commit_rows, grid, blk, 0, s, e->st, ds, (const gr_update_commit*)duc, (uint32_t)n, dst,
+                     refused);
+  HIPCHK(hipGetLastError());
+  if (status) HIPCHK(hipMemcpyAsync(status, dst, n * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(e->h_scal, refused, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return *(uint32_t*)e->h_scal ? GR_ESTATE : GR_OK;
+}
+
 // Peer.NotifyRaftLastApplied (peer.go:282-284) for a slot list: raft.applied =
 // the RSM's batched last applied index, as node.handleEvents does first in
 // every step (node.go:632-635,653). No other field changes.

@@ -48,10 +48,14 @@ __host__ __device__ inline void set_header(gr_peer& g, uint32_t S, uint64_t h) {
 // before the right-aligned run rows that need it.
 __host__ __device__ inline uint64_t get_u64_row(const gr_peer& g, uint32_t row, uint32_t S) {
   if (row < SR_HDR) {
+    // marker_index == 0: a freshly loaded group (newEntryLog, logentry.go:86-95)
+    const bool fresh = g.marker_index == 0;
     const uint64_t v[] = {g.term, g.vote, g.committed, g.applied, g.last_index, g.first_index_m1,
                           g.leader_id, g.leader_transfer_target, g.node_id, g.election_tick,
                           g.heartbeat_tick, g.randomized_election_timeout, g.election_timeout,
-                          g.heartbeat_timeout, g.entry_size_ub};
+                          g.heartbeat_timeout, g.entry_size_ub,
+                          fresh ? g.last_index : g.saved_to, fresh ? g.last_index + 1 : g.marker_index,
+                          fresh ? g.first_index_m1 : g.log_applied};
     return v[row];
   }
   if (row == SR_HDR) return header_of(g, S);
@@ -84,7 +88,7 @@ __host__ __device__ inline void set_u64_row(gr_peer& g, uint32_t row, uint32_t S
     uint64_t* f[] = {&g.term, &g.vote, &g.committed, &g.applied, &g.last_index, &g.first_index_m1,
                      &g.leader_id, &g.leader_transfer_target, &g.node_id, &g.election_tick,
                      &g.heartbeat_tick, &g.randomized_election_timeout, &g.election_timeout,
-                     &g.heartbeat_timeout, &g.entry_size_ub};
+                     &g.heartbeat_timeout, &g.entry_size_ub, &g.saved_to, &g.marker_index, &g.log_applied};
     *f[row] = v;
     return;
   }
@@ -278,6 +282,15 @@ inline int pack_inbox(const gr_inbox* in, uint32_t S, uint32_t max_peers, Packed
   return GR_OK;
 }
 
+// First index of inMemory.entriesToSave() (inmemory.go:101-108), 0 when it is
+// empty: idx = savedTo + 1; "nothing to save" when idx - markerIndex (uint64,
+// wrapping) exceeds len(entries) = lastIndex + 1 - markerIndex.
+__host__ __device__ inline uint64_t save_from(uint64_t saved_to, uint64_t marker, uint64_t last_index) {
+  const uint64_t idx = saved_to + 1;
+  if (idx - marker > last_index + 1 - marker) return 0;
+  return idx <= last_index ? idx : 0;
+}
+
 // The proposal fields of a result record from the lane rows (gr_layout.h RF_*):
 // propose_first is not stored, it follows from last_index since proposals are
 // the only appends of a pass that reports them.
@@ -294,6 +307,78 @@ __host__ __device__ inline void derive_proposals(gr_peer_result* pr, uint8_t rf,
     n += fwd_entries;
   }
   if (n) pr->propose_first = last_index - n + 1;
+}
+
+// The result record of lane l (stepping peer p) from the lane and state rows
+// after a pass: RF_* flags (gr_layout.h) select the per-pass fields; the
+// pb.Update fields (committed, last_index, save_from, term, vote) come from state.
+__host__ __device__ inline gr_peer_result make_result(const LaneBase& L, const StateBase& st, uint32_t l, uint32_t p) {
+  gr_peer_result pr{};
+  pr.peer = p;
+  const uint8_t rf = L.u8(LR_RFLAGS)[l];
+  if (rf & RF_ESCALATED) {
+    pr.escalation = L.u8(LR_ESC_REASON)[l];
+    pr.esc_item = L.u32(LR_ESC_ITEM)[l];
+  }
+  pr.last_index = st.u64(SR_LAST_INDEX)[p];
+  if (rf & (RF_PROPOSE | RF_FORWARDED))
+    derive_proposals(&pr, rf, L.u8(LR_PROP_RESULT)[l], pr.last_index, L.u32(LR_PROPOSE)[l], L.u8(LR_FWD_COUNT)[l],
+                     L.u32(LR_FWD_ENTRIES)[l]);
+  if (rf & RF_APPEND) pr.append_from = L.u64(LR_APPEND_FROM)[l];
+  if (rf & RF_READY) {
+    pr.n_ready = L.u8(LR_RTR_COUNT)[l];
+    for (int q = 0; q < GR_Q; ++q) {
+      if (q < pr.n_ready) {
+        pr.ready[q].index = L.u64(LR_RTR_INDEX + q)[l];
+        pr.ready[q].ctx_low = L.u64(LR_RTR_LO + q)[l];
+        pr.ready[q].ctx_high = L.u64(LR_RTR_HI + q)[l];
+      }
+    }
+  }
+  pr.committed = st.u64(SR_COMMITTED)[p];
+  pr.save_from = save_from(st.u64(SR_SAVED_TO)[p], st.u64(SR_MARKER)[p], pr.last_index);
+  pr.term = st.u64(SR_TERM)[p];
+  pr.vote = st.u64(SR_VOTE)[p];
+  return pr;
+}
+
+// entryLog.commitUpdate (logentry.go:325-335) on the state rows of peer p:
+// inMemory.savedLogTo(stable_log_to, stable_log_term), then entryLog.applied =
+// applied_to and inMemory.appliedLogTo (inmemory.go:92-139). Returns 0 (rows
+// written), 1 where the reference panics (invalid applyto) or 2 when the term
+// of stable_log_to lies below the term-run window; nothing is written then.
+__host__ __device__ inline int32_t commit_marks(const StateBase& st, uint32_t p, const gr_update_commit& u) {
+  uint64_t mk = st.u64(SR_MARKER)[p], sv = st.u64(SR_SAVED_TO)[p], ap = st.u64(SR_LOG_APPLIED)[p];
+  const uint64_t last = st.u64(SR_LAST_INDEX)[p], committed = st.u64(SR_COMMITTED)[p];
+  const bool inmem = last + 1 > mk;  // len(entries) > 0
+  if (u.stable_log_to > 0) {
+    const uint64_t i = u.stable_log_to;
+    if (inmem && i >= mk && i <= last) {
+      const uint64_t h = st.u64(SR_HDR)[p];
+      uint32_t nr = h_nruns(h);
+      if (nr > GR_K) nr = GR_K;
+      uint64_t t = 0;
+      bool known = false;
+      for (uint32_t r = 0; r < nr; ++r) {  // last run starting at or below i
+        if (st.u64(SR_RUN_START + run_row(nr, r))[p] <= i) {
+          t = st.u64(SR_RUN_TERM + run_row(nr, r))[p];
+          known = true;
+        }
+      }
+      if (!known) return 2;
+      if (t == u.stable_log_term) sv = i;
+    }
+  }
+  if (u.applied_to > 0) {
+    const uint64_t a = u.applied_to;
+    if (a < ap || a > committed) return 1;  // "invalid applyto" panic
+    ap = a;
+    if (inmem && a >= mk && a <= last) mk = a;
+  }
+  st.u64(SR_MARKER)[p] = mk;
+  st.u64(SR_SAVED_TO)[p] = sv;
+  st.u64(SR_LOG_APPLIED)[p] = ap;
+  return 0;
 }
 
 inline uint64_t space_total_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth = GR_C) {

@@ -151,31 +151,8 @@ __global__ void pack_outbox(SpaceView out, uint32_t nl, uint32_t S, const uint32
 // peer_of_lane == nullptr: lane l steps peer l.
 __global__ void pack_results(LaneBase L, StateBase st, const uint32_t* peer_of_lane, uint32_t first, uint32_t n,
                              gr_peer_result* out) {
-  for (uint32_t x = io_tid(); x < n; x += io_stride()) {
-    const uint32_t l = first + x;
-    gr_peer_result pr{};
-    pr.peer = peer_of_lane ? peer_of_lane[x] : l;
-    const uint8_t rf = L.u8(LR_RFLAGS)[l];
-    if (rf & RF_ESCALATED) {
-      pr.escalation = L.u8(LR_ESC_REASON)[l];
-      pr.esc_item = L.u32(LR_ESC_ITEM)[l];
-    }
-    if (rf & (RF_PROPOSE | RF_FORWARDED))
-      host::derive_proposals(&pr, rf, L.u8(LR_PROP_RESULT)[l], st.u64(SR_LAST_INDEX)[pr.peer], L.u32(LR_PROPOSE)[l],
-                             L.u8(LR_FWD_COUNT)[l], L.u32(LR_FWD_ENTRIES)[l]);
-    if (rf & RF_APPEND) pr.append_from = L.u64(LR_APPEND_FROM)[l];
-    if (rf & RF_READY) {
-      pr.n_ready = L.u8(LR_RTR_COUNT)[l];
-      for (int q = 0; q < GR_Q; ++q) {
-        if (q < pr.n_ready) {
-          pr.ready[q].index = L.u64(LR_RTR_INDEX + q)[l];
-          pr.ready[q].ctx_low = L.u64(LR_RTR_LO + q)[l];
-          pr.ready[q].ctx_high = L.u64(LR_RTR_HI + q)[l];
-        }
-      }
-    }
-    out[x] = pr;
-  }
+  for (uint32_t x = io_tid(); x < n; x += io_stride())
+    out[x] = host::make_result(L, st, first + x, peer_of_lane ? peer_of_lane[x] : first + x);
 }
 
 // Does any mailbox of the space hold a message with cold fields (nonempty and
@@ -200,6 +177,8 @@ __global__ void check_peers(const gr_peer* in, const uint32_t* slots, uint32_t n
     const gr_peer& g = in[x];
     if (g.n_runs > GR_K || g.read_index_count > GR_Q || (g.self_slot != GR_SLOT_NONE && g.self_slot >= S))
       atomicOr(err, ERR_PEER);
+    // inMemory: markerIndex <= lastIndex + 1 (entries [marker, last])
+    if (g.marker_index != 0 && g.marker_index > g.last_index + 1) atomicOr(err, ERR_PEER);
     if (slots) {  // in range and listed once, so the load is order-free
       if (slots[x] >= cap || atomicAdd(mark + slots[x], 1u) != 0) atomicOr(err, ERR_SLOT);
     }
@@ -301,6 +280,19 @@ __global__ void compact_rows(StateBase st, const uint32_t* slots, const uint64_t
       if ((uint32_t)k + 1 == nn) newest = ns[k];
     const bool ge = nn && newest >= i;
     st.u64(SR_HDR)[p] = h_make(h_state(h), h_self(h), nn, ge, h_flags(h), h_ric(h), h_rb(h));
+  }
+}
+
+// gr_commit_update: entryLog.commitUpdate (logentry.go:325-335) with
+// inMemory.savedLogTo / appliedLogTo (inmemory.go:92-139). status: 0 ok, 1 the
+// reference panics (invalid applyto), 2 the term of stable_log_to is below the
+// device window. Refused slots are not written.
+__global__ void commit_rows(StateBase st, const uint32_t* slots, const gr_update_commit* uc, uint32_t n,
+                            int32_t* status, uint32_t* refused) {
+  for (uint32_t x = io_tid(); x < n; x += io_stride()) {
+    const int32_t rc = host::commit_marks(st, slots[x], uc[x]);
+    status[x] = rc;
+    if (rc) atomicOr(refused, 1u);
   }
 }
 

@@ -38,6 +38,7 @@ enum : uint32_t {
   G_SNAP = 1u << 8,   // remotes: snapshotIndex
   G_RI = 1u << 9,     // ReadIndex FIFO
   G_EUB = 1u << 10,   // entry_size_ub
+  G_INMEM = 1u << 11, // inMemory.markerIndex / savedTo (truncating merges only)
   G_TICK = G_ETICK | G_TICKS,
 };
 // dirty bits (store)
@@ -45,7 +46,7 @@ enum : uint32_t {
   D_TERM = 1u << 0, D_VOTE = 1u << 1, D_COMMITTED = 1u << 2, D_HI = 1u << 3,
   D_LEADER = 1u << 4, D_LTT = 1u << 5, D_ETICK = 1u << 6, D_HTICK = 1u << 7,
   D_RETIMEOUT = 1u << 8, D_STATE = 1u << 9, D_FLAGS = 1u << 10, D_WIN = 1u << 11,
-  D_REM = 1u << 12, D_SNAP = 1u << 13, D_RI = 1u << 14,
+  D_REM = 1u << 12, D_SNAP = 1u << 13, D_RI = 1u << 14, D_INMEM = 1u << 15,
 };
 
 GR_HD bool is_leader_message(uint32_t t) {  // raft.go:986-989
@@ -108,6 +109,8 @@ struct Lane {
   uint64_t rii[GR_Q], rilo[GR_Q], rihi[GR_Q];
   // G_EUB
   uint64_t eub = 0;
+  // G_INMEM
+  uint64_t imk = 0, isv = 0;  // inMemory.markerIndex, savedTo
 
   // outputs of this pass
   uint32_t outcnt = 0;  // 3 bits per slot
@@ -189,6 +192,10 @@ struct Lane {
       }
     }
     if (miss & G_EUB) eub = s64(SR_ENTRY_UB);
+    if (miss & G_INMEM) {
+      imk = s64(SR_MARKER);
+      isv = s64(SR_SAVED_TO);
+    }
     loaded |= miss;
   }
 
@@ -220,6 +227,10 @@ struct Lane {
     if (dirty & D_ETICK) s64(SR_ETICK) = etick;
     if (dirty & D_HTICK) s64(SR_HTICK) = htick;
     if (dirty & D_RETIMEOUT) s64(SR_RETIMEOUT) = retimeout;
+    if (dirty & D_INMEM) {
+      s64(SR_MARKER) = imk;
+      s64(SR_SAVED_TO) = isv;
+    }
     if (dirty & D_WIN) {
 #pragma unroll
       for (int r = 0; r < GR_K; ++r) {  // oldest-first registers -> right-aligned rows
@@ -905,6 +916,19 @@ struct Lane {
     *ci = found;
     return 0;
   }
+  // inMemory.merge (inmemory.go:157-177) when the new entries start at or below
+  // lastIndex (an append at lastIndex + 1 = markerIndex + len(entries) changes
+  // neither mark): replace-all at or below markerIndex, else truncate-then-append.
+  GR_HD void merge_truncate(uint64_t first) {
+    need(G_INMEM);
+    if (first <= imk) {
+      imk = first;
+      isv = first - 1;
+    } else {
+      isv = umin(isv, first - 1);
+    }
+    dirty |= D_INMEM;
+  }
   GR_HD int conflict_index(const InMsg& m, uint64_t* ci) {
     *ci = 0;
     if (m.n == 0) return 0;
@@ -943,6 +967,7 @@ struct Lane {
         if (ci > hi + 1) return GR_ESC_PANIC;      // merge would hit a hole
         const uint64_t tprev = (ci - 1 == m.log_index) ? m.log_term : msg_term_at(m, ci - 1);
         if (tprev > msg_term_at(m, ci)) return GR_ESC_PANIC;  // checkEntriesToAppend
+        if (ci <= hi) merge_truncate(ci);
         win_truncate(ci);
         const uint32_t nr = (m.flags >> MFL_RUNS_SHIFT) & 3u;
         if (nr == 2) {
@@ -1502,6 +1527,7 @@ struct Lane {
       kp.ln.u8(LR_FWD_COUNT)[i] = (uint8_t)fwd_n;
       kp.ln.u32(LR_FWD_ENTRIES)[i] = fwd_entries;
     }
+    if (dirty & (D_TERM | D_VOTE)) rf |= RF_HARDSTATE;
     kp.ln.u8(LR_RFLAGS)[i] = rf;
     const bool adv = (dirty & D_COMMITTED) && committed > committed0;
     const bool lead = state == GR_LEADER;

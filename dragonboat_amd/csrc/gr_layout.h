@@ -49,6 +49,7 @@ constexpr uint32_t NOPOS = 0xFFFFFFFFu;
 enum U64Row : uint32_t {
   SR_TERM = 0, SR_VOTE, SR_COMMITTED, SR_APPLIED, SR_LAST_INDEX, SR_LO, SR_LEADER_ID, SR_LTT,
   SR_NODE_ID, SR_ETICK, SR_HTICK, SR_RETIMEOUT, SR_ETIMEOUT, SR_HTIMEOUT, SR_ENTRY_UB,
+  SR_SAVED_TO, SR_MARKER, SR_LOG_APPLIED,  // inMemory.savedTo / markerIndex, entryLog.applied (§8f-4)
   SR_HDR,                          // the header word (below)
   SR_RUN_START,                    // + row, right-aligned (run_row)
   SR_RUN_TERM = SR_RUN_START + GR_K,  // + r
@@ -192,6 +193,7 @@ constexpr uint8_t RF_PROPOSE = 0x02;
 constexpr uint8_t RF_READY = 0x04;
 constexpr uint8_t RF_APPEND = 0x08;
 constexpr uint8_t RF_FORWARDED = 0x10;  // forwarded Propose batches appended: LR_FWD_COUNT, LR_FWD_ENTRIES
+constexpr uint8_t RF_HARDSTATE = 0x20;  // term or vote changed (pb.Update.State differs)
 
 // ---------------------------------------------------------------- message spaces
 enum U64Field : uint32_t { MF_LOG_INDEX = 0, MF_COMMIT = 1, MF_HINT = 2, MF_HINT_HIGH = 3, MF_NUM_U64 = 4 };

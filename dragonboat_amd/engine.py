@@ -48,6 +48,7 @@ def load_library(path=LIB_PATH):
     lib.gr_sync_peers_to_host.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_notify_applied.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_compact_log.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p]
+    lib.gr_commit_update.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p]
     lib.gr_step.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.POINTER(abi.Outbox)]
     lib.gr_release_outbox.argtypes = [c.c_void_p, c.POINTER(abi.Outbox)]
     lib.gr_inbox_reserve.argtypes = [c.c_void_p, c.c_size_t, c.c_size_t, c.POINTER(abi.Inbox)]
@@ -160,6 +161,21 @@ class Engine:
                                      st.ctypes.data if len(st) else None)
         if rc not in (0, -6):
             _check(rc, "gr_compact_log")
+        return rc, st
+
+    def commit_update(self, slots, uc):
+        """entryLog.commitUpdate on the device (gr_commit_update): uc is an
+        abi.UPDATE_COMMIT array. Returns (rc, per-slot status: 0 ok, 1 the
+        reference panics, 2 term below the device window)."""
+        slots = np.ascontiguousarray(slots, np.uint32)
+        uc = np.ascontiguousarray(uc, abi.UPDATE_COMMIT)
+        assert len(slots) == len(uc)
+        st = np.zeros(len(slots), np.int32)
+        rc = self.lib.gr_commit_update(self._h, slots.ctypes.data if len(slots) else None,
+                                       uc.ctypes.data if len(uc) else None, len(slots),
+                                       st.ctypes.data if len(st) else None)
+        if rc not in (0, -6):
+            _check(rc, "gr_commit_update")
         return rc, st
 
     def step(self, msgs=None, locals_=None):

@@ -140,6 +140,15 @@ typedef struct gr_peer {
   uint64_t election_tick, heartbeat_tick, randomized_election_timeout;
   uint64_t election_timeout, heartbeat_timeout;
   uint64_t entry_size_ub;  /* upper bound of Entry.SizeUpperLimit() in this log (host-maintained) */
+  /* The in-memory log's persistence marks (inmemory.go:29-34, logentry.go:78-83),
+   * the state behind entriesToSave/commitUpdate:
+   *   saved_to     inMemory.savedTo (entries <= saved_to are in LogDB)
+   *   marker_index inMemory.markerIndex (first index kept in memory)
+   *   log_applied  entryLog.applied (advanced by gr_commit_update)
+   * marker_index == 0 means "a freshly loaded group" (newEntryLog,
+   * logentry.go:86-95): the engine takes marker_index = last_index + 1,
+   * saved_to = last_index, log_applied = first_index_m1. */
+  uint64_t saved_to, marker_index, log_applied;
   uint64_t run_start[GR_K], run_term[GR_K];
   uint64_t remote_id[GR_SMAX];
   gr_remote remotes[GR_SMAX];
@@ -209,6 +218,13 @@ typedef struct gr_peer_result {
    * batches in arrival order (slot, then mailbox order) and the local
    * ProposeEntries batch, when propose_result == GR_PROP_APPENDED, follows. */
   uint64_t propose_first;
+  /* The group's pb.Update fields after the items applied on the device
+   * (getUpdate, peer.go:311-337): */
+  uint64_t committed;      /* entryLog.committed: CommittedEntries end (start: log_applied + 1) */
+  uint64_t last_index;     /* entryLog.lastIndex() */
+  uint64_t save_from;      /* EntriesToSave = [save_from, last_index] (inMemory.entriesToSave,
+                            * inmemory.go:101-108); 0 = nothing to save */
+  uint64_t term, vote;     /* raftState(): pb.State{Term, Vote, Commit = committed} */
   gr_ready_to_read ready[GR_Q];
 } gr_peer_result;
 
@@ -270,6 +286,23 @@ int gr_notify_applied(gr_engine* e, const uint32_t* slots, const uint64_t* appli
  * and the call returns GR_ESTATE if any slot was refused. Slots out of range or
  * listed twice: GR_ERANGE before anything is written. */
 int gr_compact_log(gr_engine* e, const uint32_t* slots, const uint64_t* index, size_t n, int32_t* status);
+
+/* entryLog.commitUpdate (logentry.go:325-335) for a list of engine slots: the
+ * host reports what it persisted and applied after processing the pass's
+ * pb.Update (node.processRaftUpdate -> Peer.Commit, peer.go:250-263):
+ * inMemory.savedLogTo(stable_log_to, stable_log_term) when stable_log_to > 0,
+ * then, when applied_to > 0, entryLog.applied = applied_to and
+ * inMemory.appliedLogTo(applied_to) (inmemory.go:92-139). Snapshots stay on the
+ * host (StableSnapshotTo: reload the group). Per slot, status (may be NULL):
+ * 0 ok; 1 the reference panics ("invalid applyto": applied_to below
+ * entryLog.applied or above committed); 2 the term of stable_log_to lies below
+ * the device's term-run window (the host resolves it and reloads the group).
+ * Refused slots are left untouched and the call returns GR_ESTATE. Slots out of
+ * range or listed twice: GR_ERANGE before anything is written. */
+typedef struct gr_update_commit {
+  uint64_t stable_log_to, stable_log_term, applied_to;
+} gr_update_commit;
+int gr_commit_update(gr_engine* e, const uint32_t* slots, const gr_update_commit* uc, size_t n, int32_t* status);
 
 /* One synchronous pass over host buffers (what a cgo caller uses). */
 int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out);

@@ -267,6 +267,22 @@ void build_peer(const gr_peer& g, uint32_t S, u64 maxEntrySize, OPeer* op) {
   r.readyToRead.clear();
   op->entryUB = g.entry_size_ub;
   r.log->onTryAppend = [op](u64 ci) { op->appendFrom = op->appendFrom ? std::min(op->appendFrom, ci) : ci; };
+  // The in-memory log's persistence marks (gpuraft.h gr_peer.saved_to / marker_index /
+  // log_applied); marker_index == 0 keeps newEntryLog's (inmem at lastIndex + 1).
+  if (g.marker_index != 0) {
+    inMemory& im = r.log->inmem;
+    im.markerIndex = g.marker_index;
+    im.savedTo = g.saved_to;
+    im.entries.clear();
+    for (u64 i = g.marker_index; i <= hi; ++i) {
+      Entry e;
+      e.Index = i;
+      e.Term = db.termAt(i);
+      e.Cmd.assign(db.payload, 0);
+      im.entries.push_back(std::move(e));
+    }
+    r.log->applied = g.log_applied;
+  }
 }
 
 // Term runs of the oracle log over [lo, hi] (lo = firstIndex-1): the logdb
@@ -314,6 +330,9 @@ void export_peer(const OPeer& op, uint32_t S, gr_peer* g) {
   g->election_timeout = r.electionTimeout;
   g->heartbeat_timeout = r.heartbeatTimeout;
   g->entry_size_ub = op.entryUB;
+  g->saved_to = r.log->inmem.savedTo;
+  g->marker_index = r.log->inmem.markerIndex;
+  g->log_applied = r.log->applied;
   auto runs = log_runs(op);
   size_t first = runs.size() > GR_K ? runs.size() - GR_K : 0;
   g->n_runs = (uint8_t)(runs.size() - first);
@@ -556,6 +575,31 @@ int ob_representable(ob_pop* p, uint8_t* out, uint32_t n) {
   return GR_OK;
 }
 
+// entryLog.commitUpdate (logentry.go:325-335) for a slot list, as gr_commit_update:
+// status 1 where the reference panics ("invalid applyto"), and such a slot is left
+// untouched.
+int ob_commit_update(ob_pop* p, const uint32_t* slots, const gr_update_commit* uc, uint32_t n, int32_t* status) {
+  if (!p) return GR_EINVAL;
+  int rc = GR_OK;
+  for (uint32_t x = 0; x < n; ++x) {
+    if (slots[x] >= p->peers.size()) return GR_ERANGE;
+    entryLog& l = *p->peers[slots[x]].r->log;
+    const gr_update_commit& u = uc[x];
+    if (u.applied_to > 0 && (u.applied_to < l.applied || u.applied_to > l.committed)) {
+      status[x] = 1;
+      rc = GR_ESTATE;
+      continue;
+    }
+    UpdateCommit c;
+    c.StableLogTo = u.stable_log_to;
+    c.StableLogTerm = u.stable_log_term;
+    c.AppliedTo = u.applied_to;
+    l.commitUpdate(c);
+    status[x] = 0;
+  }
+  return rc;
+}
+
 int ob_set_truncate_runs(ob_pop* p, int on) {
   if (!p) return GR_EINVAL;
   p->truncateRuns = on != 0;
@@ -687,6 +731,13 @@ int ob_step2(ob_pop* p, const gr_inbox* in, const uint32_t* limits, const gr_pee
           res.ready[q].ctx_high = r.readyToRead[q].ctx.High;
         }
         res.append_from = op.appendFrom;
+        // getUpdate (peer.go:311-337): the log marks and raftState() after the prefix
+        res.committed = r.log->committed;
+        res.last_index = r.log->lastIndex();
+        auto es = r.log->entriesToSave();
+        res.save_from = es.empty() ? 0 : es.front().Index;
+        res.term = r.term;
+        res.vote = r.vote;
       };
       // called before item `it` runs: arms the probe for the escalated item
       auto pre = [&](uint32_t it) {

@@ -40,6 +40,7 @@ def oracle_lib():
                                  c.POINTER(c.c_size_t), c.c_void_p, c.c_uint32, c.c_char_p, c.c_size_t]
         lib.ob_fetch_out.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
         lib.ob_set_truncate_runs.argtypes = [c.c_void_p, c.c_int]
+        lib.ob_commit_update.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_void_p]
         _olib = lib
     return _olib
 
@@ -52,6 +53,8 @@ def hostlane_lib():
         lib.hl_step.argtypes = [c.c_uint32, c.c_uint64, c.c_void_p, c.c_uint32, c.POINTER(abi.Inbox),
                                 c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t), c.c_void_p,
                                 c.POINTER(c.c_size_t)]
+        lib.hl_commit_update.argtypes = [c.c_uint32, c.c_void_p, c.c_uint32, c.c_void_p, c.c_void_p, c.c_uint32,
+                                         c.c_void_p]
         lib.hl_counters.argtypes = [c.POINTER(c.c_uint64), c.POINTER(c.c_uint64)]
         lib.hl_counters.restype = None
         lib.hl_tick_lanes.restype = c.c_uint64
@@ -90,6 +93,16 @@ class OraclePopulation:
         their first two runs (a prefix of the entries, as a size-limited send);
         parity runs leave this off and such a message is an error."""
         self.lib.ob_set_truncate_runs(self._h, 1 if on else 0)
+
+    def commit_update(self, slots, uc):
+        """entryLog.commitUpdate per slot (ob_commit_update): (rc, status)."""
+        slots = np.ascontiguousarray(slots, np.uint32)
+        uc = np.ascontiguousarray(uc, abi.UPDATE_COMMIT)
+        st = np.zeros(len(slots), np.int32)
+        rc = self.lib.ob_commit_update(self._h, slots.ctypes.data if len(slots) else None,
+                                       uc.ctypes.data if len(uc) else None, len(slots),
+                                       st.ctypes.data if len(st) else None)
+        return rc, st
 
     def export(self):
         out = np.zeros(self.n, abi.PEER)
@@ -194,3 +207,16 @@ def hostlane_affine_routes(in_pos, out_pos, slots):
     mode = lib.hl_detect_affine(in_pos.ctypes.data, out_pos.ctypes.data, in_pos.shape[1], slots,
                                 base.ctypes.data, ctypes.byref(g))
     return (base, g.value, "loopback" if mode == 2 else "affine") if mode else None
+
+
+def hostlane_commit_update(peers, idx, uc, slots=3):
+    """gr_commit_update on records with the engine's commit_marks (test-only).
+    Edits `peers` in place; returns (rc, status)."""
+    lib = hostlane_lib()
+    idx = np.ascontiguousarray(idx, np.uint32)
+    uc = np.ascontiguousarray(uc, abi.UPDATE_COMMIT)
+    st = np.zeros(len(idx), np.int32)
+    assert peers.flags["C_CONTIGUOUS"] and peers.dtype == abi.PEER
+    rc = lib.hl_commit_update(slots, peers.ctypes.data, len(peers), idx.ctypes.data if len(idx) else None,
+                              uc.ctypes.data if len(uc) else None, len(idx), st.ctypes.data if len(st) else None)
+    return rc, st

@@ -122,29 +122,37 @@ extern "C" int hl_step(uint32_t slots, uint64_t max_entry_size, gr_peer* peers, 
   }
   *n_results = nl;
   if (results) {
-    for (uint32_t l = 0; l < nl; ++l) {
-      gr_peer_result& pr = results[l];
-      memset(&pr, 0, sizeof(pr));
-      pr.peer = pk.peers[l];
-      const uint8_t rf = ln.u8(LR_RFLAGS)[l];
-      if (rf & RF_ESCALATED) {
-        pr.escalation = ln.u8(LR_ESC_REASON)[l];
-        pr.esc_item = ln.u32(LR_ESC_ITEM)[l];
-      }
-      derive_proposals(&pr, rf, ln.u8(LR_PROP_RESULT)[l], st.u64(SR_LAST_INDEX)[pk.peers[l]],
-                       ln.u32(LR_PROPOSE)[l], ln.u8(LR_FWD_COUNT)[l], ln.u32(LR_FWD_ENTRIES)[l]);
-      if (rf & RF_APPEND) pr.append_from = ln.u64(LR_APPEND_FROM)[l];
-      if (rf & RF_READY) {
-        pr.n_ready = ln.u8(LR_RTR_COUNT)[l];
-        for (int q = 0; q < pr.n_ready && q < GR_Q; ++q) {
-          pr.ready[q].index = ln.u64(LR_RTR_INDEX + q)[l];
-          pr.ready[q].ctx_low = ln.u64(LR_RTR_LO + q)[l];
-          pr.ready[q].ctx_high = ln.u64(LR_RTR_HI + q)[l];
-        }
-      }
-    }
+    for (uint32_t l = 0; l < nl; ++l) results[l] = make_result(ln, st, l, pk.peers[l]);
   }
   return GR_OK;
+}
+
+// gr_commit_update on records: the same commit_marks (gr_host.h) the device runs.
+extern "C" int hl_commit_update(uint32_t slots, gr_peer* peers, uint32_t n_peers, const uint32_t* list,
+                                const gr_update_commit* uc, uint32_t n, int32_t* status) {
+  const uint32_t S = inst(slots);
+  if (!S) return GR_EINVAL;
+  int rc = GR_OK;
+  for (uint32_t x = 0; x < n; ++x) {
+    if (list[x] >= n_peers) return GR_ERANGE;
+    gr_peer& g = peers[list[x]];
+    StateBase st;
+    st.cap = 64;
+    st.S = S;
+    std::vector<uint64_t> sbuf((state_bytes(S, st.cap) + 7) / 8, 0);
+    st.base = (uint8_t*)sbuf.data();
+    for (uint32_t row = 0; row < rows_u64(S); ++row) st.u64(row)[0] = get_u64_row(g, row, S);
+    for (uint32_t row = 0; row < rows_u8(S); ++row) st.u8(row)[0] = get_u8_row(g, row, S);
+    status[x] = commit_marks(st, 0, uc[x]);
+    if (status[x]) {
+      rc = GR_ESTATE;
+      continue;
+    }
+    g.saved_to = st.u64(SR_SAVED_TO)[0];
+    g.marker_index = st.u64(SR_MARKER)[0];
+    g.log_applied = st.u64(SR_LOG_APPLIED)[0];
+  }
+  return rc;
 }
 
 // lanes finished by the fast subset / by the general lane since load

@@ -16,7 +16,7 @@ from dragonboat_amd import abi
 SCALARS = ["term", "vote", "committed", "applied", "last_index", "first_index_m1", "leader_id",
            "leader_transfer_target", "node_id", "election_tick", "heartbeat_tick",
            "randomized_election_timeout", "election_timeout", "heartbeat_timeout", "entry_size_ub",
-           "state", "self_slot", "flags", "read_index_count"]
+           "state", "self_slot", "flags", "read_index_count", "saved_to", "marker_index", "log_applied"]
 MSG_FIELDS = ["type", "slot", "reject", "term", "log_index", "log_term", "commit", "hint", "hint_high",
               "n_entries", "n_runs", "run2_offset"]
 
@@ -96,10 +96,23 @@ def _exact_equal(eng, orc, S):
     return ok
 
 
+def normalize_marks(recs):
+    """gr_peer.marker_index == 0 means a freshly loaded group (gpuraft.h): the
+    engine and the oracle take marker = last + 1, saved_to = last, log_applied =
+    first_index_m1. Returns a copy with those values filled in."""
+    recs = recs.copy()
+    fresh = recs["marker_index"] == 0
+    recs["marker_index"] = np.where(fresh, recs["last_index"] + np.uint64(1), recs["marker_index"])
+    recs["saved_to"] = np.where(fresh, recs["last_index"], recs["saved_to"])
+    recs["log_applied"] = np.where(fresh, recs["first_index_m1"], recs["log_applied"])
+    return recs
+
+
 def compare_states(eng, orc, S, peers=None, limit=20):
     idx = np.arange(len(eng)) if peers is None else np.asarray(peers, np.int64)
     if len(idx) == 0:
         return []
+    eng, orc = normalize_marks(eng), normalize_marks(orc)
     same = _exact_equal(eng[idx], orc[idx], S)
     bad = []
     for p in idx[~same]:  # field by field (the window compared semantically)
@@ -150,9 +163,13 @@ def compare_msgs(eng_msgs, orc_msgs, limit=20):
     return bad
 
 
+RESULT_FIELDS = ["propose_result", "propose_first", "append_from", "n_ready", "n_forwarded", "forwarded_entries",
+                 "committed", "last_index", "save_from", "term", "vote"]
+
+
 def compare_results(eng_res, orc_res, limit=20):
     """eng_res: results per lane (peer field); orc_res: per peer (prefix results)."""
-    fields = ["propose_result", "propose_first", "append_from", "n_ready", "n_forwarded", "forwarded_entries"]
+    fields = RESULT_FIELDS
     if len(eng_res):
         o = orc_res[eng_res["peer"].astype(np.int64)]
         same = np.ones(len(eng_res), bool)
@@ -166,8 +183,7 @@ def compare_results(eng_res, orc_res, limit=20):
     for r in eng_res:
         p = int(r["peer"])
         o = orc_res[p]
-        fields = ["propose_result", "propose_first", "append_from", "n_ready", "n_forwarded",
-                  "forwarded_entries"]
+        fields = RESULT_FIELDS
         d = [f"{f}: engine={r[f]} oracle={o[f]}" for f in fields if r[f] != o[f]]
         for q in range(min(int(r["n_ready"]), abi.GR_Q)):
             if tuple(r["ready"][q]) != tuple(o["ready"][q]):
@@ -211,3 +227,21 @@ def check_escalations(results, esc_mask, limit=20):
             if len(bad) >= limit:
                 break
     return bad
+
+
+def update_commits(recs):
+    """The pb.UpdateCommit a host sends back after persisting and applying
+    everything a pass left (oracle commit_all: entriesToSave -> LogDB, AppliedTo =
+    committed), from exported records: abi.UPDATE_COMMIT per record."""
+    r = normalize_marks(recs)
+    last, mk, sv = r["last_index"], r["marker_index"], r["saved_to"]
+    idx = sv + np.uint64(1)
+    nothing = (idx - mk) > (last + np.uint64(1) - mk)  # uint64 wrap, inmemory.go:101-108
+    has = ~nothing & (idx <= last)
+    nr = r["n_runs"].astype(np.int64)
+    last_term = r["run_term"][np.arange(len(r)), np.maximum(nr - 1, 0)]
+    uc = np.zeros(len(r), abi.UPDATE_COMMIT)
+    uc["stable_log_to"] = np.where(has, last, 0)
+    uc["stable_log_term"] = np.where(has, last_term, 0)
+    uc["applied_to"] = np.where(r["committed"] > r["log_applied"], r["committed"], 0)
+    return uc

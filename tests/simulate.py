@@ -42,6 +42,11 @@ class HostlaneBackend:
     def notify_applied(self, idx, applied):
         self.state["applied"][idx] = applied
 
+    def commit_update(self, idx, uc):
+        from oracle.pyoracle import hostlane_commit_update
+        rc, st = hostlane_commit_update(self.state, idx, uc, self.slots)
+        assert rc == 0, (rc, st[st != 0][:5])
+
     def close(self):
         pass
 
@@ -66,6 +71,10 @@ class GpuBackend:
 
     def notify_applied(self, idx, applied):
         self.eng.notify_applied(np.asarray(idx, np.uint32), np.asarray(applied, np.uint64))
+
+    def commit_update(self, idx, uc):
+        rc, st = self.eng.commit_update(np.asarray(idx, np.uint32), uc)
+        assert rc == 0, (rc, st[st != 0][:5])
 
     def close(self):
         self.eng.close()
@@ -114,9 +123,11 @@ class Lockstep:
     def apply_all(self):
         """The host applies what is committed (node.handleEvents ->
         Peer.NotifyRaftLastApplied, peer.go:282-284): raft.applied = committed."""
+        keep = np.nonzero(~self.parked)[0]
+        uc = parity.update_commits(self.pop.export()[keep])  # what the host persisted and applied
         self.pop.commit_all()
         cur = self.pop.export()
-        keep = np.nonzero(~self.parked)[0]
+        self.eng.commit_update(keep, uc)  # entryLog.commitUpdate on the device
         self.eng.notify_applied(keep, cur["committed"][keep])
 
     def step(self, msgs, loc):
