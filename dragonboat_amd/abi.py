@@ -72,6 +72,17 @@ RESULT = np.dtype([
     ("committed", u64), ("last_index", u64), ("save_from", u64), ("term", u64), ("vote", u64),
     ("ready", READY, (GR_Q,)),
 ])
+# Compact boundary records (gr_step_compact)
+CM_REJECT, CM_ENTRY, CM_LOG_TERM, CM_COMMIT, CM_HINT, CM_EXT = 0x01, 0x02, 0x04, 0x08, 0x10, 0x80
+CL_CONFIG_CHANGE, CL_EXT = 0x01, 0x80
+CR_EXT = 0x80
+CMSG = np.dtype([("peer", u32), ("type", u8), ("slot", u8), ("flags", u8), ("pad", u8), ("term", u32),
+                 ("aux", u32), ("log_index", u64)])
+CLOCAL = np.dtype([("peer", u32), ("propose_entries", u32), ("ticks", np.uint16), ("quiesced_ticks", u8),
+                   ("flags", u8), ("ext", u32), ("rand", u64)])
+CRESULT = np.dtype([("peer", u32), ("escalation", u8), ("propose_result", u8), ("flags", u8), ("pad", u8),
+                    ("esc_item", u32), ("ext", u32), ("committed", u64), ("last_index", u64), ("save_from", u64)])
+assert CMSG.itemsize == 24 and CLOCAL.itemsize == 24 and CRESULT.itemsize == 40
 UPDATE_COMMIT = np.dtype([("stable_log_to", u64), ("stable_log_term", u64), ("applied_to", u64)])
 SIZES = {"gr_peer": 664, "gr_message": 80, "gr_local_input": 48, "gr_peer_result": 168,
          "gr_remote": 32, "gr_read_status": 32}
@@ -98,6 +109,29 @@ class Outbox(ctypes.Structure):
                 ("results", ctypes.c_void_p), ("n_results", ctypes.c_size_t)]
 
 
+class CInbox(ctypes.Structure):
+    _fields_ = [("msgs", ctypes.c_void_p), ("n_msgs", ctypes.c_size_t),
+                ("ext_msgs", ctypes.c_void_p), ("n_ext_msgs", ctypes.c_size_t),
+                ("locals", ctypes.c_void_p), ("n_locals", ctypes.c_size_t),
+                ("ext_locals", ctypes.c_void_p), ("n_ext_locals", ctypes.c_size_t)]
+
+
+class COutbox(ctypes.Structure):
+    _fields_ = [("msgs", ctypes.c_void_p), ("n_msgs", ctypes.c_size_t),
+                ("ext_msgs", ctypes.c_void_p), ("n_ext_msgs", ctypes.c_size_t),
+                ("results", ctypes.c_void_p), ("n_results", ctypes.c_size_t),
+                ("ext_results", ctypes.c_void_p), ("n_ext_results", ctypes.c_size_t)]
+
+
+def cinbox_of(msgs, ext, locals_, lext):
+    """A CInbox over numpy record arrays (kept alive by the caller)."""
+    ib = CInbox()
+    for name, a in (("msgs", msgs), ("ext_msgs", ext), ("locals", locals_), ("ext_locals", lext)):
+        setattr(ib, name, a.ctypes.data if len(a) else None)
+        setattr(ib, "n_" + name, len(a))
+    return ib
+
+
 class Stats(ctypes.Structure):
     _fields_ = [("passes", ctypes.c_uint64), ("leader_commits", ctypes.c_uint64),
                 ("follower_commits", ctypes.c_uint64), ("escalations", ctypes.c_uint64),
@@ -120,7 +154,8 @@ EXPORTS = [
     "gr_sync_groups_to_host", "gr_step", "gr_inbox_reserve", "gr_release_outbox", "gr_stats_get", "gr_stats_reset",
     "gr_load_peers", "gr_sync_peers_to_host", "gr_notify_applied", "gr_compact_log", "gr_commit_update", "gr_space_bytes", "gr_space_chunk_bytes",
     "gr_space_hot_chunk_bytes", "gr_space_cold_used", "gr_bind_routes",
-    "gr_set_locals", "gr_step_device",
+    "gr_set_locals", "gr_step_device", "gr_step_compact", "gr_cinbox_reserve", "gr_release_coutbox",
+    "gr_pack_messages", "gr_unpack_messages", "gr_pack_locals",
     "gr_collect_results", "gr_space_decode", "gr_space_encode", "gr_timing_begin", "gr_timing_end",
 ]
 

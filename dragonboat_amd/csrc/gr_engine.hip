@@ -94,6 +94,9 @@ struct gr_engine {
   Buf d_scal;               // lane count, error, outbox total
   Buf d_outmsgs, d_results; // packed outbox
   Buf d_peers, d_slots;     // gr_peer records of a load/sync, slot list
+  Buf d_ext, d_lext;        // gr_step_compact: ext message / local records
+  Buf d_oc64, d_off64, d_rx, d_roff;  // compact outbox counts and offsets
+  Buf d_outext, d_resext;   // compact outbox ext records
   uint8_t* h_inmsgs = nullptr;   // pinned inbox the caller may fill in place (gr_inbox_reserve)
   uint8_t* h_inlocals = nullptr;
   size_t h_inmsgs_bytes = 0, h_inlocals_bytes = 0;
@@ -101,6 +104,12 @@ struct gr_engine {
   uint8_t* h_results = nullptr;
   uint8_t* h_scal = nullptr;
   size_t h_outmsgs_bytes = 0, h_results_bytes = 0, h_scal_bytes = 0;
+  uint8_t* h_inext = nullptr;  // gr_cinbox_reserve's ext arrays (the compact ones reuse h_inmsgs / h_inlocals)
+  uint8_t* h_inlext = nullptr;
+  size_t h_inext_bytes = 0, h_inlext_bytes = 0;
+  uint8_t* h_outext = nullptr;  // gr_step_compact's ext outputs (the compact ones reuse h_outmsgs / h_results)
+  uint8_t* h_resext = nullptr;
+  size_t h_outext_bytes = 0, h_resext_bytes = 0;
   std::mutex mu;  // one host-path pass at a time per engine
 };
 
@@ -229,6 +238,31 @@ int io_scan(gr_engine* e, const uint32_t* in, uint32_t* out, uint32_t n, hipStre
   return GR_OK;
 }
 
+int io_scan64(gr_engine* e, const uint64_t* in, uint64_t* out, uint32_t n, hipStream_t s) {
+  size_t tb = 0;
+  HIPCHK(rocprim::exclusive_scan(nullptr, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
+  const int r = grow_device(&e->d_tmp.p, &e->d_tmp.n, tb);
+  if (r) return r;
+  tb = e->d_tmp.n;
+  HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
+  return GR_OK;
+}
+
+// Stable radix sort of the inbox's mailbox keys (slot-major j*nl + lane), so
+// arrival order inside a mailbox survives; sorted keys/indexes in d_skeys/d_sidx.
+int sort_keys(gr_engine* e, uint32_t nm, uint32_t positions, hipStream_t s) {
+  uint32_t bits = 1;
+  while (bits < 32 && (1ull << bits) < positions) ++bits;
+  size_t tb = 0;
+  HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, (uint32_t*)e->d_keys.p, (uint32_t*)e->d_skeys.p,
+                                   (uint32_t*)e->d_idx.p, (uint32_t*)e->d_sidx.p, (size_t)nm, 0, bits, s));
+  const int r = grow_device(&e->d_tmp.p, &e->d_tmp.n, tb);
+  if (r) return r;
+  tb = e->d_tmp.n;
+  HIPCHK(rocprim::radix_sort_pairs(e->d_tmp.p, tb, (uint32_t*)e->d_keys.p, (uint32_t*)e->d_skeys.p,
+                                   (uint32_t*)e->d_idx.p, (uint32_t*)e->d_sidx.p, (size_t)nm, 0, bits, s));
+  return GR_OK;
+}
 
 }  // namespace
 
@@ -316,9 +350,12 @@ void gr_destroy(gr_engine* e) {
   free_timings(e);
   for (gr_engine::Buf* b : {&e->d_in, &e->d_out, &e->d_msgs, &e->d_locals, &e->d_mark, &e->d_lop, &e->d_keys,
                             &e->d_idx, &e->d_skeys, &e->d_sidx, &e->d_win, &e->d_oc, &e->d_off, &e->d_tmp,
-                            &e->d_scal, &e->d_outmsgs, &e->d_results, &e->d_peers, &e->d_slots})
+                            &e->d_scal, &e->d_outmsgs, &e->d_results, &e->d_peers, &e->d_slots, &e->d_ext,
+                            &e->d_lext, &e->d_oc64, &e->d_off64, &e->d_rx, &e->d_roff, &e->d_outext,
+                            &e->d_resext})
     if (b->p) (void)hipFree(b->p);
-  for (uint8_t* h : {e->h_outmsgs, e->h_results, e->h_scal, e->h_inmsgs, e->h_inlocals})
+  for (uint8_t* h : {e->h_outmsgs, e->h_results, e->h_scal, e->h_inmsgs, e->h_inlocals, e->h_inext, e->h_inlext,
+                     e->h_outext, e->h_resext})
     if (h) (void)hipHostFree(h);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -591,15 +628,7 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
     hipLaunchKernelGGL(io::msg_keys, dim3(io_grid(nm)), blk, 0, s, dmsgs, nm, (const uint32_t*)lop, nl,
                        (uint32_t*)e->d_keys.p, (uint32_t*)e->d_idx.p);
     HIPCHK(hipGetLastError());
-    uint32_t bits = 1;
-    while (bits < 32 && (1ull << bits) < positions) ++bits;
-    size_t tb = 0;
-    HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, (uint32_t*)e->d_keys.p, (uint32_t*)e->d_skeys.p,
-                                     (uint32_t*)e->d_idx.p, (uint32_t*)e->d_sidx.p, (size_t)nm, 0, bits, s));
-    if ((r = grow_device(&e->d_tmp.p, &e->d_tmp.n, tb))) return r;
-    tb = e->d_tmp.n;
-    HIPCHK(rocprim::radix_sort_pairs(e->d_tmp.p, tb, (uint32_t*)e->d_keys.p, (uint32_t*)e->d_skeys.p,
-                                     (uint32_t*)e->d_idx.p, (uint32_t*)e->d_sidx.p, (size_t)nm, 0, bits, s));
+    if ((r = sort_keys(e, nm, positions, s))) return r;
     hipLaunchKernelGGL(io::encode_sorted, dim3(io_grid(nm)), blk, 0, s, dmsgs, (const uint32_t*)e->d_skeys.p,
                        (const uint32_t*)e->d_sidx.p, nm, vin);
     HIPCHK(hipGetLastError());
@@ -659,6 +688,228 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
   out->n_msgs = total;
   out->results = (gr_peer_result*)e->h_results;
   out->n_results = nl;
+  return GR_OK;
+}
+
+// gr_step with compact records (gpuraft.h gr_cmsg / gr_clocal / gr_cresult):
+// the same device passes; records expand in registers on the way in and are
+// packed (with ext records for what does not fit) on the way out.
+int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out) {
+  if (!e || !in || !out) return GR_EINVAL;
+  if ((in->n_msgs && !in->msgs) || (in->n_locals && !in->locals) || (in->n_ext_msgs && !in->ext_msgs) ||
+      (in->n_ext_locals && !in->ext_locals))
+    return GR_EINVAL;
+  if (in->n_msgs + in->n_locals >= 0x80000000ull || in->n_ext_msgs >= 0x80000000ull ||
+      in->n_ext_locals >= 0x80000000ull)
+    return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  memset(out, 0, sizeof(*out));
+  const uint32_t S = e->S, cap = e->cfg.max_peers;
+  const uint32_t nm = (uint32_t)in->n_msgs, nlc = (uint32_t)in->n_locals;
+  const uint32_t nx = (uint32_t)in->n_ext_msgs, nlx = (uint32_t)in->n_ext_locals;
+  if (nm + nlc == 0) return GR_OK;
+  const hipStream_t s = e->stream;
+  const dim3 blk(io::kIoBlock);
+  int r;
+  // ---- inbox records -> lanes
+  if ((r = grow_device(&e->d_msgs.p, &e->d_msgs.n, (size_t)nm * sizeof(gr_cmsg) + 1))) return r;
+  if ((r = grow_device(&e->d_locals.p, &e->d_locals.n, (size_t)nlc * sizeof(gr_clocal) + 1))) return r;
+  if ((r = grow_device(&e->d_ext.p, &e->d_ext.n, (size_t)nx * sizeof(gr_message) + 1))) return r;
+  if ((r = grow_device(&e->d_lext.p, &e->d_lext.n, (size_t)nlx * sizeof(gr_local_input) + 1))) return r;
+  if ((r = grow_device(&e->d_mark.p, &e->d_mark.n, (size_t)cap * 4))) return r;
+  if ((r = grow_device(&e->d_lop.p, &e->d_lop.n, (size_t)cap * 4))) return r;
+  if ((r = grow_device(&e->d_scal.p, &e->d_scal.n, 16))) return r;
+  if ((r = grow_pinned(&e->h_scal, &e->h_scal_bytes, 16))) return r;
+  uint32_t* mark = (uint32_t*)e->d_mark.p;
+  uint32_t* lop = (uint32_t*)e->d_lop.p;
+  uint32_t* scal = (uint32_t*)e->d_scal.p;
+  io::CInbox ci;
+  ci.msgs = (const gr_cmsg*)e->d_msgs.p;
+  ci.ext = (const gr_message*)e->d_ext.p;
+  ci.loc = (const gr_clocal*)e->d_locals.p;
+  ci.lext = (const gr_local_input*)e->d_lext.p;
+  ci.n_msgs = nm;
+  ci.n_ext = nx;
+  ci.n_loc = nlc;
+  ci.n_lext = nlx;
+  if (nm) HIPCHK(hipMemcpyAsync(e->d_msgs.p, in->msgs, (size_t)nm * sizeof(gr_cmsg), hipMemcpyHostToDevice, s));
+  if (nlc) HIPCHK(hipMemcpyAsync(e->d_locals.p, in->locals, (size_t)nlc * sizeof(gr_clocal), hipMemcpyHostToDevice, s));
+  if (nx) HIPCHK(hipMemcpyAsync(e->d_ext.p, in->ext_msgs, (size_t)nx * sizeof(gr_message), hipMemcpyHostToDevice, s));
+  if (nlx)
+    HIPCHK(hipMemcpyAsync(e->d_lext.p, in->ext_locals, (size_t)nlx * sizeof(gr_local_input), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(mark, 0, (size_t)cap * 4, s));
+  HIPCHK(hipMemsetAsync(scal, 0, 16, s));
+  hipLaunchKernelGGL(io::mark_inputs_c, dim3(io_grid(nm + nlc)), blk, 0, s, ci, S, cap, mark, scal + 1);
+  HIPCHK(hipGetLastError());
+  if ((r = io_scan(e, mark, lop, cap, s))) return r;
+  hipLaunchKernelGGL(io::finish_lanes, dim3(1), dim3(64), 0, s, (const uint32_t*)mark, (const uint32_t*)lop, cap,
+                     (const uint32_t*)(scal + 1), scal);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->h_scal, scal, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const uint32_t nl = ((uint32_t*)e->h_scal)[0];
+  if (((uint32_t*)e->h_scal)[1]) return GR_EINVAL;  // nothing of the pass ran
+  if (nl == 0) return GR_OK;
+  uint32_t* peer_of_lane = e->ln.u32(LR_LANE_PEER);
+  hipLaunchKernelGGL(io::lane_peers, dim3(io_grid(cap)), blk, 0, s, (const uint32_t*)mark, (const uint32_t*)lop, cap,
+                     peer_of_lane);
+  HIPCHK(hipGetLastError());
+  // ---- mailboxes
+  const uint32_t positions = nl * S;
+  const size_t space = gr_space_bytes(1, positions, GR_C);
+  if ((r = grow_device(&e->d_in.p, &e->d_in.n, space))) return r;
+  if ((r = grow_device(&e->d_out.p, &e->d_out.n, space))) return r;
+  const SpaceView vin = make_view(e->d_in.p, 1, positions), vout = make_view(e->d_out.p, 1, positions);
+  HIPCHK(hipMemsetAsync(e->d_in.p, 0, vin.pc, s));  // the count bytes
+  if (nm) {
+    for (gr_engine::Buf* b : {&e->d_keys, &e->d_idx, &e->d_skeys, &e->d_sidx})
+      if ((r = grow_device(&b->p, &b->n, (size_t)nm * 4))) return r;
+    hipLaunchKernelGGL(io::msg_keys_c, dim3(io_grid(nm)), blk, 0, s, ci.msgs, nm, (const uint32_t*)lop, nl,
+                       (uint32_t*)e->d_keys.p, (uint32_t*)e->d_idx.p);
+    HIPCHK(hipGetLastError());
+    if ((r = sort_keys(e, nm, positions, s))) return r;
+    hipLaunchKernelGGL(io::encode_sorted_c, dim3(io_grid(nm)), blk, 0, s, ci, (const uint32_t*)e->d_skeys.p,
+                       (const uint32_t*)e->d_sidx.p, vin);
+    HIPCHK(hipGetLastError());
+  }
+  // ---- locals -> lane rows
+  if ((r = grow_device(&e->d_win.p, &e->d_win.n, (size_t)nl * 4))) return r;
+  HIPCHK(hipMemsetAsync(e->d_win.p, 0, (size_t)nl * 4, s));
+  if (nlc) {
+    hipLaunchKernelGGL(io::local_winner_c, dim3(io_grid(nlc)), blk, 0, s, ci.loc, nlc, (const uint32_t*)lop,
+                       (uint32_t*)e->d_win.p);
+    HIPCHK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(io::fill_locals_c, dim3(io_grid(nl)), blk, 0, s, ci, (const uint32_t*)e->d_win.p, nl, e->ln);
+  HIPCHK(hipGetLastError());
+  // ---- the pass
+  StepParams kp = base_params(e);
+  kp.has_locals = 1;
+  kp.has_lane_peer = 1;
+  kp.route_mode = RT_IDENTITY;
+  kp.in = vin;
+  kp.out = vout;
+  kp.n_lanes = nl;
+  HIPCHK(launch_slots(S, kp, e->bail, e->counters, e->cap, (uint32_t)e->launches++, s, next_timing(e)));
+  e->passes++;
+  e->locals_set = false;
+  e->routes_bound = false;
+  // ---- outbox mailboxes + lane results -> compact records (+ ext)
+  if ((r = grow_device(&e->d_oc64.p, &e->d_oc64.n, (size_t)nl * 8))) return r;
+  if ((r = grow_device(&e->d_off64.p, &e->d_off64.n, (size_t)nl * 8))) return r;
+  if ((r = grow_device(&e->d_rx.p, &e->d_rx.n, (size_t)nl * 4))) return r;
+  if ((r = grow_device(&e->d_roff.p, &e->d_roff.n, (size_t)nl * 4))) return r;
+  if ((r = grow_device(&e->d_results.p, &e->d_results.n, (size_t)nl * sizeof(gr_cresult)))) return r;
+  uint64_t* oc = (uint64_t*)e->d_oc64.p;
+  uint64_t* off = (uint64_t*)e->d_off64.p;
+  uint32_t* rx = (uint32_t*)e->d_rx.p;
+  uint32_t* roff = (uint32_t*)e->d_roff.p;
+  hipLaunchKernelGGL(io::out_counts_c, dim3(io_grid(nl)), blk, 0, s, vout, e->ln, nl, S, oc, rx);
+  HIPCHK(hipGetLastError());
+  if ((r = io_scan64(e, oc, off, nl, s))) return r;
+  if ((r = io_scan(e, rx, roff, nl, s))) return r;
+  hipLaunchKernelGGL(io::finish_total_c, dim3(1), dim3(64), 0, s, (const uint64_t*)oc, (const uint64_t*)off,
+                     (const uint32_t*)rx, (const uint32_t*)roff, nl, scal + 1);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->h_scal + 4, scal + 1, 12, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const uint32_t total = ((uint32_t*)e->h_scal)[1], text = ((uint32_t*)e->h_scal)[2], rext = ((uint32_t*)e->h_scal)[3];
+  const size_t mbytes = (size_t)total * sizeof(gr_cmsg), xbytes = (size_t)text * sizeof(gr_message);
+  const size_t rbytes = (size_t)nl * sizeof(gr_cresult), rxbytes = (size_t)rext * sizeof(gr_peer_result);
+  if ((r = grow_device(&e->d_outmsgs.p, &e->d_outmsgs.n, mbytes + 1))) return r;
+  if ((r = grow_device(&e->d_outext.p, &e->d_outext.n, xbytes + 1))) return r;
+  if ((r = grow_device(&e->d_resext.p, &e->d_resext.n, rxbytes + 1))) return r;
+  if ((r = grow_pinned(&e->h_outmsgs, &e->h_outmsgs_bytes, mbytes + 1))) return r;
+  if ((r = grow_pinned(&e->h_outext, &e->h_outext_bytes, xbytes + 1))) return r;
+  if ((r = grow_pinned(&e->h_results, &e->h_results_bytes, rbytes))) return r;
+  if ((r = grow_pinned(&e->h_resext, &e->h_resext_bytes, rxbytes + 1))) return r;
+  hipLaunchKernelGGL(io::pack_results_c, dim3(io_grid(nl)), blk, 0, s, e->ln, e->st, (const uint32_t*)peer_of_lane,
+                     nl, (const uint32_t*)roff, (gr_cresult*)e->d_results.p, (gr_peer_result*)e->d_resext.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->h_results, e->d_results.p, rbytes, hipMemcpyDeviceToHost, s));
+  if (rext) HIPCHK(hipMemcpyAsync(e->h_resext, e->d_resext.p, rxbytes, hipMemcpyDeviceToHost, s));
+  if (total) {
+    hipLaunchKernelGGL(io::pack_outbox_c, dim3(io_grid(nl)), blk, 0, s, vout, nl, S, (const uint64_t*)off,
+                       (const uint32_t*)peer_of_lane, (gr_cmsg*)e->d_outmsgs.p, (gr_message*)e->d_outext.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(e->h_outmsgs, e->d_outmsgs.p, mbytes, hipMemcpyDeviceToHost, s));
+    if (text) HIPCHK(hipMemcpyAsync(e->h_outext, e->d_outext.p, xbytes, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  out->msgs = total ? (gr_cmsg*)e->h_outmsgs : nullptr;
+  out->n_msgs = total;
+  out->ext_msgs = text ? (gr_message*)e->h_outext : nullptr;
+  out->n_ext_msgs = text;
+  out->results = (gr_cresult*)e->h_results;
+  out->n_results = nl;
+  out->ext_results = rext ? (gr_peer_result*)e->h_resext : nullptr;
+  out->n_ext_results = rext;
+  return GR_OK;
+}
+
+int gr_cinbox_reserve(gr_engine* e, size_t n_msgs, size_t n_ext_msgs, size_t n_locals, size_t n_ext_locals,
+                      gr_cinbox* in) {
+  if (!e || !in || n_msgs + n_locals >= 0x80000000ull || n_ext_msgs >= 0x80000000ull ||
+      n_ext_locals >= 0x80000000ull)
+    return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  int r;
+  if ((r = grow_pinned(&e->h_inmsgs, &e->h_inmsgs_bytes, n_msgs * sizeof(gr_cmsg) + 1))) return r;
+  if ((r = grow_pinned(&e->h_inlocals, &e->h_inlocals_bytes, n_locals * sizeof(gr_clocal) + 1))) return r;
+  if ((r = grow_pinned(&e->h_inext, &e->h_inext_bytes, n_ext_msgs * sizeof(gr_message) + 1))) return r;
+  if ((r = grow_pinned(&e->h_inlext, &e->h_inlext_bytes, n_ext_locals * sizeof(gr_local_input) + 1))) return r;
+  in->msgs = (const gr_cmsg*)e->h_inmsgs;
+  in->n_msgs = n_msgs;
+  in->ext_msgs = (const gr_message*)e->h_inext;
+  in->n_ext_msgs = n_ext_msgs;
+  in->locals = (const gr_clocal*)e->h_inlocals;
+  in->n_locals = n_locals;
+  in->ext_locals = (const gr_local_input*)e->h_inlext;
+  in->n_ext_locals = n_ext_locals;
+  return GR_OK;
+}
+
+int gr_release_coutbox(gr_engine* e, gr_coutbox* out) {
+  if (!e || !out) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);  // the pinned buffers stay for the next pass
+  memset(out, 0, sizeof(*out));
+  return GR_OK;
+}
+
+int gr_pack_messages(const gr_message* in, size_t n, gr_cmsg* out, gr_message* ext, size_t* n_ext) {
+  if ((n && (!in || !out || !ext)) || !n_ext) return GR_EINVAL;
+  size_t x = 0;
+  for (size_t k = 0; k < n; ++k) {
+    if (!host::cmsg_of(in[k], &out[k])) {
+      out[k].flags = GR_CM_EXT;
+      out[k].aux = (uint32_t)x;
+      ext[x++] = in[k];
+    }
+  }
+  *n_ext = x;
+  return GR_OK;
+}
+
+int gr_unpack_messages(const gr_cmsg* in, size_t n, const gr_message* ext, size_t n_ext, gr_message* out) {
+  if (n && (!in || !out)) return GR_EINVAL;
+  for (size_t k = 0; k < n; ++k) {
+    if ((in[k].flags & GR_CM_EXT) && (!ext || in[k].aux >= n_ext)) return GR_EINVAL;
+    out[k] = host::expand_cmsg(in[k], ext);
+  }
+  return GR_OK;
+}
+
+int gr_pack_locals(const gr_local_input* in, size_t n, gr_clocal* out, gr_local_input* ext, size_t* n_ext) {
+  if ((n && (!in || !out || !ext)) || !n_ext) return GR_EINVAL;
+  size_t x = 0;
+  for (size_t k = 0; k < n; ++k) {
+    if (!host::clocal_of(in[k], &out[k])) {
+      out[k].flags = GR_CL_EXT;
+      out[k].ext = (uint32_t)x;
+      ext[x++] = in[k];
+    }
+  }
+  *n_ext = x;
   return GR_OK;
 }
 

@@ -381,6 +381,122 @@ __host__ __device__ inline int32_t commit_marks(const StateBase& st, uint32_t p,
   return 0;
 }
 
+// ---- compact boundary records (gpuraft.h gr_cmsg / gr_clocal / gr_cresult)
+// Compact form of a message, or false when it needs an ext record. The
+// compact record always carries peer, type and slot (the sort keys).
+__host__ __device__ inline bool cmsg_of(const gr_message& m, gr_cmsg* c) {
+  c->peer = m.peer;
+  c->type = m.type;
+  c->slot = m.slot;
+  c->flags = 0;
+  c->pad = 0;
+  c->term = (uint32_t)m.term;
+  c->aux = 0;
+  c->log_index = m.log_index;
+  if ((m.term >> 32) || m.hint_high || m.run2_offset || m.run_term[1] || m.reject > 1) return false;
+  uint8_t fl = m.reject ? GR_CM_REJECT : 0;
+  if (m.n_entries) {
+    if (m.n_entries != 1 || m.n_runs != 1 || m.run_term[0] != m.term) return false;
+    fl |= GR_CM_ENTRY;
+  } else if (m.n_runs || m.run_term[0]) {
+    return false;
+  }
+  if (m.log_term) {
+    if (m.log_term != m.term) return false;
+    fl |= GR_CM_LOG_TERM;
+  }
+  if (m.commit && m.hint) return false;
+  uint32_t d = 0;
+  if (m.commit) {
+    if (!commit_delta(m.commit, m.log_index, &d)) return false;
+    fl |= GR_CM_COMMIT;
+  }
+  if (m.hint) {
+    if (!commit_delta(m.hint, m.log_index, &d)) return false;
+    fl |= GR_CM_HINT;
+  }
+  c->aux = d;
+  c->flags = fl;
+  return true;
+}
+// The full record of a compact one (not GR_CM_EXT).
+__host__ __device__ inline gr_message msg_of(const gr_cmsg& c) {
+  gr_message m{};
+  m.peer = c.peer;
+  m.type = c.type;
+  m.slot = c.slot;
+  m.reject = (c.flags & GR_CM_REJECT) ? 1 : 0;
+  m.term = c.term;
+  m.log_index = c.log_index;
+  if (c.flags & GR_CM_LOG_TERM) m.log_term = m.term;
+  if (c.flags & GR_CM_COMMIT) m.commit = commit_of(c.aux, m.log_index);
+  if (c.flags & GR_CM_HINT) m.hint = commit_of(c.aux, m.log_index);
+  if (c.flags & GR_CM_ENTRY) {
+    m.n_entries = 1;
+    m.n_runs = 1;
+    m.run_term[0] = m.term;
+  }
+  return m;
+}
+__host__ __device__ inline int validate_cmsg(const gr_cmsg& c, const gr_message* ext, uint32_t n_ext, uint32_t S,
+                                             uint32_t cap) {
+  if (c.peer >= cap || c.slot >= S || c.type > GR_TIMEOUT_NOW) return GR_EINVAL;
+  if (c.flags & GR_CM_EXT) {
+    if (c.aux >= n_ext) return GR_EINVAL;
+    const gr_message& m = ext[c.aux];
+    if (m.peer != c.peer || m.slot != c.slot || m.type != c.type) return GR_EINVAL;
+    return validate_msg(m, S, cap);
+  }
+  if (c.flags & 0x60) return GR_EINVAL;
+  if ((c.flags & GR_CM_COMMIT) && (c.flags & GR_CM_HINT)) return GR_EINVAL;
+  return GR_OK;
+}
+__host__ __device__ inline gr_message expand_cmsg(const gr_cmsg& c, const gr_message* ext) {
+  return (c.flags & GR_CM_EXT) ? ext[c.aux] : msg_of(c);
+}
+__host__ __device__ inline bool clocal_of(const gr_local_input& x, gr_clocal* c) {
+  c->peer = x.peer;
+  c->propose_entries = x.propose_entries;
+  c->ticks = (uint16_t)x.ticks;
+  c->quiesced_ticks = (uint8_t)x.quiesced_ticks;
+  c->flags = x.propose_has_config_change ? GR_CL_CONFIG_CHANGE : 0;
+  c->ext = 0;
+  c->rand = x.rand;
+  return !(x.read_index || x.read_ctx_low || x.read_ctx_high || x.ticks > 0xFFFFu || x.quiesced_ticks > 0xFFu ||
+           x.propose_has_config_change > 1);
+}
+__host__ __device__ inline gr_local_input expand_clocal(const gr_clocal& c, const gr_local_input* ext) {
+  if (c.flags & GR_CL_EXT) return ext[c.ext];
+  gr_local_input x{};
+  x.peer = c.peer;
+  x.propose_entries = c.propose_entries;
+  x.ticks = c.ticks;
+  x.quiesced_ticks = c.quiesced_ticks;
+  x.propose_has_config_change = (c.flags & GR_CL_CONFIG_CHANGE) ? 1 : 0;
+  x.rand = c.rand;
+  return x;
+}
+__host__ __device__ inline bool validate_clocal(const gr_clocal& c, const gr_local_input* ext, uint32_t n_ext,
+                                                uint32_t cap) {
+  if (c.peer >= cap || (c.flags & ~(GR_CL_EXT | GR_CL_CONFIG_CHANGE))) return false;
+  return !(c.flags & GR_CL_EXT) || (c.ext < n_ext && ext[c.ext].peer == c.peer);
+}
+// A lane's result needs the full record (ReadyToRead, forwarded batches, State change).
+__host__ __device__ inline bool result_needs_ext(uint8_t rf) {
+  return (rf & (RF_READY | RF_FORWARDED | RF_HARDSTATE)) != 0;
+}
+__host__ __device__ inline gr_cresult cresult_of(const gr_peer_result& r) {
+  gr_cresult c{};
+  c.peer = r.peer;
+  c.escalation = r.escalation;
+  c.propose_result = r.propose_result;
+  c.esc_item = r.esc_item;
+  c.committed = r.committed;
+  c.last_index = r.last_index;
+  c.save_from = r.save_from;
+  return c;
+}
+
 inline uint64_t space_total_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth = GR_C) {
   return (uint64_t)n_chunks * space_chunk_bytes_pc(space_pad_positions(positions), depth);
 }

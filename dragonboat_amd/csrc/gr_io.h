@@ -155,6 +155,140 @@ __global__ void pack_results(LaneBase L, StateBase st, const uint32_t* peer_of_l
     out[x] = host::make_result(L, st, first + x, peer_of_lane ? peer_of_lane[x] : first + x);
 }
 
+// ---- compact records (gr_step_compact): the same passes over gr_cmsg /
+// gr_clocal, with ext records for what does not fit (gr_host.h codec).
+struct CInbox {
+  const gr_cmsg* msgs;
+  const gr_message* ext;
+  const gr_clocal* loc;
+  const gr_local_input* lext;
+  uint32_t n_msgs, n_ext, n_loc, n_lext;
+};
+
+__global__ void mark_inputs_c(CInbox in, uint32_t S, uint32_t cap, uint32_t* mark, uint32_t* err) {
+  for (uint32_t k = io_tid(); k < in.n_msgs + in.n_loc; k += io_stride()) {
+    if (k < in.n_msgs) {
+      const gr_cmsg c = in.msgs[k];
+      if (host::validate_cmsg(c, in.ext, in.n_ext, S, cap) != GR_OK) {
+        atomicOr(err, 1u);
+        continue;
+      }
+      mark[c.peer] = 1;
+    } else {
+      const gr_clocal c = in.loc[k - in.n_msgs];
+      if (!host::validate_clocal(c, in.lext, in.n_lext, cap)) {
+        atomicOr(err, 1u);
+        continue;
+      }
+      mark[c.peer] = 1;
+    }
+  }
+}
+
+__global__ void msg_keys_c(const gr_cmsg* msgs, uint32_t n, const uint32_t* lane_of_peer, uint32_t nl, uint32_t* keys,
+                           uint32_t* idx) {
+  for (uint32_t k = io_tid(); k < n; k += io_stride()) {
+    keys[k] = (uint32_t)msgs[k].slot * nl + lane_of_peer[msgs[k].peer];
+    idx[k] = k;
+  }
+}
+
+// encode_sorted over compact records (expanded in registers).
+__global__ void encode_sorted_c(CInbox in, const uint32_t* skeys, const uint32_t* sidx, SpaceView v) {
+  const uint32_t n = in.n_msgs;
+  for (uint32_t s = io_tid(); s < n; s += io_stride()) {
+    const uint32_t key = skeys[s];
+    uint32_t r = 0;
+    while (r <= (uint32_t)GR_C && r < s && skeys[s - r - 1] == key) ++r;
+    const Mailbox mb = v.at(key);
+    if (r < (uint32_t)GR_C) host::encode_msg(mb, r, host::expand_cmsg(in.msgs[sidx[s]], in.ext));
+    if (s + 1 == n || skeys[s + 1] != key) mb.cnt() = (uint8_t)(r < (uint32_t)GR_C ? r + 1 : GR_C + 1);
+  }
+}
+
+__global__ void local_winner_c(const gr_clocal* loc, uint32_t n, const uint32_t* lane_of_peer, uint32_t* win) {
+  for (uint32_t k = io_tid(); k < n; k += io_stride()) atomicMax(win + lane_of_peer[loc[k].peer], k + 1);
+}
+
+__global__ void fill_locals_c(CInbox in, const uint32_t* win, uint32_t nl, LaneBase L) {
+  for (uint32_t l = io_tid(); l < nl; l += io_stride()) {
+    gr_local_input x{};
+    if (win[l]) x = host::expand_clocal(in.loc[win[l] - 1], in.lext);
+    host::locals_to_rows(x, L.u32(LR_TICKS) + l, L.u32(LR_QTICKS) + l, L.u32(LR_PROPOSE) + l, L.u8(LR_LFLAGS) + l,
+                         L.u64(LR_RI_LO) + l, L.u64(LR_RI_HI) + l, L.u64(LR_RAND) + l, L.u32(LR_LWORD) + l);
+  }
+}
+
+// Per lane: messages (high word) and those needing an ext record (low word) in
+// one u64, so one scan gives both output offsets; rx = 1 when the result needs
+// the full record.
+__global__ void out_counts_c(SpaceView out, LaneBase L, uint32_t nl, uint32_t S, uint64_t* oc, uint32_t* rx) {
+  for (uint32_t l = io_tid(); l < nl; l += io_stride()) {
+    uint32_t c = 0, e = 0;
+    for (uint32_t j = 0; j < S; ++j) {
+      const Mailbox mb = out.at(j * nl + l);
+      const uint32_t x = mb.cnt() & MB_COUNT;
+      const uint32_t cnt = x < (uint32_t)GR_C ? x : (uint32_t)GR_C;
+      c += cnt;
+      for (uint32_t k = 0; k < cnt; ++k) {
+        gr_cmsg cm;
+        if (!host::cmsg_of(host::decode_msg(mb, k), &cm)) ++e;
+      }
+    }
+    oc[l] = ((uint64_t)c << 32) | e;
+    rx[l] = host::result_needs_ext(L.u8(LR_RFLAGS)[l]) ? 1u : 0u;
+  }
+}
+
+__global__ void finish_total_c(const uint64_t* oc, const uint64_t* off, const uint32_t* rx, const uint32_t* roff,
+                               uint32_t nl, uint32_t* total3) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const uint64_t t = nl ? off[nl - 1] + oc[nl - 1] : 0;
+    total3[0] = (uint32_t)(t >> 32);
+    total3[1] = (uint32_t)t;
+    total3[2] = nl ? roff[nl - 1] + rx[nl - 1] : 0;
+  }
+}
+
+__global__ void pack_outbox_c(SpaceView out, uint32_t nl, uint32_t S, const uint64_t* off, const uint32_t* peer_of_lane,
+                              gr_cmsg* rec, gr_message* ext) {
+  for (uint32_t l = io_tid(); l < nl; l += io_stride()) {
+    uint32_t o = (uint32_t)(off[l] >> 32), eo = (uint32_t)off[l];
+    const uint32_t peer = peer_of_lane[l];
+    for (uint32_t j = 0; j < S; ++j) {
+      const Mailbox mb = out.at(j * nl + l);
+      const uint32_t x = mb.cnt() & MB_COUNT;
+      const uint32_t c = x < (uint32_t)GR_C ? x : (uint32_t)GR_C;
+      for (uint32_t k = 0; k < c; ++k) {
+        gr_message m = host::decode_msg(mb, k);
+        m.peer = peer;
+        m.slot = (uint8_t)j;
+        gr_cmsg cm;
+        if (!host::cmsg_of(m, &cm)) {
+          cm.flags = GR_CM_EXT;
+          cm.aux = eo;
+          ext[eo++] = m;
+        }
+        rec[o++] = cm;
+      }
+    }
+  }
+}
+
+__global__ void pack_results_c(LaneBase L, StateBase st, const uint32_t* peer_of_lane, uint32_t nl,
+                               const uint32_t* roff, gr_cresult* out, gr_peer_result* ext) {
+  for (uint32_t l = io_tid(); l < nl; l += io_stride()) {
+    const gr_peer_result pr = host::make_result(L, st, l, peer_of_lane[l]);
+    gr_cresult c = host::cresult_of(pr);
+    if (host::result_needs_ext(L.u8(LR_RFLAGS)[l])) {
+      c.flags = GR_CR_EXT;
+      c.ext = roff[l];
+      ext[roff[l]] = pr;
+    }
+    out[l] = c;
+  }
+}
+
 // Does any mailbox of the space hold a message with cold fields (nonempty and
 // without MB_ALLCOMPACT)? One store per wave that finds one.
 __global__ void cold_used(SpaceView v, uint32_t* flag) {

@@ -48,6 +48,13 @@ def load_library(path=LIB_PATH):
     lib.gr_sync_peers_to_host.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_notify_applied.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_compact_log.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p]
+    lib.gr_step_compact.argtypes = [c.c_void_p, c.POINTER(abi.CInbox), c.POINTER(abi.COutbox)]
+    lib.gr_cinbox_reserve.argtypes = [c.c_void_p, c.c_size_t, c.c_size_t, c.c_size_t, c.c_size_t,
+                                      c.POINTER(abi.CInbox)]
+    lib.gr_release_coutbox.argtypes = [c.c_void_p, c.POINTER(abi.COutbox)]
+    lib.gr_pack_messages.argtypes = [c.c_void_p, c.c_size_t, c.c_void_p, c.c_void_p, c.POINTER(c.c_size_t)]
+    lib.gr_unpack_messages.argtypes = [c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t, c.c_void_p]
+    lib.gr_pack_locals.argtypes = [c.c_void_p, c.c_size_t, c.c_void_p, c.c_void_p, c.POINTER(c.c_size_t)]
     lib.gr_commit_update.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p]
     lib.gr_step.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.POINTER(abi.Outbox)]
     lib.gr_release_outbox.argtypes = [c.c_void_p, c.POINTER(abi.Outbox)]
@@ -193,6 +200,52 @@ class Engine:
             ctypes.memmove(res.ctypes.data, ob.results, ob.n_results * abi.RESULT.itemsize)
         _check(self.lib.gr_release_outbox(self._h, ctypes.byref(ob)), "gr_release_outbox")
         return out, res
+
+    def pack_messages(self, msgs):
+        """gr_pack_messages: full records -> (compact records, ext records)."""
+        msgs = np.ascontiguousarray(msgs, abi.MESSAGE)
+        c = np.zeros(len(msgs), abi.CMSG)
+        ext = np.zeros(len(msgs), abi.MESSAGE)
+        nx = ctypes.c_size_t()
+        _check(self.lib.gr_pack_messages(msgs.ctypes.data if len(msgs) else None, len(msgs),
+                                         c.ctypes.data if len(c) else None, ext.ctypes.data if len(ext) else None,
+                                         ctypes.byref(nx)), "gr_pack_messages")
+        return c, ext[:nx.value].copy()
+
+    def unpack_messages(self, c, ext):
+        c = np.ascontiguousarray(c, abi.CMSG)
+        ext = np.ascontiguousarray(ext, abi.MESSAGE)
+        out = np.zeros(len(c), abi.MESSAGE)
+        _check(self.lib.gr_unpack_messages(c.ctypes.data if len(c) else None, len(c),
+                                           ext.ctypes.data if len(ext) else None, len(ext),
+                                           out.ctypes.data if len(out) else None), "gr_unpack_messages")
+        return out
+
+    def pack_locals(self, loc):
+        loc = np.ascontiguousarray(loc, abi.LOCAL)
+        c = np.zeros(len(loc), abi.CLOCAL)
+        ext = np.zeros(len(loc), abi.LOCAL)
+        nx = ctypes.c_size_t()
+        _check(self.lib.gr_pack_locals(loc.ctypes.data if len(loc) else None, len(loc),
+                                       c.ctypes.data if len(c) else None, ext.ctypes.data if len(ext) else None,
+                                       ctypes.byref(nx)), "gr_pack_locals")
+        return c, ext[:nx.value].copy()
+
+    def step_compact(self, cmsgs, ext_msgs, clocals, ext_locals):
+        """One synchronous pass with compact records (gr_step_compact). Returns
+        (cmsgs, ext msgs, cresults, ext results) copied out of the engine's outbox."""
+        ib = abi.cinbox_of(cmsgs, ext_msgs, clocals, ext_locals)
+        ob = abi.COutbox()
+        _check(self.lib.gr_step_compact(self._h, ctypes.byref(ib), ctypes.byref(ob)), "gr_step_compact")
+        out = []
+        for ptr, n, dt in ((ob.msgs, ob.n_msgs, abi.CMSG), (ob.ext_msgs, ob.n_ext_msgs, abi.MESSAGE),
+                           (ob.results, ob.n_results, abi.CRESULT), (ob.ext_results, ob.n_ext_results, abi.RESULT)):
+            a = np.zeros(n, dt)
+            if n:
+                ctypes.memmove(a.ctypes.data, ptr, n * dt.itemsize)
+            out.append(a)
+        _check(self.lib.gr_release_coutbox(self._h, ctypes.byref(ob)), "gr_release_coutbox")
+        return tuple(out)
 
     def reserve_inbox(self, n_msgs, n_locals):
         """gr_inbox_reserve: (Inbox, msgs view, locals view) over engine-owned pinned

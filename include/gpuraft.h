@@ -313,6 +313,95 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out);
  * gr_inbox_reserve or gr_destroy; gr_step may also be given any other memory. */
 int gr_inbox_reserve(gr_engine* e, size_t n_msgs, size_t n_locals, gr_inbox* in);
 int gr_release_outbox(gr_engine* e, gr_outbox* out);
+
+/*
+ * Compact records: the same pass as gr_step with the steady state's messages in
+ * 24 bytes instead of 80 and results in 40 instead of 168, so a 1M-group pass
+ * moves ~0.5 GB over PCIe instead of ~2 GB. A record that does not fit its
+ * compact form points into an "ext" array of full records (GR_*_EXT); order is
+ * always the compact array's. gr_pack_messages / gr_unpack_messages convert on
+ * the host (what a cgo caller's packer does).
+ *
+ * gr_cmsg: Term < 2^32; LogTerm, Commit, Hint and the entries follow from the
+ * flags (fields not listed are 0): GR_CM_ENTRY = one entry at Term
+ * (n_entries = n_runs = 1, run_term[0] = Term); GR_CM_LOG_TERM = LogTerm is Term;
+ * GR_CM_COMMIT / GR_CM_HINT = Commit / Hint is LogIndex + aux - 2^31. Compact
+ * Replicates, ReplicateResps, and Heartbeats / HeartbeatResps without a
+ * ReadIndex context fit; everything else is GR_CM_EXT with ext index aux (the
+ * ext record's peer, slot and type must equal the compact record's).
+ */
+#define GR_CM_REJECT 0x01
+#define GR_CM_ENTRY 0x02
+#define GR_CM_LOG_TERM 0x04
+#define GR_CM_COMMIT 0x08
+#define GR_CM_HINT 0x10
+#define GR_CM_EXT 0x80
+typedef struct gr_cmsg {
+  uint32_t peer;       /* as gr_message.peer */
+  uint8_t type, slot, flags, pad;
+  uint32_t term;
+  uint32_t aux;        /* Commit/Hint offset from LogIndex (+2^31), or the ext index */
+  uint64_t log_index;
+} gr_cmsg;
+
+/* gr_clocal: one peer's local inputs without a ReadIndex (GR_CL_EXT: ext_locals[ext]). */
+#define GR_CL_CONFIG_CHANGE 0x01 /* gr_local_input.propose_has_config_change */
+#define GR_CL_EXT 0x80
+typedef struct gr_clocal {
+  uint32_t peer;
+  uint32_t propose_entries;
+  uint16_t ticks;
+  uint8_t quiesced_ticks;
+  uint8_t flags;
+  uint32_t ext;
+  uint64_t rand;
+} gr_clocal;
+
+/* gr_cresult: a gr_peer_result without the per-pass extras. GR_CR_EXT: the lane
+ * has ReadyToRead records, forwarded proposals or a changed term/vote, and
+ * ext_results[ext] is its full record. propose_first (when propose_result is
+ * GR_PROP_APPENDED) is last_index - propose_entries + 1. */
+#define GR_CR_EXT 0x80
+typedef struct gr_cresult {
+  uint32_t peer;
+  uint8_t escalation, propose_result, flags, pad;
+  uint32_t esc_item;
+  uint32_t ext;
+  uint64_t committed, last_index, save_from; /* as gr_peer_result */
+} gr_cresult;
+
+typedef struct gr_cinbox {
+  const gr_cmsg* msgs;
+  size_t n_msgs;
+  const gr_message* ext_msgs;
+  size_t n_ext_msgs;
+  const gr_clocal* locals;
+  size_t n_locals;
+  const gr_local_input* ext_locals;
+  size_t n_ext_locals;
+} gr_cinbox;
+
+typedef struct gr_coutbox { /* engine-owned pinned memory, as gr_outbox */
+  gr_cmsg* msgs;
+  size_t n_msgs;
+  gr_message* ext_msgs;
+  size_t n_ext_msgs;
+  gr_cresult* results;
+  size_t n_results;
+  gr_peer_result* ext_results;
+  size_t n_ext_results;
+} gr_coutbox;
+
+int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out);
+/* Engine-owned pinned buffers for the next gr_step_compact inbox (as gr_inbox_reserve). */
+int gr_cinbox_reserve(gr_engine* e, size_t n_msgs, size_t n_ext_msgs, size_t n_locals, size_t n_ext_locals,
+                      gr_cinbox* in);
+int gr_release_coutbox(gr_engine* e, gr_coutbox* out);
+/* Host-side conversions (no engine): full records -> compact records plus ext
+ * records (*n_ext of them, ext must have room for n), and back. */
+int gr_pack_messages(const gr_message* in, size_t n, gr_cmsg* out, gr_message* ext, size_t* n_ext);
+int gr_unpack_messages(const gr_cmsg* in, size_t n, const gr_message* ext, size_t n_ext, gr_message* out);
+int gr_pack_locals(const gr_local_input* in, size_t n, gr_clocal* out, gr_local_input* ext, size_t* n_ext);
 int gr_stats_get(gr_engine* e, gr_stats* out);
 int gr_stats_reset(gr_engine* e);
 

@@ -167,9 +167,10 @@ RESULT_FIELDS = ["propose_result", "propose_first", "append_from", "n_ready", "n
                  "committed", "last_index", "save_from", "term", "vote"]
 
 
-def compare_results(eng_res, orc_res, limit=20):
+def compare_results(eng_res, orc_res, limit=20, fields=None):
     """eng_res: results per lane (peer field); orc_res: per peer (prefix results)."""
-    fields = RESULT_FIELDS
+    fields = fields or RESULT_FIELDS
+    all_fields = fields
     if len(eng_res):
         o = orc_res[eng_res["peer"].astype(np.int64)]
         same = np.ones(len(eng_res), bool)
@@ -183,7 +184,7 @@ def compare_results(eng_res, orc_res, limit=20):
     for r in eng_res:
         p = int(r["peer"])
         o = orc_res[p]
-        fields = RESULT_FIELDS
+        fields = all_fields
         d = [f"{f}: engine={r[f]} oracle={o[f]}" for f in fields if r[f] != o[f]]
         for q in range(min(int(r["n_ready"]), abi.GR_Q)):
             if tuple(r["ready"][q]) != tuple(o["ready"][q]):

@@ -80,6 +80,36 @@ class GpuBackend:
         self.eng.close()
 
 
+class GpuCompactBackend(GpuBackend):
+    """The compact boundary (gr_step_compact): records packed with
+    gr_pack_messages/gr_pack_locals, outputs expanded back to full records so the
+    Lockstep compares them with the oracle like any other backend. A compact
+    result carries no append_from (save_from replaces it for persistence); its
+    term/vote are the synced state's (a change would have made it an ext record)."""
+    result_fields = [f for f in parity.RESULT_FIELDS if f != "append_from"]
+
+    def step(self, msgs, loc):
+        cm, xm = self.eng.pack_messages(msgs)
+        cl, xl = self.eng.pack_locals(loc)
+        om, ox, cr, rx = self.eng.step_compact(cm, xm, cl, xl)
+        out = self.eng.unpack_messages(om, ox)
+        res = np.zeros(len(cr), abi.RESULT)
+        for f in ("peer", "escalation", "propose_result", "esc_item", "committed", "last_index", "save_from"):
+            res[f] = cr[f]
+        st = self.eng.sync(self.n)
+        p = cr["peer"].astype(np.int64)
+        res["term"], res["vote"] = st["term"][p], st["vote"][p]
+        nprop = np.zeros(self.n, np.uint64)
+        if len(loc):
+            nprop[loc["peer"].astype(np.int64)] = loc["propose_entries"]
+        app = cr["propose_result"] == abi.PROP_APPENDED
+        res["propose_first"] = np.where(app, cr["last_index"] - nprop[p] + np.uint64(1), 0)
+        x = (cr["flags"] & abi.CR_EXT) != 0
+        if x.any():
+            res[x] = rx[cr["ext"][x].astype(np.int64)]
+        return out, res
+
+
 def _threads():
     return min(16, os.cpu_count() or 1)
 
@@ -160,7 +190,7 @@ class Lockstep:
             bad_s = parity.compare_states(dev, o["mid"], self.slots, peers=keep)
             om = parity.prefix_msgs(o, lim)
             bad_m = parity.compare_msgs(out, om[~parked[om["peer"]]])
-            bad_r = parity.compare_results(res, o["results"])
+            bad_r = parity.compare_results(res, o["results"], fields=getattr(self.eng, "result_fields", None))
             bad_e = parity.check_escalations(res, o["esc_mask"])
             if bad_s or bad_m or bad_r or bad_e:
                 mr = self.max_report
