@@ -67,7 +67,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--groups", type=int, default=1_000_000, help="groups per GPU")
     ap.add_argument("--replicas", type=int, default=3)
-    ap.add_argument("--placement", choices=["local", "spread"], default=None)
+    ap.add_argument("--placement", choices=["local", "spread"], default=None,
+                    help="default: local at N=1, spread (BASELINE config 4) at N>1")
+    ap.add_argument("--banks", type=int, default=None,
+                    help="engines per rank whose exchanges overlap each other's passes (spread default 2)")
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
     ap.add_argument("--cpu-groups", type=int, default=20000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(affinity CPUs, GR_CPU_SHARE=16)")
@@ -340,38 +343,29 @@ def main():
 
     from dragonboat_amd import abi, populations as P
     from dragonboat_amd.engine import Engine
-    from dragonboat_amd.exchange import build_exchange
+    from dragonboat_amd.exchange import Pipeline
 
     R = args.replicas
     S = R
     G = args.groups
-    placement = args.placement or "local"
-    ex = build_exchange(G, R, S, world, rank, placement)
-    n = ex.n_peers
-    eng = Engine(n, S, device=ordinal)
-    eng.load(ex.peers)
-    eng.bind_routes(ex.in_pos, ex.out_pos)
-    loc = P.propose_locals(n, ex.leader_slots, pass_index=0)
-    eng.set_locals(loc)
-    spaces = ex.allocate(eng, dev)
-    stream = torch.cuda.current_stream()
-
-    def one_pass(k):
-        ex.step(eng, spaces, k, stream)
+    # N > 1: BASELINE config 4 (replicas on distinct GPUs, RCCL all-to-all per pass)
+    placement = args.placement or ("spread" if world > 1 else "local")
+    pipe = Pipeline(G, R, S, world, rank, placement, banks=args.banks)
+    pipe.setup(Engine, dev, ordinal)
 
     for k in range(args.warmup):
-        one_pass(k)
-    torch.cuda.synchronize()
+        pipe.step(k)
+    pipe.synchronize()
     if world > 1:
         dist.barrier()
-    eng.reset_stats()
+    pipe.reset_stats()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        ex.step(eng, spaces, args.warmup + k, stream)
-    torch.cuda.synchronize()
+        pipe.step(args.warmup + k)
+    pipe.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
@@ -380,14 +374,18 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    st = eng.stats()
+    st = pipe.stats()
     # Per-kernel durations for the roofline: the same passes once more, outside the
     # timed region, with HIP events around each kernel (recorded inside the library
-    # on `stream`), so the events add nothing to `value`.
-    eng.timing_begin()
+    # on the bank's stream), so the events add nothing to `value`.
+    pipe.timing_begin()
     for k in range(args.steps):
-        ex.step(eng, spaces, args.warmup + args.steps + k, stream)
-    tm = eng.timing_end()
+        pipe.step(args.warmup + args.steps + k)
+    pipe.synchronize()
+    tm = pipe.timing_end()
+    cold_x = pipe.cold_exchanges
+    banks = len(pipe.ex)
+    pipe.close()
     commits = st["leader_commits"]
     esc = st["escalations"]
     if world > 1:
@@ -402,10 +400,10 @@ def main():
     # SURVEY.md §8d's unit: one group-round (R-1 acks in, quorum commit, R-1
     # Replicates out, R-1 follower matches) = B_round(R) bytes at reference field
     # widths; a launch processes one group-round per leader commit.
-    rounds = st["leader_commits"] / args.steps
+    rounds = st["leader_commits"] / (args.steps * banks)  # per launch (one bank's pass)
     alg = b_round(R) * rounds  # algorithmic bytes per launch (this rank)
     achieved = alg / (kavg * 1e-3) / 1e9
-    refw = reference_width_bytes(st, G, R, args.steps) / args.steps
+    refw = reference_width_bytes(st, G, R, args.steps) / (args.steps * banks)
     if rank == 0:
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
@@ -435,8 +433,12 @@ def main():
             "data": "synthetic steady-state groups (BASELINE config 4 shape), 16-B proposals",
             "config": {"workload": f"{G} groups x {R} replicas per GPU, replicas {placement}, "
                                    f"1 proposal per leader per pass", "groups_total": groups_total,
-                       "replicas": R, "placement": placement},
+                       "replicas": R, "placement": placement, "banks": banks,
+                       "parallelism": f"clusterID shards x{world}" + (", replicas on distinct GPUs, RCCL "
+                                                                    "all_to_all per pass" if placement == "spread"
+                                                                    else "")},
             "escalations": esc,
+            "cold_exchanges": cold_x,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"gr_fast_kernel<{S}>", "kernel_ms": kavg,

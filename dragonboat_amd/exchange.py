@@ -182,3 +182,151 @@ class Exchange:
 
 def build_exchange(G, R, S, world, rank, placement, seed=2):
     return Exchange(G, R, S, world, rank, placement, seed=seed)
+
+
+class Pipeline:
+    """BASELINE config 4 across GPUs: the rank's groups in
+    `banks` independent engines, each with its own spaces and HIP stream, so
+    one bank's all-to-all over xGMI overlaps the other bank's pass.
+
+    Per pass k, for every bank b on its stream s_b:
+      wait for bank b's exchange of pass k-1 (the NCCL work handle: a stream
+      wait, not a host wait) -> gr_step_device -> the cold-region check as a
+      device reduction copied into pinned host memory;
+    then, bank by bank, the host reads that flag (the other banks' passes are
+    queued or running meanwhile) and issues the bank's all_to_all_single on
+    s_b with async_op=True: the hot region always, the cold region only when a
+    mailbox needs it. RCCL waits only on s_b, so bank 0's exchange runs beside
+    bank 1's kernel and vice versa. With one rank the exchange is a device copy.
+    `local` placement is one bank whose two spaces ping-pong (no exchange).
+    """
+
+    def __init__(self, G, R, S, world, rank, placement="spread", banks=None, seed=2):
+        if banks is None:
+            banks = 2 if placement == "spread" and G >= 128 else 1
+        sizes = [G // banks + (1 if b < G % banks else 0) for b in range(banks)]
+        self.R, self.S, self.world, self.rank, self.placement = R, S, world, rank, placement
+        self.ex = [Exchange(Gb, R, S, world, rank, placement, seed=seed + 7919 * b) for b, Gb in enumerate(sizes)]
+        self.groups = G
+        self.engines, self.spaces, self.streams = [], [], []
+        self.work = [[] for _ in self.ex]
+        self.cold_exchanges = 0
+
+    @property
+    def n_peers(self):
+        return sum(ex.n_peers for ex in self.ex)
+
+    def setup(self, engine_cls, device, ordinal, locals_fn=None):
+        """Engines (loaded, routes bound, locals bound), spaces, streams, pinned flags."""
+        import torch
+        from . import populations as P
+        for ex in self.ex:
+            eng = engine_cls(ex.n_peers, self.S, device=ordinal)
+            eng.load(ex.peers)
+            eng.bind_routes(ex.in_pos, ex.out_pos)
+            loc = locals_fn(ex) if locals_fn else P.propose_locals(ex.n_peers, ex.leader_slots, pass_index=0)
+            eng.set_locals(loc)
+            self.engines.append(eng)
+            self.spaces.append(ex.allocate(eng, device))
+            self.streams.append(torch.cuda.Stream(device=device))
+        self.flag_host = torch.zeros(len(self.ex), dtype=torch.uint8, pin_memory=True)
+        self.events = [torch.cuda.Event() for _ in self.ex]
+
+    def _cold_flag(self, b):
+        """Device-side: does some mailbox of bank b's out space hold a message with
+        cold fields? (count bytes: nonzero count without MB_ALLCOMPACT.)"""
+        ex, out = self.ex[b], self.spaces[b][1]
+        hb = ex.hot_region // ex.n_chunks
+        pc = pad_positions(ex.positions)
+        cnt = out[:ex.hot_region].view(ex.n_chunks, hb)[:, :pc]
+        cold = ((cnt & 7) != 0) & ((cnt & 8) == 0)
+        self.flag_host[b:b + 1].copy_(cold.any().view(1).to(self.flag_host.dtype), non_blocking=True)
+        self.events[b].record()
+
+    def step(self, k):
+        import torch
+        for b, (ex, eng) in enumerate(zip(self.ex, self.engines)):
+            s = self.streams[b]
+            with torch.cuda.stream(s):
+                for w in self.work[b]:
+                    w.wait()  # s waits for this bank's previous exchange
+                self.work[b] = []
+                if ex.placement == "local":
+                    src, dst = self.spaces[b][k % 2], self.spaces[b][(k + 1) % 2]
+                else:
+                    src, dst = self.spaces[b][0], self.spaces[b][1]
+                eng.step_device(src.data_ptr(), dst.data_ptr(), ex.n_chunks, ex.positions, ex.n_chunks,
+                                ex.positions, ex.n_peers, s.cuda_stream, depth=ex.depth)
+                if ex.placement == "spread":
+                    self._cold_flag(b)
+        if self.placement != "spread":
+            return
+        for b, ex in enumerate(self.ex):
+            s = self.streams[b]
+            self.events[b].synchronize()
+            cold = bool(self.flag_host[b].item())
+            hr = ex.hot_region
+            inp, out = self.spaces[b]
+            parts = [(slice(0, hr), ex.hot_splits)]
+            if cold:
+                parts.append((slice(hr, None), ex.cold_splits))
+                self.cold_exchanges += 1
+            with torch.cuda.stream(s):
+                for sl, (out_sp, in_sp) in parts:
+                    if self.world == 1:
+                        inp[sl].copy_(out[sl])
+                    else:
+                        self.work[b].append(_all_to_all(inp[sl], out[sl], in_sp, out_sp))
+
+    def synchronize(self):
+        import torch
+        for b, s in enumerate(self.streams):
+            with torch.cuda.stream(s):
+                for w in self.work[b]:
+                    w.wait()
+            self.work[b] = []
+        torch.cuda.synchronize()
+
+    def stats(self):
+        tot = {}
+        for eng in self.engines:
+            for f, v in eng.stats().items():
+                tot[f] = tot.get(f, 0) + v
+        return tot
+
+    def reset_stats(self):
+        for eng in self.engines:
+            eng.reset_stats()
+
+    def timing_begin(self):
+        for eng in self.engines:
+            eng.timing_begin()
+
+    def timing_end(self):
+        tot = {"passes": 0, "fast_ms": 0.0, "general_ms": 0.0, "bailed_lanes": 0}
+        for eng in self.engines:
+            for f, v in eng.timing_end().items():
+                tot[f] += v
+        return tot
+
+    def close(self):
+        for eng in self.engines:
+            eng.close()
+        self.engines = []
+
+
+def _all_to_all(inp, out, in_splits, out_splits):
+    """One all_to_all_single of byte ranges, async on the current stream (RCCL);
+    over gloo (CPU rehearsal of the N > 1 path) through host tensors."""
+    import torch.distributed as dist
+    if dist.get_backend() == "nccl":
+        return dist.all_to_all_single(inp, out, output_split_sizes=in_splits, input_split_sizes=out_splits,
+                                      async_op=True)
+    o, i = out.cpu(), inp.cpu()
+    dist.all_to_all_single(i, o, output_split_sizes=in_splits, input_split_sizes=out_splits)
+    inp.copy_(i)
+
+    class _Done:
+        def wait(self):
+            pass
+    return _Done()

@@ -255,3 +255,136 @@ def test_gloo_spread_step_regions(built, world, cold):
         p.join(timeout=60)
     assert all(e == 0 for _, e, _ in res), res
     assert all(c == int(cold) for _, _, c in res), res
+
+
+class _HostlaneEngine:
+    """A rank's engine for the CPU rehearsal of config 4: the kernels' lane code
+    compiled for the host (hl_step) stepping the rank's replicas, reading and
+    writing the same mailbox spaces (gr_space_decode/encode) that Exchange.step
+    moves between ranks with all_to_all over gloo."""
+
+    def __init__(self, ex):
+        from dragonboat_amd.engine import load_library
+        self.lib = load_library()
+        self.ex = ex
+        self.peers = ex.peers.copy()
+        self.S = ex.S
+        self.k = 0
+        self.inv = {}  # mailbox position -> (receiving peer, sender slot)
+        for j in range(ex.S):
+            for p in np.nonzero(ex.in_pos[j] != X.NOPOS)[0]:
+                self.inv[int(ex.in_pos[j, p])] = (int(p), j)
+
+    def space_bytes(self, n, positions, depth):
+        return int(self.lib.gr_space_bytes(n, positions, depth))
+
+    def chunk_bytes(self, positions, depth):
+        return int(self.lib.gr_space_chunk_bytes(positions, depth))
+
+    def hot_chunk_bytes(self, positions, depth):
+        return int(self.lib.gr_space_hot_chunk_bytes(positions, depth))
+
+    def step_device(self, in_ptr, out_ptr, in_chunks, in_positions, out_chunks, out_positions, n_peers, stream,
+                    depth=3):
+        import ctypes
+        from dragonboat_amd import abi
+        from dragonboat_amd.engine import decode_space
+        from oracle.pyoracle import hostlane_step
+        ex = self.ex
+        nbytes = self.space_bytes(in_chunks, in_positions, depth)
+        buf = np.ctypeslib.as_array(ctypes.cast(in_ptr, ctypes.POINTER(ctypes.c_uint8)), (nbytes,))
+        got = decode_space(buf.copy(), in_chunks, in_positions, depth)
+        msgs = got.copy()
+        for m in msgs:
+            m["peer"], m["slot"] = self.inv[int(m["peer"])]
+        order = np.lexsort((np.arange(len(msgs)), msgs["slot"], msgs["peer"]))
+        msgs = msgs[order]
+        loc = P.propose_locals(ex.n_peers, ex.leader_slots, pass_index=self.k)
+        self.peers, out, res = hostlane_step(self.peers, msgs, loc, self.S)
+        assert not np.any(res["escalation"]), res[res["escalation"] != 0][:3]
+        ob = np.ctypeslib.as_array(ctypes.cast(out_ptr, ctypes.POINTER(ctypes.c_uint8)), (nbytes,))
+        ob[:] = 0
+        pos = ex.out_pos[out["slot"].astype(np.int64), out["peer"].astype(np.int64)].astype(np.uint32)
+        assert np.all(pos != X.NOPOS)
+        out = np.ascontiguousarray(out)
+        rc = self.lib.gr_space_encode(ob.ctypes.data, out_chunks, out_positions, depth,
+                                      out.ctypes.data if len(out) else None, len(out),
+                                      pos.ctypes.data if len(pos) else None)
+        assert rc == 0, rc
+        self.k += 1
+
+    def cold_used(self, ptr, n_chunks, positions, depth, stream):
+        import ctypes
+        hb = self.hot_chunk_bytes(positions, depth)
+        buf = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8)), (n_chunks * hb,))
+        pc = X.pad_positions(positions)
+        cnt = buf.reshape(n_chunks, hb)[:, :pc]
+        return bool(np.any(((cnt & 7) != 0) & ((cnt & 8) == 0)))
+
+
+def _raft_worker(rank, world, port, G, passes, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class _S:
+        cuda_stream = 0
+    R = 3
+    ex = X.Exchange(G, R, R, world, rank, "spread", seed=11)
+    eng = _HostlaneEngine(ex)
+    spaces = ex.allocate(eng, torch.device("cpu"))
+    states = []
+    for k in range(passes):
+        ex.step(eng, spaces, k, _S())
+        states.append(eng.peers.copy())
+    q.put((rank, states, ex.cold_exchanges))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_spread_raft_matches_oracle(built, world):
+    """Config 4 rehearsed on CPU: every rank steps its replicas with the kernels'
+    lane code (host build), the Replicate/ReplicateResp mailboxes cross ranks
+    through Exchange.step's all_to_all_single (gloo), and after every pass each
+    rank's replicas equal a single-process oracle run of the same groups (one
+    population per home rank, messages routed inside each group)."""
+    import socket
+    from dragonboat_amd import abi
+    from oracle.pyoracle import OraclePopulation
+    import parity
+    G, R, passes = 48, 3, 6
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_raft_worker, args=(r, world, port, G, passes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        rank, states, _cold = q.get(timeout=300)
+        res[rank] = states
+    for p in procs:
+        p.join(timeout=60)
+    # the oracle: each home's groups in one process, routed within the group
+    topo = P.Topology(G, R)
+    orc = {}
+    for h in range(world):
+        peers = P.make_groups(G, R, seed=int(np.random.SeedSequence(X.group_seed(11, h)).generate_state(1)[0]))
+        pop = OraclePopulation(peers, R)
+        msgs = np.zeros(0, abi.MESSAGE)
+        orc[h] = []
+        for k in range(passes):
+            o = pop.step(msgs, P.propose_locals(R * G, np.arange(G), pass_index=k))
+            orc[h].append(pop.export())
+            msgs = topo.route_messages(o["msgs"])
+    for rank in range(world):
+        for k in range(passes):
+            dev = res[rank][k]
+            for r in range(R):
+                h = (rank - r) % world
+                sl = slice(r * G, (r + 1) * G)
+                bad = parity.compare_states(dev[sl], orc[h][k][sl], R)
+                assert not bad, (rank, k, r, bad[:2])
+    assert all(int(res[r][-1]["committed"][:G].min()) > int(res[r][0]["committed"][:G].min()) for r in res)

@@ -402,3 +402,35 @@ def test_compact_log_moves_first_index(built, gpu):
     assert dev2["first_index_m1"][G + 2] == dev1["first_index_m1"][G + 2]
     assert dev2["first_index_m1"][G + 3] == idx[2]
     eng.close()
+
+
+@pytest.mark.parametrize("banks", [1, 2])
+def test_pipeline_spread_banks(gpu, banks):
+    """bench.py's N > 1 path at N = 1 (exchange = device copy): the banked spread
+    pipeline (dragonboat_amd.exchange.Pipeline: one engine and HIP stream per
+    bank, exchanges issued per bank after a device-side cold check) equals an
+    oracle run of every bank's groups after every pass."""
+    import torch
+    from dragonboat_amd import abi
+    from dragonboat_amd.engine import Engine
+    from dragonboat_amd.exchange import Pipeline
+    from oracle.pyoracle import OraclePopulation
+    import parity
+    G, R, K = 900, 3, 5
+    pipe = Pipeline(G, R, R, 1, 0, "spread", banks=banks)
+    pipe.setup(Engine, torch.device("cuda", 0), 0)
+    pops = [OraclePopulation(ex.peers, R) for ex in pipe.ex]
+    msgs = [np.zeros(0, abi.MESSAGE) for _ in pipe.ex]
+    try:
+        for k in range(K):
+            pipe.step(k)
+            pipe.synchronize()
+            for b, ex in enumerate(pipe.ex):
+                loc = P.propose_locals(ex.n_peers, ex.leader_slots, pass_index=0)
+                o = pops[b].step(msgs[b], loc)
+                msgs[b] = P.Topology(ex.G, R).route_messages(o["msgs"])
+                bad = parity.compare_states(pipe.engines[b].sync(ex.n_peers), o["mid"], R)
+                assert not bad, (k, b, bad[:2])
+        assert sum(e.stats()["leader_commits"] for e in pipe.engines) > 0
+    finally:
+        pipe.close()
