@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--host-path", choices=["on", "off"], default="on",
                     help="also time gr_step with host records (N=1, rank 0)")
     ap.add_argument("--host-passes", type=int, default=4)
+    ap.add_argument("--host-partitions", type=int, default=2,
+                    help="concurrent step workers (engines) of the compact host-path leg")
     ap.add_argument("--check", action="store_true", help="verify the final state against a host replay")
     return ap.parse_args()
 
@@ -247,63 +249,89 @@ def host_path(args, R, ordinal):
     return {**compact, "full_records": full}
 
 
-def host_path_compact(args, R, ordinal):
+def host_path_compact(args, R, ordinal, partitions=None):
     """gr_step_compact (24-B messages, 40-B results, ext records for the rest):
-    the headline shape through the C-ABI, PCIe-inclusive. The host writes each
-    pass's inbox into the engine's pinned buffers (gr_cinbox_reserve), as a Go
-    packer would; routing the previous outbox (the transport's role) is untimed."""
+    the headline shape through the C-ABI, PCIe-inclusive, the way dragonboat's
+    step workers would call it (SURVEY.md §8b threading): the groups are split
+    clusterID % P over P partitions, each with its own engine (stream, pinned
+    inbox/outbox) and its own host thread, and every round the P workers call
+    gr_step_compact concurrently, so one partition's upload overlaps another's
+    download. The host writes each inbox into the engine's pinned buffers
+    (gr_cinbox_reserve), as a Go packer would; routing the previous outbox
+    (the transport's role) runs between rounds and is untimed."""
     import ctypes
+    import threading
     import numpy as np
     from dragonboat_amd import abi, populations as P
     from dragonboat_amd.engine import Engine
+    P_ = partitions or args.host_partitions
     G = args.groups
-    peers = P.make_groups(G, R, seed=2)
-    topo = P.Topology(G, R)
-    eng = Engine(R * G, R, device=ordinal)
-    eng.load(peers)
-    cm, cx = np.zeros(0, abi.CMSG), np.zeros(0, abi.MESSAGE)
+    sizes = [G // P_ + (1 if w < G % P_ else 0) for w in range(P_)]
+    parts = []
+    for w, Gw in enumerate(sizes):
+        eng = Engine(R * Gw, R, device=ordinal)
+        eng.load(P.make_groups(Gw, R, seed=2 + 7919 * w))
+        parts.append({"eng": eng, "G": Gw, "topo": P.Topology(Gw, R), "cm": np.zeros(0, abi.CMSG),
+                      "cx": np.zeros(0, abi.MESSAGE), "rc": 0, "n_rx": 0})
+    warm, passes = 4, args.host_passes  # warm-up grows every pinned buffer to its steady size
+
+    def call(pt):
+        pt["ob"] = abi.COutbox()
+        pt["rc"] = pt["eng"].lib.gr_step_compact(pt["eng"]._h, ctypes.byref(pt["ib"]), ctypes.byref(pt["ob"]))
+
     t_step = 0.0
-    n_in = n_out = n_x = n_rx = 0
-    warm, passes = 2, args.host_passes
+    n_in = n_out = n_x = 0
     for k in range(warm + passes):
-        loc = P.propose_locals(R * G, np.arange(G), pass_index=k)
-        cl, clx = eng.pack_locals(loc)
-        if k == warm:
-            eng.reset_stats()
-        ib = abi.CInbox()
-        assert eng.lib.gr_cinbox_reserve(eng._h, len(cm), len(cx), len(cl), len(clx), ctypes.byref(ib)) == 0
-        for ptr, a in ((ib.msgs, cm), (ib.ext_msgs, cx), (ib.locals, cl), (ib.ext_locals, clx)):
-            if len(a):
-                ctypes.memmove(ptr, a.ctypes.data, a.nbytes)
-        ob = abi.COutbox()
+        for pt in parts:  # untimed: the host packs each partition's inbox in place
+            eng = pt["eng"]
+            cl, clx = eng.pack_locals(P.propose_locals(R * pt["G"], np.arange(pt["G"]), pass_index=k))
+            if k == warm:
+                eng.reset_stats()
+            ib = abi.CInbox()
+            assert eng.lib.gr_cinbox_reserve(eng._h, len(pt["cm"]), len(pt["cx"]), len(cl), len(clx),
+                                             ctypes.byref(ib)) == 0
+            for ptr, a in ((ib.msgs, pt["cm"]), (ib.ext_msgs, pt["cx"]), (ib.locals, cl), (ib.ext_locals, clx)):
+                if len(a):
+                    ctypes.memmove(ptr, a.ctypes.data, a.nbytes)
+            pt["ib"] = ib
+        ths = [threading.Thread(target=call, args=(pt,)) for pt in parts]
         t0 = time.perf_counter()
-        rc = eng.lib.gr_step_compact(eng._h, ctypes.byref(ib), ctypes.byref(ob))
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
         t1 = time.perf_counter()
-        assert rc == 0, rc
-        om = np.zeros(ob.n_msgs, abi.CMSG)
-        ox = np.zeros(ob.n_ext_msgs, abi.MESSAGE)
-        if ob.n_msgs:
-            ctypes.memmove(om.ctypes.data, ob.msgs, om.nbytes)
-        if ob.n_ext_msgs:
-            ctypes.memmove(ox.ctypes.data, ob.ext_msgs, ox.nbytes)
+        for pt in parts:
+            assert pt["rc"] == 0, pt["rc"]
+            ob = pt["ob"]
+            om = np.zeros(ob.n_msgs, abi.CMSG)
+            ox = np.zeros(ob.n_ext_msgs, abi.MESSAGE)
+            if ob.n_msgs:
+                ctypes.memmove(om.ctypes.data, ob.msgs, om.nbytes)
+            if ob.n_ext_msgs:
+                ctypes.memmove(ox.ctypes.data, ob.ext_msgs, ox.nbytes)
+            if k >= warm:
+                n_in += len(pt["cm"])
+                n_out += len(om)
+                n_x += len(pt["cx"]) + len(ox) + ob.n_ext_results
+            pt["eng"].lib.gr_release_coutbox(pt["eng"]._h, ctypes.byref(ob))
+            pt["cm"], pt["cx"] = pt["topo"].route_unsorted(om), pt["topo"].route_unsorted(ox)
         if k >= warm:
             t_step += t1 - t0
-            n_in += len(cm)
-            n_out += len(om)
-            n_x += len(cx) + len(ox)
-            n_rx += ob.n_ext_results
-        eng.lib.gr_release_coutbox(eng._h, ctypes.byref(ob))
-        cm, cx = topo.route_unsorted(om), topo.route_unsorted(ox)
-    st = eng.stats()
-    eng.close()
+    commits = esc = 0
+    for pt in parts:
+        st = pt["eng"].stats()
+        commits += st["leader_commits"]
+        esc += st["escalations"]
+        pt["eng"].close()
     return {"path": "gr_step_compact: host gr_cmsg/gr_clocal records in, gr_cmsg/gr_cresult records out "
-                    "(+ ext records), PCIe-inclusive, pinned inbox",
-            "groups": G, "replicas": R, "passes": passes, "ms_per_pass": t_step / passes * 1e3,
-            "commits_per_s": st["leader_commits"] / t_step, "escalations": st["escalations"],
+                    "(+ ext records), PCIe-inclusive, pinned inbox, %d concurrent step workers" % P_,
+            "groups": G, "replicas": R, "partitions": P_, "passes": passes, "ms_per_pass": t_step / passes * 1e3,
+            "commits_per_s": commits / t_step, "escalations": esc,
             "msgs_in_per_pass": n_in / passes, "msgs_out_per_pass": n_out / passes,
-            "ext_records_per_pass": (n_x + n_rx) / passes,
+            "ext_records_per_pass": n_x / passes,
             "record_bytes_per_pass": (n_in + n_out) / passes * abi.CMSG.itemsize
-            + R * G * (abi.CRESULT.itemsize + abi.CLOCAL.itemsize / R)}
+            + R * G * abi.CRESULT.itemsize + G * abi.CLOCAL.itemsize}
 
 
 def copy_peak_gbs():

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -20,7 +22,7 @@ namespace gr {
 
 #define GR_EXTERN_SLOTS(SS)                                                                                  \
   extern template hipError_t launch<SS>(const StepParams&, uint32_t*, uint32_t*, uint32_t, uint32_t, hipStream_t, \
-                                        const PassTiming*);
+                                        const PassTiming*, bool);
 GR_EXTERN_SLOTS(1)
 GR_EXTERN_SLOTS(3)
 GR_EXTERN_SLOTS(5)
@@ -32,13 +34,15 @@ extern template hipError_t cover_read<5>(uint64_t*);
 extern template hipError_t cover_read<8>(uint64_t*);
 #endif
 
+// tick_lanes: launch the tick kernel (some lane may carry ticks or a ReadIndex).
 static hipError_t launch_slots(uint32_t S, const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
-                               uint32_t list_cap, uint32_t parity, hipStream_t s, const PassTiming* t) {
+                               uint32_t list_cap, uint32_t parity, hipStream_t s, const PassTiming* t,
+                               bool tick_lanes = true) {
   switch (S) {
-    case 1: return launch<1>(kp, bail_list, counters, list_cap, parity, s, t);
-    case 3: return launch<3>(kp, bail_list, counters, list_cap, parity, s, t);
-    case 5: return launch<5>(kp, bail_list, counters, list_cap, parity, s, t);
-    case 8: return launch<8>(kp, bail_list, counters, list_cap, parity, s, t);
+    case 1: return launch<1>(kp, bail_list, counters, list_cap, parity, s, t, tick_lanes);
+    case 3: return launch<3>(kp, bail_list, counters, list_cap, parity, s, t, tick_lanes);
+    case 5: return launch<5>(kp, bail_list, counters, list_cap, parity, s, t, tick_lanes);
+    case 8: return launch<8>(kp, bail_list, counters, list_cap, parity, s, t, tick_lanes);
   }
   return hipErrorInvalidValue;
 }
@@ -78,6 +82,7 @@ struct gr_engine {
   uint32_t route_g = 0, route_r = 0;
   uint32_t* route_base = nullptr;  // device [2][GR_SMAX][GR_SMAX]
   bool locals_set = false;
+  bool locals_other = false;  // some bound local input has ticks / a ReadIndex / oversized counts (LW_OTHER)
   uint64_t passes = 0;
 
   // gr_step buffers (gr_io.h), grown on demand and reused
@@ -133,6 +138,29 @@ static void free_timings(gr_engine* e) {
 
 namespace {
 
+#ifndef GR_INBOX_WC
+#define GR_INBOX_WC 1
+#endif
+const unsigned kInboxPinned = GR_INBOX_WC ? (hipHostMallocDefault | hipHostMallocWriteCombined) : hipHostMallocDefault;
+
+// GR_PHASES=1: host-side phase times of a boundary pass on stderr (profiling aid).
+struct PhaseClock {
+  bool on = getenv("GR_PHASES") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  char buf[256];
+  int len = 0;
+  void mark(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    len += snprintf(buf + len, sizeof(buf) - len, "%s %.3f ms; ", what,
+                    std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+  void report() {
+    if (on) fprintf(stderr, "gr_phases: %s\n", buf);
+  }
+};
+
 #define HIPCHK(x)                              \
   do {                                         \
     hipError_t _e = (x);                       \
@@ -158,12 +186,15 @@ int grow_device(void** p, size_t* have, size_t want) {
   *have = want;
   return GR_OK;
 }
-int grow_pinned(uint8_t** p, size_t* have, size_t want) {
+// flags: hipHostMallocDefault for what the host reads (outboxes), write-combined
+// for the inboxes the host only writes and the device reads once (no snooping of
+// dirty host cache lines during the upload).
+int grow_pinned(uint8_t** p, size_t* have, size_t want, unsigned flags = hipHostMallocDefault) {
   if (*have >= want) return GR_OK;
   if (*p) (void)hipHostFree(*p);
   *p = nullptr;
   *have = 0;
-  HIPCHK(hipHostMalloc((void**)p, want, hipHostMallocDefault));
+  HIPCHK(hipHostMalloc((void**)p, want, flags));
   *have = want;
   return GR_OK;
 }
@@ -703,6 +734,7 @@ int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out) {
       in->n_ext_locals >= 0x80000000ull)
     return GR_EINVAL;
   std::lock_guard<std::mutex> guard(e->mu);
+  PhaseClock clk;  // GR_PHASES=1: per-phase host times on stderr
   memset(out, 0, sizeof(*out));
   const uint32_t S = e->S, cap = e->cfg.max_peers;
   const uint32_t nm = (uint32_t)in->n_msgs, nlc = (uint32_t)in->n_locals;
@@ -747,6 +779,7 @@ int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(e->h_scal, scal, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  clk.mark("upload+lanes");
   const uint32_t nl = ((uint32_t*)e->h_scal)[0];
   if (((uint32_t*)e->h_scal)[1]) return GR_EINVAL;  // nothing of the pass ran
   if (nl == 0) return GR_OK;
@@ -813,6 +846,7 @@ int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(e->h_scal + 4, scal + 1, 12, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  clk.mark("mailboxes+pass+counts");
   const uint32_t total = ((uint32_t*)e->h_scal)[1], text = ((uint32_t*)e->h_scal)[2], rext = ((uint32_t*)e->h_scal)[3];
   const size_t mbytes = (size_t)total * sizeof(gr_cmsg), xbytes = (size_t)text * sizeof(gr_message);
   const size_t rbytes = (size_t)nl * sizeof(gr_cresult), rxbytes = (size_t)rext * sizeof(gr_peer_result);
@@ -836,6 +870,8 @@ int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out) {
     if (text) HIPCHK(hipMemcpyAsync(e->h_outext, e->d_outext.p, xbytes, hipMemcpyDeviceToHost, s));
   }
   HIPCHK(hipStreamSynchronize(s));
+  clk.mark("pack+download");
+  clk.report();
   out->msgs = total ? (gr_cmsg*)e->h_outmsgs : nullptr;
   out->n_msgs = total;
   out->ext_msgs = text ? (gr_message*)e->h_outext : nullptr;
@@ -854,10 +890,10 @@ int gr_cinbox_reserve(gr_engine* e, size_t n_msgs, size_t n_ext_msgs, size_t n_l
     return GR_EINVAL;
   std::lock_guard<std::mutex> guard(e->mu);
   int r;
-  if ((r = grow_pinned(&e->h_inmsgs, &e->h_inmsgs_bytes, n_msgs * sizeof(gr_cmsg) + 1))) return r;
-  if ((r = grow_pinned(&e->h_inlocals, &e->h_inlocals_bytes, n_locals * sizeof(gr_clocal) + 1))) return r;
-  if ((r = grow_pinned(&e->h_inext, &e->h_inext_bytes, n_ext_msgs * sizeof(gr_message) + 1))) return r;
-  if ((r = grow_pinned(&e->h_inlext, &e->h_inlext_bytes, n_ext_locals * sizeof(gr_local_input) + 1))) return r;
+  if ((r = grow_pinned(&e->h_inmsgs, &e->h_inmsgs_bytes, n_msgs * sizeof(gr_cmsg) + 1, kInboxPinned))) return r;
+  if ((r = grow_pinned(&e->h_inlocals, &e->h_inlocals_bytes, n_locals * sizeof(gr_clocal) + 1, kInboxPinned))) return r;
+  if ((r = grow_pinned(&e->h_inext, &e->h_inext_bytes, n_ext_msgs * sizeof(gr_message) + 1, kInboxPinned))) return r;
+  if ((r = grow_pinned(&e->h_inlext, &e->h_inlext_bytes, n_ext_locals * sizeof(gr_local_input) + 1, kInboxPinned))) return r;
   in->msgs = (const gr_cmsg*)e->h_inmsgs;
   in->n_msgs = n_msgs;
   in->ext_msgs = (const gr_message*)e->h_inext;
@@ -917,8 +953,8 @@ int gr_inbox_reserve(gr_engine* e, size_t n_msgs, size_t n_locals, gr_inbox* in)
   if (!e || !in || n_msgs + n_locals >= 0x80000000ull) return GR_EINVAL;
   std::lock_guard<std::mutex> guard(e->mu);
   int r;
-  if ((r = grow_pinned(&e->h_inmsgs, &e->h_inmsgs_bytes, n_msgs * sizeof(gr_message) + 1))) return r;
-  if ((r = grow_pinned(&e->h_inlocals, &e->h_inlocals_bytes, n_locals * sizeof(gr_local_input) + 1))) return r;
+  if ((r = grow_pinned(&e->h_inmsgs, &e->h_inmsgs_bytes, n_msgs * sizeof(gr_message) + 1, kInboxPinned))) return r;
+  if ((r = grow_pinned(&e->h_inlocals, &e->h_inlocals_bytes, n_locals * sizeof(gr_local_input) + 1, kInboxPinned))) return r;
   in->msgs = (const gr_message*)e->h_inmsgs;
   in->n_msgs = n_msgs;
   in->locals = (const gr_local_input*)e->h_inlocals;
@@ -1054,6 +1090,14 @@ int gr_set_locals(gr_engine* e, const gr_local_input* locals, size_t n) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   e->locals_set = n > 0;
+  bool other = false;
+  for (size_t k = 0; k < n && !other; ++k) {
+    const gr_local_input& x = locals[k];
+    other = local_word(x.ticks, x.quiesced_ticks, x.propose_entries,
+                       (x.read_index ? LF_READ_INDEX : 0) | (x.propose_has_config_change ? LF_PROPOSE_CC : 0)) &
+            LW_OTHER;
+  }
+  e->locals_other = other;
   return GR_OK;
 }
 
@@ -1074,7 +1118,7 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
   kp.n_lanes = n_peers;
   kp.hints = e->hints;  // lane = peer here, so a wave's hint carries over between passes
   HIPCHK(launch_slots(e->S, kp, e->bail, e->counters, e->cap, (uint32_t)e->launches++, (hipStream_t)stream,
-                      next_timing(e)));
+                      next_timing(e), kp.has_locals && e->locals_other));
   e->passes++;
   return GR_OK;
 }

@@ -69,7 +69,23 @@ __device__ inline void block_stats(const StepParams& kp, const LaneStats& ls) {
 // appends over 16 counters 256 B apart keeps them from serialising when every
 // wave bails a few lanes (one shared counter: 105 us instead of 37 us on
 // config 3); no barrier, so waves of steady-state populations retire freely.
-constexpr uint32_t kBailLists = 16, kCounterStride = 64;  // counters 256 B apart
+// Lists 0..7 followers, 8..15 leaders (the general kernel's), 16..23 lanes with
+// ticks or a ReadIndex (LW_OTHER), which the tick kernel takes first.
+constexpr uint32_t kBailLists = 24, kGeneralLists = 16, kTickList0 = 16, kCounterStride = 64;  // counters 256 B apart
+
+// One wave's appends to bail list `list`: one returning atomic for the wave,
+// the wave's lanes contiguous and ascending.
+__device__ inline void bail_append(bool mine, uint32_t list, uint32_t* bail_list, uint32_t* counters,
+                                   uint32_t list_cap, uint32_t i) {
+  const uint64_t bm = __ballot(mine);
+  if (!bm) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t first = (uint32_t)__ffsll((unsigned long long)bm) - 1;
+  uint32_t base = 0;
+  if (lane == first) base = atomicAdd(counters + list * kCounterStride, (uint32_t)__popcll(bm));
+  base = __shfl(base, (int)first);
+  if (mine) bail_list[(uint64_t)list * list_cap + base + (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
+}
 
 template <int S>
 #ifndef GR_FAST_MIN_WAVES
@@ -95,27 +111,70 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
     const uint32_t nh = same == act ? first : 0u;
     if ((threadIdx.x & 63) == 0 && nh != hint) kp.hints[wave] = (uint8_t)nh;
   }
-  // followers into lists 0..7, leaders into 8..15: the general kernel walks the
-  // lists in order, so its waves hold one role and diverge less
+  // followers into lists 0..7, leaders into 8..15, lanes with ticks or a
+  // ReadIndex into 16..23 (the tick kernel's): the later kernels walk their lists
+  // in order, so their waves hold one kind of lane and diverge less
   const bool lead = role == GR_LEADER;
+  const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
 #pragma unroll
-  for (uint32_t side = 0; side < 2; ++side) {
-    const bool mine = bail && (lead == (side == 1));
-    const uint64_t bm = __ballot(mine);
-    if (bm) {
-      const uint32_t list = (blockIdx.x % (kBailLists / 2)) + side * (kBailLists / 2);
-      const uint32_t lane = threadIdx.x & 63;
-      const uint32_t first = (uint32_t)__ffsll((unsigned long long)bm) - 1;
-      uint32_t base = 0;
-      if (lane == first) base = atomicAdd(counters + list * kCounterStride, (uint32_t)__popcll(bm));
-      base = __shfl(base, (int)first);
-      if (mine) bail_list[(uint64_t)list * list_cap + base + (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
-    }
+  for (uint32_t side = 0; side < 3; ++side) {
+    const bool mine = bail && (side == 2 ? tickish : !tickish && lead == (side == 1));
+    bail_append(mine, (blockIdx.x % 8) + side * 8, bail_list, counters, list_cap, i);
   }
   if (kp.stats) block_stats(kp, ls);
 }
 
-// Pass 2: the general lane (every handler, escalation with prefix re-run)
+// Pass 2a: the heartbeat/ReadIndex/tick lane (gr_tick.h) over the lanes pass 1
+// handed over with ticks or a ReadIndex (lists 16..23), in a kernel of its own so
+// its register budget (and occupancy) is its own; what it cannot finish goes to
+// the general lists. Launched only when some lane may carry LW_OTHER.
+#ifndef GR_TICK_MIN_WAVES
+#define GR_TICK_MIN_WAVES 1
+#endif
+template <int S>
+__global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(StepParams kp, uint32_t* bail_list,
+                                                                             uint32_t* counters, uint32_t list_cap) {
+  uint32_t start[9];
+  start[0] = 0;
+#pragma unroll
+  for (uint32_t l = 0; l < 8; ++l) start[l + 1] = start[l] + counters[(kTickList0 + l) * kCounterStride];
+  const uint32_t n = start[8];
+  if (blockIdx.x * kBlock >= n) return;
+  LaneStats acc;
+  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    const uint32_t x = base + threadIdx.x;
+    bool hand = false;
+    uint32_t i = 0;
+    if (x < n) {
+      uint32_t l = 0;
+#pragma unroll
+      for (uint32_t k = 1; k < 8; ++k) l = x >= start[k] ? k : l;
+      uint32_t off = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) off = (k == l) ? x - start[k] : off;
+      i = bail_list[(uint64_t)(kTickList0 + l) * list_cap + off];
+      const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+      LaneStats ls;
+      if (tick_step<S>(kp, i, p, &ls)) {
+        acc.leader_commit += ls.leader_commit;
+        acc.follower_commit += ls.follower_commit;
+        acc.escalated += ls.escalated;
+        acc.msgs_in += ls.msgs_in;
+        acc.msgs_out += ls.msgs_out;
+        acc.leader_in += ls.leader_in;
+        acc.leader_out += ls.leader_out;
+        acc.entries += ls.entries;
+        acc.bailed += 1;
+      } else {
+        hand = true;  // the general lane steps it
+      }
+    }
+    bail_append(hand, blockIdx.x % 8, bail_list, counters, list_cap, i);
+  }
+  if (kp.stats) block_stats(kp, acc);
+}
+
+// Pass 2b: the general lane (every handler, escalation with prefix re-run)
 // over the bailed lanes only, grid-stride over the concatenated lists; also
 // clears the counters the next pass's fast kernel will use.
 #ifndef GR_GENERAL_MIN_WAVES
@@ -125,11 +184,11 @@ template <int S>
 __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(StepParams kp, const uint32_t* bail_list,
                                                          const uint32_t* counters, uint32_t* next_counters,
                                                          uint32_t list_cap) {
-  uint32_t start[kBailLists + 1];
+  uint32_t start[kGeneralLists + 1];
   start[0] = 0;
 #pragma unroll
-  for (uint32_t l = 0; l < kBailLists; ++l) start[l + 1] = start[l] + counters[l * kCounterStride];
-  const uint32_t n = start[kBailLists];
+  for (uint32_t l = 0; l < kGeneralLists; ++l) start[l + 1] = start[l] + counters[l * kCounterStride];
+  const uint32_t n = start[kGeneralLists];
   if (blockIdx.x == 0 && threadIdx.x < kBailLists) next_counters[threadIdx.x * kCounterStride] = 0;
   if (blockIdx.x * kBlock >= n) return;  // uniform per block: nothing to do, no stats row touched
   LaneStats acc;
@@ -138,20 +197,15 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
     if (x < n) {
       uint32_t l = 0;
 #pragma unroll
-      for (uint32_t k = 1; k < kBailLists; ++k) l = x >= start[k] ? k : l;
+      for (uint32_t k = 1; k < kGeneralLists; ++k) l = x >= start[k] ? k : l;
       uint32_t off = 0;
 #pragma unroll
-      for (uint32_t k = 0; k < kBailLists; ++k) off = (k == l) ? x - start[k] : off;
+      for (uint32_t k = 0; k < kGeneralLists; ++k) off = (k == l) ? x - start[k] : off;
       const uint32_t i = bail_list[(uint64_t)l * list_cap + off];
       const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
       LaneStats ls;
-      // lanes with ticks or a ReadIndex (LW_OTHER) try the heartbeat/ReadIndex/tick
-      // lane first; the rest (and its hand-overs) take the general lane
-      const bool tickish = kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
-      if (!tickish || !tick_step<S>(kp, i, p, &ls)) {
-        Lane<S> L(kp, i, p);
-        L.step(&ls);
-      }
+      Lane<S> L(kp, i, p);
+      L.step(&ls);
       acc.leader_commit += ls.leader_commit;
       acc.follower_commit += ls.follower_commit;
       acc.escalated += ls.escalated;
@@ -177,9 +231,12 @@ struct PassTiming {
   hipEvent_t ev[3];
 };
 
+// The tick kernel's grid: its lanes are at most the active share of a pass.
+constexpr uint32_t kTickBlocks = 1024;
+
 template <int S>
 hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters, uint32_t list_cap,
-                         uint32_t parity, hipStream_t s, const PassTiming* t) {
+                         uint32_t parity, hipStream_t s, const PassTiming* t, bool tick_lanes) {
   if (kp.n_lanes == 0) return hipSuccess;
   const uint32_t blocks = (kp.n_lanes + kBlock - 1) / kBlock;
   uint32_t* cur = counters + (parity & 1) * kBailLists * kCounterStride;
@@ -189,6 +246,11 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   hipLaunchKernelGGL(gr_fast_kernel<S>, dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
   if ((err = hipGetLastError()) != hipSuccess) return err;
   if (t && (err = hipEventRecord(t->ev[1], s)) != hipSuccess) return err;
+  if (tick_lanes) {  // some lane may carry ticks or a ReadIndex (LW_OTHER)
+    const uint32_t tblocks = blocks < kTickBlocks ? blocks : kTickBlocks;
+    hipLaunchKernelGGL(gr_tick_kernel<S>, dim3(tblocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
+    if ((err = hipGetLastError()) != hipSuccess) return err;
+  }
   const uint32_t gblocks = blocks < kGeneralBlocks ? blocks : kGeneralBlocks;
   hipLaunchKernelGGL(gr_step_kernel<S>, dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list,
                      (const uint32_t*)cur, nxt, list_cap);
@@ -216,7 +278,7 @@ hipError_t cover_read(uint64_t* out) {
 #define GR_INSTANTIATE_SLOTS(SS)                                                                               \
   namespace gr {                                                                                              \
   template hipError_t launch<SS>(const StepParams&, uint32_t*, uint32_t*, uint32_t, uint32_t, hipStream_t,      \
-                                 const PassTiming*);                                                          \
+                                 const PassTiming*, bool);                                                    \
   GR_INSTANTIATE_COVER(SS)                                                                                    \
   }
 #ifdef GR_COVERAGE

@@ -1,3 +1,4 @@
+#include <cstring>
 // PMC calibration: kernels that move a known number of bytes with the access
 // widths gr_step_kernel uses (8-B and 1-B per lane, coalesced), so the
 // FETCH_SIZE / WRITE_SIZE readings of the step kernel can be converted to
@@ -93,8 +94,66 @@ static int copy_mode() {
   return 0;
 }
 
+// PCIe paths for the boundary's records: DMA (hipMemcpyAsync from/to pinned
+// memory, one stream and two streams splitting the range) and kernels that read
+// or write pinned host memory directly (zero-copy), 256 MiB each way.
+__global__ void copy_f4_gs(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    b[i] = a[i];
+}
+static int pcie_mode() {
+  const size_t bytes = 256ull << 20;
+  void *h, *d;
+  CK(hipHostMalloc(&h, bytes, hipHostMallocDefault));
+  CK(hipMalloc(&d, bytes));
+  memset(h, 1, bytes);
+  CK(hipMemset(d, 0, bytes));
+  hipStream_t s0, s1;
+  CK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  auto timed = [&](auto&& f) {
+    float best = 1e9;
+    for (int rep = 0; rep < 4; ++rep) {
+      (void)(hipDeviceSynchronize());
+      (void)(hipEventRecord(a, s0));
+      f();
+      (void)(hipStreamSynchronize(s1));
+      (void)(hipEventRecord(b, s0));
+      (void)(hipEventSynchronize(b));
+      float ms;
+      (void)(hipEventElapsedTime(&ms, a, b));
+      best = ms < best ? ms : best;
+    }
+    return bytes / best / 1e6;
+  };
+  const size_t n4 = bytes / 16, half = bytes / 2;
+  const double h2d = timed([&] { (void)(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s0)); });
+  const double d2h = timed([&] { (void)(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s0)); });
+  const double h2d2 = timed([&] {
+    (void)(hipMemcpyAsync(d, h, half, hipMemcpyHostToDevice, s0));
+    (void)(hipMemcpyAsync((char*)d + half, (char*)h + half, half, hipMemcpyHostToDevice, s1));
+  });
+  const double d2h2 = timed([&] {
+    (void)(hipMemcpyAsync(h, d, half, hipMemcpyDeviceToHost, s0));
+    (void)(hipMemcpyAsync((char*)h + half, (char*)d + half, half, hipMemcpyDeviceToHost, s1));
+  });
+  const double kread = timed([&] { copy_f4_gs<<<2048, 256, 0, s0>>>((const float4*)h, (float4*)d, n4); });
+  const double kwrite = timed([&] { copy_f4_gs<<<2048, 256, 0, s0>>>((const float4*)d, (float4*)h, n4); });
+  const double kread8 = timed([&] { copy_f4_gs<<<8192, 256, 0, s0>>>((const float4*)h, (float4*)d, n4); });
+  const double kwrite8 = timed([&] { copy_f4_gs<<<8192, 256, 0, s0>>>((const float4*)d, (float4*)h, n4); });
+  printf("{\"pcie_bytes\": %zu, \"h2d_dma_GBs\": %.1f, \"d2h_dma_GBs\": %.1f, \"h2d_dma_2streams_GBs\": %.1f, "
+         "\"d2h_dma_2streams_GBs\": %.1f, \"h2d_kernel_read_GBs\": %.1f, \"d2h_kernel_write_GBs\": %.1f, "
+         "\"h2d_kernel_read_8k_GBs\": %.1f, \"d2h_kernel_write_8k_GBs\": %.1f}\n",
+         bytes, h2d, d2h, h2d2, d2h2, kread, kwrite, kread8, kwrite8);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && argv[1][0] == 'c') return copy_mode();
+  if (argc > 1 && argv[1][0] == 'p') return pcie_mode();
   const size_t bytes = 2ull << 30;
   void* buf;
   uint64_t* out;

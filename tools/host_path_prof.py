@@ -11,5 +11,8 @@ import bench  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--groups", type=int, default=1_000_000)
 ap.add_argument("--host-passes", type=int, default=4)
+ap.add_argument("--host-partitions", type=int, default=2)
 a = ap.parse_args()
+print(json.dumps(bench.host_path_compact(a, 3, 0)))
+a.host_partitions = 1
 print(json.dumps(bench.host_path_compact(a, 3, 0)))
