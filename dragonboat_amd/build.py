@@ -108,6 +108,38 @@ def build_hostlane(force=False):
     return HOSTLANE_LIB
 
 
+ORACLE_SAN_LIB = os.path.join(ROOT, "oracle", "_build", "liboracle_san.so")
+KAT_SAN_BIN = os.path.join(ROOT, "oracle", "_build", "kat_tests_san")
+HOSTLANE_SAN_LIB = os.path.join(ROOT, "tests", "_build", "libhostlane_san.so")
+SAN_FLAGS = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"]
+
+
+def build_sanitized(force=False):
+    """ASAN + UBSAN builds of the host code the CPU tests run:
+    the oracle library and KAT binary (g++), and the host build of the lane code
+    (hipcc host-only; -fno-gpu-sanitize: host code only). tests/test_sanitizers.py
+    runs parity workloads through them with the matching runtime preloaded."""
+    odir = os.path.join(ROOT, "oracle")
+    hdrs = [os.path.join(odir, f) for f in ("raft_oracle.hpp", "oracle_testkit.hpp")] + \
+        [os.path.join(ROOT, "include", "gpuraft.h")]
+    src = os.path.join(odir, "batch.cpp")
+    os.makedirs(os.path.dirname(ORACLE_SAN_LIB), exist_ok=True)
+    os.makedirs(os.path.dirname(HOSTLANE_SAN_LIB), exist_ok=True)
+    if force or _stale(ORACLE_SAN_LIB, hdrs + [src]):
+        _run(["g++", "-std=c++17", "-O1", "-g", "-fPIC", "-shared", *SAN_FLAGS, "-I" + odir,
+              "-I" + os.path.join(ROOT, "include"), src, "-o", ORACLE_SAN_LIB, "-lpthread"])
+    kat = os.path.join(odir, "kat_tests.cpp")
+    if force or _stale(KAT_SAN_BIN, hdrs + [kat]):
+        _run(["g++", "-std=c++17", "-O1", "-g", *SAN_FLAGS, "-I" + odir, kat, "-o", KAT_SAN_BIN])
+    hsrc = os.path.join(ROOT, "tests", "native", "hostlane.hip")
+    if force or _stale(HOSTLANE_SAN_LIB, ENGINE_DEPS + [hsrc]):
+        _run([HIPCC, "--cuda-host-only", "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-DGR_COVERAGE",
+              "-fno-gpu-sanitize", *SAN_FLAGS, "-shared-libsan",
+              "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "dragonboat_amd", "csrc"),
+              hsrc, "-o", HOSTLANE_SAN_LIB])
+    return ORACLE_SAN_LIB, HOSTLANE_SAN_LIB
+
+
 def build_wire(force=False):
     """libgrwire.so: the wire codec (include/gpuraft_wire.h)."""
     os.makedirs(os.path.dirname(WIRE_LIB), exist_ok=True)

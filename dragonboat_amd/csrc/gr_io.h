@@ -350,14 +350,17 @@ __global__ void set_row_u64(StateBase st, uint32_t row, const uint32_t* slots, c
 
 // gr_compact_log: LogReader.Compact(index) (logreader.go:251-269) mirrored into
 // entryLog.firstIndex()-1 (logentry.go:97-104). status: 0 ok, 1 ErrCompacted
-// (index below firstIndex-1), 2 ErrUnavailable (index past lastIndex); only ok
+// (index below firstIndex-1), 2 ErrUnavailable (index past the persisted lastIndex); only ok
 // slots are written. H_GE_LO follows the new firstIndex-1.
 template <int S>
 __global__ void compact_rows(StateBase st, const uint32_t* slots, const uint64_t* idx, uint32_t n, int32_t* status,
                              uint32_t* refused) {
   for (uint32_t x = io_tid(); x < n; x += io_stride()) {
     const uint32_t p = slots[x];
-    const uint64_t i = idx[x], lo = st.u64(SR_LO)[p], last = st.u64(SR_LAST_INDEX)[p];
+    // LogReader.Compact checks its own range: markerIndex (firstIndex - 1 here)
+    // and the persisted lastIndex, i.e. inMemory.savedTo (entries above it are
+    // not in LogDB yet), not entryLog.lastIndex (logreader.go:251-269).
+    const uint64_t i = idx[x], lo = st.u64(SR_LO)[p], last = st.u64(SR_SAVED_TO)[p];
     const int32_t rc = i < lo ? 1 : i > last ? 2 : 0;
     status[x] = rc;
     if (rc) {

@@ -104,6 +104,7 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
   if (active) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     bail = !fast_step<S>(kp, i, p, &ls, &role, hint, &myhint);  // leaves ls zero when it bails
+    if (!bail) GR_CHECK_STATE(kp.st, p);
   }
   if (kp.hints) {  // next pass's hint: this wave's role if every active lane shares it
     const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane(myhint);
@@ -156,6 +157,7 @@ __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(Step
       const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
       LaneStats ls;
       if (tick_step<S>(kp, i, p, &ls)) {
+        GR_CHECK_STATE(kp.st, p);
         acc.leader_commit += ls.leader_commit;
         acc.follower_commit += ls.follower_commit;
         acc.escalated += ls.escalated;
@@ -206,6 +208,7 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
       LaneStats ls;
       Lane<S> L(kp, i, p);
       L.step(&ls);
+      GR_CHECK_STATE(kp.st, p);
       acc.leader_commit += ls.leader_commit;
       acc.follower_commit += ls.follower_commit;
       acc.escalated += ls.escalated;

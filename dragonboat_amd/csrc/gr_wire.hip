@@ -30,7 +30,9 @@
 
 #pragma clang diagnostic ignored "-Wunused-value"
 
+#include <algorithm>
 #include <cstdlib>
+#include <vector>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -1053,6 +1055,26 @@ __global__ void frame_sizes(grw_batch* batches, u32 n, EncScratch s, const u32* 
   u64 body = s.pos[bt.first_msg + bt.n_msgs] - s.pos[bt.first_msg];
   u64 tail = 1 + sov(bt.deployment_id) + 1 + (u64)bt.source_len + sov(bt.source_len) + 1 + sov(bt.bin_ver);
   s.flen[b] = panic_flag[b] ? 0 : body + tail;
+  if (!panic_flag[b] && body + tail > 0xFFFFFFFFull) atomicOr(s.bad, 2u);  // frame_len is 32-bit
+}
+
+// Every record an encode reads must lie inside the arrays it was given: a
+// message's entries inside ents, every Cmd / Snapshot / SourceAddress inside the
+// payload buffer. One bad record fails the call (GR_EINVAL) before any byte is
+// read out of range.
+__device__ __forceinline__ bool out_of(u64 off, u64 len, u64 cap) { return len && (off > cap || len > cap - off); }
+__global__ void check_records(const grw_batch* batches, u32 n, const grw_message* msgs, u32 nm, const grw_entry* ents,
+                              u64 n_ents, u64 payload_len, EncScratch s) {
+  const u64 t = blockIdx.x * (u64)blockDim.x + threadIdx.x;
+  bool bad = false;
+  if (t < nm) {
+    const grw_message& m = msgs[t];
+    bad |= (u64)m.first_entry + m.n_entries > n_ents;
+    bad |= out_of(m.snapshot_off, m.snapshot_len, payload_len);
+  }
+  if (t < n_ents) bad |= out_of(ents[t].cmd_off, ents[t].cmd_len, payload_len);
+  if (t < n) bad |= out_of(batches[t].source_off, batches[t].source_len, payload_len);
+  if (bad) atomicOr(s.bad, 1u);
 }
 
 __global__ void frame_finish(grw_batch* batches, u32 n, EncScratch s, const u32* panic_flag) {
@@ -1193,7 +1215,7 @@ struct grw_ctx {
   // host-path staging
   Buf d_buf, d_batches, d_msgs, d_ents;
   u8* h_scal = nullptr;
-  std::mutex mu;
+  std::recursive_mutex mu;  // host and device entry points alike: one call at a time per context
 };
 
 #define HIPCHK(x)                            \
@@ -1276,6 +1298,7 @@ int grw_decode_device(grw_ctx* c, const uint8_t* d_buf, size_t buf_len, grw_batc
                       grw_message* d_msgs, size_t msg_cap, grw_entry* d_ents, size_t ent_cap, size_t* n_msgs,
                       size_t* n_ents) {
   if (!c || !n_msgs || !n_ents || (n && (!d_buf || !d_batches)) || n > 0xFFFFFFFFull) return GR_EINVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);  // shares scratch, stream and events with every other call
   *n_msgs = *n_ents = 0;
   if (n == 0) return GR_OK;
   HIPCHK(hipSetDevice(c->device));
@@ -1385,9 +1408,16 @@ int grw_decode_device(grw_ctx* c, const uint8_t* d_buf, size_t buf_len, grw_batc
 int grw_decode(grw_ctx* c, const uint8_t* buf, size_t buf_len, grw_batch* batches, size_t n, grw_message* msgs,
                size_t msg_cap, grw_entry* ents, size_t ent_cap, size_t* n_msgs, size_t* n_ents) {
   if (!c || !n_msgs || !n_ents || (n && (!buf || !batches))) return GR_EINVAL;
-  for (size_t b = 0; b < n; ++b)
-    if (batches[b].frame_off + (u64)batches[b].frame_len > buf_len) return GR_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
+  for (size_t b = 0; b < n; ++b)  // in range, written so that it cannot wrap
+    if (batches[b].frame_off > buf_len || batches[b].frame_len > buf_len - batches[b].frame_off) return GR_EINVAL;
+  if (n > 1) {  // frames must not overlap (their spans share scratch slots)
+    std::vector<std::pair<u64, u64>> iv(n);
+    for (size_t b = 0; b < n; ++b) iv[b] = {batches[b].frame_off, batches[b].frame_off + batches[b].frame_len};
+    std::sort(iv.begin(), iv.end());
+    for (size_t b = 1; b < n; ++b)
+      if (iv[b].first < iv[b - 1].second) return GR_EINVAL;
+  }
+  std::lock_guard<std::recursive_mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   int r;
   if ((r = grow(c->d_buf, buf_len + 16)) || (r = grow(c->d_batches, n * sizeof(grw_batch)))) return r;
@@ -1411,9 +1441,9 @@ int grw_decode(grw_ctx* c, const uint8_t* buf, size_t buf_len, grw_batch* batche
 int grw_encode_device(grw_ctx* c, const uint8_t* d_payload, size_t payload_len, grw_batch* d_batches, size_t n,
                       const grw_message* d_msgs, size_t n_msgs, const grw_entry* d_ents, size_t n_ents, uint8_t* d_out,
                       size_t out_cap, size_t* out_len) {
-  (void)payload_len;
-  (void)n_ents;
   if (!c || !out_len || (n && !d_batches) || n > 0xFFFFFFFFull || n_msgs > 0xFFFFFFFFull) return GR_EINVAL;
+  if ((n_msgs && !d_msgs) || (n_ents && !d_ents)) return GR_EINVAL;
+  std::lock_guard<std::recursive_mutex> g(c->mu);  // shares scratch, stream and events with every other call
   *out_len = 0;
   if (n == 0) return GR_OK;
   HIPCHK(hipSetDevice(c->device));
@@ -1430,6 +1460,8 @@ int grw_encode_device(grw_ctx* c, const uint8_t* d_payload, size_t payload_len, 
   HIPCHK(hipEventRecord(c->ev[0], s));
   HIPCHK(hipMemsetAsync(es.bad, 0, 4, s));
   check_contig<<<nblk(n, 256), 256, 0, s>>>(d_batches, (u32)n, total, es);
+  check_records<<<nblk(std::max<u64>(std::max<u64>(n, total), n_ents), 256), 256, 0, s>>>(
+      d_batches, (u32)n, d_msgs, total, d_ents, (u64)n_ents, (u64)payload_len, es);
   enc_map<<<(unsigned)n, 64, 0, s>>>(d_batches, (u32)n, total, es, pflag);
   HIPCHK(hipMemcpyAsync(c->h_scal, es.bad, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -1446,8 +1478,10 @@ int grw_encode_device(grw_ctx* c, const uint8_t* d_payload, size_t payload_len, 
   frame_finish<<<nblk(n, 256), 256, 0, s>>>(d_batches, (u32)n, es, pflag);
   HIPCHK(hipMemcpyAsync(c->h_scal, es.foff + n - 1, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(c->h_scal + 8, es.flen + n - 1, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(c->h_scal + 16, es.bad, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipEventRecord(c->ev[2], s));
   HIPCHK(hipStreamSynchronize(s));
+  if (*(u32*)(c->h_scal + 16)) return GR_EINVAL;  // a frame longer than 2^32 - 1 bytes
   u64 need = ((u64*)c->h_scal)[0] + ((u64*)c->h_scal)[1];
   *out_len = need;
   if (need > out_cap || (need && !d_out)) return GR_ECAPACITY;
@@ -1470,7 +1504,7 @@ int grw_encode(grw_ctx* c, const uint8_t* payload, size_t payload_len, grw_batch
                const grw_message* msgs, size_t n_msgs, const grw_entry* ents, size_t n_ents, uint8_t* out,
                size_t out_cap, size_t* out_len) {
   if (!c || !out_len || (n && !batches)) return GR_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
+  std::lock_guard<std::recursive_mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   int r;
   if ((r = grow(c->d_buf, payload_len + 16)) || (r = grow(c->d_batches, n * sizeof(grw_batch))) ||

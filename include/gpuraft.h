@@ -282,7 +282,8 @@ int gr_notify_applied(gr_engine* e, const uint32_t* slots, const uint64_t* appli
  * mirrored into entryLog.firstIndex()-1 (logentry.go:97-104): call it when the
  * host compacts a loaded group's LogDB range (node.compactLog). Per slot,
  * status (may be NULL) gets 0, 1 = ErrCompacted (index below firstIndex-1) or
- * 2 = ErrUnavailable (index past lastIndex); only status-0 slots are written
+ * 2 = ErrUnavailable (index past the persisted lastIndex, inMemory.savedTo:
+ * LogReader's own range, not the unsaved in-memory tail); only status-0 slots are written
  * and the call returns GR_ESTATE if any slot was refused. Slots out of range or
  * listed twice: GR_ERANGE before anything is written. */
 int gr_compact_log(gr_engine* e, const uint32_t* slots, const uint64_t* index, size_t n, int32_t* status);

@@ -18,7 +18,14 @@
  * (offset + length into the input buffer), which is what a zero-copy Go binding
  * slices. A Message whose Snapshot field is not the zero Snapshot is flagged
  * (snapshot_host) and the host decodes that one message span with the Go code:
- * InstallSnapshot is rare and off the step path.
+ * InstallSnapshot is rare and off the step path. The device does not validate
+ * the Snapshot bytes, so for a frame holding a snapshot_host message the host's
+ * re-decode of that span comes first: if the Go code rejects the Snapshot, that
+ * error is the frame's error, whatever status the device reported for a later
+ * message of the frame.
+ *
+ * A context runs one call at a time (host and device entry points alike share
+ * its scratch, stream and events; calls from several threads serialise).
  *
  * Conventions as gpuraft.h: int return, 0 = OK, negative gr_error; never aborts.
  * A frame the reference would reject gets a per-batch status naming the Go
@@ -116,8 +123,10 @@ const char* grw_status_name(int status);
  * totals exceed msg_cap / ent_cap, returns GR_ECAPACITY (-5) with *n_msgs /
  * *n_ents set to the totals needed and no records written.
  *
- * grw_decode takes host pointers (one DMA each way); grw_decode_device takes
- * device pointers (inputs already in HBM), and only the two totals cross PCIe.
+ * grw_decode takes host pointers (one DMA each way) and refuses (GR_EINVAL,
+ * nothing decoded) a frame range outside buf or two frames that overlap;
+ * grw_decode_device takes device pointers (inputs already in HBM), and only the
+ * two totals cross PCIe: there the caller guarantees the frame ranges.
  */
 int grw_decode(grw_ctx* c, const uint8_t* buf, size_t buf_len, grw_batch* batches, size_t n,
                grw_message* msgs, size_t msg_cap, grw_entry* ents, size_t ent_cap,
@@ -131,7 +140,10 @@ int grw_decode_device(grw_ctx* c, const uint8_t* d_buf, size_t buf_len, grw_batc
  * message's entries are ents[first_entry .. +n_entries); Cmd, SourceAddress and
  * non-zero Snapshot bytes come from payload. Frames are written back to back
  * into out; batches[i].frame_off/frame_len report where. Returns GR_ECAPACITY
- * with *out_len = the bytes needed when out_cap is too small.
+ * with *out_len = the bytes needed when out_cap is too small. Every record is
+ * checked on the device before any byte is read through it: a message's
+ * entries past n_ents, or a Cmd / Snapshot / SourceAddress past payload_len,
+ * and a frame longer than 2^32 - 1 bytes, return GR_EINVAL.
  */
 int grw_encode(grw_ctx* c, const uint8_t* payload, size_t payload_len, grw_batch* batches, size_t n,
                const grw_message* msgs, size_t n_msgs, const grw_entry* ents, size_t n_ents,

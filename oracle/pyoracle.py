@@ -12,8 +12,10 @@ import numpy as np
 from dragonboat_amd import abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
-HOSTLANE_LIB = os.path.join(ROOT, "tests", "_build", "libhostlane.so")
+# GR_ORACLE_LIB / GR_HOSTLANE_LIB: another build of the same code (the
+# sanitizer builds of tests/test_sanitizers.py)
+ORACLE_LIB = os.environ.get("GR_ORACLE_LIB") or os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+HOSTLANE_LIB = os.environ.get("GR_HOSTLANE_LIB") or os.path.join(ROOT, "tests", "_build", "libhostlane.so")
 KAT_BIN = os.path.join(ROOT, "oracle", "_build", "kat_tests")
 
 _olib = None

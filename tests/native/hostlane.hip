@@ -35,17 +35,20 @@ void run_lanes(const StepParams& kp) {
     const uint32_t pick = (w >> 13) % (2u + S);
     const uint32_t hint = pick == 0 ? 0u : pick == 1 ? WH_LEADER : (WH_FOLLOWER | ((pick - 2) << WH_SLOT_SHIFT));
     if (!fast_step<S>(kp, i, p, &ls, nullptr, hint)) bailed.push_back(i);
+    else GR_CHECK_STATE(kp.st, p);
   }
   for (uint32_t i : bailed) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     LaneStats ls;
     const bool tickish = kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
     if (tickish && tick_step<S>(kp, i, p, &ls)) {
+      GR_CHECK_STATE(kp.st, p);
       g_tick_lanes++;
       continue;
     }
     Lane<S> L(kp, i, p);
     L.step(&ls);
+    GR_CHECK_STATE(kp.st, p);
   }
   g_hint_salt += 0x9E3779B9u;
   g_fast_lanes += kp.n_lanes - bailed.size();

@@ -3,7 +3,9 @@ lanes of gr_fast.h and gr_tick.h, every escalation reason) is reached by the
 parity workloads (tests/coverage_workloads.py), each pass checked against the
 oracle. On the CPU the counts come from the host build of the lane code; under
 -m gpu from libgpuraft_cover.so, the same engine built with -DGR_COVERAGE, so
-the branches are reached on the GPU itself."""
+the branches are reached on the GPU itself. The same builds are the checked
+builds: after every lane's store the entryLog invariants of the SoA rows are
+tested (gr_cover.h check_state) and no BAD_* counter may move."""
 import ctypes
 
 import numpy as np
@@ -17,8 +19,12 @@ def _names(raw):
 
 
 def _check(counts, names, out):
-    missing = [n for n, c in zip(names, counts) if c == 0]
+    """Every branch id reached; every BAD_* id (the checked build's invariant
+    violations, gr_cover.h check_state) still zero."""
+    missing = [n for n, c in zip(names, counts) if c == 0 and not n.startswith("BAD_")]
     assert not missing, f"branches never reached: {missing}\n{out}"
+    bad = {n: int(c) for n, c in zip(names, counts) if c and n.startswith("BAD_")}
+    assert not bad, f"invariants violated: {bad}\n{out}"
 
 
 def test_coverage_hostlane(built):

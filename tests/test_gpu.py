@@ -390,7 +390,7 @@ def test_compact_log_moves_first_index(built, gpu):
     snap = {int(r["peer"]) for r in res if r["escalation"] == 7}  # GR_ESC_SNAPSHOT
     assert snap == set(int(x) for x in comp)
 
-    # Compact's refusals: index below firstIndex-1, index past lastIndex
+    # Compact's refusals: index below firstIndex-1, index past the persisted lastIndex
     dev1 = eng.sync(R * G)
     probe = np.array([G + 1, G + 2, G + 3], np.uint32)
     idx = np.array([dev1["first_index_m1"][G + 1] - 1, dev1["last_index"][G + 2] + 1,
@@ -401,6 +401,14 @@ def test_compact_log_moves_first_index(built, gpu):
     assert dev2["first_index_m1"][G + 1] == dev1["first_index_m1"][G + 1]
     assert dev2["first_index_m1"][G + 2] == dev1["first_index_m1"][G + 2]
     assert dev2["first_index_m1"][G + 3] == idx[2]
+    # past the persisted end but inside the log (the pass's unsaved append):
+    # LogReader.Compact refuses it (its lastIndex is what LogDB holds)
+    p4 = G + 4
+    assert dev2["saved_to"][p4] < dev2["last_index"][p4]
+    rc, st = eng.compact_log(np.array([p4], np.uint32), np.array([dev2["last_index"][p4]], np.uint64))
+    assert rc == -6 and list(st) == [2]
+    rc, st = eng.compact_log(np.array([p4], np.uint32), np.array([dev2["saved_to"][p4]], np.uint64))
+    assert rc == 0 and list(st) == [0]
     eng.close()
 
 

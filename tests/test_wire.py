@@ -419,3 +419,60 @@ def test_gpu_large_frame_segment_walk(wbuilt, gpu, seg_shift, monkeypatch):
     bo, mo, eo = PW.decode(buf, b.copy())
     assert compare(buf, bd, md, ed, bo, mo, eo) == []
     assert (bo["status"] != 0).any() and (bo["status"] == 0).any()
+
+
+@pytest.mark.gpu
+def test_gpu_encode_refuses_out_of_range_records(wbuilt, gpu):
+    """grw_encode validates every record on the device before reading through it
+    (ADVICE r01): an entry range past the entry array, a Cmd / Snapshot /
+    SourceAddress past the payload buffer -> GR_EINVAL, nothing read out of range;
+    the untouched records still encode after each refusal."""
+    codec = W.WireCodec(0)
+    payload, b, m, e = PW.make_records(8, 6, seed=5, steady=False, snap_frac=0.3)
+    good = codec.marshal(payload, b.copy(), m, e)
+    assert len(good) > 0
+    P_ = len(payload)
+    cases = []
+    m1 = m.copy()
+    m1["first_entry"][0] = len(e)  # entries past the array
+    m1["n_entries"][0] = 1
+    cases.append(("entries", b, m1, e))
+    if len(e):
+        e1 = e.copy()
+        e1["cmd_off"][0], e1["cmd_len"][0] = P_ - 1, 2
+        cases.append(("cmd", b, m, e1))
+        e2 = e.copy()
+        e2["cmd_off"][0], e2["cmd_len"][0] = 2**63, 1  # would wrap
+        cases.append(("cmd wrap", b, m, e2))
+    m2 = m.copy()
+    m2["snapshot_off"][0], m2["snapshot_len"][0] = P_, 4
+    cases.append(("snapshot", b, m2, e))
+    b1 = b.copy()
+    b1["source_off"][0], b1["source_len"][0] = P_ + 5, 1
+    cases.append(("source", b1, m, e))
+    for name, bb, mm, ee in cases:
+        with pytest.raises(W.WireError, match=r"\(-1\)"):
+            codec.marshal(payload, bb.copy(), mm, ee)
+        assert codec.marshal(payload, b.copy(), m, e).tobytes() == good.tobytes(), name
+
+
+@pytest.mark.gpu
+def test_decode_refuses_overlapping_or_wrapping_frames(wbuilt, gpu):
+    """grw_decode's host checks: a frame range that wraps 2^64 or two
+    frames that overlap are refused before anything runs."""
+    codec = W.WireCodec(0)
+    payload, b, m, e = PW.make_records(4, 3, seed=6, steady=True)
+    out = PW.encode(payload, b, m, e)
+    fr = W.frames_table(b["frame_off"], b["frame_len"])
+    bad = fr.copy()
+    bad["frame_off"][1] = 2**64 - 4
+    with pytest.raises(W.WireError, match=r"\(-1\)"):
+        codec.unmarshal(out, bad)
+    if len(fr) > 1:
+        ov = fr.copy()
+        ov["frame_off"][1] = ov["frame_off"][0] + 1
+        ov["frame_len"][1] = 1
+        with pytest.raises(W.WireError, match=r"\(-1\)"):
+            codec.unmarshal(out, ov)
+    b1, _, _ = codec.unmarshal(out, fr.copy())
+    assert (b1["status"] == 0).all()
