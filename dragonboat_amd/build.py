@@ -54,6 +54,27 @@ def _run(cmd):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r.stderr
+
+
+# Kernels that must not touch scratch memory: one spilled register array in the
+# lean lane made a 1M x 3 pass 6x slower (0.82 vs 0.13 ms) and moved 3 GB of
+# scratch traffic per launch. The compiler's resource remarks are checked at
+# build time, so such a build fails instead of shipping.
+NO_SCRATCH_KERNELS = ("gr_fast_kernel",)
+RESOURCE_REMARKS = "-Rpass-analysis=kernel-resource-usage"
+
+
+def check_no_scratch(remarks, src):
+    """Parse hipcc's kernel-resource-usage remarks; raise if a NO_SCRATCH kernel uses scratch."""
+    name = None
+    for ln in remarks.splitlines():
+        if "Function Name:" in ln:
+            name = ln.split("Function Name:", 1)[1].split("[")[0].strip()
+        elif "ScratchSize" in ln and name and any(k in name for k in NO_SCRATCH_KERNELS):
+            size = int(ln.split(":")[-1].split("[")[0].strip())
+            if size:
+                raise RuntimeError(f"{os.path.basename(src)}: {name} uses {size} B/lane of scratch")
 
 
 def _hip_lib(out, srcs, deps, extra=(), force=False):
@@ -67,8 +88,9 @@ def _hip_lib(out, srcs, deps, extra=(), force=False):
              "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
     objs = [os.path.join(odir, os.path.basename(s) + ".o") for s in srcs]
     with ThreadPoolExecutor(JOBS) as ex:
-        for f in [ex.submit(_run, [HIPCC, *flags, "-c", s, "-o", o]) for s, o in zip(srcs, objs)]:
-            f.result()
+        futs = [ex.submit(_run, [HIPCC, *flags, RESOURCE_REMARKS, "-c", s, "-o", o]) for s, o in zip(srcs, objs)]
+        for s, f in zip(srcs, futs):
+            check_no_scratch(f.result(), s)
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out])
     return out
 
@@ -118,7 +140,16 @@ def build_sanitized(force=False):
     """ASAN + UBSAN builds of the host code the CPU tests run:
     the oracle library and KAT binary (g++), and the host build of the lane code
     (hipcc host-only; -fno-gpu-sanitize: host code only). tests/test_sanitizers.py
-    runs parity workloads through them with the matching runtime preloaded."""
+    runs parity workloads through them with the matching runtime preloaded.
+    Test workers call this concurrently: one builds, the others wait on the lock."""
+    import fcntl
+    os.makedirs(os.path.dirname(HOSTLANE_SAN_LIB), exist_ok=True)
+    with open(HOSTLANE_SAN_LIB + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        return _build_sanitized(force)
+
+
+def _build_sanitized(force):
     odir = os.path.join(ROOT, "oracle")
     hdrs = [os.path.join(odir, f) for f in ("raft_oracle.hpp", "oracle_testkit.hpp")] + \
         [os.path.join(ROOT, "include", "gpuraft.h")]

@@ -538,6 +538,10 @@ uint64_t gr_space_hot_chunk_bytes(uint32_t positions, uint32_t depth) {
   if (depth == 0 || depth > GR_C) return 0;
   return space_hot_chunk_bytes_pc(space_pad_positions(positions), depth);
 }
+uint64_t gr_space_hot_tile_bytes(uint32_t depth) {
+  if (depth == 0 || depth > GR_C) return 0;
+  return tile_hot_bytes(depth);
+}
 
 int gr_space_cold_used(gr_engine* e, const void* space, uint32_t n_chunks, uint32_t positions, uint32_t depth,
                        void* stream, uint32_t* out) {
@@ -652,7 +656,8 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
   if ((r = grow_device(&e->d_in.p, &e->d_in.n, space))) return r;
   if ((r = grow_device(&e->d_out.p, &e->d_out.n, space))) return r;
   const SpaceView vin = make_view(e->d_in.p, 1, positions), vout = make_view(e->d_out.p, 1, positions);
-  HIPCHK(hipMemsetAsync(e->d_in.p, 0, vin.pc, s));  // the count bytes
+  hipLaunchKernelGGL(io::clear_counts, dim3(io_grid(vin.pc)), blk, 0, s, vin, vin.pc);  // the count bytes
+  HIPCHK(hipGetLastError());
   if (nm) {
     for (gr_engine::Buf* b : {&e->d_keys, &e->d_idx, &e->d_skeys, &e->d_sidx})
       if ((r = grow_device(&b->p, &b->n, (size_t)nm * 4))) return r;
@@ -793,7 +798,8 @@ int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out) {
   if ((r = grow_device(&e->d_in.p, &e->d_in.n, space))) return r;
   if ((r = grow_device(&e->d_out.p, &e->d_out.n, space))) return r;
   const SpaceView vin = make_view(e->d_in.p, 1, positions), vout = make_view(e->d_out.p, 1, positions);
-  HIPCHK(hipMemsetAsync(e->d_in.p, 0, vin.pc, s));  // the count bytes
+  hipLaunchKernelGGL(io::clear_counts, dim3(io_grid(vin.pc)), blk, 0, s, vin, vin.pc);  // the count bytes
+  HIPCHK(hipGetLastError());
   if (nm) {
     for (gr_engine::Buf* b : {&e->d_keys, &e->d_idx, &e->d_skeys, &e->d_sidx})
       if ((r = grow_device(&b->p, &b->n, (size_t)nm * 4))) return r;

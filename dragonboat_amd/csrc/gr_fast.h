@@ -37,6 +37,7 @@ struct FastLane {
   // Leaders with input run here for up to 3 slots; wider groups' leaders take
   // the general lane (keeps this kernel's code and registers small for S = 5)
   static constexpr bool kLeaderPath = S <= 3;
+  static constexpr bool kSync = has_sync_bits(S);  // header sync bits (gr_layout.h)
 
   const StepParams& kp;
   const uint32_t i, p;
@@ -54,11 +55,13 @@ struct FastLane {
   uint32_t mdirty = 0;  // slots whose match/next changed
   uint32_t sdirty = 0;  // slots whose state/active byte changed
   uint32_t snapz = 0;
+  uint32_t have_m = 0, have_n = 0;  // slots whose MATCH / NEXT row was loaded with the hint
+  bool synced = false;              // after the pass: every member slot's next and own match in sync
   // emission
   uint32_t gout[S];
   uint32_t outc[S];
-  uint32_t outnc = 0;    // out mailboxes holding a message that is not compact (MB_ALLCOMPACT)
-  bool resp_nc = false;  // a reject (carries Hint) went out
+  uint32_t n1out = 0;    // leader: bit 4j + k = out Replicate k of slot j carries an entry
+  uint32_t rejout = 0;   // follower: bit k = out ReplicateResp k is a reject (not uniform: tags written)
   uint32_t nmo = 0, nmi = 0, nent = 0;
   uint32_t lslot_out = 0;  // F_LSLOT after the pass (the wave hint)
   bool had_input = false;   // messages or proposals this pass
@@ -91,50 +94,60 @@ struct FastLane {
     nruns++;
     pushed = true;
   }
-  // raft.send (raft.go:457-461) of a Replicate into slot j.
+  // raft.send (raft.go:457-461) of a Replicate into slot j. The lean lane sends
+  // only what a uniform mailbox carries (a compact Replicate: LogTerm = Term, at
+  // most one entry at Term, narrow Commit); anything else is the general lane's.
   GF_HD void emit_replicate(int j, uint64_t log_index, uint64_t log_term, uint32_t n, uint64_t rt0) {
-    GF_BAIL(gout[j] == NOPOS || outc[j] >= kp.out.depth);
-    GF_BAIL(wide_term(term, log_term, n ? rt0 : 0, 0));  // GR_ESC_WIDE_TERM in the general lane
+    GF_BAIL(gout[j] == NOPOS || outc[j] >= kp.out.depth || outc[j] >= kUniformMax);
+    GF_BAIL(wide_term(term, 0, 0, 0));  // GR_ESC_WIDE_TERM in the general lane
+    uint32_t cd;
+    GF_BAIL(!commit_delta(committed, log_index, &cd) || log_term != term || (n && rt0 != term));  // n <= 1 here
     if (!ok) return;
     const Mailbox mb = kp.out.at(gout[j]);
     const uint32_t c = outc[j];
-    uint32_t cd;
-    const bool narrow = commit_delta(committed, log_index, &cd);
-    const bool compact = narrow && log_term == term && (n == 0 || rt0 == term);  // n <= 1 here
-    uint32_t fl = (n ? (1u << MFL_RUNS_SHIFT) : 0u) | (narrow ? 0u : MFL_WIDE_COMMIT);
-    if (compact) fl |= MFL_COMPACT | (n ? MFL_N1 : 0u);
-    else outnc |= 1u << j;
-    ntst(mb.type(c), (uint8_t)(GR_REPLICATE));
-    ntst(mb.flags(c), (uint8_t)(fl));
-    ntst(mb.t32(c, MT_TERM), (uint32_t)((term)));
+    n1out |= (n ? 1u : 0u) << (4 * j + c);  // MB_N1 bits: finish_out
     ntst(mb.u64(c, MF_LOG_INDEX), (uint64_t)(log_index));
-    if (narrow) ntst(mb.t32(c, MT_CDELTA), (uint32_t)(cd));
-    else mb.u64(c, MF_COMMIT) = committed;
-    if (!compact) {
-      ntst(mb.n(c), (uint32_t)(n));
-      ntst(mb.t32(c, MT_LOG_TERM), (uint32_t)((log_term)));
-      if (n) ntst(mb.t32(c, MT_RT0), (uint32_t)((rt0)));
-    }
+    ntst(mb.t32(c, MT_CDELTA), (uint32_t)(cd));
     outc[j] = c + 1;
     nmo++;
   }
-  // ... and of a ReplicateResp into the mailbox at gpos.
+  // ... and of a ReplicateResp into the mailbox at gpos (reject bits into rejout).
   GF_HD void emit_resp(uint32_t gpos, uint32_t* cnt, uint64_t log_index, bool reject, uint64_t hint) {
-    GF_BAIL(gpos == NOPOS || *cnt >= kp.out.depth);
+    GF_BAIL(gpos == NOPOS || *cnt >= kp.out.depth || *cnt >= kUniformMax);
     GF_BAIL(wide_term(term, 0, 0, 0));
     if (!ok) return;
     const Mailbox mb = kp.out.at(gpos);
     const uint32_t c = *cnt;
-    ntst(mb.type(c), (uint8_t)(GR_REPLICATE_RESP));
-    ntst(mb.flags(c), (uint8_t)((reject ? MFL_REJECT : 0u)));
-    ntst(mb.t32(c, MT_TERM), (uint32_t)((term)));
+    rejout |= (reject ? 1u : 0u) << c;  // tags and terms: finish_out
     ntst(mb.u64(c, MF_LOG_INDEX), (uint64_t)(log_index));
-    if (reject) {
-      ntst(mb.u64(c, MF_HINT), (uint64_t)(hint));
-      resp_nc = true;
-    }
+    if (reject) ntst(mb.u64(c, MF_HINT), (uint64_t)(hint));
     *cnt = c + 1;
     nmo++;
+  }
+
+  // The count byte of out mailbox j, and the tags and terms its messages need:
+  // a leader's compact Replicates and a follower's accepts make a uniform mailbox
+  // (MB_UNIFORM, the term word, the entry bits); a follower's mailbox with a
+  // reject gets every tag and term.
+  GF_HD void finish_out(int j, bool lead) {
+    const uint32_t c = outc[j];
+    uint32_t cb = c;
+    if (c) {
+      const Mailbox mb = kp.out.at(gout[j]);
+      if (lead || !rejout) {
+        cb |= MB_UNIFORM | (lead ? 0u : (uint32_t)MB_RESP) | (lead ? ((n1out >> (4 * j)) & 7u) << MB_N1_SHIFT : 0u);
+        ntst(mb.mterm(), (uint32_t)term);
+      } else {
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)GR_C; ++k) {
+          if (k < c) {
+            ntst(mb.tag(k), (uint16_t)(GR_REPLICATE_RESP | (((rejout >> k) & 1u) ? (uint32_t)MFL_REJECT << 8 : 0u)));
+            ntst(mb.t32(k, MT_TERM), (uint32_t)term);
+          }
+        }
+      }
+    }
+    ntst(kp.out.at(gout[j]).cnt(), (uint8_t)cb);
   }
 
   // ------------------------------------------------------------- leader
@@ -273,9 +286,11 @@ struct FastLane {
   // before the lane knows its state; a lane whose role differs from the hint
   // loads what it needs afterwards, so the hint never changes a result.
   GF_HD bool step(LaneStats* ls, uint32_t hint) {
-    const bool hl = kLeaderPath && hint == WH_LEADER;
+    const bool hl = kLeaderPath && (hint & WH_ROLE) == WH_LEADER;
     const bool hf = (hint & WH_ROLE) == WH_FOLLOWER;
     const uint32_t hL = hint >> WH_SLOT_SHIFT;
+    const uint32_t hself = (hint >> WH_SLOT_SHIFT) & 7u;  // leader hints: the self slot
+    const bool hsync = kSync && hl && (hint & WH_SYNC);   // ... whose remote rows were in sync
     // ---- round 1: core (one header word), the newest run (a fixed row), locals,
     //      routes, mailbox counts, and the hinted role's loads
     hdr = ntld(s64(SR_HDR));
@@ -292,53 +307,54 @@ struct FastLane {
       gout[j] = route_of(kp, 1, j, i);
       outc[j] = 0;
     }
-    uint32_t cnt[S];
-    uint32_t allc = 0;  // in mailboxes whose messages are all compact (MB_ALLCOMPACT)
+    // Mailboxes: the lean lane reads uniform ones only (MB_UNIFORM: every tag and
+    // term implied by the count byte and the term word); any other hands over
+    uint32_t cnt[S], cbs[S];
+    uint32_t nonu = 0;  // in mailboxes holding messages without MB_UNIFORM
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       const uint32_t b = gin[j] != NOPOS ? (uint32_t)ntld(kp.in.at(gin[j]).cnt()) : 0u;
       cnt[j] = b & MB_COUNT;
-      allc |= (b & MB_ALLCOMPACT) ? (1u << j) : 0u;
+      cbs[j] = b;
+      nonu |= ((b & MB_COUNT) && !(b & MB_UNIFORM)) ? (1u << j) : 0u;
     }
-    // leader: ReplicateResp (tag, term, LogIndex) from every slot
-    uint32_t lh[S][MK], lterm[S][MK];
+    // leader: the term word and LogIndexes of every in-mailbox (ReplicateResp accepts)
+    uint32_t lmt[S];
     uint64_t lidx[S][MK];
-    if (hl) {  // speculative: match/next and both messages of every in-mailbox
+    if (hl) {  // speculative: match/next (those a synced wave needs), the term word and LogIndexes
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        match[j] = ntld(s64(Rw::MATCH + j));
-        next[j] = ntld(s64(Rw::NEXT + j));
-#pragma unroll
-        for (int k = 0; k < MK; ++k) {
-          lh[j][k] = 0;
-          lterm[j][k] = 0;
-          lidx[j][k] = 0;
-          if (gin[j] != NOPOS) {
-            const Mailbox mb = kp.in.at(gin[j]);
-            lh[j][k] = ntld(mb.tag(k));
-            lterm[j][k] = ntld(mb.t32(k, MT_TERM));
-            lidx[j][k] = ntld(mb.u64(k, MF_LOG_INDEX));
-          }
+        if (!hsync || (uint32_t)j != hself) {
+          match[j] = ntld(s64(Rw::MATCH + j));
+          have_m |= 1u << j;
         }
+        if (!hsync) {
+          next[j] = ntld(s64(Rw::NEXT + j));
+          have_n |= 1u << j;
+        }
+        lmt[j] = gin[j] != NOPOS ? ntld(kp.in.at(gin[j]).mterm()) : 0u;
+#pragma unroll
+        for (int k = 0; k < MK; ++k) lidx[j][k] = gin[j] != NOPOS ? ntld(kp.in.at(gin[j]).u64(k, MF_LOG_INDEX)) : 0;
       }
     }
-    // follower: Replicate fields from the one slot L that sent, + its node id
-    uint32_t fh[MK], fn[MK], fterm[MK], flt[MK], frt0[MK], fcd[MK];
+    // follower: the term word, LogIndexes and Commit offsets of the one slot L that sent
+    uint32_t fcd[MK];
     uint64_t fidx[MK];
+    uint32_t fmt = 0;  // the sender's term word
 #pragma unroll
     for (int k = 0; k < MK; ++k) {
-      fh[k] = 0; fn[k] = 0; fterm[k] = 0; fidx[k] = 0; flt[k] = 0; fcd[k] = 0; frt0[k] = 0;
+      fidx[k] = 0;
+      fcd[k] = 0;
     }
     uint32_t ghL = NOPOS;
-    if (hf) {  // speculative: the hinted leader slot's two compact Replicates
+    if (hf) {  // speculative: the hinted leader slot's term word and two compact Replicates
 #pragma unroll
       for (int j = 0; j < S; ++j) ghL = ((uint32_t)j == hL) ? gin[j] : ghL;
       if (ghL != NOPOS) {
         const Mailbox mb = kp.in.at(ghL);
+        fmt = ntld(mb.mterm());
 #pragma unroll
         for (int k = 0; k < MK; ++k) {
-          fh[k] = ntld(mb.tag(k));
-          fterm[k] = ntld(mb.t32(k, MT_TERM));
           fidx[k] = ntld(mb.u64(k, MF_LOG_INDEX));
           fcd[k] = ntld(mb.t32(k, MT_CDELTA));
         }
@@ -368,27 +384,26 @@ struct FastLane {
         ract[j] = rb_active(rb, j);
         rkind[j] = rb_kind(rb, j);
       }
+      // remote rows: stale ones (sync bits) from lastIndex, the rest loaded unless the hint did
+      const uint64_t sb = kSync ? hdr : 0;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        if (h_ms(sb) && (uint32_t)j == self) match[j] = hi;
+        else if (!((have_m >> j) & 1u)) match[j] = ntld(s64(Rw::MATCH + j));
+        if (h_nx(sb, (uint32_t)j)) next[j] = hi + 1;
+        else if (!((have_n >> j) & 1u)) next[j] = ntld(s64(Rw::NEXT + j));
+      }
       if (!hl) {
 #pragma unroll
         for (int j = 0; j < S; ++j) {
-          match[j] = ntld(s64(Rw::MATCH + j));
-          next[j] = ntld(s64(Rw::NEXT + j));
+          lmt[j] = cnt[j] ? ntld(kp.in.at(gin[j]).mterm()) : 0u;
 #pragma unroll
-          for (int k = 0; k < MK; ++k) {
-            lh[j][k] = 0;
-            lterm[j][k] = 0;
-            lidx[j][k] = 0;
-            if ((uint32_t)k < cnt[j]) {
-              const Mailbox mb = kp.in.at(gin[j]);
-              lh[j][k] = ntld(mb.tag(k));
-              lterm[j][k] = ntld(mb.t32(k, MT_TERM));
-              lidx[j][k] = ntld(mb.u64(k, MF_LOG_INDEX));
-            }
-          }
+          for (int k = 0; k < MK; ++k)
+            lidx[j][k] = (uint32_t)k < cnt[j] ? ntld(kp.in.at(gin[j]).u64(k, MF_LOG_INDEX)) : 0;
         }
       }
     }
-    uint32_t L = 0, nsrc = 0, c = 0, gl = 0, go = NOPOS, lc = 0;
+    uint32_t L = 0, nsrc = 0, c = 0, gl = 0, go = NOPOS, cbL = 0;
     uint64_t rid = 0;
     if (!(kLeaderPath && leader)) {
 #pragma unroll
@@ -398,27 +413,19 @@ struct FastLane {
           c = cnt[j];
           gl = gin[j];
           go = gout[j];
-          lc = (allc >> j) & 1u;
+          cbL = cbs[j];
           nsrc++;
         }
       }
       const uint32_t cc = c < (uint32_t)MK ? c : (uint32_t)MK;
       const bool spec = hf && L == hL;  // the hinted mailbox is the one that sent
+      if (c && !spec) fmt = ntld(kp.in.at(gl).mterm());
 #pragma unroll
       for (int k = 0; k < MK; ++k) {
-        if ((uint32_t)k < cc) {
+        if ((uint32_t)k < cc && !spec) {
           const Mailbox mb = kp.in.at(gl);
-          if (!spec) {
-            fh[k] = ntld(mb.tag(k));
-            fterm[k] = ntld(mb.t32(k, MT_TERM));
-            fidx[k] = ntld(mb.u64(k, MF_LOG_INDEX));
-            fcd[k] = ntld(mb.t32(k, MT_CDELTA));
-          }
-          if (!lc) {  // a compact mailbox carries none of these
-            fn[k] = ntld(mb.n(k));
-            flt[k] = ntld(mb.t32(k, MT_LOG_TERM));
-            frt0[k] = ntld(mb.t32(k, MT_RT0));
-          }
+          fidx[k] = ntld(mb.u64(k, MF_LOG_INDEX));
+          fcd[k] = ntld(mb.t32(k, MT_CDELTA));
         }
       }
       // electionTick = 0 and leaderID = remote_id(L) are usually already so
@@ -451,17 +458,17 @@ struct FastLane {
     GF_BAIL(np && !leader);
     GF_BAIL(!kLeaderPath && leader && any_input);
     GF_BAIL(any_input && !gelo);  // the window test needs firstIndex-1
+    // a non-leader whose remote rows are stale (sync bits) and whose lastIndex
+    // may move: the general lane writes the rows out first (Lane::store)
+    GF_BAIL(kSync && !(kLeaderPath && leader) && any_input && (hdr & H_SYNC_MASK));
     committed0 = committed;
     hi0 = hi;
     if (kLeaderPath && leader) {
       GF_BAIL(flags & F_LTT);  // leader transfer in progress
 #pragma unroll
-      for (int j = 0; j < S; ++j) {
-        GF_BAIL(cnt[j] > (uint32_t)MK);
-#pragma unroll
-        for (int k = 0; k < MK; ++k)
-          if ((uint32_t)k < cnt[j]) GF_BAIL(lh[j][k] != GR_REPLICATE_RESP || (uint64_t)lterm[j][k] != term);
-      }
+      for (int j = 0; j < S; ++j)  // uniform accepts (ReplicateResp, flags 0) at the current term
+        GF_BAIL(cnt[j] && (cnt[j] > (uint32_t)MK || !(cbs[j] & MB_RESP) || (uint64_t)lmt[j] != term));
+      GF_BAIL(nonu);
       // messages in node.handleReceivedMessages order: slot, then arrival
 #pragma unroll
       for (int j = 0; j < S; ++j) {
@@ -475,32 +482,22 @@ struct FastLane {
       }
       if (np) propose(np);
     } else {
-      GF_BAIL(nsrc > 1 || c > (uint32_t)MK);
-#pragma unroll
-      for (int k = 0; k < MK; ++k) {
-        if ((uint32_t)k < c) {
-          GF_BAIL((fh[k] & 0xFFu) != GR_REPLICATE || (uint64_t)fterm[k] != term);
-          GF_BAIL(fh[k] & ((uint32_t)MFL_WIDE_COMMIT << 8));
-          if (fh[k] & ((uint32_t)MFL_COMPACT << 8)) {  // LogTerm = Term, <= 1 entry at Term
-            fn[k] = (fh[k] & ((uint32_t)MFL_N1 << 8)) ? 1u : 0u;
-            flt[k] = fterm[k];
-            frt0[k] = fterm[k];
-          }
-          const uint32_t nr = (fh[k] >> (8 + MFL_RUNS_SHIFT)) & 3u;
-          GF_BAIL(fn[k] != 0 && nr != 1);
-        }
-      }
+      // uniform compact Replicates (LogTerm = Term, at most one entry at Term,
+      // narrow Commit) from one remote at the current term
+      GF_BAIL(nsrc > 1 || c > (uint32_t)MK || nonu || (c && ((cbL & MB_RESP) || (uint64_t)fmt != term)));
       uint32_t oc = 0;
 #pragma unroll
       for (int k = 0; k < MK; ++k) {
         if ((uint32_t)k < c) {
           nmi++;
-          replicate(fidx[k], (uint64_t)flt[k], commit_of(fcd[k], fidx[k]), fn[k], (uint64_t)frt0[k], go, &oc);
+          const uint32_t n1 = (cbL >> (MB_N1_SHIFT + k)) & 1u;
+          replicate(fidx[k], term, commit_of(fcd[k], fidx[k]), n1, term, go, &oc);
         }
       }
 #pragma unroll
-      for (int j = 0; j < S; ++j) outc[j] = ((uint32_t)j == L) ? oc : 0u;
-      if (resp_nc) outnc |= 1u << L;
+      for (int j = 0; j < S; ++j) {
+        outc[j] = ((uint32_t)j == L) ? oc : 0u;
+      }
     }
     if (!ok) return false;
     // ---- stores (nothing above this line has written state)
@@ -520,18 +517,33 @@ struct FastLane {
     }
     if (kLeaderPath && leader) {
       uint64_t rb = h_rb(nh);
+      // sync bits: a row in sync with the final lastIndex is not stored (its bit
+      // says so); a row that leaves sync, or changed, is
+      uint64_t sbits = 0;
+      bool all_nx = true, own_ms = false;
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        if ((mdirty >> j) & 1u) {
+        const bool nx_now = kSync && next[j] == hi + 1;
+        const bool ms_now = kSync && (uint32_t)j == self && match[j] == hi;
+        const bool dj = (mdirty >> j) & 1u;
+        if ((dj || (kSync && h_ms(hdr) && (uint32_t)j == self)) && !ms_now)
           ntst(s64(Rw::MATCH + j), (uint64_t)(match[j]));
-          ntst(s64(Rw::NEXT + j), (uint64_t)(next[j]));
-        }
+        if ((dj || (kSync && h_nx(hdr, (uint32_t)j))) && !nx_now) ntst(s64(Rw::NEXT + j), (uint64_t)(next[j]));
+        sbits |= (nx_now ? 1ull : 0ull) << (H_NX_SHIFT + j);
+        sbits |= (ms_now ? 1ull : 0ull) << H_MS_BIT;
+        own_ms = own_ms || ms_now;
+        if (rkind[j] != GR_SLOT_EMPTY && !nx_now) all_nx = false;
+      }
+      synced = kSync && own_ms && all_nx;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
         if ((sdirty >> j) & 1u) {
           rb = rb_with(rb, j, 0, 2, rst[j]);
           rb = rb_with(rb, j, 2, 1, ract[j]);
         }
       }
       nh = (nh & ((1ull << H_REM_SHIFT) - 1)) | (rb << H_REM_SHIFT);
+      if (kSync) nh = (nh & ~H_SYNC_MASK) | sbits;
 #pragma unroll
       for (int j = 0; j < S; ++j)
         if ((snapz >> j) & 1u) ntst(s64(Rw::SNAP + j), (uint64_t)(0));
@@ -551,8 +563,7 @@ struct FastLane {
     if (nh != hdr) ntst(s64(SR_HDR), nh);
 #pragma unroll
     for (int j = 0; j < S; ++j)
-      if (gout[j] != NOPOS)
-        ntst(kp.out.at(gout[j]).cnt(), (uint8_t)((outc[j] | (((outnc >> j) & 1u) ? 0u : MB_ALLCOMPACT))));
+      if (gout[j] != NOPOS) finish_out(j, kLeaderPath && leader);
     uint8_t rf = 0;
     if (prop_result) {  // propose_first = last_index - n + 1 (gr_layout.h)
       rf |= RF_PROPOSE;
@@ -580,7 +591,8 @@ struct FastLane {
   // pass when it finished here, what it was when it handed over.
   GF_HD uint32_t role_hint() const {
     if (!had_input) return 0;  // quiesced or idle: nothing to speculate on
-    if (state == GR_LEADER) return WH_LEADER;
+    if (state == GR_LEADER)
+      return WH_LEADER | (self < 8u ? self << WH_SLOT_SHIFT : 0u) | (synced && self < 8u ? WH_SYNC : 0u);
     if (state != GR_FOLLOWER || !lslot_out) return 0;
     return WH_FOLLOWER | ((lslot_out - 1) << WH_SLOT_SHIFT);
   }

@@ -44,6 +44,15 @@ __host__ __device__ inline void set_header(gr_peer& g, uint32_t S, uint64_t h) {
   }
 }
 
+// The header's sync bits (gr_layout.h): the rows they cover are stale and the
+// values follow from lastIndex. Applied after every row of g has been set.
+__host__ __device__ inline void resolve_sync(gr_peer& g, uint32_t S, uint64_t h) {
+  if (!has_sync_bits((int)S)) return;  // wider groups: those header bits are remote state
+  for (uint32_t j = 0; j < S; ++j)
+    if (h_nx(h, j)) g.remotes[j].next = g.last_index + 1;
+  if (h_ms(h) && g.self_slot < S) g.remotes[g.self_slot].match = g.last_index;
+}
+
 // Rows are converted in ascending order: SR_HDR (which carries n_runs) comes
 // before the right-aligned run rows that need it.
 __host__ __device__ inline uint64_t get_u64_row(const gr_peer& g, uint32_t row, uint32_t S) {
@@ -164,14 +173,51 @@ __host__ __device__ inline void encode_msg(const Mailbox& mb, uint32_t k, const 
   mb.t32(k, MT_RT1) = (uint32_t)(m.run_term[1]);
 }
 
+// Can m travel in a uniform mailbox (gr_layout.h MB_UNIFORM)? 0 = no; else
+// 1 | 2 for a ReplicateResp accept | 4 for a Replicate carrying its one entry.
+// A uniform Replicate is compact (LogTerm = Term, at most one entry at Term,
+// narrow Commit), so its compact decode equals the full one.
+__host__ __device__ inline uint32_t uniform_class(const gr_message& m) {
+  if (wide_term(m.term, m.log_term, m.run_term[0], m.run_term[1])) return 0;
+  if (m.type == GR_REPLICATE_RESP) return m.reject ? 0u : 3u;  // an accept carries Term and LogIndex
+  if (m.type != GR_REPLICATE) return 0;
+  uint32_t cd;
+  if (!commit_delta(m.commit, m.log_index, &cd) || m.log_term != m.term) return 0;
+  if (m.n_entries == 0) return m.n_runs == 0 ? 1u : 0u;
+  return (m.n_entries == 1 && m.n_runs == 1 && m.run_term[0] == m.term) ? 5u : 0u;
+}
+// The count byte of a mailbox whose `count` messages (at(q), q < count) are
+// encoded: MB_UNIFORM with the term word written when they all allow it.
+template <class MsgAt>
+__host__ __device__ inline uint8_t count_byte(const Mailbox& mb, uint32_t count, MsgAt at) {
+  if (count == 0 || count > kUniformMax) return (uint8_t)count;
+  uint32_t cb = count | MB_UNIFORM;
+  uint64_t t0 = 0;
+  for (uint32_t q = 0; q < count; ++q) {
+    const gr_message m = at(q);
+    const uint32_t u = uniform_class(m);
+    if (!u) return (uint8_t)count;
+    if (q == 0) {
+      t0 = m.term;
+      if (u & 2) cb |= MB_RESP;
+    } else if (m.term != t0 || ((u & 2) != 0) != ((cb & MB_RESP) != 0)) {
+      return (uint8_t)count;
+    }
+    if (u & 4) cb |= 1u << (MB_N1_SHIFT + q);
+  }
+  mb.mterm() = (uint32_t)t0;
+  return (uint8_t)cb;
+}
+
 // Decode one message; fields a type does not carry on the device are zero.
 __host__ __device__ inline gr_message decode_msg(const Mailbox& mb, uint32_t k) {
   gr_message m{};  // no padding in gr_message: every byte is a zeroed field
-  m.type = mb.type(k);
-  const uint8_t fl = mb.flags(k);
+  const uint32_t cb = mb.cnt(), tg = mb.tag_at(k, cb);  // MB_UNIFORM: tag and term implied
+  m.type = (uint8_t)tg;
+  const uint8_t fl = (uint8_t)(tg >> 8);
   m.reject = (fl & MFL_REJECT) ? 1 : 0;
   m.n_runs = (fl >> MFL_RUNS_SHIFT) & 3u;
-  m.term = (uint64_t)mb.t32(k, MT_TERM);
+  m.term = (uint64_t)mb.term_at(k, cb);
   switch (m.type) {
     case GR_REPLICATE:
       if (fl & MFL_COMPACT) {  // gr_layout.h: LogTerm = Term, <= 1 entry at Term, narrow Commit
@@ -514,6 +560,7 @@ inline SpaceView make_view(const void* base, uint32_t n_chunks, uint32_t positio
 
 inline void encode_inbox(const gr_inbox* in, const PackedInbox& pk, void* space) {
   const SpaceView v = make_view(space, 1, pk.in_positions);
+  std::vector<std::vector<size_t>> by_pos(pk.in_positions);  // messages of each mailbox, in order
   for (size_t k = 0; k < in->n_msgs; ++k) {
     const Mailbox mb = v.at(pk.msg_pos[k].first);
     if (pk.msg_pos[k].second >= GR_C) {
@@ -522,6 +569,12 @@ inline void encode_inbox(const gr_inbox* in, const PackedInbox& pk, void* space)
     }
     encode_msg(mb, pk.msg_pos[k].second, in->msgs[k]);
     mb.cnt() = (uint8_t)(pk.msg_pos[k].second + 1);
+    by_pos[pk.msg_pos[k].first].push_back(k);
+  }
+  for (uint32_t g = 0; g < pk.in_positions; ++g) {
+    const Mailbox mb = v.at(g);
+    if (by_pos[g].empty() || mb.cnt() > GR_C) continue;
+    mb.cnt() = count_byte(mb, (uint32_t)by_pos[g].size(), [&](uint32_t q) { return in->msgs[by_pos[g][q]]; });
   }
 }
 

@@ -90,7 +90,9 @@ __global__ void encode_sorted(const gr_message* msgs, const uint32_t* skeys, con
     while (r <= (uint32_t)GR_C && r < s && skeys[s - r - 1] == key) ++r;
     const Mailbox mb = v.at(key);
     if (r < (uint32_t)GR_C) host::encode_msg(mb, r, msgs[sidx[s]]);
-    if (s + 1 == n || skeys[s + 1] != key) mb.cnt() = (uint8_t)(r < (uint32_t)GR_C ? r + 1 : GR_C + 1);
+    if (s + 1 == n || skeys[s + 1] != key)  // the mailbox's last record: its count byte (uniform when it can be)
+      mb.cnt() = r < (uint32_t)GR_C ? host::count_byte(mb, r + 1, [&](uint32_t q) { return msgs[sidx[s - r + q]]; })
+                                    : (uint8_t)(GR_C + 1);
   }
 }
 
@@ -202,7 +204,10 @@ __global__ void encode_sorted_c(CInbox in, const uint32_t* skeys, const uint32_t
     while (r <= (uint32_t)GR_C && r < s && skeys[s - r - 1] == key) ++r;
     const Mailbox mb = v.at(key);
     if (r < (uint32_t)GR_C) host::encode_msg(mb, r, host::expand_cmsg(in.msgs[sidx[s]], in.ext));
-    if (s + 1 == n || skeys[s + 1] != key) mb.cnt() = (uint8_t)(r < (uint32_t)GR_C ? r + 1 : GR_C + 1);
+    if (s + 1 == n || skeys[s + 1] != key)
+      mb.cnt() = r < (uint32_t)GR_C ? host::count_byte(mb, r + 1, [&](uint32_t q) {
+        return host::expand_cmsg(in.msgs[sidx[s - r + q]], in.ext);
+      }) : (uint8_t)(GR_C + 1);
   }
 }
 
@@ -290,14 +295,21 @@ __global__ void pack_results_c(LaneBase L, StateBase st, const uint32_t* peer_of
 }
 
 // Does any mailbox of the space hold a message with cold fields (nonempty and
-// without MB_ALLCOMPACT)? One store per wave that finds one.
+// without MB_UNIFORM)? One store per wave that finds one.
 __global__ void cold_used(SpaceView v, uint32_t* flag) {
   const uint64_t n = (uint64_t)v.n_chunks * v.pc;
   for (uint64_t g = io_tid(); g < n; g += io_stride()) {
-    const uint8_t c = v.base[(g / v.pc) * v.hot_bytes + g % v.pc];
-    const bool cold = (c & MB_COUNT) && !(c & MB_ALLCOMPACT);
+    const uint8_t c = v.at((uint32_t)g).cnt();
+    const bool cold = (c & MB_COUNT) && !(c & MB_UNIFORM);
     if (__ballot(cold) && (threadIdx.x & 63) == 0) *flag = 1;
   }
+}
+
+// Zero the mailbox counts of chunk 0's first `positions` positions (the
+// host-path inbox before encoding): one byte row untiled, the first 64 bytes of
+// each tile with GR_TILE.
+__global__ void clear_counts(SpaceView v, uint32_t positions) {
+  for (uint32_t g = io_tid(); g < positions; g += io_stride()) v.at(g).cnt() = 0;
 }
 
 // ---- gr_peer records <-> SoA state rows: gr_load_groups/gr_sync_groups_to_host
@@ -338,6 +350,7 @@ __global__ void rows_to_peers(StateBase st, const uint32_t* slots, uint32_t firs
     const uint32_t p = slots ? slots[x] : first + x;
     gr_peer& g = out[x];
     for (uint32_t r = 0; r < n64; ++r) host::set_u64_row(g, r, S, st.u64(r)[p]);
+    host::resolve_sync(g, S, st.u64(SR_HDR)[p]);
     for (uint32_t r = 0; r < n8; ++r) host::set_u8_row(g, r, S, st.u8(r)[p]);
   }
 }

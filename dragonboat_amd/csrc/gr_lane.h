@@ -90,6 +90,7 @@ struct Lane {
 
   // G_CORE
   uint64_t hdr0 = 0;  // the header word as loaded
+  uint64_t hi_ld = 0;  // lastIndex as loaded (the sync bits' reference, gr_layout.h)
   uint32_t state = 0, flags = 0, self = GR_SLOT_NONE;
   uint64_t term = 0, committed = 0, hi = 0;
   // G_ETICK / G_TICKS
@@ -114,6 +115,7 @@ struct Lane {
 
   // outputs of this pass
   uint32_t outcnt = 0;  // 3 bits per slot
+  uint64_t outu = 0;    // 5 bits per slot: not uniform, ReplicateResp kind, MB_N1 of messages 0..2
   uint32_t rtrc = 0, prop_result = 0;
   bool rand_used = false;
   uint64_t append_from = 0, propose_first = 0;
@@ -141,6 +143,7 @@ struct Lane {
       committed = s64(SR_COMMITTED);
       committed0 = committed;
       hi = s64(SR_LAST_INDEX);
+      hi_ld = hi;
     }
     if (miss & G_ETICK) etick = s64(SR_ETICK);
     if (miss & G_LID) leader_id = s64(SR_LEADER_ID);
@@ -168,10 +171,11 @@ struct Lane {
     }
     if (miss & G_REM) {
       rb = h_rb(hdr0) & ((1ull << (5 * S)) - 1);
+      const uint64_t sb = has_sync_bits(S) ? hdr0 : 0;  // stale rows: values from lastIndex as loaded
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        match[j] = s64(R::MATCH + j);
-        next[j] = s64(R::NEXT + j);
+        match[j] = (h_ms(sb) && (uint32_t)j == h_self(hdr0)) ? hi_ld : s64(R::MATCH + j);
+        next[j] = h_nx(sb, (uint32_t)j) ? hi_ld + 1 : s64(R::NEXT + j);
       }
     }
     if (miss & G_SNAP) {
@@ -201,6 +205,13 @@ struct Lane {
 
 
   GR_HD void store() {
+    // Sync bits (gr_layout.h) hold only while lastIndex and the remote rows do:
+    // a pass that changes either writes the remote rows out and clears them.
+    const bool unsync = has_sync_bits(S) && (hdr0 & H_SYNC_MASK) && (dirty & (D_HI | D_REM));
+    if (unsync) {
+      need(G_REM);
+      dirty |= D_REM;
+    }
     if (dirty & (D_LTT | D_ETICK | D_LEADER)) {  // device-internal flag bits (gr_layout.h)
       need(G_CORE);
       uint32_t nf = flags;
@@ -268,7 +279,7 @@ struct Lane {
     if (dirty & (D_STATE | D_FLAGS | D_WIN | D_REM | D_RI)) {  // one header word for the small fields
       uint64_t h = hdr0;
       const uint64_t remmask = ((1ull << (5 * S)) - 1) << H_REM_SHIFT;
-      const uint64_t keep_rem = h & (~0ull << H_REM_SHIFT) & ~remmask;  // bits above this S (none in practice)
+      const uint64_t keep_rem = h & (~0ull << H_REM_SHIFT) & ~remmask & ~(unsync ? H_SYNC_MASK : 0ull);
       uint32_t nr = h_nruns(h);
       bool gelo = h_gelo(h);
       if (dirty & D_WIN) {
@@ -527,6 +538,25 @@ struct Lane {
         mb.t32(c, MT_RT1) = (uint32_t)(m.rt1);
         break;
     }
+    // uniform mailbox bookkeeping (gr_layout.h MB_UNIFORM): compact Replicates or
+    // accepts of one kind and one term, at most kUniformMax; the term word is
+    // written with message 0 and compared with it by the later ones
+    uint32_t cd0;
+    const uint32_t runs = (m.flags >> MFL_RUNS_SHIFT) & 3u;
+    const bool resp = m.type == GR_REPLICATE_RESP;
+    const bool uni = resp ? !(m.flags & MFL_REJECT)
+                          : m.type == GR_REPLICATE && commit_delta(m.commit, m.log_index, &cd0) &&
+                                m.log_term == mterm &&
+                                (m.n == 0 ? runs == 0 : (m.n == 1 && runs == 1 && m.rt0 == mterm));
+    const uint32_t sh = 5 * j;
+    if (c == 0) {
+      mb.mterm() = (uint32_t)mterm;
+      if (resp) outu |= 2ull << sh;
+    } else if (mb.mterm() != (uint32_t)mterm || resp != (((outu >> sh) & 2ull) != 0)) {
+      outu |= 1ull << sh;
+    }
+    if (!uni || c >= kUniformMax) outu |= 1ull << sh;
+    else if (!resp && m.n) outu |= 4ull << (sh + c);
     outcnt += 1u << (3 * j);
     msgs_out++;
     return 0;
@@ -1117,10 +1147,11 @@ struct Lane {
   }
 
   // ---------------------------------------------------------------- messages
-  GR_HD void read_msg(const Mailbox& mb, uint32_t k, InMsg& m) const {
-    m.type = mb.type(k);
-    m.flags = mb.flags(k);
-    m.term = (uint64_t)mb.t32(k, MT_TERM);
+  GR_HD void read_msg(const Mailbox& mb, uint32_t cb, uint32_t k, InMsg& m) const {
+    const uint32_t tg = mb.tag_at(k, cb);  // cb: the count byte (MB_UNIFORM: tag and term implied)
+    m.type = (uint8_t)tg;
+    m.flags = (uint8_t)(tg >> 8);
+    m.term = (uint64_t)mb.term_at(k, cb);
     m.n = 0; m.run2 = 0;
     m.log_index = 0; m.log_term = 0; m.commit = 0; m.hint = 0; m.hint_high = 0; m.rt0 = 0; m.rt1 = 0;
     switch (m.type) {
@@ -1396,6 +1427,7 @@ struct Lane {
 
   // ---------------------------------------------------------------- driver
   GR_HD void begin() {
+    outu = 0;
     loaded = 0;
     dirty = 0;
     snapz = 0;
@@ -1420,13 +1452,13 @@ struct Lane {
       const uint32_t g = in_gpos(j);
       if (g == NOPOS) continue;
       const Mailbox mb = kp.in.at(g);
-      const uint32_t c = mb.cnt() & MB_COUNT;
+      const uint32_t cb = mb.cnt(), c = cb & MB_COUNT;
 #pragma unroll 1
       for (uint32_t k = 0; k < c; ++k) {
         if (item == limit) { *at = item; return 0; }
         if (k == kp.in.depth) { *at = item; return GR_ESC_CAPACITY; }  // overflowed mailbox
         InMsg m;
-        read_msg(mb, k, m);
+        read_msg(mb, cb, k, m);
         if (m.type == MT_WIDE) { *at = item; return GR_ESC_WIDE_TERM; }  // terms >= 2^32: host path
         const int e = handle(m, j);
         if (e) { *at = item; return e; }
@@ -1501,7 +1533,11 @@ struct Lane {
 #pragma unroll 1
     for (uint32_t j = 0; j < (uint32_t)S; ++j) {  // every routed mailbox is rewritten each pass
       const uint32_t g = out_gpos(j);
-      if (g != NOPOS) kp.out.at(g).cnt() = (uint8_t)((outcnt >> (3 * j)) & 7u);
+      if (g == NOPOS) continue;
+      const uint32_t c = (outcnt >> (3 * j)) & 7u, u = (uint32_t)(outu >> (5 * j)) & 31u;
+      kp.out.at(g).cnt() = (uint8_t)(c && !(u & 1u) ? c | MB_UNIFORM | ((u & 2u) ? (uint32_t)MB_RESP : 0u) |
+                                                         ((u >> 2) << MB_N1_SHIFT)
+                                                   : c);
     }
     uint8_t rf = 0;
     if (esc) {

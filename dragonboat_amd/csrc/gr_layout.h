@@ -22,15 +22,14 @@
 // chunk so a wave of lanes reading "message k of its mailbox" is coalesced.
 // A space is n_chunks hot chunks followed by n_chunks cold chunks
 // (pc = positions per chunk, a multiple of 64; depth = messages per mailbox):
-//   hot chunk:  [cnt u8 x pc] then for k < depth:
-//               [tag u16 x pc = type | flags << 8][term u32 x pc][commit offset u32 x pc][LogIndex u64 x pc]
-//   cold chunk: for k < depth: [n u32][run2 u32][log term u32][run term 0 u32][run term 1 u32]
-//               [Commit u64][Hint u64][HintHigh u64] (each x pc)
-// Compact Replicates and non-reject ReplicateResps -- every steady-state message --
-// live in the hot chunk alone (18 B), and a mailbox whose messages all do carries
-// MB_ALLCOMPACT, so its readers never touch the cold chunk. An exchange between
-// GPUs moves the hot region always and the cold region only when some mailbox
-// lacks the bit (gr_space_cold_used).
+//   hot chunk:  [cnt u8 x pc][term word u32 x pc] then for k < depth:
+//               [commit offset u32 x pc][LogIndex u64 x pc]
+//   cold chunk: for k < depth: [tag u16 x pc = type | flags << 8][term u32][n u32][run2 u32]
+//               [log term u32][run term 0 u32][run term 1 u32][Commit u64][Hint u64][HintHigh u64] (each x pc)
+// A uniform mailbox (MB_UNIFORM: the lean lane's steady-state compact Replicates
+// or accepts, one term) lives in the hot chunk alone: 5 B plus 12 B per message.
+// An exchange between GPUs moves the hot region always and the cold region only
+// when some mailbox lacks the bit (gr_space_cold_used).
 // Terms travel as 32 bits: a message whose term, log term or entry-run terms
 // reach 2^32 never enters a mailbox (the sender escalates GR_ESC_WIDE_TERM;
 // a host-encoded inbox marks it MT_WIDE and the receiver escalates there), so
@@ -101,6 +100,20 @@ __host__ __device__ inline uint64_t h_make(uint32_t state, uint32_t self, uint32
          ((uint64_t)(gelo ? 1u : 0u) << H_GE_LO_BIT) | ((uint64_t)(flags & 0xFFu) << H_FLAGS_SHIFT) |
          ((uint64_t)(ric & 7u) << H_RIC_SHIFT) | (rb << H_REM_SHIFT);
 }
+// Sync bits (S <= 3; above rb): bit H_NX_SHIFT + j says next[j] == lastIndex + 1
+// and the NEXT row of slot j is stale; H_MS_BIT says match[self] == lastIndex and
+// the MATCH row of the self slot is stale. Those are a steady-state leader's
+// values (appendEntries advances its own remote, raft.go:643-654; every send in
+// the Replicate state moves next to lastIndex + 1, remote.go:120-128), so the lean
+// lane keeps them in the header instead of loading and storing 4 of its 6 remote
+// rows per pass. Every other writer of lastIndex or of the remote rows first
+// materialises the rows and clears the bits (Lane::store); the tick lane only
+// reads them; host conversion resolves them (host::resolve_sync).
+constexpr uint32_t H_NX_SHIFT = 56, H_MS_BIT = 59;
+constexpr uint64_t H_SYNC_MASK = (7ull << H_NX_SHIFT) | (1ull << H_MS_BIT);
+__host__ __device__ constexpr bool has_sync_bits(int S) { return S <= 3; }
+__host__ __device__ inline bool h_nx(uint64_t h, uint32_t j) { return (h >> (H_NX_SHIFT + j)) & 1u; }
+__host__ __device__ inline bool h_ms(uint64_t h) { return (h >> H_MS_BIT) & 1u; }
 // per-slot fields of rb (5 bits per slot: state(2) active(1) kind(2))
 __host__ __device__ inline uint32_t rb_state(uint64_t rb, uint32_t j) { return (uint32_t)(rb >> (5 * j)) & 3u; }
 __host__ __device__ inline uint32_t rb_active(uint64_t rb, uint32_t j) { return (uint32_t)(rb >> (5 * j + 2)) & 1u; }
@@ -113,16 +126,40 @@ __host__ __device__ inline uint64_t state_bytes(uint32_t S, uint32_t cap) {
   return (uint64_t)cap * (8ull * rows_u64(S) + rows_u8(S));
 }
 
+// GR_TILE = 1: the rows are tiled by 64 slots (one wave): tile t holds every
+// row of slots 64t..64t+63, row-major inside the tile, so a wave's fields are
+// one contiguous block (a few KB) instead of ~30 separate row streams
+// (24 MB apart at 1M x 3). GR_TILE = 0: plain rows over all slots.
+#ifndef GR_TILE
+#define GR_TILE 1
+#endif
+template <class T>
+struct TileRow {  // row `row` of a tiled region with `nrows` rows per tile
+  T* b;
+  uint32_t row, nrows;
+  __host__ __device__ inline T& operator[](uint64_t p) const {
+    return b[((p >> 6) * nrows + row) * 64 + (p & 63)];
+  }
+};
 struct StateBase {
   uint8_t* base;
   uint32_t cap;  // padded, multiple of 64
   uint32_t S;
+#if GR_TILE
+  __host__ __device__ inline TileRow<uint64_t> u64(uint32_t row) const {
+    return {reinterpret_cast<uint64_t*>(base), row, rows_u64(S)};
+  }
+  __host__ __device__ inline TileRow<uint8_t> u8(uint32_t row) const {
+    return {base + 8ull * cap * rows_u64(S), row, rows_u8(S)};
+  }
+#else
   __host__ __device__ inline uint64_t* u64(uint32_t row) const {
     return reinterpret_cast<uint64_t*>(base) + (uint64_t)row * cap;
   }
   __host__ __device__ inline uint8_t* u8(uint32_t row) const {
     return base + 8ull * cap * rows_u64(S) + (uint64_t)row * cap;
   }
+#endif
 };
 
 // ---------------------------------------------------------------- lane rows
@@ -207,9 +244,15 @@ constexpr uint8_t MFL_WIDE_COMMIT = 0x08; // Replicate: Commit in MF_COMMIT (els
 constexpr uint8_t MFL_COMPACT = 0x10;
 constexpr uint8_t MFL_N1 = 0x20;
 // The mailbox count byte: bits 0-2 the count (GR_C + 1 marks an overflowed
-// host-encoded mailbox), bit 3 set when every message in it is a compact
-// Replicate or a non-reject ReplicateResp, so a reader can skip the other fields.
-constexpr uint8_t MB_COUNT = 0x07, MB_ALLCOMPACT = 0x08;
+// host-encoded mailbox). Bit 3 (MB_UNIFORM): at most kUniformMax messages, all
+// compact Replicates (bit 4 clear) or all non-reject ReplicateResps (bit 4 set),
+// all at the mailbox's term word; bits 5.. give MFL_N1 of message 0, 1, 2. Such
+// a mailbox stores only the hot fields (the term word, and LogIndex + Commit
+// offset per message): readers rebuild every tag and term from the count byte,
+// so they touch neither the per-message tags and terms nor the cold chunk. Only
+// the lean lane writes uniform mailboxes; every other writer stores all fields.
+constexpr uint8_t MB_COUNT = 0x07, MB_UNIFORM = 0x08, MB_RESP = 0x10;
+constexpr uint32_t MB_N1_SHIFT = 5, kUniformMax = 3;
 // A Replicate's Commit travels as a 32-bit offset from its LogIndex when
 // |Commit - LogIndex| < 2^31 (always, unless a follower lags by 2^31 entries);
 // otherwise in full with MFL_WIDE_COMMIT. Both decode exactly.
@@ -230,13 +273,19 @@ __host__ __device__ inline bool wide_term(uint64_t a, uint64_t b, uint64_t c, ui
 __host__ __device__ inline uint32_t space_pad_positions(uint32_t positions) {
   return (positions + 63u) & ~63u;
 }
-constexpr uint32_t kHotK = 18;   // bytes per position per message, hot chunk
-constexpr uint32_t kColdK = 44;  // ... cold chunk
+constexpr uint32_t kHotH = 5;    // bytes per position, hot chunk header: count + term word
+constexpr uint32_t kHotK = 12;   // bytes per position per message, hot chunk: Commit offset + LogIndex
+constexpr uint32_t kColdK = 50;  // ... cold chunk: tag, term and the rest
 __host__ __device__ inline uint64_t round256(uint64_t b) { return (b + 255u) & ~(uint64_t)255u; }
 // A space's mailbox depth (1..GR_C) fixes its chunk sizes: spaces that cross
 // xGMI use the depth the steady state needs (2).
+// GR_TILE: a chunk's positions are tiled by 64 (pc is a multiple of 64): tile t
+// of the hot region holds the counts and hot fields of positions 64t..64t+63,
+// the same SoA order as an untiled chunk of 64 positions; the cold region alike.
+__host__ __device__ inline uint64_t tile_hot_bytes(uint32_t depth) { return 64ull * (kHotH + kHotK * depth); }
+__host__ __device__ inline uint64_t tile_cold_bytes(uint32_t depth) { return 64ull * kColdK * depth; }
 __host__ __device__ inline uint64_t space_hot_chunk_bytes_pc(uint32_t pc, uint32_t depth = GR_C) {
-  return round256((uint64_t)pc * (1 + kHotK * depth));
+  return round256((uint64_t)pc * (kHotH + kHotK * depth));  // = pc/64 tiles when tiled
 }
 __host__ __device__ inline uint64_t space_cold_chunk_bytes_pc(uint32_t pc, uint32_t depth = GR_C) {
   return round256((uint64_t)pc * kColdK * depth);
@@ -278,27 +327,46 @@ struct Mailbox {
   uint8_t* cold;  // ... and its cold part
   uint32_t local;
   uint32_t pc;
-  __host__ __device__ inline uint8_t* hk(uint32_t k) const { return hot + pc + (uint64_t)k * kHotK * pc; }
+  // hot:  [count u8][term word u32], then per message [Commit offset u32][LogIndex u64]
+  // cold: per message [tag u16][term u32][n u32][run2 u32][log term u32][rt0 u32][rt1 u32]
+  //       [Commit u64][Hint u64][HintHigh u64]     (each field x pc positions)
+  __host__ __device__ inline uint8_t* hk(uint32_t k) const { return hot + (kHotH + (uint64_t)k * kHotK) * pc; }
   __host__ __device__ inline uint8_t* ck(uint32_t k) const { return cold + (uint64_t)k * kColdK * pc; }
   __host__ __device__ inline uint8_t& cnt() const { return hot[local]; }
-  __host__ __device__ inline uint8_t& type(uint32_t k) const { return hk(k)[2 * local]; }
-  __host__ __device__ inline uint8_t& flags(uint32_t k) const { return hk(k)[2 * local + 1]; }
+  __host__ __device__ inline uint32_t& mterm() const { return reinterpret_cast<uint32_t*>(hot + pc)[local]; }
+  __host__ __device__ inline uint8_t& type(uint32_t k) const { return ck(k)[2 * local]; }
+  __host__ __device__ inline uint8_t& flags(uint32_t k) const { return ck(k)[2 * local + 1]; }
   // type | flags << 8 in one access (little-endian)
-  __host__ __device__ inline uint16_t& tag(uint32_t k) const { return reinterpret_cast<uint16_t*>(hk(k))[local]; }
-  __host__ __device__ inline uint32_t& n(uint32_t k) const { return reinterpret_cast<uint32_t*>(ck(k))[local]; }
+  __host__ __device__ inline uint16_t& tag(uint32_t k) const { return reinterpret_cast<uint16_t*>(ck(k))[local]; }
+  __host__ __device__ inline uint32_t& n(uint32_t k) const {
+    return reinterpret_cast<uint32_t*>(ck(k) + 6ull * pc)[local];
+  }
   __host__ __device__ inline uint32_t& run2(uint32_t k) const {
-    return reinterpret_cast<uint32_t*>(ck(k) + 4ull * pc)[local];
+    return reinterpret_cast<uint32_t*>(ck(k) + 10ull * pc)[local];
   }
   __host__ __device__ inline uint32_t& t32(uint32_t k, uint32_t f) const {
-    if (f == MT_TERM) return reinterpret_cast<uint32_t*>(hk(k) + 2ull * pc)[local];
-    if (f == MT_CDELTA) return reinterpret_cast<uint32_t*>(hk(k) + 6ull * pc)[local];
-    // MT_LOG_TERM, MT_RT0, MT_RT1: cold words 2..4
-    return reinterpret_cast<uint32_t*>(ck(k) + (8ull + 4ull * (f - MT_LOG_TERM)) * pc)[local];
+    if (f == MT_CDELTA) return reinterpret_cast<uint32_t*>(hk(k))[local];
+    if (f == MT_TERM) return reinterpret_cast<uint32_t*>(ck(k) + 2ull * pc)[local];
+    // MT_LOG_TERM, MT_RT0, MT_RT1: cold words at 14, 18, 22
+    return reinterpret_cast<uint32_t*>(ck(k) + (14ull + 4ull * (f - MT_LOG_TERM)) * pc)[local];
   }
   __host__ __device__ inline uint64_t& u64(uint32_t k, uint32_t f) const {
-    if (f == MF_LOG_INDEX) return reinterpret_cast<uint64_t*>(hk(k) + 10ull * pc)[local];
+    if (f == MF_LOG_INDEX) return reinterpret_cast<uint64_t*>(hk(k) + 4ull * pc)[local];
     // MF_COMMIT, MF_HINT, MF_HINT_HIGH
-    return reinterpret_cast<uint64_t*>(ck(k) + (20ull + 8ull * (f - MF_COMMIT)) * pc)[local];
+    return reinterpret_cast<uint64_t*>(ck(k) + (26ull + 8ull * (f - MF_COMMIT)) * pc)[local];
+  }
+  // Tag and term of message k given the mailbox's count byte `cb` (MB_UNIFORM:
+  // rebuilt from the count byte and the term word, else the stored fields).
+  __host__ __device__ inline uint32_t tag_at(uint32_t k, uint32_t cb) const {
+    return (cb & MB_UNIFORM) ? uniform_tag(cb, k) : (uint32_t)tag(k);
+  }
+  __host__ __device__ inline uint32_t term_at(uint32_t k, uint32_t cb) const {
+    return (cb & MB_UNIFORM) ? mterm() : t32(k, MT_TERM);
+  }
+  __host__ __device__ static inline uint32_t uniform_tag(uint32_t cb, uint32_t k) {
+    if (cb & MB_RESP) return GR_REPLICATE_RESP;  // flags 0: an accept
+    const bool n1 = (cb >> (MB_N1_SHIFT + k)) & 1u;
+    return GR_REPLICATE | ((uint32_t)(MFL_COMPACT | (n1 ? (MFL_N1 | (1u << MFL_RUNS_SHIFT)) : 0u)) << 8);
   }
 };
 
@@ -315,7 +383,15 @@ struct SpaceView {
     m.hot = base + (uint64_t)c * hot_bytes;
     m.cold = base + (uint64_t)n_chunks * hot_bytes + (uint64_t)c * cold_bytes;
     m.local = gpos - c * pc;
+#if GR_TILE
+    const uint32_t t = m.local >> 6;
+    m.hot += t * tile_hot_bytes(depth);
+    m.cold += t * tile_cold_bytes(depth);
+    m.local &= 63u;
+    m.pc = 64;
+#else
     m.pc = pc;
+#endif
     return m;
   }
 };
@@ -351,7 +427,10 @@ constexpr uint8_t RT_IDENTITY = 0, RT_TABLE = 1, RT_AFFINE = 2, RT_LOOPBACK = 3;
 // Wave hints: one byte per wave of lanes (device-resident path), what the
 // wave's lanes were at the end of the previous pass, so the lean lane can issue
 // that role's loads with its first round (gr_fast.h). 0 = mixed or idle.
-constexpr uint32_t WH_ROLE = 3, WH_LEADER = 1, WH_FOLLOWER = 2, WH_SLOT_SHIFT = 2;
+// Follower hints carry the leader's slot in bits 2..; leader hints carry the
+// self slot in bits 2-4 and WH_SYNC when every lane's remote rows were in sync
+// (H_NX for every member slot and H_MS), so no NEXT row or own MATCH row is loaded.
+constexpr uint32_t WH_ROLE = 3, WH_LEADER = 1, WH_FOLLOWER = 2, WH_SLOT_SHIFT = 2, WH_SYNC = 0x20;
 
 // Kernel argument (small, passed by value, lives in SGPRs).
 // Lane i steps peer lane_peer[i] (identity when has_lane_peer == 0).

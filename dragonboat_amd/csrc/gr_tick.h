@@ -222,13 +222,14 @@ struct TickLane {
       rclo = kp.ln.u64(LR_RI_LO)[i];
       rchi = kp.ln.u64(LR_RI_HI)[i];
     }
-    uint32_t gin[S], cnt[S];
+    uint32_t gin[S], cnt[S], cbs[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       gin[j] = route_of(kp, 0, j, i);
       gout[j] = route_of(kp, 1, j, i);
       outc[j] = 0;
-      cnt[j] = gin[j] != NOPOS ? (uint32_t)(kp.in.at(gin[j]).cnt() & MB_COUNT) : 0u;
+      cbs[j] = gin[j] != NOPOS ? (uint32_t)kp.in.at(gin[j]).cnt() : 0u;
+      cnt[j] = cbs[j] & MB_COUNT;
     }
     const bool leader = state == GR_LEADER;
     GT_BAIL(!leader && state != GR_FOLLOWER);
@@ -249,8 +250,8 @@ struct TickLane {
         mh[j][k] = 0; mterm[j][k] = 0; mcom[j][k] = 0; mlo[j][k] = 0; mhi[j][k] = 0;
         if ((uint32_t)k < cnt[j]) {
           const Mailbox mb = kp.in.at(gin[j]);
-          mh[j][k] = mb.type(k);
-          mterm[j][k] = mb.t32(k, MT_TERM);
+          mh[j][k] = mb.tag_at(k, cbs[j]) & 0xFFu;  // MB_UNIFORM: implied by the count byte
+          mterm[j][k] = mb.term_at(k, cbs[j]);
           if (!leader) mcom[j][k] = mb.u64(k, MF_COMMIT);
           mlo[j][k] = mb.u64(k, MF_HINT);
           mhi[j][k] = mb.u64(k, MF_HINT_HIGH);
@@ -265,7 +266,8 @@ struct TickLane {
       const uint64_t rb = h_rb(hdr);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        match[j] = s64(Rw::MATCH + j);
+        // H_MS: the self slot's MATCH row is stale, its match is lastIndex
+        match[j] = (has_sync_bits(S) && h_ms(hdr) && (uint32_t)j == self) ? hi : s64(Rw::MATCH + j);
         rst[j] = rb_state(rb, j);
         ract[j] = rb_active(rb, j);
         rkind[j] = rb_kind(rb, j);

@@ -67,6 +67,8 @@ def load_library(path=LIB_PATH):
     lib.gr_space_chunk_bytes.argtypes = [c.c_uint32, c.c_uint32]
     lib.gr_space_hot_chunk_bytes.restype = c.c_uint64
     lib.gr_space_hot_chunk_bytes.argtypes = [c.c_uint32, c.c_uint32]
+    lib.gr_space_hot_tile_bytes.restype = c.c_uint64
+    lib.gr_space_hot_tile_bytes.argtypes = [c.c_uint32]
     lib.gr_space_cold_used.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p,
                                        c.POINTER(c.c_uint32)]
     lib.gr_bind_routes.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32]
@@ -284,6 +286,10 @@ class Engine:
 
     def hot_chunk_bytes(self, positions, depth=MAILBOX_DEPTH):
         return int(self.lib.gr_space_hot_chunk_bytes(positions, depth))
+
+    def hot_tile_bytes(self, depth=MAILBOX_DEPTH):
+        """Bytes per 64-position tile of a hot chunk (its first 64 are the count bytes)."""
+        return int(self.lib.gr_space_hot_tile_bytes(depth))
 
     def cold_used(self, space_ptr, n_chunks, positions, depth=MAILBOX_DEPTH, stream=0):
         """True when some mailbox of the device space needs its cold fields (waits for `stream`)."""

@@ -31,6 +31,14 @@ from . import populations as P
 NOPOS = 0xFFFFFFFF
 
 
+def count_bytes(hot, n_chunks, hot_chunk, hot_tile, positions):
+    """The mailbox count bytes of a hot region, [n_chunks, tiles, 64] (gr_layout.h:
+    a chunk's positions are tiled by 64, each tile starting with its 64 count bytes).
+    Works on a torch tensor or a numpy array."""
+    tiles = pad_positions(positions) // 64
+    return hot.reshape(n_chunks, hot_chunk)[:, :tiles * hot_tile].reshape(n_chunks, tiles, hot_tile)[:, :, :64]
+
+
 def pad_positions(positions):
     """gr_layout.h space_pad_positions: chunks hold a multiple of 64 mailboxes."""
     return (positions + 63) & ~63
@@ -139,6 +147,7 @@ class Exchange:
         hb = eng.hot_chunk_bytes(self.positions, self.depth)
         assert nbytes == self.n_chunks * cb and 0 < hb < cb
         self.hot_region = self.n_chunks * hb  # hot chunks first, then the cold chunks
+        self.hot_tile = eng.hot_tile_bytes(self.depth)  # positions tiled by 64, counts first in a tile
         self.cold_exchanges = 0
         if self.placement == "spread":  # all_to_all split sizes, bytes per peer rank
             self.hot_splits = ([hb if d in self.dests else 0 for d in range(self.world)],
@@ -234,11 +243,10 @@ class Pipeline:
 
     def _cold_flag(self, b):
         """Device-side: does some mailbox of bank b's out space hold a message with
-        cold fields? (count bytes: nonzero count without MB_ALLCOMPACT.)"""
+        cold fields? (count bytes: nonzero count without MB_UNIFORM.)"""
         ex, out = self.ex[b], self.spaces[b][1]
-        hb = ex.hot_region // ex.n_chunks
-        pc = pad_positions(ex.positions)
-        cnt = out[:ex.hot_region].view(ex.n_chunks, hb)[:, :pc]
+        cnt = count_bytes(out[:ex.hot_region], ex.n_chunks, ex.hot_region // ex.n_chunks, ex.hot_tile,
+                          ex.positions)
         cold = ((cnt & 7) != 0) & ((cnt & 8) == 0)
         self.flag_host[b:b + 1].copy_(cold.any().view(1).to(self.flag_host.dtype), non_blocking=True)
         self.events[b].record()

@@ -439,6 +439,11 @@ int gr_timing_end(gr_engine* e, gr_timing* out);
 uint64_t gr_space_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth);
 uint64_t gr_space_chunk_bytes(uint32_t positions, uint32_t depth);
 uint64_t gr_space_hot_chunk_bytes(uint32_t positions, uint32_t depth);
+/* A chunk's positions are tiled by 64: tile t of its hot region starts at
+ * t * gr_space_hot_tile_bytes(depth), and the tile's first 64 bytes are the
+ * count bytes of positions 64t..64t+63 (bit 3 set: the mailbox needs no cold
+ * fields). 0 when depth is not in 1..GR_C. */
+uint64_t gr_space_hot_tile_bytes(uint32_t depth);
 /* *out = 1 when some mailbox of the (device) space holds a message with cold
  * fields, i.e. the cold region must travel with the hot one; runs on `stream`
  * and waits for it. */

@@ -60,11 +60,14 @@ def fuzz(backend, G=200, passes=10, seed=7):
         m["n_entries"] = ne
         m["n_runs"] = (ne > 0).astype(np.uint8)
         m["run_term"][:, 0] = np.where(ne > 0, np.where(m["type"] == abi.PROPOSE, 0, t), 0)
-        two = (ne == 2) & (rng.random(n) < 0.3) & (m["type"] == abi.REPLICATE)
+        # two runs (t-1, t): a leader never sends an entry above its own term, so the
+        # message stays one a real leader could send (the checked build's
+        # BAD_LAST_TERM_ABOVE_TERM counts what the device does to valid input)
+        two = (ne == 2) & (rng.random(n) < 0.3) & (m["type"] == abi.REPLICATE) & (t >= 1)
         m["n_runs"] = np.where(two, 2, m["n_runs"])
         m["run2_offset"] = np.where(two, 1, 0)
-        m["run_term"][:, 1] = np.where(two, t + 1, 0)
-        m["run_term"][:, 0] = np.where(two, t, m["run_term"][:, 0])
+        m["run_term"][:, 1] = np.where(two, t, 0)
+        m["run_term"][:, 0] = np.where(two, t - 1, m["run_term"][:, 0])
         return m
     return SIM.simulate(backend, peers, topo, passes, BS._locals(M, G, seed + 1, tick=0.4, ri=0.2,
                                                                  prop_everywhere=0.1),

@@ -119,6 +119,7 @@ extern "C" int hl_step(uint32_t slots, uint64_t max_entry_size, gr_peer* peers, 
     gr_peer g;
     memset(&g, 0, sizeof(g));
     for (uint32_t row = 0; row < rows_u64(S); ++row) set_u64_row(g, row, S, st.u64(row)[p]);
+    resolve_sync(g, S, st.u64(SR_HDR)[p]);
     for (uint32_t row = 0; row < rows_u8(S); ++row) set_u8_row(g, row, S, st.u8(row)[p]);
     for (uint32_t j = S; j < GR_SMAX; ++j) g.remotes[j].kind = GR_SLOT_EMPTY;
     peers[p] = g;

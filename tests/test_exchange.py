@@ -203,6 +203,9 @@ class _MockEngine:
     def hot_chunk_bytes(self, positions, depth):
         return int(self.lib.gr_space_hot_chunk_bytes(positions, depth))
 
+    def hot_tile_bytes(self, depth):
+        return int(self.lib.gr_space_hot_tile_bytes(depth))
+
     def step_device(self, *a, **k):
         pass
 
@@ -284,6 +287,9 @@ class _HostlaneEngine:
     def hot_chunk_bytes(self, positions, depth):
         return int(self.lib.gr_space_hot_chunk_bytes(positions, depth))
 
+    def hot_tile_bytes(self, depth):
+        return int(self.lib.gr_space_hot_tile_bytes(depth))
+
     def step_device(self, in_ptr, out_ptr, in_chunks, in_positions, out_chunks, out_positions, n_peers, stream,
                     depth=3):
         import ctypes
@@ -317,8 +323,7 @@ class _HostlaneEngine:
         import ctypes
         hb = self.hot_chunk_bytes(positions, depth)
         buf = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8)), (n_chunks * hb,))
-        pc = X.pad_positions(positions)
-        cnt = buf.reshape(n_chunks, hb)[:, :pc]
+        cnt = X.count_bytes(buf, n_chunks, hb, self.hot_tile_bytes(depth), positions)
         return bool(np.any(((cnt & 7) != 0) & ((cnt & 8) == 0)))
 
 
