@@ -30,13 +30,20 @@ namespace gr {
 // before `ok` is checked.
 #define GF_BAIL(c) (ok = ok && !(c))
 
-template <int S>
+// Lane roles a lean-lane instance is built for (gr_kernels.h launches one
+// kernel per role over the waves whose hint names it): FL_ANY steps leaders and
+// followers; FL_LEADER and FL_FOLLOWER drop the other role's code (and its
+// registers) and hand such a lane to the general lane.
+constexpr int FL_ANY = 0, FL_LEADER = 1, FL_FOLLOWER = 2;
+
+template <int S, int R = FL_ANY>
 struct FastLane {
   using Rw = Rows<S>;
   static constexpr int MK = 2;  // messages per mailbox handled here
   // Leaders with input run here for up to 3 slots; wider groups' leaders take
   // the general lane (keeps this kernel's code and registers small for S = 5)
-  static constexpr bool kLeaderPath = S <= 3;
+  static constexpr bool kLeaderPath = S <= 3 && R != FL_FOLLOWER;
+  static constexpr bool kFollowerPath = R != FL_LEADER;
   static constexpr bool kSync = has_sync_bits(S);  // header sync bits (gr_layout.h)
 
   const StepParams& kp;
@@ -301,12 +308,9 @@ struct FastLane {
     rtn0 = ntld(s64(SR_RUN_TERM + GR_K - 1));
     const uint32_t lw = kp.has_locals ? ntld(kp.ln.u32(LR_LWORD)[i]) : 0u;  // packed locals (gr_layout.h)
     uint32_t gin[S];
+    routes_of<S>(kp, i, gin, gout);
 #pragma unroll
-    for (int j = 0; j < S; ++j) {
-      gin[j] = route_of(kp, 0, j, i);
-      gout[j] = route_of(kp, 1, j, i);
-      outc[j] = 0;
-    }
+    for (int j = 0; j < S; ++j) outc[j] = 0;
     // Mailboxes: the lean lane reads uniform ones only (MB_UNIFORM: every tag and
     // term implied by the count byte and the term word); any other hands over
     uint32_t cnt[S], cbs[S];
@@ -405,7 +409,7 @@ struct FastLane {
     }
     uint32_t L = 0, nsrc = 0, c = 0, gl = 0, go = NOPOS, cbL = 0;
     uint64_t rid = 0;
-    if (!(kLeaderPath && leader)) {
+    if (kFollowerPath && !(kLeaderPath && leader)) {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         if (cnt[j]) {
@@ -457,6 +461,7 @@ struct FastLane {
     GF_BAIL(!leader && state != GR_FOLLOWER);
     GF_BAIL(np && !leader);
     GF_BAIL(!kLeaderPath && leader && any_input);
+    GF_BAIL(!kFollowerPath && !leader && any_input);
     GF_BAIL(any_input && !gelo);  // the window test needs firstIndex-1
     // a non-leader whose remote rows are stale (sync bits) and whose lastIndex
     // may move: the general lane writes the rows out first (Lane::store)
@@ -481,7 +486,7 @@ struct FastLane {
         }
       }
       if (np) propose(np);
-    } else {
+    } else if (kFollowerPath) {
       // uniform compact Replicates (LogTerm = Term, at most one entry at Term,
       // narrow Commit) from one remote at the current term
       GF_BAIL(nsrc > 1 || c > (uint32_t)MK || nonu || (c && ((cbL & MB_RESP) || (uint64_t)fmt != term)));
@@ -639,10 +644,10 @@ struct FastLane {
 
 // Kernel-side entry: the lean lane for lane i; false = hand the lane to the general kernel.
 // *state = the role the lane entered the pass with; *hint_out = its role hint (WH_*).
-template <int S>
+template <int S, int R = FL_ANY>
 GF_HD bool fast_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, uint32_t* state = nullptr,
                      uint32_t hint = 0, uint32_t* hint_out = nullptr) {
-  FastLane<S> L(kp, i, p);
+  FastLane<S, R> L(kp, i, p);
   const bool done = L.step(ls, hint);
   if (state) *state = L.state;
   if (hint_out) *hint_out = L.role_hint();

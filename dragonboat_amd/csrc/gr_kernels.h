@@ -87,30 +87,47 @@ __device__ inline void bail_append(bool mine, uint32_t list, uint32_t* bail_list
   if (mine) bail_list[(uint64_t)list * list_cap + base + (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
 }
 
-template <int S>
 #ifndef GR_FAST_MIN_WAVES
 #define GR_FAST_MIN_WAVES 1  // waves per SIMD the register allocation must allow (A/B builds)
 #endif
+// Three instances per slot count: R = FL_LEADER and FL_FOLLOWER step the waves
+// whose hint (as the pass started) names that role, with the other role's code
+// and registers compiled out; R = FL_ANY steps the rest (no hint, or none on
+// the host path). A block none of whose waves is this instance's returns at
+// once; a wave that is not joins the block's barriers only.
+template <int S, int R>
 __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
                                                                              uint32_t* counters, uint32_t list_cap) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   // the wave's hint: one byte, the same address for every lane (a scalar load)
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
   const uint32_t hint = kp.hints ? (uint32_t)kp.hints[wave] : 0u;
+  bool mine = true;
+  if (kp.hints) {
+    const uint32_t w0 = blockIdx.x * (kBlock / 64), nw = (kp.n_lanes + 63) / 64;
+    bool any = false;
+#pragma unroll
+    for (uint32_t w = 0; w < kBlock / 64; ++w)
+      any = any || (w0 + w < nw && wave_kernel(kp.hints[w0 + w], S) == R);
+    if (!any) return;  // block-uniform
+    mine = wave_kernel(hint, S) == R;
+  } else if (R != FL_ANY) {
+    return;
+  }
   LaneStats ls;
   bool bail = false;
   uint32_t role = 0, myhint = 0;
-  const bool active = i < kp.n_lanes;
+  const bool active = mine && i < kp.n_lanes;
   if (active) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-    bail = !fast_step<S>(kp, i, p, &ls, &role, hint, &myhint);  // leaves ls zero when it bails
+    bail = !fast_step<S, R>(kp, i, p, &ls, &role, hint, &myhint);  // leaves ls zero when it bails
     if (!bail) GR_CHECK_STATE(kp.st, p);
   }
-  if (kp.hints) {  // next pass's hint: this wave's role if every active lane shares it
+  if (kp.hints && mine) {  // next pass's hint: this wave's role if every active lane shares it
     const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane(myhint);
     const uint64_t same = __ballot(active && myhint == first), act = __ballot(active);
     const uint32_t nh = same == act ? first : 0u;
-    if ((threadIdx.x & 63) == 0 && nh != hint) kp.hints[wave] = (uint8_t)nh;
+    if ((threadIdx.x & 63) == 0) kp.hints_out[wave] = (uint8_t)nh;
   }
   // followers into lists 0..7, leaders into 8..15, lanes with ticks or a
   // ReadIndex into 16..23 (the tick kernel's): the later kernels walk their lists
@@ -246,7 +263,17 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   uint32_t* nxt = counters + ((parity + 1) & 1) * kBailLists * kCounterStride;
   hipError_t err;
   if (t && (err = hipEventRecord(t->ev[0], s)) != hipSuccess) return err;
-  hipLaunchKernelGGL(gr_fast_kernel<S>, dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
+  if (kp.hints) {  // the role-specialised instances first, then the rest (FL_ANY)
+    hipLaunchKernelGGL((gr_fast_kernel<S, FL_FOLLOWER>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
+                       list_cap);
+    if ((err = hipGetLastError()) != hipSuccess) return err;
+    if (S <= 3) {
+      hipLaunchKernelGGL((gr_fast_kernel<S, FL_LEADER>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
+                         list_cap);
+      if ((err = hipGetLastError()) != hipSuccess) return err;
+    }
+  }
+  hipLaunchKernelGGL((gr_fast_kernel<S, FL_ANY>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
   if ((err = hipGetLastError()) != hipSuccess) return err;
   if (t && (err = hipEventRecord(t->ev[1], s)) != hipSuccess) return err;
   if (tick_lanes) {  // some lane may carry ticks or a ReadIndex (LW_OTHER)

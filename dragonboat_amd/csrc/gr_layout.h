@@ -378,7 +378,7 @@ struct SpaceView {
   uint64_t cold_bytes;  // per chunk; the cold region follows the hot region
   uint32_t depth;  // messages per mailbox (1..GR_C); emitting more escalates CAPACITY
   __host__ __device__ inline Mailbox at(uint32_t gpos) const {
-    uint32_t c = gpos / pc;
+    const uint32_t c = n_chunks == 1 ? 0u : gpos / pc;  // one chunk (loopback spaces): no division
     Mailbox m;
     m.hot = base + (uint64_t)c * hot_bytes;
     m.cold = base + (uint64_t)n_chunks * hot_bytes + (uint64_t)c * cold_bytes;
@@ -431,6 +431,12 @@ constexpr uint8_t RT_IDENTITY = 0, RT_TABLE = 1, RT_AFFINE = 2, RT_LOOPBACK = 3;
 // self slot in bits 2-4 and WH_SYNC when every lane's remote rows were in sync
 // (H_NX for every member slot and H_MS), so no NEXT row or own MATCH row is loaded.
 constexpr uint32_t WH_ROLE = 3, WH_LEADER = 1, WH_FOLLOWER = 2, WH_SLOT_SHIFT = 2, WH_SYNC = 0x20;
+// The lean kernel (FL_* of gr_fast.h) that steps a wave with hint h.
+__host__ __device__ inline int wave_kernel(uint32_t h, int S) {
+  if ((h & WH_ROLE) == WH_LEADER && S <= 3) return 1;  // FL_LEADER
+  if ((h & WH_ROLE) == WH_FOLLOWER) return 2;          // FL_FOLLOWER
+  return 0;                                            // FL_ANY
+}
 
 // Kernel argument (small, passed by value, lives in SGPRs).
 // Lane i steps peer lane_peer[i] (identity when has_lane_peer == 0).
@@ -439,7 +445,8 @@ struct StepParams {
   LaneBase ln;
   SpaceView in, out;
   uint64_t* stats;     // [gridDim.x][NSTAT] or nullptr
-  uint8_t* hints;      // [n_lanes / 64] wave hints (WH_*) or nullptr
+  uint8_t* hints;      // [n_lanes / 64] wave hints (WH_*) as the pass started, or nullptr
+  uint8_t* hints_out;  // ... the next pass's (written by the kernel that steps the wave)
   const uint32_t* route_base;  // RT_AFFINE: [2][GR_SMAX][GR_SMAX]
   uint64_t max_entry_size;
   uint32_t n_lanes;
@@ -451,6 +458,34 @@ struct StepParams {
   uint8_t pad;
 };
 
+// Every route of lane i at once (in[j], out[j] for j < S): the lane's replica
+// block and group are divided out once, not once per slot and direction.
+template <int S>
+__host__ __device__ inline void routes_of(const StepParams& kp, uint32_t i, uint32_t* in, uint32_t* out) {
+  if (kp.route_mode == RT_LOOPBACK || kp.route_mode == RT_AFFINE) {
+    const uint32_t r = i / kp.route_g, g = i - r * kp.route_g;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      if (kp.route_mode == RT_LOOPBACK) {
+        const bool none = (uint32_t)j == r || (uint32_t)j >= kp.route_r;
+        const uint32_t n = kp.route_r * kp.route_g;
+        in[j] = none ? NOPOS : j * n + i;
+        out[j] = none ? NOPOS : r * n + j * kp.route_g + g;
+      } else {
+        const uint32_t bi = kp.route_base[(0 * GR_SMAX + r) * GR_SMAX + j];
+        const uint32_t bo = kp.route_base[(1 * GR_SMAX + r) * GR_SMAX + j];
+        in[j] = bi == NOPOS ? NOPOS : bi + g;
+        out[j] = bo == NOPOS ? NOPOS : bo + g;
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    in[j] = kp.route_mode == RT_TABLE ? kp.ln.in_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
+    out[j] = kp.route_mode == RT_TABLE ? kp.ln.out_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
+  }
+}
 __host__ __device__ inline uint32_t route_of(const StepParams& kp, uint32_t dir, uint32_t j, uint32_t i) {
   if (kp.route_mode == RT_TABLE)
     return (dir ? kp.ln.out_pos() : kp.ln.in_pos())[(uint64_t)j * kp.ln.lcap + i];

@@ -31,10 +31,32 @@ void run_lanes(const StepParams& kp) {
     LaneStats ls;
     // an arbitrary wave hint (gr_fast.h): it must never change a result, so
     // the host build draws one per wave to exercise every speculative path
+    // Three waves in four get the hint the device would give (the wave's first
+    // lane's role as loaded), the rest a random one, WH_SYNC included: a wrong
+    // hint may only cost a hand-over to the general lane (role-specialised
+    // kernels, gr_kernels.h), never a different result.
     const uint32_t w = (i >> 6) * 2654435761u + g_hint_salt;
-    const uint32_t pick = (w >> 13) % (2u + S);
-    const uint32_t hint = pick == 0 ? 0u : pick == 1 ? WH_LEADER : (WH_FOLLOWER | ((pick - 2) << WH_SLOT_SHIFT));
-    if (!fast_step<S>(kp, i, p, &ls, nullptr, hint)) bailed.push_back(i);
+    uint32_t hint;
+    if ((w >> 7) & 3u) {
+      const uint32_t i0 = i & ~63u;
+      const uint64_t h = kp.st.u64(SR_HDR)[kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i0] : i0];
+      const uint32_t ls0 = (h_flags(h) & F_LSLOT) >> F_LSLOT_SHIFT;
+      hint = h_state(h) == GR_LEADER ? (WH_LEADER | ((h_self(h) & 7u) << WH_SLOT_SHIFT) |
+                                        ((h & H_SYNC_MASK) ? WH_SYNC : 0u))
+             : (h_state(h) == GR_FOLLOWER && ls0) ? (WH_FOLLOWER | ((ls0 - 1) << WH_SLOT_SHIFT))
+                                                  : 0u;
+    } else {
+      const uint32_t pick = (w >> 13) % (2u + S);
+      hint = pick == 0 ? 0u
+             : pick == 1 ? (WH_LEADER | (((w >> 20) % S) << WH_SLOT_SHIFT) | (((w >> 24) & 1u) ? WH_SYNC : 0u))
+                         : (WH_FOLLOWER | ((pick - 2) << WH_SLOT_SHIFT));
+    }
+    // the kernel variant the device would run for this hint (gr_kernels.h)
+    const int fk = wave_kernel(hint, S);
+    const bool done = fk == FL_LEADER     ? fast_step<S, FL_LEADER>(kp, i, p, &ls, nullptr, hint)
+                      : fk == FL_FOLLOWER ? fast_step<S, FL_FOLLOWER>(kp, i, p, &ls, nullptr, hint)
+                                          : fast_step<S>(kp, i, p, &ls, nullptr, hint);
+    if (!done) bailed.push_back(i);
     else GR_CHECK_STATE(kp.st, p);
   }
   for (uint32_t i : bailed) {
