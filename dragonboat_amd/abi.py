@@ -9,7 +9,7 @@ import numpy as np
 
 GR_K = 4
 GR_Q = 4
-GR_C = 4
+GR_C = 6
 GR_SMAX = 8
 GR_SLOT_NONE = 0xFF
 

@@ -1128,6 +1128,9 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
   const size_t hs = e->cap / 64 + 1, hf = e->hint_flip++ & 1;
   kp.hints = e->hints + hf * hs;
   kp.hints_out = e->hints + (1 - hf) * hs;
+  // the follower instance of its own pays off only when the pass is large (a
+  // 10k x 3 pass is launch-bound: one instance there, 24 vs 41 us per pass)
+  kp.split = n_peers >= kSplitMinLanes ? 1 : 0;
   HIPCHK(launch_slots(e->S, kp, e->bail, e->counters, e->cap, (uint32_t)e->launches++, (hipStream_t)stream,
                       next_timing(e), kp.has_locals && e->locals_other));
   e->passes++;

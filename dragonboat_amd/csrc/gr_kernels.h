@@ -18,9 +18,10 @@
 namespace gr {
 
 constexpr int kBlock = 256;
+constexpr uint32_t kSplitMinLanes = 1u << 18;  // StepParams::split: role instances from this many lanes up
 
-// Per-workgroup partial counters (no atomics on global memory): row b of the
-// stats block belongs to workgroup b of whichever kernel runs.
+// Per-workgroup partial counters: row b of the stats block belongs to workgroup
+// b of whichever kernel runs (uncontended adds, no return value waited for).
 __device__ inline uint32_t wave_sum(uint32_t v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -48,17 +49,16 @@ __device__ inline void block_stats(const StepParams& kp, const LaneStats& ls) {
     atomicAdd(&red[8], f8);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t* row = kp.stats + (uint64_t)blockIdx.x * NSTAT;
-    row[ST_LEADER_COMMITS] += red[0];
-    row[ST_FOLLOWER_COMMITS] += red[1];
-    row[ST_ESCALATIONS] += red[2];
-    row[ST_MSGS_IN] += red[3];
-    row[ST_MSGS_OUT] += red[4];
-    row[ST_LEADER_MSGS_IN] += red[5];
-    row[ST_LEADER_MSGS_OUT] += red[6];
-    row[ST_REPLICATE_ENTRIES] += red[7];
-    row[ST_BAILED] += red[8];
+  // fire-and-forget adds to the workgroup's own row (never contended): a
+  // read-modify-write would add a dependent memory round to every block's end
+  if (threadIdx.x < N) {
+    constexpr uint32_t field[N] = {ST_LEADER_COMMITS, ST_FOLLOWER_COMMITS, ST_ESCALATIONS, ST_MSGS_IN, ST_MSGS_OUT,
+                                   ST_LEADER_MSGS_IN, ST_LEADER_MSGS_OUT, ST_REPLICATE_ENTRIES, ST_BAILED};
+    uint32_t f = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < N; ++k) f = threadIdx.x == k ? field[k] : f;
+    const uint32_t v = red[threadIdx.x];
+    if (v) atomicAdd((unsigned long long*)(kp.stats + (uint64_t)blockIdx.x * NSTAT + f), (unsigned long long)v);
   }
 }
 
@@ -90,11 +90,15 @@ __device__ inline void bail_append(bool mine, uint32_t list, uint32_t* bail_list
 #ifndef GR_FAST_MIN_WAVES
 #define GR_FAST_MIN_WAVES 1  // waves per SIMD the register allocation must allow (A/B builds)
 #endif
-// Three instances per slot count: R = FL_LEADER and FL_FOLLOWER step the waves
-// whose hint (as the pass started) names that role, with the other role's code
-// and registers compiled out; R = FL_ANY steps the rest (no hint, or none on
-// the host path). A block none of whose waves is this instance's returns at
-// once; a wave that is not joins the block's barriers only.
+// Two instances per slot count, one after the other: R = FL_FOLLOWER steps the
+// waves whose hint (as the pass started) names a follower role, with the leader
+// code and registers compiled out (66 VGPRs at S = 3, 7 waves per SIMD); R =
+// FL_ANY steps the rest, leader-hinted waves with the follower code compiled
+// out (FastLane<S, FL_LEADER>) and unhinted ones with both (110 VGPRs, 4 waves).
+// A block none of whose waves is this instance's returns at once; a wave that
+// is not joins the block's barriers only. Running the two instances concurrently
+// on two streams measured slower (0.133 vs 0.124 ms per 1M x 3 pass; the second
+// stream's fork and join also cost config 2 ~19 us per pass).
 template <int S, int R>
 __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
                                                                              uint32_t* counters, uint32_t list_cap) {
@@ -103,16 +107,16 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
   const uint32_t hint = kp.hints ? (uint32_t)kp.hints[wave] : 0u;
   bool mine = true;
-  if (kp.hints) {
+  if (kp.hints && kp.split) {
     const uint32_t w0 = blockIdx.x * (kBlock / 64), nw = (kp.n_lanes + 63) / 64;
     bool any = false;
 #pragma unroll
     for (uint32_t w = 0; w < kBlock / 64; ++w)
-      any = any || (w0 + w < nw && wave_kernel(kp.hints[w0 + w], S) == R);
+      any = any || (w0 + w < nw && (wave_kernel(kp.hints[w0 + w], S) == FL_FOLLOWER) == (R == FL_FOLLOWER));
     if (!any) return;  // block-uniform
-    mine = wave_kernel(hint, S) == R;
+    mine = (wave_kernel(hint, S) == FL_FOLLOWER) == (R == FL_FOLLOWER);
   } else if (R != FL_ANY) {
-    return;
+    return;  // one instance steps every wave
   }
   LaneStats ls;
   bool bail = false;
@@ -120,7 +124,11 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
   const bool active = mine && i < kp.n_lanes;
   if (active) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-    bail = !fast_step<S, R>(kp, i, p, &ls, &role, hint, &myhint);  // leaves ls zero when it bails
+    // leaves ls zero when it bails
+    if (R == FL_FOLLOWER || wave_kernel(hint, S) == FL_FOLLOWER)
+      bail = !fast_step<S, FL_FOLLOWER>(kp, i, p, &ls, &role, hint, &myhint);
+    else if (wave_kernel(hint, S) == FL_LEADER) bail = !fast_step<S, FL_LEADER>(kp, i, p, &ls, &role, hint, &myhint);
+    else bail = !fast_step<S, FL_ANY>(kp, i, p, &ls, &role, hint, &myhint);
     if (!bail) GR_CHECK_STATE(kp.st, p);
   }
   if (kp.hints && mine) {  // next pass's hint: this wave's role if every active lane shares it
@@ -251,6 +259,7 @@ struct PassTiming {
   hipEvent_t ev[3];
 };
 
+
 // The tick kernel's grid: its lanes are at most the active share of a pass.
 constexpr uint32_t kTickBlocks = 1024;
 
@@ -263,15 +272,10 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   uint32_t* nxt = counters + ((parity + 1) & 1) * kBailLists * kCounterStride;
   hipError_t err;
   if (t && (err = hipEventRecord(t->ev[0], s)) != hipSuccess) return err;
-  if (kp.hints) {  // the role-specialised instances first, then the rest (FL_ANY)
+  if (kp.hints && kp.split) {
     hipLaunchKernelGGL((gr_fast_kernel<S, FL_FOLLOWER>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
                        list_cap);
     if ((err = hipGetLastError()) != hipSuccess) return err;
-    if (S <= 3) {
-      hipLaunchKernelGGL((gr_fast_kernel<S, FL_LEADER>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
-                         list_cap);
-      if ((err = hipGetLastError()) != hipSuccess) return err;
-    }
   }
   hipLaunchKernelGGL((gr_fast_kernel<S, FL_ANY>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
   if ((err = hipGetLastError()) != hipSuccess) return err;

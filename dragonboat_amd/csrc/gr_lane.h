@@ -1524,6 +1524,9 @@ struct Lane {
 #pragma unroll 1
     for (int attempt = 0; attempt < 2; ++attempt) {  // one call site keeps run() inlined
       begin();
+      // the groups nearly every handed-over lane reads, in one round of loads
+      // instead of one dependent round per group as the handlers reach them
+      need(G_CORE | G_WIN | G_REM | G_ETICK | G_LID);
       const int e = run(limit, &at);
       if (!e) break;
       esc = e;  // second attempt re-runs the prefix and cannot escalate

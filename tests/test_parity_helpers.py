@@ -42,8 +42,8 @@ def test_escalation_predicate(built):
     """The oracle's escalation predicate (batch.cpp) justifies an escalation only
     when the item needs the host: a steady leader's ReplicateResp does not, a
     follower whose election timeout fires with committed <= applied does
-    (ELECTION), a second reset in one pass does (RANDOM), a sixth message into
-    a depth-4 mailbox does (CAPACITY)."""
+    (ELECTION), a second reset in one pass does (RANDOM), a message past GR_C
+    in one mailbox does (CAPACITY)."""
     import numpy as np
     from dragonboat_amd import abi, populations as P
     from oracle.pyoracle import OraclePopulation
@@ -76,10 +76,10 @@ def test_escalation_predicate(built):
     o = pop.step(None, loc, lim, dev_before=p2)
     assert (int(o["esc_mask"][f]) >> abi.ESC_NAMES.index("election")) & 1
     assert not (int(o["esc_mask"][f]) >> abi.ESC_NAMES.index("capacity")) & 1
-    # six Heartbeats into one depth-4 mailbox: the fifth is a CAPACITY item
-    hb = np.zeros(6, abi.MESSAGE)
+    # GR_C + 2 Heartbeats into one depth-GR_C mailbox: item GR_C is a CAPACITY item
+    hb = np.zeros(abi.GR_C + 2, abi.MESSAGE)
     hb["peer"], hb["type"], hb["slot"], hb["term"] = f, abi.HEARTBEAT, 0, p2["term"][f]
     pop = OraclePopulation(peers, R)
-    lim[f] = 4
+    lim[f] = abi.GR_C
     o = pop.step(hb, None, lim, dev_before=peers)
     assert (int(o["esc_mask"][f]) >> abi.ESC_NAMES.index("capacity")) & 1
