@@ -58,12 +58,20 @@ struct FastLane {
   bool ok = true;             // still on the steady-state path
   // leader remotes
   uint64_t match[S], next[S];
-  uint32_t rst[S], ract[S], rkind[S];
+  // per remote slot state (2 bits), active (1), kind (2): the header's rb
+  // layout (gr_layout.h), one register instead of 3S
+  uint64_t rbw = 0;
+  GF_HD uint32_t rst(int j) const { return rb_state(rbw, (uint32_t)j); }
+  GF_HD uint32_t ract(int j) const { return rb_active(rbw, (uint32_t)j); }
+  GF_HD uint32_t rkind(int j) const { return rb_kind(rbw, (uint32_t)j); }
+  GF_HD void set_rst(int j, uint32_t v) { rbw = rb_with(rbw, (uint32_t)j, 0, 2, v); }
+  GF_HD void set_ract(int j, uint32_t v) { rbw = rb_with(rbw, (uint32_t)j, 2, 1, v); }
   uint32_t mdirty = 0;  // slots whose match/next changed
   uint32_t sdirty = 0;  // slots whose state/active byte changed
   uint32_t snapz = 0;
   uint32_t have_m = 0, have_n = 0;  // slots whose MATCH / NEXT row was loaded with the hint
   bool synced = false;              // after the pass: every member slot's next and own match in sync
+  bool skipped = false;             // the lane is the other role instance's (step returned false)
   // emission
   uint32_t gout[S];
   uint32_t outc[S];
@@ -166,7 +174,7 @@ struct FastLane {
     int nv = 0;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      const bool v = rkind[j] == GR_SLOT_VOTER;
+      const bool v = rkind(j) == GR_SLOT_VOTER;
       m[j] = v ? match[j] : ~0ull;
       nv += v;
     }
@@ -193,7 +201,7 @@ struct FastLane {
   }
   // sendReplicateMessage / makeReplicateMessage (raft.go:474-532), one entry at most.
   GF_HD void send_replicate(int j) {
-    if (rst[j] == GR_WAIT || rst[j] == GR_SNAPSHOT_ST) return;  // isPaused, remote.go:158-171
+    if (rst(j) == GR_WAIT || rst(j) == GR_SNAPSHOT_ST) return;  // isPaused, remote.go:158-171
     const uint64_t nx = next[j];
     const uint64_t lt = term_of(nx - 1);
     uint32_t n = 0;
@@ -202,13 +210,13 @@ struct FastLane {
       // (InstallSnapshot path): with H_GE_LO, nx > rsn implies nx > firstIndex-1
       GF_BAIL(nruns == 0 || nx <= rsn);
       GF_BAIL(hi - nx + 1 > 1);         // several entries: MaxEntrySize check
-      GF_BAIL(rst[j] != GR_REPLICATE_ST && rst[j] != GR_RETRY);
+      GF_BAIL(rst(j) != GR_REPLICATE_ST && rst(j) != GR_RETRY);
       n = 1;
-      if (rst[j] == GR_REPLICATE_ST) {  // remote.progress, remote.go:120-128
+      if (rst(j) == GR_REPLICATE_ST) {  // remote.progress, remote.go:120-128
         next[j] = hi + 1;
         mdirty |= 1u << j;
       } else {
-        rst[j] = GR_WAIT;
+        set_rst(j, GR_WAIT);
         sdirty |= 1u << j;
       }
     }
@@ -217,10 +225,10 @@ struct FastLane {
   GF_HD void broadcast() {  // raft.go:534-546: voters (not self), then observers
 #pragma unroll
     for (int j = 0; j < S; ++j)
-      if (rkind[j] == GR_SLOT_VOTER && (uint32_t)j != self) send_replicate(j);
+      if (rkind(j) == GR_SLOT_VOTER && (uint32_t)j != self) send_replicate(j);
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      if (rkind[j] == GR_SLOT_OBSERVER) {
+      if (rkind(j) == GR_SLOT_OBSERVER) {
         GF_BAIL((uint32_t)j == self);
         send_replicate(j);
       }
@@ -233,8 +241,8 @@ struct FastLane {
       mdirty |= 1u << j;
     }
     if (match[j] < index) {
-      if (rst[j] == GR_WAIT) {
-        rst[j] = GR_RETRY;
+      if (rst(j) == GR_WAIT) {
+        set_rst(j, GR_RETRY);
         sdirty |= 1u << j;
       }
       match[j] = index;
@@ -245,17 +253,17 @@ struct FastLane {
   }
   // handleLeaderReplicateResp, accept path (raft.go:1205-1221); no leader transfer.
   GF_HD void replicate_resp(int j, uint64_t index) {
-    if (!ract[j]) {
-      ract[j] = 1;
+    if (!ract(j)) {
+      set_ract(j, 1);
       sdirty |= 1u << j;
     }
-    const bool paused = rst[j] == GR_WAIT || rst[j] == GR_SNAPSHOT_ST;
+    const bool paused = rst(j) == GR_WAIT || rst(j) == GR_SNAPSHOT_ST;
     if (!try_update(j, index)) return;
-    GF_BAIL(rst[j] == GR_SNAPSHOT_ST);
-    if (rst[j] == GR_RETRY) {  // respondedTo -> becomeReplicate (remote.go:92-96,130-138)
+    GF_BAIL(rst(j) == GR_SNAPSHOT_ST);
+    if (rst(j) == GR_RETRY) {  // respondedTo -> becomeReplicate (remote.go:92-96,130-138)
       next[j] = match[j] + 1;
       snapz |= 1u << j;
-      rst[j] = GR_REPLICATE_ST;
+      set_rst(j, GR_REPLICATE_ST);
       mdirty |= 1u << j;
       sdirty |= 1u << j;
     }
@@ -266,7 +274,7 @@ struct FastLane {
   GF_HD void propose(uint32_t np) {
     uint32_t sk = GR_SLOT_EMPTY;
 #pragma unroll
-    for (int j = 0; j < S; ++j) sk = ((uint32_t)j == self) ? rkind[j] : sk;
+    for (int j = 0; j < S; ++j) sk = ((uint32_t)j == self) ? rkind(j) : sk;
     if (sk != GR_SLOT_VOTER) {  // selfRemoved: dropped (raft.go:1126-1129)
       prop_result = GR_PROP_DROPPED;
       return;
@@ -280,7 +288,7 @@ struct FastLane {
       if ((uint32_t)j == self) try_update(j, hi);
     int nv = 0;
 #pragma unroll
-    for (int j = 0; j < S; ++j) nv += rkind[j] == GR_SLOT_VOTER;
+    for (int j = 0; j < S; ++j) nv += rkind(j) == GR_SLOT_VOTER;
     if (nv / 2 + 1 == 1) try_commit();
     broadcast();
     prop_result = GR_PROP_APPENDED;
@@ -292,7 +300,10 @@ struct FastLane {
   // The loads that role needs are then issued with the header, in one round,
   // before the lane knows its state; a lane whose role differs from the hint
   // loads what it needs afterwards, so the hint never changes a result.
-  GF_HD bool step(LaneStats* ls, uint32_t hint) {
+  // `take`: FL_ANY = step the lane whatever its role; FL_LEADER / FL_FOLLOWER =
+  // step it only in that role (a leader / not a leader), else leave it untouched
+  // with `skipped` set: the other role instance steps it (unhinted waves).
+  GF_HD bool step(LaneStats* ls, uint32_t hint, int take = FL_ANY) {
     const bool hl = kLeaderPath && (hint & WH_ROLE) == WH_LEADER;
     const bool hf = (hint & WH_ROLE) == WH_FOLLOWER;
     const uint32_t hL = hint >> WH_SLOT_SHIFT;
@@ -375,19 +386,17 @@ struct FastLane {
       rtn = rtn0;
     }
     const bool leader = state == GR_LEADER;
+    if ((take == FL_LEADER && !leader) || (take == FL_FOLLOWER && leader)) {
+      skipped = true;
+      return false;
+    }
     const uint32_t np = lw & 0xFFFFu;
     const uint32_t nq = (lw >> LW_QT_SHIFT) & LW_QT_MAX;
     uint64_t etick = 0;
     if (nq) etick = ntld(s64(SR_ETICK));
     // ---- round 2 (only where the hint did not match): leader remotes and messages
     if (kLeaderPath && leader) {
-      const uint64_t rb = h_rb(hdr);
-#pragma unroll
-      for (int j = 0; j < S; ++j) {
-        rst[j] = rb_state(rb, j);
-        ract[j] = rb_active(rb, j);
-        rkind[j] = rb_kind(rb, j);
-      }
+      rbw = h_rb(hdr) & ((1ull << (5 * S)) - 1);
       // remote rows: stale ones (sync bits) from lastIndex, the rest loaded unless the hint did
       const uint64_t sb = kSync ? hdr : 0;
 #pragma unroll
@@ -481,7 +490,7 @@ struct FastLane {
         for (int k = 0; k < MK; ++k) {
           if ((uint32_t)k < cnt[j]) {
             nmi++;
-            if (rkind[j] != GR_SLOT_EMPTY) replicate_resp(j, lidx[j][k]);
+            if (rkind(j) != GR_SLOT_EMPTY) replicate_resp(j, lidx[j][k]);
           }
         }
       }
@@ -537,14 +546,14 @@ struct FastLane {
         sbits |= (nx_now ? 1ull : 0ull) << (H_NX_SHIFT + j);
         sbits |= (ms_now ? 1ull : 0ull) << H_MS_BIT;
         own_ms = own_ms || ms_now;
-        if (rkind[j] != GR_SLOT_EMPTY && !nx_now) all_nx = false;
+        if (rkind(j) != GR_SLOT_EMPTY && !nx_now) all_nx = false;
       }
       synced = kSync && own_ms && all_nx;
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         if ((sdirty >> j) & 1u) {
-          rb = rb_with(rb, j, 0, 2, rst[j]);
-          rb = rb_with(rb, j, 2, 1, ract[j]);
+          rb = rb_with(rb, j, 0, 2, rst(j));
+          rb = rb_with(rb, j, 2, 1, ract(j));
         }
       }
       nh = (nh & ((1ull << H_REM_SHIFT) - 1)) | (rb << H_REM_SHIFT);
@@ -644,13 +653,16 @@ struct FastLane {
 
 // Kernel-side entry: the lean lane for lane i; false = hand the lane to the general kernel.
 // *state = the role the lane entered the pass with; *hint_out = its role hint (WH_*).
+// take (FastLane::step): a lane whose role is not `take` is left alone, *skipped = true.
 template <int S, int R = FL_ANY>
 GF_HD bool fast_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, uint32_t* state = nullptr,
-                     uint32_t hint = 0, uint32_t* hint_out = nullptr) {
+                     uint32_t hint = 0, uint32_t* hint_out = nullptr, int take = FL_ANY,
+                     bool* skipped = nullptr) {
   FastLane<S, R> L(kp, i, p);
-  const bool done = L.step(ls, hint);
+  const bool done = L.step(ls, hint, take);
   if (state) *state = L.state;
   if (hint_out) *hint_out = L.role_hint();
+  if (skipped) *skipped = L.skipped;
   return done;
 }
 

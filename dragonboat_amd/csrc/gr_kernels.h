@@ -90,15 +90,17 @@ __device__ inline void bail_append(bool mine, uint32_t list, uint32_t* bail_list
 #ifndef GR_FAST_MIN_WAVES
 #define GR_FAST_MIN_WAVES 1  // waves per SIMD the register allocation must allow (A/B builds)
 #endif
-// Two instances per slot count, one after the other: R = FL_FOLLOWER steps the
-// waves whose hint (as the pass started) names a follower role, with the leader
-// code and registers compiled out (66 VGPRs at S = 3, 7 waves per SIMD); R =
-// FL_ANY steps the rest, leader-hinted waves with the follower code compiled
-// out (FastLane<S, FL_LEADER>) and unhinted ones with both (110 VGPRs, 4 waves).
-// A block none of whose waves is this instance's returns at once; a wave that
-// is not joins the block's barriers only. Running the two instances concurrently
-// on two streams measured slower (0.133 vs 0.124 ms per 1M x 3 pass; the second
-// stream's fork and join also cost config 2 ~19 us per pass).
+// Role instances. A large pass (StepParams::split) runs R = FL_FOLLOWER then R =
+// FL_LEADER, each with the other role's code and registers compiled out (66 and
+// 92 VGPRs at S = 3: 7 and 5 waves per SIMD): a wave whose hint (as the pass
+// started) names a role goes to that instance, and an unhinted wave to both, each
+// stepping the lanes of its role and leaving the others untouched (FastLane
+// `take`). A small pass runs the single instance R = FL_ANY, which picks the
+// lean-lane variant per wave from its hint. A block none of whose waves is an
+// instance's returns at once; a wave that is not joins the block's barriers only.
+// Measured and dropped: the two instances concurrently on two streams (0.133 vs
+// 0.124 ms per 1M x 3 pass), and a third instance for unhinted waves (~8 us for a
+// mostly empty launch).
 template <int S, int R>
 __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
                                                                              uint32_t* counters, uint32_t list_cap) {
@@ -106,36 +108,43 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
   // the wave's hint: one byte, the same address for every lane (a scalar load)
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
   const uint32_t hint = kp.hints ? (uint32_t)kp.hints[wave] : 0u;
+  const int wk = wave_kernel(hint, S);  // FL_ANY: unhinted
   bool mine = true;
-  if (kp.hints && kp.split) {
+  if (R != FL_ANY) {  // a split pass (the launcher runs these only then)
     const uint32_t w0 = blockIdx.x * (kBlock / 64), nw = (kp.n_lanes + 63) / 64;
     bool any = false;
 #pragma unroll
-    for (uint32_t w = 0; w < kBlock / 64; ++w)
-      any = any || (w0 + w < nw && (wave_kernel(kp.hints[w0 + w], S) == FL_FOLLOWER) == (R == FL_FOLLOWER));
+    for (uint32_t w = 0; w < kBlock / 64; ++w) {
+      const int k = w0 + w < nw ? wave_kernel(kp.hints[w0 + w], S) : R == FL_LEADER ? FL_FOLLOWER : FL_LEADER;
+      any = any || k == R || k == FL_ANY;
+    }
     if (!any) return;  // block-uniform
-    mine = (wave_kernel(hint, S) == FL_FOLLOWER) == (R == FL_FOLLOWER);
-  } else if (R != FL_ANY) {
-    return;  // one instance steps every wave
+    mine = wk == R || wk == FL_ANY;
   }
   LaneStats ls;
-  bool bail = false;
+  bool bail = false, skip = false;
   uint32_t role = 0, myhint = 0;
   const bool active = mine && i < kp.n_lanes;
   if (active) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     // leaves ls zero when it bails
-    if (R == FL_FOLLOWER || wave_kernel(hint, S) == FL_FOLLOWER)
-      bail = !fast_step<S, FL_FOLLOWER>(kp, i, p, &ls, &role, hint, &myhint);
-    else if (wave_kernel(hint, S) == FL_LEADER) bail = !fast_step<S, FL_LEADER>(kp, i, p, &ls, &role, hint, &myhint);
+    if (R != FL_ANY)
+      bail = !fast_step<S, R>(kp, i, p, &ls, &role, hint, &myhint, wk == FL_ANY ? R : FL_ANY, &skip);
+    else if (wk == FL_FOLLOWER) bail = !fast_step<S, FL_FOLLOWER>(kp, i, p, &ls, &role, hint, &myhint);
+    else if (wk == FL_LEADER) bail = !fast_step<S, FL_LEADER>(kp, i, p, &ls, &role, hint, &myhint);
     else bail = !fast_step<S, FL_ANY>(kp, i, p, &ls, &role, hint, &myhint);
-    if (!bail) GR_CHECK_STATE(kp.st, p);
+    bail = bail && !skip;  // a skipped lane is the other instance's
+    if (!bail && !skip) GR_CHECK_STATE(kp.st, p);
   }
-  if (kp.hints && mine) {  // next pass's hint: this wave's role if every active lane shares it
+  if (kp.hints && mine) {
+    // next pass's hint: this wave's role if every active lane was stepped here
+    // and shares it; written by each instance that stepped a lane of the wave
+    // (both write 0 when an unhinted wave's lanes split between them)
+    const bool done = active && !skip;
     const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane(myhint);
-    const uint64_t same = __ballot(active && myhint == first), act = __ballot(active);
+    const uint64_t same = __ballot(done && myhint == first), act = __ballot(i < kp.n_lanes), dn = __ballot(done);
     const uint32_t nh = same == act ? first : 0u;
-    if ((threadIdx.x & 63) == 0) kp.hints_out[wave] = (uint8_t)nh;
+    if ((threadIdx.x & 63) == 0 && dn) kp.hints_out[wave] = (uint8_t)nh;
   }
   // followers into lists 0..7, leaders into 8..15, lanes with ticks or a
   // ReadIndex into 16..23 (the tick kernel's): the later kernels walk their lists
@@ -272,12 +281,15 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   uint32_t* nxt = counters + ((parity + 1) & 1) * kBailLists * kCounterStride;
   hipError_t err;
   if (t && (err = hipEventRecord(t->ev[0], s)) != hipSuccess) return err;
-  if (kp.hints && kp.split) {
+  if (kp.hints && kp.split) {  // the two role instances (a large pass)
     hipLaunchKernelGGL((gr_fast_kernel<S, FL_FOLLOWER>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
                        list_cap);
     if ((err = hipGetLastError()) != hipSuccess) return err;
+    hipLaunchKernelGGL((gr_fast_kernel<S, FL_LEADER>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
+                       list_cap);
+  } else {
+    hipLaunchKernelGGL((gr_fast_kernel<S, FL_ANY>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
   }
-  hipLaunchKernelGGL((gr_fast_kernel<S, FL_ANY>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
   if ((err = hipGetLastError()) != hipSuccess) return err;
   if (t && (err = hipEventRecord(t->ev[1], s)) != hipSuccess) return err;
   if (tick_lanes) {  // some lane may carry ticks or a ReadIndex (LW_OTHER)

@@ -51,11 +51,28 @@ void run_lanes(const StepParams& kp) {
              : pick == 1 ? (WH_LEADER | (((w >> 20) % S) << WH_SLOT_SHIFT) | (((w >> 24) & 1u) ? WH_SYNC : 0u))
                          : (WH_FOLLOWER | ((pick - 2) << WH_SLOT_SHIFT));
     }
-    // the kernel variant the device would run for this hint (gr_kernels.h)
+    // the lean-lane variant the device would run for this hint (gr_kernels.h):
+    // a split pass (drawn half the time here) runs the two role instances, an
+    // unhinted wave through both (each takes the lanes of its role); a small
+    // pass runs the FL_ANY instance
     const int fk = wave_kernel(hint, S);
-    const bool done = fk == FL_LEADER     ? fast_step<S, FL_LEADER>(kp, i, p, &ls, nullptr, hint)
-                      : fk == FL_FOLLOWER ? fast_step<S, FL_FOLLOWER>(kp, i, p, &ls, nullptr, hint)
-                                          : fast_step<S>(kp, i, p, &ls, nullptr, hint);
+    const bool split = (g_hint_salt >> 3) & 1u;
+    bool done;
+    if (fk == FL_LEADER) {
+      done = fast_step<S, FL_LEADER>(kp, i, p, &ls, nullptr, hint);
+    } else if (fk == FL_FOLLOWER) {
+      done = fast_step<S, FL_FOLLOWER>(kp, i, p, &ls, nullptr, hint);
+    } else if (split) {
+      bool skip = false;
+      done = fast_step<S, FL_FOLLOWER>(kp, i, p, &ls, nullptr, hint, nullptr, FL_FOLLOWER, &skip);
+      if (skip) {
+        ls = LaneStats{};
+        done = fast_step<S, FL_LEADER>(kp, i, p, &ls, nullptr, hint, nullptr, FL_LEADER, &skip);
+        if (skip) abort();  // no instance takes it: impossible (a lane leads or it does not)
+      }
+    } else {
+      done = fast_step<S>(kp, i, p, &ls, nullptr, hint);
+    }
     if (!done) bailed.push_back(i);
     else GR_CHECK_STATE(kp.st, p);
   }
