@@ -118,6 +118,11 @@ struct gr_engine {
   uint8_t* h_resext = nullptr;
   size_t h_outext_bytes = 0, h_resext_bytes = 0;
   std::mutex mu;  // one host-path pass at a time per engine
+  // gr_step_compact_begin -> _end: the uploaded pass waiting for its second half
+  struct CPending {
+    bool on = false;
+    uint32_t nm = 0, nlc = 0, nx = 0, nlx = 0, nl = 0;
+  } cpend;
 };
 
 // A fresh timing record for the next pass (nullptr when timing is off or a
@@ -540,6 +545,7 @@ uint64_t gr_space_hot_chunk_bytes(uint32_t positions, uint32_t depth) {
   if (depth == 0 || depth > GR_C) return 0;
   return space_hot_chunk_bytes_pc(space_pad_positions(positions), depth);
 }
+uint32_t gr_space_tile_positions(void) { return kTileW; }
 uint64_t gr_space_hot_tile_bytes(uint32_t depth) {
   if (depth == 0 || depth > GR_C) return 0;
   return tile_hot_bytes(depth);
@@ -732,8 +738,8 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
 // gr_step with compact records (gpuraft.h gr_cmsg / gr_clocal / gr_cresult):
 // the same device passes; records expand in registers on the way in and are
 // packed (with ext records for what does not fit) on the way out.
-int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out) {
-  if (!e || !in || !out) return GR_EINVAL;
+int gr_step_compact_begin(gr_engine* e, const gr_cinbox* in) {
+  if (!e || !in) return GR_EINVAL;
   if ((in->n_msgs && !in->msgs) || (in->n_locals && !in->locals) || (in->n_ext_msgs && !in->ext_msgs) ||
       (in->n_ext_locals && !in->ext_locals))
     return GR_EINVAL;
@@ -741,12 +747,16 @@ int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out) {
       in->n_ext_locals >= 0x80000000ull)
     return GR_EINVAL;
   std::lock_guard<std::mutex> guard(e->mu);
+  if (e->cpend.on) return GR_EINVAL;  // the previous begin was not ended
   PhaseClock clk;  // GR_PHASES=1: per-phase host times on stderr
-  memset(out, 0, sizeof(*out));
   const uint32_t S = e->S, cap = e->cfg.max_peers;
   const uint32_t nm = (uint32_t)in->n_msgs, nlc = (uint32_t)in->n_locals;
   const uint32_t nx = (uint32_t)in->n_ext_msgs, nlx = (uint32_t)in->n_ext_locals;
-  if (nm + nlc == 0) return GR_OK;
+  e->cpend = gr_engine::CPending{};
+  if (nm + nlc == 0) {
+    e->cpend.on = true;  // an empty pass: _end returns an empty outbox
+    return GR_OK;
+  }
   const hipStream_t s = e->stream;
   const dim3 blk(io::kIoBlock);
   int r;
@@ -789,7 +799,42 @@ int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out) {
   clk.mark("upload+lanes");
   const uint32_t nl = ((uint32_t*)e->h_scal)[0];
   if (((uint32_t*)e->h_scal)[1]) return GR_EINVAL;  // nothing of the pass ran
+  e->cpend.on = true;
+  e->cpend.nm = nm;
+  e->cpend.nlc = nlc;
+  e->cpend.nx = nx;
+  e->cpend.nlx = nlx;
+  e->cpend.nl = nl;
+  return GR_OK;
+}
+
+int gr_step_compact_end(gr_engine* e, gr_coutbox* out) {
+  if (!e || !out) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  if (!e->cpend.on) return GR_EINVAL;  // no pass was begun
+  const gr_engine::CPending pend = e->cpend;
+  e->cpend.on = false;
+  memset(out, 0, sizeof(*out));
+  PhaseClock clk;
+  const uint32_t S = e->S, cap = e->cfg.max_peers;
+  const uint32_t nm = pend.nm, nlc = pend.nlc, nx = pend.nx, nlx = pend.nlx, nl = pend.nl;
   if (nl == 0) return GR_OK;
+  const hipStream_t s = e->stream;
+  const dim3 blk(io::kIoBlock);
+  int r;
+  uint32_t* mark = (uint32_t*)e->d_mark.p;
+  uint32_t* lop = (uint32_t*)e->d_lop.p;
+  uint32_t* scal = (uint32_t*)e->d_scal.p;
+  io::CInbox ci;
+  ci.msgs = (const gr_cmsg*)e->d_msgs.p;
+  ci.ext = (const gr_message*)e->d_ext.p;
+  ci.loc = (const gr_clocal*)e->d_locals.p;
+  ci.lext = (const gr_local_input*)e->d_lext.p;
+  ci.n_msgs = nm;
+  ci.n_ext = nx;
+  ci.n_loc = nlc;
+  ci.n_lext = nlx;
+  (void)nlx;
   uint32_t* peer_of_lane = e->ln.u32(LR_LANE_PEER);
   hipLaunchKernelGGL(io::lane_peers, dim3(io_grid(cap)), blk, 0, s, (const uint32_t*)mark, (const uint32_t*)lop, cap,
                      peer_of_lane);
@@ -889,6 +934,13 @@ int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out) {
   out->ext_results = rext ? (gr_peer_result*)e->h_resext : nullptr;
   out->n_ext_results = rext;
   return GR_OK;
+}
+
+int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out) {
+  if (!e || !in || !out) return GR_EINVAL;
+  memset(out, 0, sizeof(*out));
+  const int r = gr_step_compact_begin(e, in);
+  return r ? r : gr_step_compact_end(e, out);
 }
 
 int gr_cinbox_reserve(gr_engine* e, size_t n_msgs, size_t n_ext_msgs, size_t n_locals, size_t n_ext_locals,

@@ -49,6 +49,8 @@ def load_library(path=LIB_PATH):
     lib.gr_notify_applied.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_compact_log.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p]
     lib.gr_step_compact.argtypes = [c.c_void_p, c.POINTER(abi.CInbox), c.POINTER(abi.COutbox)]
+    lib.gr_step_compact_begin.argtypes = [c.c_void_p, c.POINTER(abi.CInbox)]
+    lib.gr_step_compact_end.argtypes = [c.c_void_p, c.POINTER(abi.COutbox)]
     lib.gr_cinbox_reserve.argtypes = [c.c_void_p, c.c_size_t, c.c_size_t, c.c_size_t, c.c_size_t,
                                       c.POINTER(abi.CInbox)]
     lib.gr_release_coutbox.argtypes = [c.c_void_p, c.POINTER(abi.COutbox)]
@@ -69,6 +71,8 @@ def load_library(path=LIB_PATH):
     lib.gr_space_hot_chunk_bytes.argtypes = [c.c_uint32, c.c_uint32]
     lib.gr_space_hot_tile_bytes.restype = c.c_uint64
     lib.gr_space_hot_tile_bytes.argtypes = [c.c_uint32]
+    lib.gr_space_tile_positions.restype = c.c_uint32
+    lib.gr_space_tile_positions.argtypes = []
     lib.gr_space_cold_used.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p,
                                        c.POINTER(c.c_uint32)]
     lib.gr_bind_routes.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32]

@@ -32,16 +32,20 @@ NOPOS = 0xFFFFFFFF
 
 
 def count_bytes(hot, n_chunks, hot_chunk, hot_tile, positions):
-    """The mailbox count bytes of a hot region, [n_chunks, tiles, 64] (gr_layout.h:
-    a chunk's positions are tiled by 64, each tile starting with its 64 count bytes).
-    Works on a torch tensor or a numpy array."""
-    tiles = pad_positions(positions) // 64
-    return hot.reshape(n_chunks, hot_chunk)[:, :tiles * hot_tile].reshape(n_chunks, tiles, hot_tile)[:, :, :64]
+    """The mailbox count bytes of a hot region, [n_chunks, tiles, W] (gr_layout.h:
+    a chunk's positions are tiled by W, each tile starting with its W count bytes;
+    W = hot_tile / hot bytes per position). Works on a torch tensor or a numpy array."""
+    w = TILE_W
+    tiles = pad_positions(positions) // w
+    return hot.reshape(n_chunks, hot_chunk)[:, :tiles * hot_tile].reshape(n_chunks, tiles, hot_tile)[:, :, :w]
+
+
+TILE_W = 256  # gr_layout.h kTileW (GR_TILE_SHIFT = 8); Exchange checks it against the library
 
 
 def pad_positions(positions):
-    """gr_layout.h space_pad_positions: chunks hold a multiple of 64 mailboxes."""
-    return (positions + 63) & ~63
+    """gr_layout.h space_pad_positions: chunks hold a multiple of TILE_W mailboxes."""
+    return (positions + TILE_W - 1) & ~(TILE_W - 1)
 
 
 def offset_pairs(R, N):
@@ -142,6 +146,7 @@ class Exchange:
 
     def allocate(self, eng, device):
         import torch
+        assert int(eng.lib.gr_space_tile_positions()) == TILE_W, "library tile width differs from TILE_W"
         nbytes = eng.space_bytes(self.n_chunks, self.positions, self.depth)
         cb = eng.chunk_bytes(self.positions, self.depth)
         hb = eng.hot_chunk_bytes(self.positions, self.depth)

@@ -394,6 +394,14 @@ typedef struct gr_coutbox { /* engine-owned pinned memory, as gr_outbox */
 } gr_coutbox;
 
 int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out);
+/* gr_step_compact in two halves, so a step worker can overlap one partition's
+ * upload with another's kernels and download (PCIe is full duplex): _begin
+ * validates the inbox, copies it to the device and returns once the copy is
+ * done (the inbox buffers may then be reused); _end runs the pass and fills
+ * `out`. Every _begin is followed by exactly one _end on the same engine
+ * (GR_EINVAL otherwise); another thread may call _end. */
+int gr_step_compact_begin(gr_engine* e, const gr_cinbox* in);
+int gr_step_compact_end(gr_engine* e, gr_coutbox* out);
 /* Engine-owned pinned buffers for the next gr_step_compact inbox (as gr_inbox_reserve). */
 int gr_cinbox_reserve(gr_engine* e, size_t n_msgs, size_t n_ext_msgs, size_t n_locals, size_t n_ext_locals,
                       gr_cinbox* in);
@@ -439,11 +447,13 @@ int gr_timing_end(gr_engine* e, gr_timing* out);
 uint64_t gr_space_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth);
 uint64_t gr_space_chunk_bytes(uint32_t positions, uint32_t depth);
 uint64_t gr_space_hot_chunk_bytes(uint32_t positions, uint32_t depth);
-/* A chunk's positions are tiled by 64: tile t of its hot region starts at
- * t * gr_space_hot_tile_bytes(depth), and the tile's first 64 bytes are the
- * count bytes of positions 64t..64t+63 (bit 3 set: the mailbox needs no cold
- * fields). 0 when depth is not in 1..GR_C. */
+/* A chunk's positions are tiled by W = gr_space_tile_positions(): tile t of its
+ * hot region starts at t * gr_space_hot_tile_bytes(depth), and the tile's first
+ * W bytes are the count bytes of positions Wt..Wt+W-1 (bit 3 set: the mailbox
+ * needs no cold fields). 0 when depth is not in 1..GR_C. */
 uint64_t gr_space_hot_tile_bytes(uint32_t depth);
+/* Positions (and state slots) per tile: chunks hold a multiple of it. */
+uint32_t gr_space_tile_positions(void);
 /* *out = 1 when some mailbox of the (device) space holds a message with cold
  * fields, i.e. the cold region must travel with the hot one; runs on `stream`
  * and waits for it. */

@@ -180,7 +180,7 @@ extern "C" int hl_commit_update(uint32_t slots, gr_peer* peers, uint32_t n_peers
     if (list[x] >= n_peers) return GR_ERANGE;
     gr_peer& g = peers[list[x]];
     StateBase st;
-    st.cap = 64;
+    st.cap = pad_cap(1);  // one tile
     st.S = S;
     std::vector<uint64_t> sbuf((state_bytes(S, st.cap) + 7) / 8, 0);
     st.base = (uint8_t*)sbuf.data();

@@ -27,6 +27,12 @@ def counters(d, kernel_sub):
     return {k: [v[x] for x in sorted(v, key=int)] for k, v in per.items()}
 
 
+# The lean kernel's instances (gr_kernels.h): a split pass runs <S, 2> (followers)
+# then <S, 1> (leaders); a small or host-path pass runs <S, 0>. A device pass's
+# lean-kernel bytes are the sum over the instances it ran.
+ROLE_INSTANCES = ("gr_fast_kernel<3, 2>", "gr_fast_kernel<3, 1>")
+
+
 def main(o):
     s = {}
     st = rows(os.path.join(o, "trace", "**", "*kernel_stats.csv"))
@@ -59,13 +65,25 @@ def main(o):
         sq = counters(os.path.join(o, "sq"), kname)
         k["sq"] = {c: sum(v[3:] or v) / len(v[3:] or v) for c, v in sq.items() if v}
         s["kernels"][kname] = k
+    for kname in ROLE_INSTANCES:  # per instance, for the per-pass sum below
+        f = counters(os.path.join(o, "fetch"), kname).get("FETCH_SIZE", [])
+        w = counters(os.path.join(o, "write"), kname).get("WRITE_SIZE", [])
+        f_ss, w_ss = f[3:] or f, w[3:] or w
+        if f_ss and w_ss:
+            fu, wu = sum(f_ss) / len(f_ss), sum(w_ss) / len(w_ss)
+            s["kernels"][kname] = {"launches": len(f), "read_bytes": fu * kf, "write_bytes": wu * kw,
+                                   "hbm_bytes_per_launch": fu * kf + wu * kw}
     fk = s["kernels"].get("gr_fast_kernel", {})
+    if all(k in s["kernels"] for k in ROLE_INSTANCES):  # split passes: one pass = both instances
+        fk = {key: sum(s["kernels"][k][key] for k in ROLE_INSTANCES)
+              for key in ("read_bytes", "write_bytes", "hbm_bytes_per_launch")}
+        s["lean_kernel_bytes_per_pass"] = fk
     if "hbm_bytes_per_launch" in fk:
         groups = int(os.environ.get("GROUPS", "1000000"))
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         from dragonboat_amd.build import source_digest
         with open(os.path.join(o, "pmc_latest.json"), "w") as fh:
-            json.dump({"kernel": "gr_fast_kernel<3>", "groups": groups, "replicas": 3,
+            json.dump({"kernel": "gr_fast_kernel<3, *> (the instances of one pass)", "groups": groups, "replicas": 3,
                        "source_digest": source_digest(),
                        "hbm_bytes_per_launch": fk["hbm_bytes_per_launch"],
                        "read_bytes": fk["read_bytes"], "write_bytes": fk["write_bytes"],
