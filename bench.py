@@ -80,7 +80,7 @@ def parse():
     ap.add_argument("--host-passes", type=int, default=4)
     ap.add_argument("--host-partitions", type=int, default=2,
                     help="concurrent step workers (engines) of the compact host-path leg")
-    ap.add_argument("--host-pipeline-partitions", type=int, default=8,
+    ap.add_argument("--host-pipeline-partitions", type=int, default=4,
                     help="partitions of the pipelined compact host-path leg (begin/end halves)")
     ap.add_argument("--check", action="store_true", help="verify the final state against a host replay")
     return ap.parse_args()
