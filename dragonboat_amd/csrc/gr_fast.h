@@ -54,6 +54,19 @@ struct FastLane {
   uint64_t term = 0, committed = 0, committed0 = 0, hi = 0, hi0 = 0;
   uint64_t rsn = 0, rtn = 0;  // newest term run (start, term)
   uint64_t rsn0 = 0, rtn0 = 0;  // ... as loaded (moves one row down when a run is pushed)
+  // run bits (gr_layout.h): with both set and the rows not loaded, rsn is
+  // unknown but at most cload (committed as loaded) and rtn is term
+  static constexpr bool kRuns = has_run_bits(S);
+  bool rknown = true;
+  uint64_t cload = 0;
+  bool runs_out = false;  // both run bits set after the pass (the wave hint)
+  // "x is below the newest run's start" when rsn is unknown is answered only for
+  // x at or above cload (no); below it the lane hands over
+  GF_HD bool below_newest(uint64_t x) {
+    if (rknown) return x < rsn;
+    GF_BAIL(x < cload);
+    return false;
+  }
   bool pushed = false;        // a run was appended this pass (row nruns-1)
   bool ok = true;             // still on the steady-state path
   // leader remotes
@@ -95,7 +108,7 @@ struct FastLane {
   // run (an older run, or below firstIndex-1) hands the lane over.
   GF_HD uint64_t term_of(uint64_t x) {
     if (x > hi) return 0;
-    GF_BAIL(nruns == 0 || x < rsn);
+    GF_BAIL(nruns == 0 || below_newest(x));
     return rtn;
   }
   // win_push (gr_lane.h) for one new run per pass onto a window of at most one
@@ -103,7 +116,7 @@ struct FastLane {
   // (a longer window would shift every run: the general lane does that).
   GF_HD void win_push(uint64_t start, uint64_t t) {
     if (nruns > 0 && rtn == t) return;
-    GF_BAIL(pushed || nruns >= 2);
+    GF_BAIL(pushed || nruns >= 2 || !rknown);  // moving the old newest run down needs its rows
     rsn = start;
     rtn = t;
     nruns++;
@@ -208,7 +221,7 @@ struct FastLane {
     if (nx <= hi) {
       // nx <= rsn covers entries in an older run and nx <= firstIndex-1
       // (InstallSnapshot path): with H_GE_LO, nx > rsn implies nx > firstIndex-1
-      GF_BAIL(nruns == 0 || nx <= rsn);
+      GF_BAIL(nruns == 0 || below_newest(nx - 1));  // nx <= rsn
       GF_BAIL(hi - nx + 1 > 1);         // several entries: MaxEntrySize check
       GF_BAIL(rst(j) != GR_REPLICATE_ST && rst(j) != GR_RETRY);
       n = 1;
@@ -306,7 +319,8 @@ struct FastLane {
   GF_HD bool step(LaneStats* ls, uint32_t hint, int take = FL_ANY) {
     const bool hl = kLeaderPath && (hint & WH_ROLE) == WH_LEADER;
     const bool hf = (hint & WH_ROLE) == WH_FOLLOWER;
-    const uint32_t hL = hint >> WH_SLOT_SHIFT;
+    const uint32_t hL = (hint >> WH_SLOT_SHIFT) & 7u;
+    const bool hruns = kRuns && (hint & WH_RUNS);  // the wave's run bits were set: skip the run rows
     const uint32_t hself = (hint >> WH_SLOT_SHIFT) & 7u;  // leader hints: the self slot
     const bool hsync = kSync && hl && (hint & WH_SYNC);   // ... whose remote rows were in sync
     // ---- round 1: core (one header word), the newest run (a fixed row), locals,
@@ -315,8 +329,10 @@ struct FastLane {
     term = ntld(s64(SR_TERM));
     committed = ntld(s64(SR_COMMITTED));
     hi = ntld(s64(SR_LAST_INDEX));
-    rsn0 = ntld(s64(SR_RUN_START + GR_K - 1));  // meaningful when nruns > 0
-    rtn0 = ntld(s64(SR_RUN_TERM + GR_K - 1));
+    if (!hruns) {
+      rsn0 = ntld(s64(SR_RUN_START + GR_K - 1));  // meaningful when nruns > 0
+      rtn0 = ntld(s64(SR_RUN_TERM + GR_K - 1));
+    }
     const uint32_t lw = kp.has_locals ? ntld(kp.ln.u32(LR_LWORD)[i]) : 0u;  // packed locals (gr_layout.h)
     uint32_t gin[S];
     routes_of<S>(kp, i, gin, gout);
@@ -381,9 +397,19 @@ struct FastLane {
     const bool gelo = h_gelo(hdr);
     const uint32_t flags = h_flags(hdr);
     lslot_out = (flags & F_LSLOT) >> F_LSLOT_SHIFT;
+    cload = committed;
     if (nruns) {
-      rsn = rsn0;
-      rtn = rtn0;
+      if (hruns && kRuns && (hdr & H_RUN_MASK) == H_RUN_MASK) {
+        rknown = false;  // rsn <= cload, rtn = term: the rows stay unread
+        rtn = term;
+      } else {
+        if (hruns) {  // the hint misjudged this lane: its rows now
+          rsn0 = ntld(s64(SR_RUN_START + GR_K - 1));
+          rtn0 = ntld(s64(SR_RUN_TERM + GR_K - 1));
+        }
+        rsn = rsn0;
+        rtn = rtn0;
+      }
     }
     const bool leader = state == GR_LEADER;
     if ((take == FL_LEADER && !leader) || (take == FL_FOLLOWER && leader)) {
@@ -573,6 +599,14 @@ struct FastLane {
       }
       nh = (nh & ~(0xFFull << H_FLAGS_SHIFT)) | ((uint64_t)nf << H_FLAGS_SHIFT);
     }
+    if (kRuns) {  // run bits (gr_layout.h) after the pass
+      uint64_t rbits = 0;
+      if (nruns)
+        rbits = (rtn == term ? 1ull << H_RTT_BIT : 0ull) |
+                ((rknown ? rsn <= committed : true) ? 1ull << H_RLC_BIT : 0ull);  // unknown: rsn <= cload
+      nh = (nh & ~H_RUN_MASK) | rbits;
+      runs_out = rbits == H_RUN_MASK;
+    }
     lslot_out = (h_flags(nh) & F_LSLOT) >> F_LSLOT_SHIFT;
     if (nh != hdr) ntst(s64(SR_HDR), nh);
 #pragma unroll
@@ -605,10 +639,11 @@ struct FastLane {
   // pass when it finished here, what it was when it handed over.
   GF_HD uint32_t role_hint() const {
     if (!had_input) return 0;  // quiesced or idle: nothing to speculate on
+    const uint32_t rh = runs_out ? WH_RUNS : 0u;
     if (state == GR_LEADER)
-      return WH_LEADER | (self < 8u ? self << WH_SLOT_SHIFT : 0u) | (synced && self < 8u ? WH_SYNC : 0u);
+      return WH_LEADER | (self < 8u ? self << WH_SLOT_SHIFT : 0u) | (synced && self < 8u ? WH_SYNC : 0u) | rh;
     if (state != GR_FOLLOWER || !lslot_out) return 0;
-    return WH_FOLLOWER | ((lslot_out - 1) << WH_SLOT_SHIFT);
+    return WH_FOLLOWER | ((lslot_out - 1) << WH_SLOT_SHIFT) | rh;
   }
 
   // handleReplicateMessage (raft.go:953-976) for an append at the log's end.
@@ -627,14 +662,14 @@ struct FastLane {
     if (n) {  // getConflictIndex over the newest run (logentry.go:305-312)
       const uint64_t a = li + 1, b = li + n;  // a >= rsn >= firstIndex-1 below (H_GE_LO)
       if (a <= hi) {
-        GF_BAIL(nruns == 0 || a < rsn);
+        GF_BAIL(nruns == 0 || below_newest(a));
         if (rtn != rt0) ci = a;
       }
       if (ci == 0 && b > hi && rt0 != 0) ci = a > hi + 1 ? a : hi + 1;
     }
     if (ci) {
       GF_BAIL(ci <= committed || ci != hi + 1);  // panic / truncation: general lane
-      GF_BAIL(nruns && rsn > hi);                // a run beyond lastIndex would be truncated
+      GF_BAIL(nruns && rknown && rsn > hi);      // a run beyond lastIndex would be truncated
       const uint64_t tprev = (ci - 1 == li) ? lterm : rt0;
       GF_BAIL(tprev > rt0);  // checkEntriesToAppend
       win_push(ci, rt0);

@@ -28,7 +28,9 @@ __host__ __device__ inline uint64_t header_of(const gr_peer& g, uint32_t S) {
   for (uint32_t j = 0; j < S; ++j)
     rb |= (uint64_t)((g.remotes[j].state & 3u) | ((g.remotes[j].active & 1u) << 2) | ((g.remotes[j].kind & 3u) << 3))
           << (5 * j);
-  return h_make(g.state, g.self_slot, n, gelo, flags, g.read_index_count, rb);
+  uint64_t h = h_make(g.state, g.self_slot, n, gelo, flags, g.read_index_count, rb);
+  if (has_run_bits((int)S) && n) h |= run_bits(n, g.run_start[n - 1], g.run_term[n - 1], g.term, g.committed);
+  return h;
 }
 __host__ __device__ inline void set_header(gr_peer& g, uint32_t S, uint64_t h) {
   g.state = (uint8_t)h_state(h);

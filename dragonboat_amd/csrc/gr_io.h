@@ -429,7 +429,8 @@ __global__ void compact_rows(StateBase st, const uint32_t* slots, const uint64_t
     for (int k = 0; k < GR_K; ++k)
       if ((uint32_t)k + 1 == nn) newest = ns[k];
     const bool ge = nn && newest >= i;
-    st.u64(SR_HDR)[p] = h_make(h_state(h), h_self(h), nn, ge, h_flags(h), h_ric(h), h_rb(h));
+    // the run bits are cleared (the covering run may now start above committed)
+    st.u64(SR_HDR)[p] = h_make(h_state(h), h_self(h), nn, ge, h_flags(h), h_ric(h), h_rb(h)) & ~H_RUN_MASK;
   }
 }
 

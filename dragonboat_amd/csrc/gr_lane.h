@@ -276,7 +276,11 @@ struct Lane {
         s8(R::B_RIACK + q) = (uint8_t)(riack >> (8 * q));
       }
     }
-    if (dirty & (D_STATE | D_FLAGS | D_WIN | D_REM | D_RI)) {  // one header word for the small fields
+    // one header word for the small fields; the run bits follow term, committed
+    // and the window (gr_layout.h)
+    const uint32_t hdr_dirty = D_STATE | D_FLAGS | D_WIN | D_REM | D_RI |
+                               (has_run_bits(S) ? (D_TERM | D_COMMITTED | D_HI) : 0u);
+    if (dirty & hdr_dirty) {
       uint64_t h = hdr0;
       const uint64_t remmask = ((1ull << (5 * S)) - 1) << H_REM_SHIFT;
       const uint64_t keep_rem = h & (~0ull << H_REM_SHIFT) & ~remmask & ~(unsync ? H_SYNC_MASK : 0ull);
@@ -292,6 +296,18 @@ struct Lane {
       const uint64_t rbits = (dirty & D_REM) ? rb : (h_rb(h) & ((1ull << (5 * S)) - 1));
       h = h_make(state, self, nr, gelo, flags, (dirty & D_RI) ? ric : h_ric(h), 0) | keep_rem |
           (rbits << H_REM_SHIFT);
+      if (has_run_bits(S)) {
+        h &= ~H_RUN_MASK;
+        if (loaded & G_WIN) {
+          uint64_t ns = 0, nt = 0;
+#pragma unroll
+          for (int r = 0; r < GR_K; ++r) {
+            ns = ((uint32_t)r + 1 == nruns) ? rs[r] : ns;
+            nt = ((uint32_t)r + 1 == nruns) ? rt[r] : nt;
+          }
+          h |= run_bits(nruns, ns, nt, term, committed);
+        }  // else: cleared (the window was not read)
+      }
       if (h != hdr0) s64(SR_HDR) = h;
     }
   }

@@ -121,6 +121,21 @@ constexpr uint64_t H_SYNC_MASK = (7ull << H_NX_SHIFT) | (1ull << H_MS_BIT);
 __host__ __device__ constexpr bool has_sync_bits(int S) { return S <= 3; }
 __host__ __device__ inline bool h_nx(uint64_t h, uint32_t j) { return (h >> (H_NX_SHIFT + j)) & 1u; }
 __host__ __device__ inline bool h_ms(uint64_t h) { return (h >> H_MS_BIT) & 1u; }
+// Run bits (S <= 6; above rb and the sync bits): H_RTT says the window's newest
+// run has the current term, H_RLC that it starts at or below committed. Both
+// hold in steady state (the leader's term's run began before the commit point),
+// and then every index at or above committed is in the newest run at the
+// current term: the lean lane tests the bits instead of loading the run's two
+// rows. They are summaries (the rows stay exact): set only with at least one
+// run; every writer of term, committed or the window recomputes or clears them.
+constexpr uint32_t H_RTT_BIT = 60, H_RLC_BIT = 61;
+constexpr uint64_t H_RUN_MASK = (1ull << H_RTT_BIT) | (1ull << H_RLC_BIT);
+__host__ __device__ constexpr bool has_run_bits(int S) { return S <= 6; }
+__host__ __device__ inline uint64_t run_bits(uint32_t nruns, uint64_t newest_start, uint64_t newest_term,
+                                             uint64_t term, uint64_t committed) {
+  if (!nruns) return 0;
+  return (newest_term == term ? 1ull << H_RTT_BIT : 0ull) | (newest_start <= committed ? 1ull << H_RLC_BIT : 0ull);
+}
 // per-slot fields of rb (5 bits per slot: state(2) active(1) kind(2))
 __host__ __device__ inline uint32_t rb_state(uint64_t rb, uint32_t j) { return (uint32_t)(rb >> (5 * j)) & 3u; }
 __host__ __device__ inline uint32_t rb_active(uint64_t rb, uint32_t j) { return (uint32_t)(rb >> (5 * j + 2)) & 1u; }
@@ -437,7 +452,8 @@ constexpr uint8_t RT_IDENTITY = 0, RT_TABLE = 1, RT_AFFINE = 2, RT_LOOPBACK = 3;
 // Follower hints carry the leader's slot in bits 2..; leader hints carry the
 // self slot in bits 2-4 and WH_SYNC when every lane's remote rows were in sync
 // (H_NX for every member slot and H_MS), so no NEXT row or own MATCH row is loaded.
-constexpr uint32_t WH_ROLE = 3, WH_LEADER = 1, WH_FOLLOWER = 2, WH_SLOT_SHIFT = 2, WH_SYNC = 0x20;
+// WH_RUNS: every lane's run bits were set, so no lane loads the newest run's rows.
+constexpr uint32_t WH_ROLE = 3, WH_LEADER = 1, WH_FOLLOWER = 2, WH_SLOT_SHIFT = 2, WH_SYNC = 0x20, WH_RUNS = 0x40;
 // The lean kernel (FL_* of gr_fast.h) that steps a wave with hint h.
 __host__ __device__ inline int wave_kernel(uint32_t h, int S) {
   if ((h & WH_ROLE) == WH_LEADER && S <= 3) return 1;  // FL_LEADER

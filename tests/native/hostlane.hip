@@ -41,15 +41,17 @@ void run_lanes(const StepParams& kp) {
       const uint32_t i0 = i & ~63u;
       const uint64_t h = kp.st.u64(SR_HDR)[kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i0] : i0];
       const uint32_t ls0 = (h_flags(h) & F_LSLOT) >> F_LSLOT_SHIFT;
+      const uint32_t rh = (h & H_RUN_MASK) == H_RUN_MASK ? WH_RUNS : 0u;
       hint = h_state(h) == GR_LEADER ? (WH_LEADER | ((h_self(h) & 7u) << WH_SLOT_SHIFT) |
-                                        ((h & H_SYNC_MASK) ? WH_SYNC : 0u))
-             : (h_state(h) == GR_FOLLOWER && ls0) ? (WH_FOLLOWER | ((ls0 - 1) << WH_SLOT_SHIFT))
+                                        ((h & H_SYNC_MASK) ? WH_SYNC : 0u) | rh)
+             : (h_state(h) == GR_FOLLOWER && ls0) ? (WH_FOLLOWER | ((ls0 - 1) << WH_SLOT_SHIFT) | rh)
                                                   : 0u;
     } else {
       const uint32_t pick = (w >> 13) % (2u + S);
+      const uint32_t rh = ((w >> 25) & 1u) ? WH_RUNS : 0u;
       hint = pick == 0 ? 0u
-             : pick == 1 ? (WH_LEADER | (((w >> 20) % S) << WH_SLOT_SHIFT) | (((w >> 24) & 1u) ? WH_SYNC : 0u))
-                         : (WH_FOLLOWER | ((pick - 2) << WH_SLOT_SHIFT));
+             : pick == 1 ? (WH_LEADER | (((w >> 20) % S) << WH_SLOT_SHIFT) | (((w >> 24) & 1u) ? WH_SYNC : 0u) | rh)
+                         : (WH_FOLLOWER | ((pick - 2) << WH_SLOT_SHIFT) | rh);
     }
     // the lean-lane variant the device would run for this hint (gr_kernels.h):
     // a split pass (drawn half the time here) runs the two role instances, an
