@@ -49,7 +49,7 @@ enum U64Row : uint32_t {
   SR_TERM = 0, SR_VOTE, SR_COMMITTED, SR_APPLIED, SR_LAST_INDEX, SR_LO, SR_LEADER_ID, SR_LTT,
   SR_NODE_ID, SR_ETICK, SR_HTICK, SR_RETIMEOUT, SR_ETIMEOUT, SR_HTIMEOUT, SR_ENTRY_UB,
   SR_SAVED_TO, SR_MARKER, SR_LOG_APPLIED,  // inMemory.savedTo / markerIndex, entryLog.applied (§8f-4)
-  SR_HDR,                          // the header word (below)
+  SR_HDR,                          // the header word (below); 18: phys_row (GR_PAIR) pairs it with SR_TERM
   SR_RUN_START,                    // + row, right-aligned (run_row)
   SR_RUN_TERM = SR_RUN_START + GR_K,  // + r
   SR_REMOTE = SR_RUN_TERM + GR_K,     // remote rows start; see below
@@ -155,11 +155,34 @@ __host__ __device__ inline uint64_t state_bytes(uint32_t S, uint32_t cap) {
 #ifndef GR_TILE
 #define GR_TILE 1
 #endif
+// GR_PAIR = 1: inside a tile, the u64 rows every steady-state lane reads come
+// in interleaved pairs, (term, header) and (committed, lastIndex): a lane's two
+// fields of a pair are adjacent, so each pair loads and stores as one 16-byte
+// access. Physical rows 0..3 hold the pairs; the other rows follow in order.
+#ifndef GR_PAIR
+#define GR_PAIR 0
+#endif
+__host__ __device__ constexpr uint32_t phys_row(uint32_t r) {
+#if GR_PAIR
+  return r == 0 ? 0u : r == 18 ? 1u : r == 2 ? 2u : r == 4 ? 3u  // SR_TERM, SR_HDR, SR_COMMITTED, SR_LAST_INDEX
+         : 4u + r - (r > 0) - (r > 2) - (r > 4) - (r > 18);
+#else
+  return r;
+#endif
+}
 template <class T>
 struct TileRow {  // row `row` of a tiled region with `nrows` rows per tile
   T* b;
   uint32_t row, nrows;
   __host__ __device__ inline T& operator[](uint64_t p) const {
+#if GR_PAIR
+    if (sizeof(T) == 8) {
+      const uint32_t ph = phys_row(row);
+      if (ph < 4)
+        return b[(((p >> GR_TILE_SHIFT) * nrows + (ph & ~1u)) * kTileW + 2 * (p & kTileM)) + (ph & 1u)];
+      return b[((p >> GR_TILE_SHIFT) * nrows + ph) * kTileW + (p & kTileM)];
+    }
+#endif
     return b[((p >> GR_TILE_SHIFT) * nrows + row) * kTileW + (p & kTileM)];
   }
 };

@@ -237,12 +237,17 @@ class Engine:
                                        ctypes.byref(nx)), "gr_pack_locals")
         return c, ext[:nx.value].copy()
 
-    def step_compact(self, cmsgs, ext_msgs, clocals, ext_locals):
-        """One synchronous pass with compact records (gr_step_compact). Returns
+    def step_compact(self, cmsgs, ext_msgs, clocals, ext_locals, halves=False):
+        """One synchronous pass with compact records (gr_step_compact, or with
+        halves=True its two halves gr_step_compact_begin + _end). Returns
         (cmsgs, ext msgs, cresults, ext results) copied out of the engine's outbox."""
         ib = abi.cinbox_of(cmsgs, ext_msgs, clocals, ext_locals)
         ob = abi.COutbox()
-        _check(self.lib.gr_step_compact(self._h, ctypes.byref(ib), ctypes.byref(ob)), "gr_step_compact")
+        if halves:
+            _check(self.lib.gr_step_compact_begin(self._h, ctypes.byref(ib)), "gr_step_compact_begin")
+            _check(self.lib.gr_step_compact_end(self._h, ctypes.byref(ob)), "gr_step_compact_end")
+        else:
+            _check(self.lib.gr_step_compact(self._h, ctypes.byref(ib), ctypes.byref(ob)), "gr_step_compact")
         out = []
         for ptr, n, dt in ((ob.msgs, ob.n_msgs, abi.CMSG), (ob.ext_msgs, ob.n_ext_msgs, abi.MESSAGE),
                            (ob.results, ob.n_results, abi.CRESULT), (ob.ext_results, ob.n_ext_results, abi.RESULT)):

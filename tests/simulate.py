@@ -88,10 +88,12 @@ class GpuCompactBackend(GpuBackend):
     term/vote are the synced state's (a change would have made it an ext record)."""
     result_fields = [f for f in parity.RESULT_FIELDS if f != "append_from"]
 
+    halves = False  # GpuCompactHalvesBackend: gr_step_compact_begin + _end
+
     def step(self, msgs, loc):
         cm, xm = self.eng.pack_messages(msgs)
         cl, xl = self.eng.pack_locals(loc)
-        om, ox, cr, rx = self.eng.step_compact(cm, xm, cl, xl)
+        om, ox, cr, rx = self.eng.step_compact(cm, xm, cl, xl, halves=self.halves)
         out = self.eng.unpack_messages(om, ox)
         res = np.zeros(len(cr), abi.RESULT)
         for f in ("peer", "escalation", "propose_result", "esc_item", "committed", "last_index", "save_from"):
@@ -108,6 +110,11 @@ class GpuCompactBackend(GpuBackend):
         if x.any():
             res[x] = rx[cr["ext"][x].astype(np.int64)]
         return out, res
+
+
+class GpuCompactHalvesBackend(GpuCompactBackend):
+    """gr_step_compact as its two halves (the pipelined host path)."""
+    halves = True
 
 
 def _threads():

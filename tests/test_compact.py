@@ -118,13 +118,14 @@ def test_pack_locals_round_trip(built):
     assert np.array_equal((c["flags"][y] & abi.CL_CONFIG_CHANGE) != 0, loc["propose_has_config_change"][y] != 0)
 
 
-def _sim(G, passes, seed, R=3, locals_fn=None, inject_p=0.0, peers=None, drop_fn=None, **mk):
+def _sim(G, passes, seed, R=3, locals_fn=None, inject_p=0.0, peers=None, drop_fn=None, halves=False, **mk):
     peers = P.make_groups(G, R, seed=seed, **mk) if peers is None else peers
     topo = P.Topology(G, R)
     rng = np.random.default_rng(seed)
     lf = locals_fn or (lambda k: P.propose_locals(R * G, np.arange(G), pass_index=k))
     inj = (lambda k, cur: P.inject_leader_change(cur, topo, inject_p, rng)) if inject_p else None
-    return SIM.simulate(SIM.GpuCompactBackend, peers, topo, passes, lf, inject_fn=inj, slots=R, drop_fn=drop_fn)
+    backend = SIM.GpuCompactHalvesBackend if halves else SIM.GpuCompactBackend
+    return SIM.simulate(backend, peers, topo, passes, lf, inject_fn=inj, slots=R, drop_fn=drop_fn)
 
 
 @pytest.mark.gpu
@@ -162,3 +163,27 @@ def test_compact_config3(gpu):
     st = _sim(G, 8, seed=33, R=R, peers=peers, locals_fn=lambda k: P.config3_locals(G, R, active, k),
               drop_fn=lambda k, m: P.drop_acks(m, 0.1, rng))
     assert st["ready"] > 0
+
+
+@pytest.mark.gpu
+def test_compact_halves(gpu):
+    """gr_step_compact_begin + _end (the pipelined host path of bench.py) equal the
+    oracle after every pass like gr_step_compact, and refuse misuse: _end without a
+    _begin, a second _begin before its _end (GR_EINVAL, nothing run)."""
+    st = _sim(600, 8, seed=7, inject_p=0.1, halves=True)
+    assert st["commits"] > 0
+    from dragonboat_amd.engine import Engine
+    eng = Engine(64 * 3, 3)
+    eng.load(P.make_groups(64, 3, seed=1))
+    ob = abi.COutbox()
+    assert eng.lib.gr_step_compact_end(eng._h, ctypes.byref(ob)) == -1  # GR_EINVAL
+    cm, xm = eng.pack_messages(np.zeros(0, abi.MESSAGE))
+    cl, xl = eng.pack_locals(P.propose_locals(64 * 3, np.arange(64), pass_index=0))
+    ib = abi.cinbox_of(cm, xm, cl, xl)
+    assert eng.lib.gr_step_compact_begin(eng._h, ctypes.byref(ib)) == 0
+    assert eng.lib.gr_step_compact_begin(eng._h, ctypes.byref(ib)) == -1
+    assert eng.lib.gr_step_compact_end(eng._h, ctypes.byref(ob)) == 0
+    assert ob.n_results == 64 * 3 or ob.n_results == 64  # a result per lane with input
+    assert eng.lib.gr_release_coutbox(eng._h, ctypes.byref(ob)) == 0
+    eng.close()
+
