@@ -27,37 +27,25 @@ __device__ inline uint32_t wave_sum(uint32_t v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
 }
+// Each wave adds its own sums: the nine totals are wave-uniform after the
+// butterfly, lane k adds total k with a non-returning atomic. No LDS and no
+// barrier, so a wave never waits for the rest of its workgroup to finish.
 __device__ inline void block_stats(const StepParams& kp, const LaneStats& ls) {
   constexpr int N = 9;
-  __shared__ uint32_t red[N];
-  if (threadIdx.x < N) red[threadIdx.x] = 0;
-  __syncthreads();
   // one named field at a time: a register array indexed in a loop was put in scratch
   const uint32_t f0 = wave_sum(ls.leader_commit), f1 = wave_sum(ls.follower_commit),
                  f2 = wave_sum(ls.escalated), f3 = wave_sum(ls.msgs_in), f4 = wave_sum(ls.msgs_out),
                  f5 = wave_sum(ls.leader_in), f6 = wave_sum(ls.leader_out), f7 = wave_sum(ls.entries),
                  f8 = wave_sum(ls.bailed);
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&red[0], f0);
-    atomicAdd(&red[1], f1);
-    atomicAdd(&red[2], f2);
-    atomicAdd(&red[3], f3);
-    atomicAdd(&red[4], f4);
-    atomicAdd(&red[5], f5);
-    atomicAdd(&red[6], f6);
-    atomicAdd(&red[7], f7);
-    atomicAdd(&red[8], f8);
-  }
-  __syncthreads();
-  // fire-and-forget adds to the workgroup's own row (never contended): a
-  // read-modify-write would add a dependent memory round to every block's end
-  if (threadIdx.x < N) {
+  const uint32_t k = threadIdx.x & 63;
+  if (k < (uint32_t)N) {
     constexpr uint32_t field[N] = {ST_LEADER_COMMITS, ST_FOLLOWER_COMMITS, ST_ESCALATIONS, ST_MSGS_IN, ST_MSGS_OUT,
                                    ST_LEADER_MSGS_IN, ST_LEADER_MSGS_OUT, ST_REPLICATE_ENTRIES, ST_BAILED};
+    const uint32_t v = k == 0 ? f0 : k == 1 ? f1 : k == 2 ? f2 : k == 3 ? f3 : k == 4 ? f4 : k == 5 ? f5
+                     : k == 6 ? f6 : k == 7 ? f7 : f8;
     uint32_t f = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < N; ++k) f = threadIdx.x == k ? field[k] : f;
-    const uint32_t v = red[threadIdx.x];
+    for (uint32_t x = 0; x < (uint32_t)N; ++x) f = k == x ? field[x] : f;
     if (v) atomicAdd((unsigned long long*)(kp.stats + (uint64_t)blockIdx.x * NSTAT + f), (unsigned long long)v);
   }
 }
@@ -97,7 +85,7 @@ __device__ inline void bail_append(bool mine, uint32_t list, uint32_t* bail_list
 // stepping the lanes of its role and leaving the others untouched (FastLane
 // `take`). A small pass runs the single instance R = FL_ANY, which picks the
 // lean-lane variant per wave from its hint. A block none of whose waves is an
-// instance's returns at once; a wave that is not joins the block's barriers only.
+// instance's returns at once.
 // Measured and dropped: the two instances concurrently on two streams (0.133 vs
 // 0.124 ms per 1M x 3 pass), and a third instance for unhinted waves (~8 us for a
 // mostly empty launch).
