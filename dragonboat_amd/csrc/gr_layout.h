@@ -148,10 +148,10 @@ __host__ __device__ inline uint64_t state_bytes(uint32_t S, uint32_t cap) {
   return (uint64_t)cap * (8ull * rows_u64(S) + rows_u8(S));
 }
 
-// GR_TILE = 1: the rows are tiled by 64 slots (one wave): tile t holds every
-// row of slots 64t..64t+63, row-major inside the tile, so a wave's fields are
-// one contiguous block (a few KB) instead of ~30 separate row streams
-// (24 MB apart at 1M x 3). GR_TILE = 0: plain rows over all slots.
+// GR_TILE = 1: the rows are tiled by kTileW slots (256, one workgroup): tile t
+// holds every row of its slots, row-major inside the tile, so a workgroup's
+// fields are one contiguous block instead of ~30 separate row streams (24 MB
+// apart at 1M x 3). GR_TILE = 0: plain rows over all slots.
 #ifndef GR_TILE
 #define GR_TILE 1
 #endif
@@ -324,9 +324,9 @@ constexpr uint32_t kColdK = 50;  // ... cold chunk: tag, term and the rest
 __host__ __device__ inline uint64_t round256(uint64_t b) { return (b + 255u) & ~(uint64_t)255u; }
 // A space's mailbox depth (1..GR_C) fixes its chunk sizes: spaces that cross
 // xGMI use the depth the steady state needs (2).
-// GR_TILE: a chunk's positions are tiled by 64 (pc is a multiple of 64): tile t
-// of the hot region holds the counts and hot fields of positions 64t..64t+63,
-// the same SoA order as an untiled chunk of 64 positions; the cold region alike.
+// GR_TILE: a chunk's positions are tiled by kTileW (pc is a multiple of it): tile
+// t of the hot region holds the counts and hot fields of its kTileW positions, the
+// same SoA order as an untiled chunk of kTileW positions; the cold region alike.
 __host__ __device__ inline uint64_t tile_hot_bytes(uint32_t depth) { return (uint64_t)kTileW * (kHotH + kHotK * depth); }
 __host__ __device__ inline uint64_t tile_cold_bytes(uint32_t depth) { return (uint64_t)kTileW * kColdK * depth; }
 __host__ __device__ inline uint64_t space_hot_chunk_bytes_pc(uint32_t pc, uint32_t depth = GR_C) {
