@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstdio>
@@ -123,7 +124,19 @@ struct gr_engine {
     bool on = false;
     uint32_t nm = 0, nlc = 0, nx = 0, nlx = 0, nl = 0;
   } cpend;
+  // cpend.on, readable without the mutex: between _begin and _end the pending
+  // pass owns the shared scratch (d_mark, d_lop, d_msgs, d_locals, d_ext,
+  // d_lext, d_scal) and the lane rows, so every other entry point that uses
+  // them or steps the engine refuses with GR_ESTATE until _end has run.
+  std::atomic<bool> pending{false};
 };
+
+// GR_ESTATE while a gr_step_compact_begin waits for its _end (gpuraft.h).
+#define GR_REFUSE_PENDING(e)                          \
+  do {                                                \
+    if ((e)->pending.load(std::memory_order_acquire)) \
+      return GR_ESTATE;                               \
+  } while (0)
 
 // A fresh timing record for the next pass (nullptr when timing is off or a
 // HIP call fails: the pass then runs untimed and gr_timing_end reports it).
@@ -224,6 +237,7 @@ int transfer(gr_engine* e, const uint32_t* slots, uint32_t first, size_t n, gr_p
     for (size_t x = 0; x < n; ++x)
       if (slots[x] >= cap) return GR_ERANGE;
   std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
   HIPCHK(hipDeviceSynchronize());  // passes in flight on other streams own the rows
   const hipStream_t s = e->stream;
   const size_t bytes = n * sizeof(gr_peer);
@@ -433,6 +447,7 @@ int gr_compact_log(gr_engine* e, const uint32_t* slots, const uint64_t* index, s
     seen[p >> 6] |= 1ull << (p & 63);
   }
   std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
   HIPCHK(hipDeviceSynchronize());  // passes in flight on other streams own the rows
   const hipStream_t s = e->stream;
   int r;
@@ -481,6 +496,7 @@ int gr_commit_update(gr_engine* e, const uint32_t* slots, const gr_update_commit
     seen[p >> 6] |= 1ull << (p & 63);
   }
   std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
   HIPCHK(hipDeviceSynchronize());  // passes in flight on other streams own the rows
   const hipStream_t s = e->stream;
   int r;
@@ -520,6 +536,7 @@ int gr_notify_applied(gr_engine* e, const uint32_t* slots, const uint64_t* appli
     seen[p >> 6] |= 1ull << (p & 63);
   }
   std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
   HIPCHK(hipDeviceSynchronize());  // passes in flight on other streams own the rows
   const hipStream_t s = e->stream;
   int r;
@@ -555,6 +572,7 @@ int gr_space_cold_used(gr_engine* e, const void* space, uint32_t n_chunks, uint3
                        void* stream, uint32_t* out) {
   if (!e || !space || !out || depth == 0 || depth > GR_C) return GR_EINVAL;
   std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
   int r;
   if ((r = grow_device(&e->d_scal.p, &e->d_scal.n, 16))) return r;
   if ((r = grow_pinned(&e->h_scal, &e->h_scal_bytes, 16))) return r;
@@ -615,6 +633,7 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
   if ((in->n_msgs && !in->msgs) || (in->n_locals && !in->locals)) return GR_EINVAL;
   if (in->n_msgs + in->n_locals >= 0x80000000ull) return GR_EINVAL;
   std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
   out->msgs = nullptr;
   out->n_msgs = 0;
   out->results = nullptr;
@@ -748,6 +767,7 @@ int gr_step_compact_begin(gr_engine* e, const gr_cinbox* in) {
     return GR_EINVAL;
   std::lock_guard<std::mutex> guard(e->mu);
   if (e->cpend.on) return GR_EINVAL;  // the previous begin was not ended
+  GR_REFUSE_PENDING(e);
   PhaseClock clk;  // GR_PHASES=1: per-phase host times on stderr
   const uint32_t S = e->S, cap = e->cfg.max_peers;
   const uint32_t nm = (uint32_t)in->n_msgs, nlc = (uint32_t)in->n_locals;
@@ -755,6 +775,7 @@ int gr_step_compact_begin(gr_engine* e, const gr_cinbox* in) {
   e->cpend = gr_engine::CPending{};
   if (nm + nlc == 0) {
     e->cpend.on = true;  // an empty pass: _end returns an empty outbox
+    e->pending.store(true, std::memory_order_release);
     return GR_OK;
   }
   const hipStream_t s = e->stream;
@@ -800,6 +821,7 @@ int gr_step_compact_begin(gr_engine* e, const gr_cinbox* in) {
   const uint32_t nl = ((uint32_t*)e->h_scal)[0];
   if (((uint32_t*)e->h_scal)[1]) return GR_EINVAL;  // nothing of the pass ran
   e->cpend.on = true;
+  e->pending.store(true, std::memory_order_release);
   e->cpend.nm = nm;
   e->cpend.nlc = nlc;
   e->cpend.nx = nx;
@@ -814,6 +836,7 @@ int gr_step_compact_end(gr_engine* e, gr_coutbox* out) {
   if (!e->cpend.on) return GR_EINVAL;  // no pass was begun
   const gr_engine::CPending pend = e->cpend;
   e->cpend.on = false;
+  e->pending.store(false, std::memory_order_release);
   memset(out, 0, sizeof(*out));
   PhaseClock clk;
   const uint32_t S = e->S, cap = e->cfg.max_peers;
@@ -1104,6 +1127,7 @@ int gr_stats_reset(gr_engine* e) {
 
 int gr_bind_routes(gr_engine* e, const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n_peers) {
   if (!e || !in_pos || !out_pos || n_peers > e->cfg.max_peers) return GR_EINVAL;
+  GR_REFUSE_PENDING(e);
   HIPCHK(hipDeviceSynchronize());
   std::vector<uint32_t> base(2 * GR_SMAX * GR_SMAX, NOPOS);
   uint32_t g = 0, rr = 0;
@@ -1132,6 +1156,7 @@ int gr_set_locals(gr_engine* e, const gr_local_input* locals, size_t n) {
   for (size_t k = 0; k < n; ++k)
     if (locals[k].peer >= cap) return GR_EINVAL;
   std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
   HIPCHK(hipDeviceSynchronize());  // a pass in flight on another stream may read the rows
   const hipStream_t s = e->stream;
   int r;
@@ -1166,6 +1191,7 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
                    uint32_t n_peers, void* stream) {
   if (!e || !in_space || !out_space || n_peers > e->cfg.max_peers || depth == 0 || depth > GR_C)
     return GR_EINVAL;
+  GR_REFUSE_PENDING(e);  // the pending compact pass owns the lane rows and bail lists
   StepParams kp = base_params(e);
   kp.has_locals = e->locals_set ? 1 : 0;
   kp.has_lane_peer = 0;
@@ -1193,6 +1219,7 @@ int gr_collect_results(gr_engine* e, uint32_t first, gr_peer_result* out, size_t
   if (!e || (n && !out) || (uint64_t)first + n > e->cfg.max_peers) return GR_EINVAL;
   if (n == 0) return GR_OK;
   std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
   HIPCHK(hipDeviceSynchronize());
   const size_t bytes = n * sizeof(gr_peer_result);
   int r;

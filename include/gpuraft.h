@@ -399,7 +399,12 @@ int gr_step_compact(gr_engine* e, const gr_cinbox* in, gr_coutbox* out);
  * validates the inbox, copies it to the device and returns once the copy is
  * done (the inbox buffers may then be reused); _end runs the pass and fills
  * `out`. Every _begin is followed by exactly one _end on the same engine
- * (GR_EINVAL otherwise); another thread may call _end. */
+ * (GR_EINVAL otherwise); another thread may call _end. Between the two the
+ * pending pass owns the engine's scratch and lane rows: every other call on
+ * that engine that steps it or uses them (gr_step, gr_step_compact{,_begin},
+ * gr_step_device, gr_load_* / gr_sync_*, gr_set_locals, gr_bind_routes,
+ * gr_compact_log, gr_commit_update, gr_notify_applied, gr_collect_results,
+ * gr_space_cold_used) returns GR_ESTATE and changes nothing. */
 int gr_step_compact_begin(gr_engine* e, const gr_cinbox* in);
 int gr_step_compact_end(gr_engine* e, gr_coutbox* out);
 /* Engine-owned pinned buffers for the next gr_step_compact inbox (as gr_inbox_reserve). */

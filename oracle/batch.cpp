@@ -142,7 +142,14 @@ struct WorkerPool {
   void run(uint32_t n, const std::function<void(uint32_t)>& f) {
     if (th.size() != n) {
       stop();
-      for (uint32_t t = 0; t < n; ++t) th.emplace_back([this, t]() { loop(t); });
+      // a new worker starts having seen the current generation, so it waits for
+      // this run's job and never picks up a previous (finished) one
+      uint64_t g0;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        g0 = gen;
+      }
+      for (uint32_t t = 0; t < n; ++t) th.emplace_back([this, t, g0]() { loop(t, g0); });
     }
     std::unique_lock<std::mutex> g(mu);
     job = f;
@@ -150,9 +157,9 @@ struct WorkerPool {
     gen++;
     go.notify_all();
     done.wait(g, [this]() { return pending == 0; });
+    job = nullptr;  // f's captures belong to the caller's frame
   }
-  void loop(uint32_t t) {
-    uint64_t seen = 0;
+  void loop(uint32_t t, uint64_t seen) {
     for (;;) {
       std::function<void(uint32_t)> f;
       {
@@ -615,9 +622,8 @@ int ob_export(ob_pop* p, gr_peer* out, uint32_t n) {
 // Persist and apply everything after a pass (node.go processRaftUpdate /
 // Peer.Commit): entriesToSave -> LogDB, StableLogTo, AppliedTo = committed,
 // NotifyRaftLastApplied(committed). Keeps in-memory logs bounded in long runs.
-int ob_commit_all(ob_pop* p) {
-  if (!p) return GR_EINVAL;
-  for (auto& op : p->peers) {
+static void commit_peer(OPeer& op) {
+  {
     raft& r = *op.r;
     auto es = r.log->entriesToSave();
     if (!es.empty()) {
@@ -634,7 +640,49 @@ int ob_commit_all(ob_pop* p) {
     }
     r.applied = r.log->committed;
   }
+}
+
+int ob_commit_all(ob_pop* p) {
+  if (!p) return GR_EINVAL;
+  for (auto& op : p->peers) commit_peer(op);
   return GR_OK;
+}
+
+// ob_commit_all on the step's partition (peer p on worker p % T, as ob_step2
+// with n_threads = T): each worker frees and reallocates the log memory of its
+// own peers, so its allocations stay in its own malloc arena instead of
+// bouncing through the arena of the thread that first built them.
+int ob_commit_all_mt(ob_pop* p, uint32_t n_threads) {
+  if (!p) return GR_EINVAL;
+  if (n_threads <= 1) return ob_commit_all(p);
+  const uint32_t n = (uint32_t)p->peers.size();
+  p->pool.run(n_threads, [&](uint32_t t) {
+    for (uint32_t pi = t; pi < n; pi += n_threads) commit_peer(p->peers[pi]);
+  });
+  return GR_OK;
+}
+
+// Rebuild every peer from its own record on the worker that will step it
+// (partition p % T): the CPU baseline's per-thread heaps start out local too.
+int ob_rehome(ob_pop* p, uint32_t n_threads) {
+  if (!p) return GR_EINVAL;
+  if (n_threads <= 1) return GR_OK;
+  const uint32_t n = (uint32_t)p->peers.size();
+  std::vector<gr_peer> recs(n);
+  for (uint32_t k = 0; k < n; ++k) export_peer(p->peers[k], p->S, &recs[k]);
+  std::atomic<int> bad{0};
+  p->pool.run(n_threads, [&](uint32_t t) {
+    for (uint32_t pi = t; pi < n; pi += n_threads) {
+      try {
+        OPeer fresh;
+        build_peer(recs[pi], p->S, p->maxEntrySize, &fresh);
+        p->peers[pi] = std::move(fresh);
+      } catch (const std::exception&) {
+        bad = 1;
+      }
+    }
+  });
+  return bad ? GR_ESTATE : GR_OK;
 }
 
 // One pass over the population. For peer p, items are numbered as the engine

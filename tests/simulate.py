@@ -117,6 +117,14 @@ class GpuCompactHalvesBackend(GpuCompactBackend):
     halves = True
 
 
+def res_esc_free(res, n):
+    """Peers that did not escalate this pass (their device state is the pass's)."""
+    ok = np.ones(n, bool)
+    esc = res[res["escalation"] != 0]
+    ok[esc["peer"].astype(np.int64)] = False
+    return ok
+
+
 def _threads():
     return min(16, os.cpu_count() or 1)
 
@@ -143,7 +151,7 @@ class Lockstep:
         self.parked = np.zeros(self.n, bool)
         self.k = 0
         self.stats = {"msgs": 0, "escalations": 0, "esc_reasons": {}, "commits": 0, "ready": 0, "forwarded": 0,
-                      "parked": 0}
+                      "parked": 0, "snapshot_left": 0}
         self.last_out = np.zeros(0, abi.MESSAGE)  # the engine's outbox of the last pass (device prefix)
         self.last_ready = {}                      # peer -> [(index, ctx_low, ctx_high)] of the last pass
 
@@ -205,6 +213,11 @@ class Lockstep:
                     f"pass {self.k}: state {bad_s[:mr]} msgs {bad_m[:mr]} results {bad_r[:mr]}"
                     f" unjustified escalations {bad_e[:mr]}")
             st["commits"] += int(np.sum(dev["committed"] > before))
+            # remotes a leader moved out of the Snapshot state this pass on the
+            # device (respondedTo -> becomeRetry, remote.go:130-138)
+            lead = (dev0["state"] == abi.LEADER) & (dev["state"] == abi.LEADER) & (res_esc_free(res, self.n))
+            rs0, rs1 = dev0["remotes"]["state"], dev["remotes"]["state"]
+            st["snapshot_left"] += int(np.sum(lead[:, None] & (rs0 == abi.SNAPSHOT_ST) & (rs1 != abi.SNAPSHOT_ST)))
         self.last_out = out
         # ReadyToRead of the whole pass (device prefix + host suffix): the oracle's
         self.last_ready = {}

@@ -180,10 +180,34 @@ def test_compact_halves(gpu):
     cm, xm = eng.pack_messages(np.zeros(0, abi.MESSAGE))
     cl, xl = eng.pack_locals(P.propose_locals(64 * 3, np.arange(64), pass_index=0))
     ib = abi.cinbox_of(cm, xm, cl, xl)
+    before = eng.sync_peers(np.arange(4))
     assert eng.lib.gr_step_compact_begin(eng._h, ctypes.byref(ib)) == 0
     assert eng.lib.gr_step_compact_begin(eng._h, ctypes.byref(ib)) == -1
+    # between _begin and _end the pending pass owns the scratch and lane rows:
+    # every entry point that would use them refuses (GR_ESTATE), nothing written
+    ESTATE = -6
+    sl = np.arange(4, dtype=np.uint32)
+    pe = P.make_groups(64, 3, seed=2)[:4]
+    assert eng.lib.gr_load_peers(eng._h, sl.ctypes.data, pe.ctypes.data, 4) == ESTATE
+    assert eng.lib.gr_load_groups(eng._h, 0, pe.ctypes.data, 4) == ESTATE
+    assert eng.lib.gr_sync_peers_to_host(eng._h, sl.ctypes.data, pe.ctypes.data, 4) == ESTATE
+    ap = np.zeros(4, np.uint64)
+    assert eng.lib.gr_notify_applied(eng._h, sl.ctypes.data, ap.ctypes.data, 4) == ESTATE
+    assert eng.lib.gr_compact_log(eng._h, sl.ctypes.data, ap.ctypes.data, 4, None) == ESTATE
+    loc = P.propose_locals(64 * 3, np.arange(64), pass_index=1)
+    assert eng.lib.gr_set_locals(eng._h, loc.ctypes.data, len(loc)) == ESTATE
+    sib = abi.inbox_of(np.zeros(0, abi.MESSAGE), loc)
+    sob = abi.Outbox()
+    assert eng.lib.gr_step(eng._h, ctypes.byref(sib), ctypes.byref(sob)) == ESTATE
+    res = np.zeros(4, abi.RESULT)
+    assert eng.lib.gr_collect_results(eng._h, 0, res.ctypes.data, 4) == ESTATE
     assert eng.lib.gr_step_compact_end(eng._h, ctypes.byref(ob)) == 0
     assert ob.n_results == 64 * 3 or ob.n_results == 64  # a result per lane with input
     assert eng.lib.gr_release_coutbox(eng._h, ctypes.byref(ob)) == 0
+    # the refused load wrote nothing (slots 0..3 are as the pass left them, which
+    # differs from `pe`), and after _end the engine takes calls again
+    after = eng.sync_peers(np.arange(4))
+    assert after.tobytes() != pe.tobytes() and after["node_id"].tobytes() == before["node_id"].tobytes()
+    eng.load_peers(np.arange(4), after)
     eng.close()
 

@@ -340,7 +340,7 @@ def test_leader_read_index_committed_at_term(be, known, request):
 #      proposals one per send, committed/lastIndex traced per node after every send
 @pytest.mark.parametrize("be", BACKENDS)
 def test_config1_trace(be, request):
-    n_props = 1000 if be == "cpu" else 300
+    n_props = 1000  # BASELINE config 1 / SURVEY.md §8d: 1,000 16-B proposals on every backend
     net = Net(_backend(be, request), [1, 2, 3], copies=1, payload=16)
     _election(net, 1)
     assert _committed(net, 1) == 1

@@ -7,7 +7,7 @@ OUT=gpurun_out
 mkdir -p $OUT
 timeout -k 10 240 python -c "import torch; print('cuda', torch.cuda.is_available(), torch.cuda.get_device_name(0))" > $OUT/warm.log 2>&1 || exit $?
 echo "warm ok"
-timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > $OUT/gpu_tests.log 2>&1
+timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread --durations=25 ${PYTEST_ARGS:-} > $OUT/gpu_tests.log 2>&1
 rc=$?
 tail -15 $OUT/gpu_tests.log
 [ $rc -le 1 ] || exit $rc
