@@ -118,12 +118,13 @@ def _oracle_rate(peers, topo, R, locals_fn, threads, seconds, inject=None, drop=
     from oracle.pyoracle import OraclePopulation
     pop = OraclePopulation(peers, R)
     pop.set_truncate_runs()  # long churn runs build >2-run Replicates; the records carry a prefix
+    pop.rehome(threads)  # each worker's peers live in its own heap arena (batch.cpp ob_rehome)
     G = topo.G
     msgs = np.zeros(0, abi.MESSAGE)
     for k in range(2):  # to steady state
         o = pop.step(msgs, locals_fn(k, pop), threads=threads)
         msgs = topo.route_messages(o["msgs"])
-        pop.commit_all()
+        pop.commit_all(threads)
     passes, t_step, commits = 0, 0.0, 0
     t_end = time.time() + seconds
     k = 2
@@ -140,7 +141,7 @@ def _oracle_rate(peers, topo, R, locals_fn, threads, seconds, inject=None, drop=
         msgs = topo.route_messages(o["msgs"])
         if drop is not None:
             msgs = drop(k, msgs)
-        pop.commit_all()
+        pop.commit_all(threads)
         passes += 1
         k += 1
     return commits / t_step, G * passes / t_step, passes

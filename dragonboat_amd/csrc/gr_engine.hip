@@ -73,7 +73,7 @@ struct gr_engine {
   uint32_t stats_rows = 0;
   uint32_t* bail = nullptr;      // kBailLists lists of cap lanes each
   uint32_t* counters = nullptr;  // [2 (pass parity)][kBailLists][kCounterStride]
-  uint8_t* hints = nullptr;      // 2 x [cap / 64 + 1] wave hints of the device-resident path (gr_layout.h WH_*):
+  uint8_t* hints = nullptr;      // 2 x [hint_stride(cap)] wave hints of the device-resident path (gr_layout.h WH_*):
                                  // one set read by a pass, the other written for the next
   uint64_t hint_flip = 0;
   uint64_t launches = 0;         // never reset: selects the live counter set
@@ -367,7 +367,7 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
       hipMalloc((void**)&e->bail, (size_t)kBailLists * e->cap * 4) != hipSuccess ||
       hipMalloc((void**)&e->counters, 2 * kBailLists * kCounterStride * 4) != hipSuccess ||
       hipMalloc((void**)&e->route_base, 2 * GR_SMAX * GR_SMAX * 4) != hipSuccess ||
-      hipMalloc((void**)&e->hints, 2 * (e->cap / 64 + 1)) != hipSuccess) {
+      hipMalloc((void**)&e->hints, 2 * hint_stride(e->cap)) != hipSuccess) {
     if (ds) (void)hipFree(ds);
     if (dl) (void)hipFree(dl);
     e->st.base = nullptr;
@@ -380,7 +380,7 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
   if (hipMemset(ds, 0, sb) != hipSuccess || hipMemset(dl, 0, lb) != hipSuccess ||
       hipMemset(e->stats, 0, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
       hipMemset(e->counters, 0, 2 * kBailLists * kCounterStride * 4) != hipSuccess ||
-      hipMemset(e->hints, 0, 2 * (e->cap / 64 + 1)) != hipSuccess ||
+      hipMemset(e->hints, 0, 2 * hint_stride(e->cap)) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     gr_destroy(e);
     return GR_EDEVICE;
@@ -1199,11 +1199,12 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
   kp.route_g = e->route_g;
   kp.route_r = e->route_r;
   kp.route_base = e->route_base;
+  kp.route_wu = (kp.route_mode == RT_LOOPBACK || kp.route_mode == RT_AFFINE) && e->route_g % 64 == 0 ? 1 : 0;
   kp.in = make_view(in_space, in_chunks, in_positions, depth);
   kp.out = make_view(out_space, out_chunks, out_positions, depth);
   kp.n_lanes = n_peers;
   // lane = peer here, so a wave's hint carries over between passes
-  const size_t hs = e->cap / 64 + 1, hf = e->hint_flip++ & 1;
+  const size_t hs = hint_stride(e->cap), hf = e->hint_flip++ & 1;
   kp.hints = e->hints + hf * hs;
   kp.hints_out = e->hints + (1 - hf) * hs;
   // the follower instance of its own pays off only when the pass is large (a

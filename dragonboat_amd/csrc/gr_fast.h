@@ -36,9 +36,14 @@ namespace gr {
 // registers) and hand such a lane to the general lane.
 constexpr int FL_ANY = 0, FL_LEADER = 1, FL_FOLLOWER = 2;
 
-template <int S, int R = FL_ANY>
+template <int S, int R = FL_ANY, int RM = RM_ANY>
 struct FastLane {
   using Rw = Rows<S>;
+  // RM: the route mode this instance is built for (gr_layout.h routes_of);
+  // RT_LOOPBACK spaces have one chunk, so a mailbox address is plain arithmetic
+  static constexpr bool kOneChunk = RM == RT_LOOPBACK;
+  GF_HD Mailbox min_at(uint32_t g) const { return kp.in.template at<kOneChunk>(g); }
+  GF_HD Mailbox mout_at(uint32_t g) const { return kp.out.template at<kOneChunk>(g); }
   static constexpr int MK = 2;  // messages per mailbox handled here
   // Leaders with input run here for up to 3 slots; wider groups' leaders take
   // the general lane (keeps this kernel's code and registers small for S = 5)
@@ -131,7 +136,7 @@ struct FastLane {
     uint32_t cd;
     GF_BAIL(!commit_delta(committed, log_index, &cd) || log_term != term || (n && rt0 != term));  // n <= 1 here
     if (!ok) return;
-    const Mailbox mb = kp.out.at(gout[j]);
+    const Mailbox mb = mout_at(gout[j]);
     const uint32_t c = outc[j];
     n1out |= (n ? 1u : 0u) << (4 * j + c);  // MB_N1 bits: finish_out
     ntst(mb.u64(c, MF_LOG_INDEX), (uint64_t)(log_index));
@@ -144,7 +149,7 @@ struct FastLane {
     GF_BAIL(gpos == NOPOS || *cnt >= kp.out.depth || *cnt >= kUniformMax);
     GF_BAIL(wide_term(term, 0, 0, 0));
     if (!ok) return;
-    const Mailbox mb = kp.out.at(gpos);
+    const Mailbox mb = mout_at(gpos);
     const uint32_t c = *cnt;
     rejout |= (reject ? 1u : 0u) << c;  // tags and terms: finish_out
     ntst(mb.u64(c, MF_LOG_INDEX), (uint64_t)(log_index));
@@ -161,7 +166,7 @@ struct FastLane {
     const uint32_t c = outc[j];
     uint32_t cb = c;
     if (c) {
-      const Mailbox mb = kp.out.at(gout[j]);
+      const Mailbox mb = mout_at(gout[j]);
       if (lead || !rejout) {
         cb |= MB_UNIFORM | (lead ? 0u : (uint32_t)MB_RESP) | (lead ? ((n1out >> (4 * j)) & 7u) << MB_N1_SHIFT : 0u);
         ntst(mb.mterm(), (uint32_t)term);
@@ -175,7 +180,7 @@ struct FastLane {
         }
       }
     }
-    ntst(kp.out.at(gout[j]).cnt(), (uint8_t)cb);
+    ntst(mout_at(gout[j]).cnt(), (uint8_t)cb);
   }
 
   // ------------------------------------------------------------- leader
@@ -323,8 +328,11 @@ struct FastLane {
     const bool hruns = kRuns && (hint & WH_RUNS);  // the wave's run bits were set: skip the run rows
     const uint32_t hself = (hint >> WH_SLOT_SHIFT) & 7u;  // leader hints: the self slot
     const bool hsync = kSync && hl && (hint & WH_SYNC);   // ... whose remote rows were in sync
+    // ---- routes first: pure arithmetic, so no address of round 1 waits on a load
+    uint32_t gin[S];
+    routes_of<S, RM>(kp, i, gin, gout);
     // ---- round 1: core (one header word), the newest run (a fixed row), locals,
-    //      routes, mailbox counts, and the hinted role's loads
+    //      mailbox counts, and the hinted role's loads
     hdr = ntld(s64(SR_HDR));
     term = ntld(s64(SR_TERM));
     committed = ntld(s64(SR_COMMITTED));
@@ -334,8 +342,6 @@ struct FastLane {
       rtn0 = ntld(s64(SR_RUN_TERM + GR_K - 1));
     }
     const uint32_t lw = kp.has_locals ? ntld(kp.ln.u32(LR_LWORD)[i]) : 0u;  // packed locals (gr_layout.h)
-    uint32_t gin[S];
-    routes_of<S>(kp, i, gin, gout);
 #pragma unroll
     for (int j = 0; j < S; ++j) outc[j] = 0;
     // Mailboxes: the lean lane reads uniform ones only (MB_UNIFORM: every tag and
@@ -344,7 +350,7 @@ struct FastLane {
     uint32_t nonu = 0;  // in mailboxes holding messages without MB_UNIFORM
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      const uint32_t b = gin[j] != NOPOS ? (uint32_t)ntld(kp.in.at(gin[j]).cnt()) : 0u;
+      const uint32_t b = gin[j] != NOPOS ? (uint32_t)ntld(min_at(gin[j]).cnt()) : 0u;
       cnt[j] = b & MB_COUNT;
       cbs[j] = b;
       nonu |= ((b & MB_COUNT) && !(b & MB_UNIFORM)) ? (1u << j) : 0u;
@@ -363,9 +369,9 @@ struct FastLane {
           next[j] = ntld(s64(Rw::NEXT + j));
           have_n |= 1u << j;
         }
-        lmt[j] = gin[j] != NOPOS ? ntld(kp.in.at(gin[j]).mterm()) : 0u;
+        lmt[j] = gin[j] != NOPOS ? ntld(min_at(gin[j]).mterm()) : 0u;
 #pragma unroll
-        for (int k = 0; k < MK; ++k) lidx[j][k] = gin[j] != NOPOS ? ntld(kp.in.at(gin[j]).u64(k, MF_LOG_INDEX)) : 0;
+        for (int k = 0; k < MK; ++k) lidx[j][k] = gin[j] != NOPOS ? ntld(min_at(gin[j]).u64(k, MF_LOG_INDEX)) : 0;
       }
     }
     // follower: the term word, LogIndexes and Commit offsets of the one slot L that sent
@@ -382,7 +388,7 @@ struct FastLane {
 #pragma unroll
       for (int j = 0; j < S; ++j) ghL = ((uint32_t)j == hL) ? gin[j] : ghL;
       if (ghL != NOPOS) {
-        const Mailbox mb = kp.in.at(ghL);
+        const Mailbox mb = min_at(ghL);
         fmt = ntld(mb.mterm());
 #pragma unroll
         for (int k = 0; k < MK; ++k) {
@@ -435,10 +441,10 @@ struct FastLane {
       if (!hl) {
 #pragma unroll
         for (int j = 0; j < S; ++j) {
-          lmt[j] = cnt[j] ? ntld(kp.in.at(gin[j]).mterm()) : 0u;
+          lmt[j] = cnt[j] ? ntld(min_at(gin[j]).mterm()) : 0u;
 #pragma unroll
           for (int k = 0; k < MK; ++k)
-            lidx[j][k] = (uint32_t)k < cnt[j] ? ntld(kp.in.at(gin[j]).u64(k, MF_LOG_INDEX)) : 0;
+            lidx[j][k] = (uint32_t)k < cnt[j] ? ntld(min_at(gin[j]).u64(k, MF_LOG_INDEX)) : 0;
         }
       }
     }
@@ -458,11 +464,11 @@ struct FastLane {
       }
       const uint32_t cc = c < (uint32_t)MK ? c : (uint32_t)MK;
       const bool spec = hf && L == hL;  // the hinted mailbox is the one that sent
-      if (c && !spec) fmt = ntld(kp.in.at(gl).mterm());
+      if (c && !spec) fmt = ntld(min_at(gl).mterm());
 #pragma unroll
       for (int k = 0; k < MK; ++k) {
         if ((uint32_t)k < cc && !spec) {
-          const Mailbox mb = kp.in.at(gl);
+          const Mailbox mb = min_at(gl);
           fidx[k] = ntld(mb.u64(k, MF_LOG_INDEX));
           fcd[k] = ntld(mb.t32(k, MT_CDELTA));
         }
@@ -488,7 +494,7 @@ struct FastLane {
       if (flags & F_ETZ) ntst(s64(SR_HDR), hdr & ~((uint64_t)F_ETZ << H_FLAGS_SHIFT));
 #pragma unroll
       for (int j = 0; j < S; ++j)
-        if (gout[j] != NOPOS) ntst(kp.out.at(gout[j]).cnt(), (uint8_t)(0));
+        if (gout[j] != NOPOS) ntst(mout_at(gout[j]).cnt(), (uint8_t)(0));
       ntst(kp.ln.u8(LR_RFLAGS)[i], (uint8_t)(0));
       GR_COVER(FAST_QUIESCED);
       return true;  // *ls stays zero
@@ -689,11 +695,11 @@ struct FastLane {
 // Kernel-side entry: the lean lane for lane i; false = hand the lane to the general kernel.
 // *state = the role the lane entered the pass with; *hint_out = its role hint (WH_*).
 // take (FastLane::step): a lane whose role is not `take` is left alone, *skipped = true.
-template <int S, int R = FL_ANY>
+template <int S, int R = FL_ANY, int RM = RM_ANY>
 GF_HD bool fast_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, uint32_t* state = nullptr,
                      uint32_t hint = 0, uint32_t* hint_out = nullptr, int take = FL_ANY,
                      bool* skipped = nullptr) {
-  FastLane<S, R> L(kp, i, p);
+  FastLane<S, R, RM> L(kp, i, p);
   const bool done = L.step(ls, hint, take);
   if (state) *state = L.state;
   if (hint_out) *hint_out = L.role_hint();

@@ -89,13 +89,23 @@ __device__ inline void bail_append(bool mine, uint32_t list, uint32_t* bail_list
 // Measured and dropped: the two instances concurrently on two streams (0.133 vs
 // 0.124 ms per 1M x 3 pass), and a third instance for unhinted waves (~8 us for a
 // mostly empty launch).
-template <int S, int R>
+// A wave-uniform 32-bit load through the scalar cache (constant address
+// space: s_load_dword). Only for data no wave of the running kernel writes.
+__device__ inline uint32_t sload_u32(const uint8_t* p) {
+  typedef const __attribute__((address_space(4))) uint32_t cu32;
+  return *(cu32*)(uintptr_t)p;
+}
+
+template <int S, int R, int RM>
 __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
                                                                              uint32_t* counters, uint32_t list_cap) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  // the wave's hint: one byte, the same address for every lane (a scalar load)
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
-  const uint32_t hint = kp.hints ? (uint32_t)kp.hints[wave] : 0u;
+  // the workgroup's four wave hints in one scalar load (the set the previous
+  // pass wrote; this pass writes the other one), so no lane waits on a vector
+  // load before its first round
+  const uint32_t hw = kp.hints ? sload_u32(kp.hints + (uint64_t)blockIdx.x * (kBlock / 64)) : 0u;
+  const uint32_t hint = (hw >> (8 * (wave & 3))) & 0xFFu;
   const int wk = wave_kernel(hint, S);  // FL_ANY: unhinted
   bool mine = true;
   if (R != FL_ANY) {  // a split pass (the launcher runs these only then)
@@ -103,7 +113,7 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
     bool any = false;
 #pragma unroll
     for (uint32_t w = 0; w < kBlock / 64; ++w) {
-      const int k = w0 + w < nw ? wave_kernel(kp.hints[w0 + w], S) : R == FL_LEADER ? FL_FOLLOWER : FL_LEADER;
+      const int k = w0 + w < nw ? wave_kernel((hw >> (8 * w)) & 0xFFu, S) : R == FL_LEADER ? FL_FOLLOWER : FL_LEADER;
       any = any || k == R || k == FL_ANY;
     }
     if (!any) return;  // block-uniform
@@ -117,10 +127,10 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     // leaves ls zero when it bails
     if (R != FL_ANY)
-      bail = !fast_step<S, R>(kp, i, p, &ls, &role, hint, &myhint, wk == FL_ANY ? R : FL_ANY, &skip);
-    else if (wk == FL_FOLLOWER) bail = !fast_step<S, FL_FOLLOWER>(kp, i, p, &ls, &role, hint, &myhint);
-    else if (wk == FL_LEADER) bail = !fast_step<S, FL_LEADER>(kp, i, p, &ls, &role, hint, &myhint);
-    else bail = !fast_step<S, FL_ANY>(kp, i, p, &ls, &role, hint, &myhint);
+      bail = !fast_step<S, R, RM>(kp, i, p, &ls, &role, hint, &myhint, wk == FL_ANY ? R : FL_ANY, &skip);
+    else if (wk == FL_FOLLOWER) bail = !fast_step<S, FL_FOLLOWER, RM>(kp, i, p, &ls, &role, hint, &myhint);
+    else if (wk == FL_LEADER) bail = !fast_step<S, FL_LEADER, RM>(kp, i, p, &ls, &role, hint, &myhint);
+    else bail = !fast_step<S, FL_ANY, RM>(kp, i, p, &ls, &role, hint, &myhint);
     bail = bail && !skip;  // a skipped lane is the other instance's
     if (!bail && !skip) GR_CHECK_STATE(kp.st, p);
   }
@@ -260,6 +270,23 @@ struct PassTiming {
 // The tick kernel's grid: its lanes are at most the active share of a pass.
 constexpr uint32_t kTickBlocks = 1024;
 
+template <int S, int RM>
+hipError_t launch_fast(const StepParams& kp, uint32_t blocks, uint32_t* bail_list, uint32_t* cur, uint32_t list_cap,
+                       hipStream_t s) {
+  if (kp.hints && kp.split) {  // the two role instances (a large pass)
+    hipLaunchKernelGGL((gr_fast_kernel<S, FL_FOLLOWER, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
+                       list_cap);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL((gr_fast_kernel<S, FL_LEADER, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
+                       list_cap);
+  } else {
+    hipLaunchKernelGGL((gr_fast_kernel<S, FL_ANY, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
+                       list_cap);
+  }
+  return hipGetLastError();
+}
+
 template <int S>
 hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters, uint32_t list_cap,
                          uint32_t parity, hipStream_t s, const PassTiming* t, bool tick_lanes) {
@@ -269,16 +296,13 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   uint32_t* nxt = counters + ((parity + 1) & 1) * kBailLists * kCounterStride;
   hipError_t err;
   if (t && (err = hipEventRecord(t->ev[0], s)) != hipSuccess) return err;
-  if (kp.hints && kp.split) {  // the two role instances (a large pass)
-    hipLaunchKernelGGL((gr_fast_kernel<S, FL_FOLLOWER>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
-                       list_cap);
-    if ((err = hipGetLastError()) != hipSuccess) return err;
-    hipLaunchKernelGGL((gr_fast_kernel<S, FL_LEADER>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
-                       list_cap);
-  } else {
-    hipLaunchKernelGGL((gr_fast_kernel<S, FL_ANY>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
-  }
-  if ((err = hipGetLastError()) != hipSuccess) return err;
+  // the lean instances built for the bound route mode (no route branches); a
+  // loopback instance also assumes one-chunk spaces
+  const bool loop1 = kp.route_mode == RT_LOOPBACK && kp.in.n_chunks == 1 && kp.out.n_chunks == 1;
+  if (loop1) err = launch_fast<S, RT_LOOPBACK>(kp, blocks, bail_list, cur, list_cap, s);
+  else if (kp.route_mode == RT_AFFINE) err = launch_fast<S, RT_AFFINE>(kp, blocks, bail_list, cur, list_cap, s);
+  else err = launch_fast<S, RM_ANY>(kp, blocks, bail_list, cur, list_cap, s);
+  if (err != hipSuccess) return err;
   if (t && (err = hipEventRecord(t->ev[1], s)) != hipSuccess) return err;
   if (tick_lanes) {  // some lane may carry ticks or a ReadIndex (LW_OTHER)
     const uint32_t tblocks = blocks < kTickBlocks ? blocks : kTickBlocks;

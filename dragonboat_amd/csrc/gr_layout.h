@@ -422,8 +422,11 @@ struct SpaceView {
   uint64_t hot_bytes;   // per chunk; the hot region is n_chunks * hot_bytes at base
   uint64_t cold_bytes;  // per chunk; the cold region follows the hot region
   uint32_t depth;  // messages per mailbox (1..GR_C); emitting more escalates CAPACITY
+  // ONE: the space is known to have one chunk (loopback spaces; the lean
+  // kernel's RT_LOOPBACK instance): no chunk division or branch.
+  template <bool ONE = false>
   __host__ __device__ inline Mailbox at(uint32_t gpos) const {
-    const uint32_t c = n_chunks == 1 ? 0u : gpos / pc;  // one chunk (loopback spaces): no division
+    const uint32_t c = (ONE || n_chunks == 1) ? 0u : gpos / pc;  // one chunk (loopback spaces): no division
     Mailbox m;
     m.hot = base + (uint64_t)c * hot_bytes;
     m.cold = base + (uint64_t)n_chunks * hot_bytes + (uint64_t)c * cold_bytes;
@@ -477,6 +480,9 @@ constexpr uint8_t RT_IDENTITY = 0, RT_TABLE = 1, RT_AFFINE = 2, RT_LOOPBACK = 3;
 // (H_NX for every member slot and H_MS), so no NEXT row or own MATCH row is loaded.
 // WH_RUNS: every lane's run bits were set, so no lane loads the newest run's rows.
 constexpr uint32_t WH_ROLE = 3, WH_LEADER = 1, WH_FOLLOWER = 2, WH_SLOT_SHIFT = 2, WH_SYNC = 0x20, WH_RUNS = 0x40;
+// Bytes per hint set: a byte per wave, padded so each set starts 16-byte
+// aligned and a workgroup's four hints load as one scalar dword (gr_kernels.h).
+__host__ __device__ inline uint64_t hint_stride(uint32_t cap) { return ((uint64_t)cap / 64 + 16) & ~(uint64_t)15; }
 // The lean kernel (FL_* of gr_fast.h) that steps a wave with hint h.
 __host__ __device__ inline int wave_kernel(uint32_t h, int S) {
   if ((h & WH_ROLE) == WH_LEADER && S <= 3) return 1;  // FL_LEADER
@@ -502,17 +508,35 @@ struct StepParams {
   uint8_t has_lane_peer;
   uint8_t route_mode;
   uint8_t split;       // follower-hinted waves go to the FL_FOLLOWER instance (gr_kernels.h)
+  uint8_t route_wu;    // route_g % 64 == 0: replica_of is wave-uniform
 };
 
+// Route mode as a compile-time parameter of the lean kernel instances
+// (gr_kernels.h): RM_ANY reads StepParams::route_mode at run time; an instance
+// built for RT_LOOPBACK or RT_AFFINE has no route branches, so every address of
+// the lane's first load round is known before any load is issued (with the run
+// time switch the compiler kept the route arithmetic behind a wait for the
+// state loads: two dependent memory rounds instead of one).
+constexpr int RM_ANY = -1;
+// The replica block of lane i (RT_LOOPBACK / RT_AFFINE: lane i = r * route_g + g).
+// StepParams::route_wu (route_g a multiple of 64): a wave's lanes share r, so it
+// is one scalar division per wave instead of a vector division per lane.
+__host__ __device__ inline uint32_t replica_of(const StepParams& kp, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (kp.route_wu) return __builtin_amdgcn_readfirstlane(i) / kp.route_g;
+#endif
+  return i / kp.route_g;
+}
 // Every route of lane i at once (in[j], out[j] for j < S): the lane's replica
 // block and group are divided out once, not once per slot and direction.
-template <int S>
+template <int S, int RM = RM_ANY>
 __host__ __device__ inline void routes_of(const StepParams& kp, uint32_t i, uint32_t* in, uint32_t* out) {
-  if (kp.route_mode == RT_LOOPBACK || kp.route_mode == RT_AFFINE) {
-    const uint32_t r = i / kp.route_g, g = i - r * kp.route_g;
+  const uint32_t mode = RM == RM_ANY ? (uint32_t)kp.route_mode : (uint32_t)RM;
+  if (mode == RT_LOOPBACK || mode == RT_AFFINE) {
+    const uint32_t r = replica_of(kp, i), g = i - r * kp.route_g;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      if (kp.route_mode == RT_LOOPBACK) {
+      if (mode == RT_LOOPBACK) {
         const bool none = (uint32_t)j == r || (uint32_t)j >= kp.route_r;
         const uint32_t n = kp.route_r * kp.route_g;
         in[j] = none ? NOPOS : j * n + i;
@@ -528,8 +552,8 @@ __host__ __device__ inline void routes_of(const StepParams& kp, uint32_t i, uint
   }
 #pragma unroll
   for (int j = 0; j < S; ++j) {
-    in[j] = kp.route_mode == RT_TABLE ? kp.ln.in_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
-    out[j] = kp.route_mode == RT_TABLE ? kp.ln.out_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
+    in[j] = mode == RT_TABLE ? kp.ln.in_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
+    out[j] = mode == RT_TABLE ? kp.ln.out_pos()[(uint64_t)j * kp.ln.lcap + i] : j * kp.n_lanes + i;
   }
 }
 __host__ __device__ inline uint32_t route_of(const StepParams& kp, uint32_t dir, uint32_t j, uint32_t i) {

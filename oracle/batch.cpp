@@ -12,6 +12,10 @@
 // Peer.Handle (peer.go:199-209), then Peer.ReadIndex, Peer.Tick x n,
 // Peer.QuiescedTick x n, Peer.ProposeEntries.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -674,9 +678,7 @@ int ob_rehome(ob_pop* p, uint32_t n_threads) {
   p->pool.run(n_threads, [&](uint32_t t) {
     for (uint32_t pi = t; pi < n; pi += n_threads) {
       try {
-        OPeer fresh;
-        build_peer(recs[pi], p->S, p->maxEntrySize, &fresh);
-        p->peers[pi] = std::move(fresh);
+        build_peer(recs[pi], p->S, p->maxEntrySize, &p->peers[pi]);  // frees the old objects here
       } catch (const std::exception&) {
         bad = 1;
       }
@@ -737,7 +739,13 @@ int ob_step2(ob_pop* p, const gr_inbox* in, const uint32_t* limits, const gr_pee
   };
   std::vector<PerThread> outv(n_threads);
   std::vector<std::string> errs(n_threads);
+  static const bool kTime = getenv("GR_OB_TIMING") != nullptr;  // TEMP
+  std::vector<double> tw(n_threads, 0);
+  auto t_all0 = std::chrono::steady_clock::now();
   auto work = [&](uint32_t t) {
+    auto tw0 = std::chrono::steady_clock::now();
+    struct TW { std::vector<double>& v; uint32_t t; std::chrono::steady_clock::time_point a;
+      ~TW() { v[t] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count(); } } twg{tw, t, tw0};
     ItemProbe probe;
     g_probe = &probe;
     for (uint32_t pi = t; pi < n; pi += n_threads) {
@@ -938,8 +946,16 @@ int ob_step2(ob_pop* p, const gr_inbox* in, const uint32_t* limits, const gr_pee
     }
     g_probe = nullptr;
   };
+  auto t_w0 = std::chrono::steady_clock::now();
   if (n_threads == 1) work(0);
   else p->pool.run(n_threads, work);
+  if (kTime) {
+    auto t_w1 = std::chrono::steady_clock::now();
+    fprintf(stderr, "ob_step2: pre %.2f ms, run %.2f ms, threads:", std::chrono::duration<double, std::milli>(t_w0 - t_all0).count(),
+            std::chrono::duration<double, std::milli>(t_w1 - t_w0).count());
+    for (double x : tw) fprintf(stderr, " %.1f", x);
+    fprintf(stderr, "\n");
+  }
   size_t k = 0;
   bool bad = false;
   if (!out) {  // kept for ob_fetch_out (the caller sizes its buffers exactly)

@@ -32,6 +32,8 @@ def oracle_lib():
         lib.ob_destroy.restype = None
         lib.ob_export.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32]
         lib.ob_commit_all.argtypes = [c.c_void_p]
+        lib.ob_commit_all_mt.argtypes = [c.c_void_p, c.c_uint32]
+        lib.ob_rehome.argtypes = [c.c_void_p, c.c_uint32]
         lib.ob_representable.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32]
         lib.ob_reload.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p]
         lib.ob_step.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.c_void_p, c.c_void_p, c.c_void_p,
@@ -125,8 +127,17 @@ class OraclePopulation:
             if rc:
                 raise OracleError(f"ob_reload failed {rc}")
 
-    def commit_all(self):
-        self.lib.ob_commit_all(self._h)
+    def commit_all(self, threads=1):
+        """Persist + apply everything (threads > 1: on the step's worker partition)."""
+        if threads > 1:
+            self.lib.ob_commit_all_mt(self._h, threads)
+        else:
+            self.lib.ob_commit_all(self._h)
+
+    def rehome(self, threads):
+        """Rebuild each peer on the worker thread that steps it (CPU baseline)."""
+        if self.lib.ob_rehome(self._h, threads):
+            raise OracleError("ob_rehome failed")
 
     def step(self, msgs=None, locals_=None, limits=None, threads=1, allow_error=False, dev_before=None,
              in_depth=abi.GR_C, out_depth=abi.GR_C, has_locals=True, want_mid=True):
