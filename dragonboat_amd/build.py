@@ -17,7 +17,7 @@ CSRC = os.path.join(ROOT, "dragonboat_amd", "csrc")
 # the C-ABI + boundary passes, and one translation unit per slot count (compiled in parallel)
 ENGINE_SRC = [os.path.join(CSRC, "gr_engine.hip")] + [os.path.join(CSRC, f"gr_kernels_s{s}.hip") for s in (1, 3, 5, 8)]
 ENGINE_DEPS = ENGINE_SRC + [os.path.join(CSRC, f)
-                            for f in ("gr_lane.h", "gr_layout.h", "gr_host.h", "gr_fast.h", "gr_tick.h", "gr_io.h",
+                            for f in ("gr_lane.h", "gr_layout.h", "gr_host.h", "gr_fast.h", "gr_steady.h", "gr_tick.h", "gr_io.h",
                                       "gr_cover.h", "gr_kernels.h")] + \
     [os.path.join(ROOT, "include", "gpuraft.h")]
 JOBS = max(1, min(8, os.cpu_count() or 1))
@@ -33,13 +33,22 @@ WIRE_ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "liboraclewire.so")
 HBM_CALIB = os.path.join(ROOT, "tools", "hbm_calib")
 
 
+def _code_only(text):
+    """C/C++ source without comments or blank lines (string literals kept)."""
+    import re
+    pat = re.compile(r'"(?:\\.|[^"\\])*"|//[^\n]*|/\*.*?\*/', re.S)
+    text = pat.sub(lambda m: m.group(0) if m.group(0).startswith('"') else " ", text)
+    return "\n".join(ln.rstrip() for ln in text.splitlines() if ln.strip())
+
+
 def source_digest():
-    """Digest of the engine sources: ties a PMC measurement (profiles/) to the build it measured."""
+    """Digest of the engine's code (comments and blank lines stripped): ties a
+    PMC measurement (profiles/) to the build it measured; comment edits keep it."""
     import hashlib
     h = hashlib.sha1()
     for f in sorted(ENGINE_DEPS):
-        with open(f, "rb") as fh:
-            h.update(fh.read())
+        with open(f, encoding="utf-8") as fh:
+            h.update(_code_only(fh.read()).encode())
     return h.hexdigest()[:16]
 
 

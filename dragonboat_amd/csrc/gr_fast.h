@@ -692,11 +692,12 @@ struct FastLane {
   }
 };
 
-// Kernel-side entry: the lean lane for lane i; false = hand the lane to the general kernel.
+// The lean lane for lane i (fast_step in gr_steady.h tries the closed-form
+// steady lanes first); false = hand the lane to the general kernel.
 // *state = the role the lane entered the pass with; *hint_out = its role hint (WH_*).
 // take (FastLane::step): a lane whose role is not `take` is left alone, *skipped = true.
 template <int S, int R = FL_ANY, int RM = RM_ANY>
-GF_HD bool fast_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, uint32_t* state = nullptr,
+GF_HD bool lean_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, uint32_t* state = nullptr,
                      uint32_t hint = 0, uint32_t* hint_out = nullptr, int take = FL_ANY,
                      bool* skipped = nullptr) {
   FastLane<S, R, RM> L(kp, i, p);

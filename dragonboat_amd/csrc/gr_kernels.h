@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include "gr_fast.h"
+#include "gr_steady.h"
 #include "gr_lane.h"
 #include "gr_tick.h"
 
@@ -59,7 +60,10 @@ __device__ inline void block_stats(const StepParams& kp, const LaneStats& ls) {
 // config 3); no barrier, so waves of steady-state populations retire freely.
 // Lists 0..7 followers, 8..15 leaders (the general kernel's), 16..23 lanes with
 // ticks or a ReadIndex (LW_OTHER), which the tick kernel takes first.
-constexpr uint32_t kBailLists = 24, kGeneralLists = 16, kTickList0 = 16, kCounterStride = 64;  // counters 256 B apart
+// Lists 24..31: lanes a split pass's steady kernel did not finish, which the
+// role instances step with FastLane before anything goes to the general kernel.
+constexpr uint32_t kBailLists = 32, kGeneralLists = 16, kTickList0 = 16, kRetryList0 = 24,
+                   kCounterStride = 64;  // counters 256 B apart
 
 // One wave's appends to bail list `list`: one returning atomic for the wave,
 // the wave's lanes contiguous and ascending.
@@ -96,6 +100,34 @@ __device__ inline uint32_t sload_u32(const uint8_t* p) {
   return *(cu32*)(uintptr_t)p;
 }
 
+// Per-wave bookkeeping shared by the lean and steady kernels: the next pass's
+// hint of this wave (its lanes' common role hint when every active lane was
+// stepped here, else 0; written by each instance that stepped a lane of the
+// wave, both write 0 when an unhinted wave's lanes split between them), the
+// bail lists (followers into lists 0..7, leaders into 8..15, lanes with ticks
+// or a ReadIndex into 16..23, the tick kernel's: the later kernels walk their
+// lists in order, so their waves hold one kind of lane and diverge less), and
+// the stats.
+__device__ inline void wave_finish(const StepParams& kp, uint32_t i, uint32_t wave, bool mine, bool active,
+                                   bool skip, bool bail, uint32_t role, uint32_t myhint, const LaneStats& ls,
+                                   uint32_t* bail_list, uint32_t* counters, uint32_t list_cap) {
+  if (kp.hints && mine) {
+    const bool done = active && !skip;
+    const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane(myhint);
+    const uint64_t same = __ballot(done && myhint == first), act = __ballot(i < kp.n_lanes), dn = __ballot(done);
+    const uint32_t nh = same == act ? first : 0u;
+    if ((threadIdx.x & 63) == 0 && dn) kp.hints_out[wave] = (uint8_t)nh;
+  }
+  const bool lead = role == GR_LEADER;
+  const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
+#pragma unroll
+  for (uint32_t side = 0; side < 3; ++side) {
+    const bool m = bail && (side == 2 ? tickish : !tickish && lead == (side == 1));
+    bail_append(m, (blockIdx.x % 8) + side * 8, bail_list, counters, list_cap, i);
+  }
+  if (kp.stats) block_stats(kp, ls);
+}
+
 template <int S, int R, int RM>
 __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
                                                                              uint32_t* counters, uint32_t list_cap) {
@@ -108,53 +140,127 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
   const uint32_t hint = (hw >> (8 * (wave & 3))) & 0xFFu;
   const int wk = wave_kernel(hint, S);  // FL_ANY: unhinted
   bool mine = true;
-  if (R != FL_ANY) {  // a split pass (the launcher runs these only then)
+  bool blk = true;  // this block has waves of this instance
+  if (R != FL_ANY) {  // a split pass (the launcher runs these only then): with
+                      // kp.steady, waves hinted steady are gr_steady_kernel's
     const uint32_t w0 = blockIdx.x * (kBlock / 64), nw = (kp.n_lanes + 63) / 64;
     bool any = false;
 #pragma unroll
     for (uint32_t w = 0; w < kBlock / 64; ++w) {
-      const int k = w0 + w < nw ? wave_kernel((hw >> (8 * w)) & 0xFFu, S) : R == FL_LEADER ? FL_FOLLOWER : FL_LEADER;
+      const uint32_t hx = (hw >> (8 * w)) & 0xFFu;
+      const bool theirs = w0 + w >= nw || (kp.steady && steady_hint<S>(hx));
+      const int k = !theirs ? wave_kernel(hx, S) : R == FL_LEADER ? FL_FOLLOWER : FL_LEADER;
       any = any || k == R || k == FL_ANY;
     }
-    if (!any) return;  // block-uniform
-    mine = wk == R || wk == FL_ANY;
+    blk = any;  // block-uniform
+    mine = (wk == R || wk == FL_ANY) && !(kp.steady && steady_hint<S>(hint));
   }
+  if (blk) {
+    LaneStats ls;
+    bool bail = false, skip = false;
+    uint32_t role = 0, myhint = 0;
+    const bool active = mine && i < kp.n_lanes;
+    if (active) {
+      const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+      // leaves ls zero when it bails
+      if (R != FL_ANY)
+        bail = !lean_step<S, R, RM>(kp, i, p, &ls, &role, hint, &myhint, wk == FL_ANY ? R : FL_ANY, &skip);
+      else if (wk == FL_FOLLOWER) bail = !fast_step<S, FL_FOLLOWER, RM>(kp, i, p, &ls, &role, hint, &myhint);
+      else if (wk == FL_LEADER) bail = !fast_step<S, FL_LEADER, RM>(kp, i, p, &ls, &role, hint, &myhint);
+      else bail = !fast_step<S, FL_ANY, RM>(kp, i, p, &ls, &role, hint, &myhint);
+      bail = bail && !skip;  // a skipped lane is the other instance's
+      if (!bail && !skip) GR_CHECK_STATE(kp.st, p);
+    }
+    wave_finish(kp, i, wave, mine, active, skip, bail, role, myhint, ls, bail_list, counters, list_cap);
+  }
+  if (R != FL_ANY && kp.steady) {
+    // the lanes the steady kernel left (lists 24..31, final: it ran before this
+    // launch on the stream), grid-stride; each role instance takes the lanes of
+    // its role. No hint is written for them (their waves were the steady kernel's).
+    uint32_t start[9];
+    start[0] = 0;
+#pragma unroll
+    for (uint32_t l = 0; l < 8; ++l) start[l + 1] = start[l] + counters[(kRetryList0 + l) * kCounterStride];
+    const uint32_t n = start[8];
+    LaneStats acc;
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+      const uint32_t x = base + threadIdx.x;
+      bool bail = false;
+      uint32_t role = 0, li = 0;
+      if (x < n) {
+        uint32_t l = 0;
+#pragma unroll
+        for (uint32_t k = 1; k < 8; ++k) l = x >= start[k] ? k : l;
+        uint32_t off = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) off = (k == l) ? x - start[k] : off;
+        li = bail_list[(uint64_t)(kRetryList0 + l) * list_cap + off];
+        LaneStats ls;
+        bool skip = false;
+        uint32_t h = 0;
+        bail = !lean_step<S, R, RM>(kp, li, li, &ls, &role, 0u, &h, R, &skip);
+        bail = bail && !skip;
+        if (!bail && !skip) {
+          GR_CHECK_STATE(kp.st, li);
+          acc.leader_commit += ls.leader_commit;
+          acc.follower_commit += ls.follower_commit;
+          acc.msgs_in += ls.msgs_in;
+          acc.msgs_out += ls.msgs_out;
+          acc.leader_in += ls.leader_in;
+          acc.leader_out += ls.leader_out;
+          acc.entries += ls.entries;
+        }
+      }
+      const bool lead = role == GR_LEADER;
+      const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[li] & LW_OTHER);
+#pragma unroll
+      for (uint32_t side = 0; side < 3; ++side) {
+        const bool m = bail && (side == 2 ? tickish : !tickish && lead == (side == 1));
+        bail_append(m, (blockIdx.x % 8) + side * 8, bail_list, counters, list_cap, li);
+      }
+    }
+    if (kp.stats && n > blockIdx.x * kBlock) block_stats(kp, acc);
+  }
+}
+
+// The steady lanes (gr_steady.h) of a split pass, in a kernel of their own so
+// their register budget is their own (46 VGPRs for the leader's closed form;
+// with FastLane in the same kernel the allocation rose to FastLane's and
+// beyond): the waves whose hint says they were steady. A lane whose
+// preconditions fail stores nothing and is queued for FastLane (lists 24..31).
+template <int S, int RM>
+__global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(StepParams kp, uint32_t* bail_list,
+                                                                               uint32_t* counters, uint32_t list_cap) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
+  const uint32_t hw = sload_u32(kp.hints + (uint64_t)blockIdx.x * (kBlock / 64));
+  const uint32_t hint = (hw >> (8 * (wave & 3))) & 0xFFu;
+  {
+    const uint32_t w0 = blockIdx.x * (kBlock / 64), nw = (kp.n_lanes + 63) / 64;
+    bool any = false;
+#pragma unroll
+    for (uint32_t w = 0; w < kBlock / 64; ++w) any = any || (w0 + w < nw && steady_hint<S>((hw >> (8 * w)) & 0xFFu));
+    if (!any) return;  // block-uniform
+  }
+  const bool mine = steady_hint<S>(hint);
   LaneStats ls;
-  bool bail = false, skip = false;
-  uint32_t role = 0, myhint = 0;
+  bool done = false;
+  uint32_t myhint = 0, role = 0;
   const bool active = mine && i < kp.n_lanes;
   if (active) {
-    const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-    // leaves ls zero when it bails
-    if (R != FL_ANY)
-      bail = !fast_step<S, R, RM>(kp, i, p, &ls, &role, hint, &myhint, wk == FL_ANY ? R : FL_ANY, &skip);
-    else if (wk == FL_FOLLOWER) bail = !fast_step<S, FL_FOLLOWER, RM>(kp, i, p, &ls, &role, hint, &myhint);
-    else if (wk == FL_LEADER) bail = !fast_step<S, FL_LEADER, RM>(kp, i, p, &ls, &role, hint, &myhint);
-    else bail = !fast_step<S, FL_ANY, RM>(kp, i, p, &ls, &role, hint, &myhint);
-    bail = bail && !skip;  // a skipped lane is the other instance's
-    if (!bail && !skip) GR_CHECK_STATE(kp.st, p);
+    if constexpr (S == 3) {
+      if (steady_leader_hint(hint)) {
+        role = GR_LEADER;
+        done = SteadyLeader<S, RM>(kp, i, i).step(&ls, hint, &myhint);
+      }
+    }
+    if (steady_follower_hint(hint)) done = SteadyFollower<S, RM>(kp, i, i).step(&ls, hint, &myhint);
+    if (done) GR_CHECK_STATE(kp.st, i);
   }
-  if (kp.hints && mine) {
-    // next pass's hint: this wave's role if every active lane was stepped here
-    // and shares it; written by each instance that stepped a lane of the wave
-    // (both write 0 when an unhinted wave's lanes split between them)
-    const bool done = active && !skip;
-    const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane(myhint);
-    const uint64_t same = __ballot(done && myhint == first), act = __ballot(i < kp.n_lanes), dn = __ballot(done);
-    const uint32_t nh = same == act ? first : 0u;
-    if ((threadIdx.x & 63) == 0 && dn) kp.hints_out[wave] = (uint8_t)nh;
-  }
-  // followers into lists 0..7, leaders into 8..15, lanes with ticks or a
-  // ReadIndex into 16..23 (the tick kernel's): the later kernels walk their lists
-  // in order, so their waves hold one kind of lane and diverge less
-  const bool lead = role == GR_LEADER;
-  const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
-#pragma unroll
-  for (uint32_t side = 0; side < 3; ++side) {
-    const bool mine = bail && (side == 2 ? tickish : !tickish && lead == (side == 1));
-    bail_append(mine, (blockIdx.x % 8) + side * 8, bail_list, counters, list_cap, i);
-  }
-  if (kp.stats) block_stats(kp, ls);
+  // lanes not finished here (nothing stored) go to FastLane in the role
+  // instances that follow (lists 24..31), not straight to the general kernel
+  wave_finish(kp, i, wave, mine, active, false, false, role, myhint, ls, bail_list, counters, list_cap);
+  bail_append(active && !done, kRetryList0 + blockIdx.x % 8, bail_list, counters, list_cap, i);
 }
 
 // Pass 2a: the heartbeat/ReadIndex/tick lane (gr_tick.h) over the lanes pass 1
@@ -271,9 +377,17 @@ struct PassTiming {
 constexpr uint32_t kTickBlocks = 1024;
 
 template <int S, int RM>
-hipError_t launch_fast(const StepParams& kp, uint32_t blocks, uint32_t* bail_list, uint32_t* cur, uint32_t list_cap,
+hipError_t launch_fast(const StepParams& kp0, uint32_t blocks, uint32_t* bail_list, uint32_t* cur, uint32_t list_cap,
                        hipStream_t s) {
-  if (kp.hints && kp.split) {  // the two role instances (a large pass)
+  StepParams kp = kp0;
+  if (kp.hints && kp.split) {  // the steady lanes, then the two role instances (a large pass)
+    // the steady kernel steps lane i = peer i with compile-time routes
+    kp.steady = RM != RM_ANY && !kp.has_lane_peer ? 1 : 0;
+    if (kp.steady) {
+      hipLaunchKernelGGL((gr_steady_kernel<S, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
+      const hipError_t e0 = hipGetLastError();
+      if (e0 != hipSuccess) return e0;
+    }
     hipLaunchKernelGGL((gr_fast_kernel<S, FL_FOLLOWER, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
                        list_cap);
     const hipError_t err = hipGetLastError();
@@ -281,6 +395,7 @@ hipError_t launch_fast(const StepParams& kp, uint32_t blocks, uint32_t* bail_lis
     hipLaunchKernelGGL((gr_fast_kernel<S, FL_LEADER, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
                        list_cap);
   } else {
+    kp.steady = 0;
     hipLaunchKernelGGL((gr_fast_kernel<S, FL_ANY, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
                        list_cap);
   }

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "gr_fast.h"
+#include "gr_steady.h"
 #include "gr_host.h"
 #include "gr_lane.h"
 #include "gr_tick.h"
@@ -18,7 +19,7 @@ using namespace gr::host;
 
 namespace {
 
-static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0, g_tick_lanes = 0;
+static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0, g_tick_lanes = 0, g_steady_lanes = 0;
 static uint32_t g_hint_salt = 0;  // varies the drawn wave hints from call to call
 
 template <int S>
@@ -59,8 +60,27 @@ void run_lanes(const StepParams& kp) {
     // pass runs the FL_ANY instance
     const int fk = wave_kernel(hint, S);
     const bool split = (g_hint_salt >> 3) & 1u;
-    bool done;
-    if (fk == FL_LEADER) {
+    bool done = false;
+    uint32_t sh = 0;
+    if (split && steady_hint<S>(hint)) {
+      // a split pass's steady kernel (gr_kernels.h gr_steady_kernel): the closed
+      // form only; a lane it does not finish goes to the general lane
+      if constexpr (S == 3) {
+        if (steady_leader_hint(hint)) done = SteadyLeader<S, RM_ANY>(kp, i, p).step(&ls, hint, &sh);
+      }
+      if (steady_follower_hint(hint)) done = SteadyFollower<S, RM_ANY>(kp, i, p).step(&ls, hint, &sh);
+      g_steady_lanes += done;
+      if (!done) {  // the role instances' retry pass: FastLane without a hint, by role
+        bool skip = false;
+        ls = LaneStats{};
+        done = lean_step<S, FL_FOLLOWER>(kp, i, p, &ls, nullptr, 0u, nullptr, FL_FOLLOWER, &skip);
+        if (skip) {
+          ls = LaneStats{};
+          done = lean_step<S, FL_LEADER>(kp, i, p, &ls, nullptr, 0u, nullptr, FL_LEADER, &skip);
+          if (skip) abort();
+        }
+      }
+    } else if (fk == FL_LEADER) {
       done = fast_step<S, FL_LEADER>(kp, i, p, &ls, nullptr, hint);
     } else if (fk == FL_FOLLOWER) {
       done = fast_step<S, FL_FOLLOWER>(kp, i, p, &ls, nullptr, hint);
@@ -208,6 +228,9 @@ extern "C" void hl_counters(uint64_t* fast, uint64_t* bailed) {
 
 // lanes the heartbeat/ReadIndex/tick lane finished (of the bailed ones)
 extern "C" uint64_t hl_tick_lanes() { return g_tick_lanes; }
+
+// lanes the split pass's steady kernel emulation finished (gr_steady.h)
+extern "C" uint64_t hl_steady_lanes() { return g_steady_lanes; }
 
 // gr_bind_routes' affine-route detection, for the CPU tests
 extern "C" int hl_detect_affine(const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n, uint32_t S,

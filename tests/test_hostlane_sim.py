@@ -21,14 +21,18 @@ def _run(G, passes, seed, locals_fn=None, inject_p=0.0, **mk):
 def test_steady_state_commit(built):
     """BASELINE config 2 shape: leader commits one index per pass after warm-up.
     The lean steady-state lane (gr_fast.h) must finish almost every lane."""
-    from oracle.pyoracle import hostlane_counters
+    from oracle.pyoracle import hostlane_counters, hostlane_steady_lanes
     f0, b0 = hostlane_counters()
+    s0 = hostlane_steady_lanes()
     st = _run(64, 6, seed=3)
     f1, b1 = hostlane_counters()
     assert st["escalations"] == 0
     assert st["commits"] > 0
     fast, bailed = f1 - f0, b1 - b0
     assert fast > 0 and bailed <= fast // 4, (fast, bailed)
+    # the closed-form steady lanes (gr_steady.h) finished lanes of both roles'
+    # steady waves, checked against the oracle like every other lane
+    assert hostlane_steady_lanes() - s0 > 0
 
 
 def test_leader_change_churn(built):

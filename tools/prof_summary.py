@@ -30,7 +30,7 @@ def counters(d, kernel_sub):
 # The lean kernel's instances (gr_kernels.h): a split pass runs <S, 2> (followers)
 # then <S, 1> (leaders); a small or host-path pass runs <S, 0>. A device pass's
 # lean-kernel bytes are the sum over the instances it ran.
-ROLE_INSTANCES = ("gr_fast_kernel<3, 2>", "gr_fast_kernel<3, 1>")
+ROLE_INSTANCES = ("gr_fast_kernel<3, 2", "gr_fast_kernel<3, 1")  # <S, R, route mode>: substring match
 
 
 def main(o):
@@ -62,8 +62,9 @@ def main(o):
             wu = sum(w_ss) / len(w_ss)
             k.update({"fetch_size_units": fu, "write_size_units": wu, "read_bytes": fu * kf,
                       "write_bytes": wu * kw, "hbm_bytes_per_launch": fu * kf + wu * kw})
-        sq = counters(os.path.join(o, "sq"), kname)
-        k["sq"] = {c: sum(v[3:] or v) / len(v[3:] or v) for c, v in sq.items() if v}
+        for sub in ("sq", "sq2"):
+            sq = counters(os.path.join(o, sub), kname)
+            k.setdefault("sq", {}).update({c: sum(v[3:] or v) / len(v[3:] or v) for c, v in sq.items() if v})
         s["kernels"][kname] = k
     for kname in ROLE_INSTANCES:  # per instance, for the per-pass sum below
         f = counters(os.path.join(o, "fetch"), kname).get("FETCH_SIZE", [])
@@ -73,6 +74,11 @@ def main(o):
             fu, wu = sum(f_ss) / len(f_ss), sum(w_ss) / len(w_ss)
             s["kernels"][kname] = {"launches": len(f), "read_bytes": fu * kf, "write_bytes": wu * kw,
                                    "hbm_bytes_per_launch": fu * kf + wu * kw}
+            sqk = {}
+            for sub in ("sq", "sq2"):
+                sq = counters(os.path.join(o, sub), kname)
+                sqk.update({c: sum(v[3:] or v) / len(v[3:] or v) for c, v in sq.items() if v})
+            s["kernels"][kname]["sq"] = sqk
     fk = s["kernels"].get("gr_fast_kernel", {})
     if all(k in s["kernels"] for k in ROLE_INSTANCES):  # split passes: one pass = both instances
         fk = {key: sum(s["kernels"][k][key] for k in ROLE_INSTANCES)
