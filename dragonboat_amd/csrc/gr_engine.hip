@@ -71,8 +71,11 @@ struct gr_engine {
   LaneBase ln{};
   uint64_t* stats = nullptr;
   uint32_t stats_rows = 0;
-  uint32_t* bail = nullptr;      // kBailLists lists of cap lanes each
-  uint32_t* counters = nullptr;  // [2 (pass parity)][kBailLists][kCounterStride]
+  uint32_t* bail = nullptr;      // kBailLists lists of cap lanes each, then the wave lists (bail_words)
+  uint32_t* counters = nullptr;  // [2 (pass parity)][kCounters][kCounterStride]
+  // gr_step_device passes of at least this many lanes run the role instances
+  // (StepParams::split); GR_SPLIT_MIN_LANES at gr_create overrides it (tests)
+  uint32_t split_min = kSplitMinLanes;
   uint8_t* hints = nullptr;      // 2 x [hint_stride(cap)] wave hints of the device-resident path (gr_layout.h WH_*):
                                  // one set read by a pass, the other written for the next
   uint64_t hint_flip = 0;
@@ -361,11 +364,15 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
   e->ln.S = S;
   const size_t sb = state_bytes(S, e->cap), lb = lane_bytes(S, e->cap);
   e->stats_rows = (e->cap + kBlock - 1) / kBlock;
+  if (const char* sm = getenv("GR_SPLIT_MIN_LANES")) {
+    const long v = strtol(sm, nullptr, 10);
+    if (v > 0) e->split_min = (uint32_t)v;
+  }
   void *ds = nullptr, *dl = nullptr;
   if (hipMalloc(&ds, sb) != hipSuccess || hipMalloc(&dl, lb) != hipSuccess ||
       hipMalloc((void**)&e->stats, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
-      hipMalloc((void**)&e->bail, (size_t)kBailLists * e->cap * 4) != hipSuccess ||
-      hipMalloc((void**)&e->counters, 2 * kBailLists * kCounterStride * 4) != hipSuccess ||
+      hipMalloc((void**)&e->bail, bail_words(e->cap) * 4) != hipSuccess ||
+      hipMalloc((void**)&e->counters, 2 * kCounters * kCounterStride * 4) != hipSuccess ||
       hipMalloc((void**)&e->route_base, 2 * GR_SMAX * GR_SMAX * 4) != hipSuccess ||
       hipMalloc((void**)&e->hints, 2 * hint_stride(e->cap)) != hipSuccess) {
     if (ds) (void)hipFree(ds);
@@ -379,7 +386,7 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
   e->ln.base = (uint8_t*)dl;
   if (hipMemset(ds, 0, sb) != hipSuccess || hipMemset(dl, 0, lb) != hipSuccess ||
       hipMemset(e->stats, 0, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
-      hipMemset(e->counters, 0, 2 * kBailLists * kCounterStride * 4) != hipSuccess ||
+      hipMemset(e->counters, 0, 2 * kCounters * kCounterStride * 4) != hipSuccess ||
       hipMemset(e->hints, 0, 2 * hint_stride(e->cap)) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     gr_destroy(e);
@@ -1209,7 +1216,7 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
   kp.hints_out = e->hints + (1 - hf) * hs;
   // the follower instance of its own pays off only when the pass is large (a
   // 10k x 3 pass is launch-bound: one instance there, 24 vs 41 us per pass)
-  kp.split = n_peers >= kSplitMinLanes ? 1 : 0;
+  kp.split = n_peers >= e->split_min ? 1 : 0;
   HIPCHK(launch_slots(e->S, kp, e->bail, e->counters, e->cap, (uint32_t)e->launches++, (hipStream_t)stream,
                       next_timing(e), kp.has_locals && e->locals_other));
   e->passes++;

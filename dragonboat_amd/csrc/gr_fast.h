@@ -28,7 +28,14 @@ namespace gr {
 // (branch-light, no early exits: keeps the exec-mask nesting shallow) and
 // hands over at the end. Nothing but uncounted message bodies is stored
 // before `ok` is checked.
+#ifdef GR_BAIL_TRACE
+// Diagnostic host build of the lane code only (tools/bail_trace.py): counts, per
+// source line, the first steady-state condition that handed a lane over.
+void gr_bail_trace(int line);
+#define GF_BAIL(c) (ok = ok && !((c) ? (gr_bail_trace(__LINE__), true) : false))
+#else
 #define GF_BAIL(c) (ok = ok && !(c))
+#endif
 
 // Lane roles a lean-lane instance is built for (gr_kernels.h launches one
 // kernel per role over the waves whose hint names it): FL_ANY steps leaders and

@@ -11,6 +11,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "gr_fast.h"
 #include "gr_steady.h"
 #include "gr_lane.h"
@@ -62,8 +64,28 @@ __device__ inline void block_stats(const StepParams& kp, const LaneStats& ls) {
 // ticks or a ReadIndex (LW_OTHER), which the tick kernel takes first.
 // Lists 24..31: lanes a split pass's steady kernel did not finish, which the
 // role instances step with FastLane before anything goes to the general kernel.
-constexpr uint32_t kBailLists = 32, kGeneralLists = 16, kTickList0 = 16, kRetryList0 = 24,
+// After the lane lists' storage: one flag byte and one lane mask per wave, the
+// waves a split pass's steady kernel leaves to the role instances (flag =
+// WF_LISTED | the wave's hint as the pass started; mask = its lanes still to
+// step: the steady kernel finishes quiesced lanes itself and sends lanes with
+// ticks or a ReadIndex straight to the tick lists). Every wave's flag is
+// rewritten every split pass, so no counter or atomic is involved: the role
+// instances scan the flags, 64 waves per load, instead of launching one
+// workgroup per 256 lanes, most of which would find nothing to do.
+constexpr uint32_t kBailLists = 32, kGeneralLists = 16, kTickList0 = 16, kRetryList0 = 24, kCounters = kBailLists,
                    kCounterStride = 64;  // counters 256 B apart
+constexpr uint32_t WF_LISTED = 0x80;     // wave flag: the role instances step this wave's masked lanes
+__host__ __device__ inline uint64_t wave_flag_words(uint32_t cap) { return ((uint64_t)cap / 64 + 64) / 4 * 2; }
+// u32 words of the list storage: kBailLists lane lists of cap, the wave flags, the wave masks (u64)
+__host__ __device__ inline uint64_t bail_words(uint32_t cap) {
+  return (uint64_t)kBailLists * cap + wave_flag_words(cap) + 2 * ((uint64_t)cap / 64 + 1);
+}
+__host__ __device__ inline uint8_t* wave_flags(uint32_t* bail_list, uint32_t cap) {
+  return (uint8_t*)(bail_list + (uint64_t)kBailLists * cap);
+}
+__host__ __device__ inline uint64_t* wave_masks(uint32_t* bail_list, uint32_t cap) {
+  return (uint64_t*)(bail_list + (uint64_t)kBailLists * cap + wave_flag_words(cap));
+}
 
 // One wave's appends to bail list `list`: one returning atomic for the wave,
 // the wave's lanes contiguous and ascending.
@@ -111,12 +133,16 @@ __device__ inline uint32_t sload_u32(const uint8_t* p) {
 __device__ inline void wave_finish(const StepParams& kp, uint32_t i, uint32_t wave, bool mine, bool active,
                                    bool skip, bool bail, uint32_t role, uint32_t myhint, const LaneStats& ls,
                                    uint32_t* bail_list, uint32_t* counters, uint32_t list_cap) {
-  if (kp.hints && mine) {
-    const bool done = active && !skip;
-    const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane(myhint);
-    const uint64_t same = __ballot(done && myhint == first), act = __ballot(i < kp.n_lanes), dn = __ballot(done);
-    const uint32_t nh = same == act ? first : 0u;
-    if ((threadIdx.x & 63) == 0 && dn) kp.hints_out[wave] = (uint8_t)nh;
+  if (kp.hints) {
+    // over the lanes that are this kernel's (mine), written by the first of them
+    const uint64_t mm = __ballot(mine);
+    if (mine) {
+      const bool done = active && !skip;
+      const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane(myhint);
+      const uint64_t same = __ballot(done && myhint == first), act = __ballot(i < kp.n_lanes), dn = __ballot(done);
+      const uint32_t nh = same == act ? first : 0u;
+      if ((threadIdx.x & 63) == (uint32_t)__ffsll((unsigned long long)mm) - 1 && dn) kp.hints_out[wave] = (uint8_t)nh;
+    }
   }
   const bool lead = role == GR_LEADER;
   const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
@@ -128,59 +154,103 @@ __device__ inline void wave_finish(const StepParams& kp, uint32_t i, uint32_t wa
   if (kp.stats) block_stats(kp, ls);
 }
 
+// One wave of a lean-kernel instance: lane i of wave `wave`, whose hint as the
+// pass started is `hint` (wk = wave_kernel(hint)); mine = the wave is this
+// instance's. Steps the lane, then the wave's hint, bail lists and stats.
 template <int S, int R, int RM>
+__device__ inline void fast_wave(const StepParams& kp, uint32_t i, uint32_t wave, uint32_t hint, int wk, bool mine,
+                                 uint32_t* bail_list, uint32_t* counters, uint32_t list_cap) {
+  LaneStats ls;
+  bool bail = false, skip = false;
+  uint32_t role = 0, myhint = 0;
+  const bool active = mine && i < kp.n_lanes;
+  if (active) {
+    const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+    // leaves ls zero when it bails
+    if (R != FL_ANY)
+      bail = !lean_step<S, R, RM>(kp, i, p, &ls, &role, hint, &myhint, wk == FL_ANY ? R : FL_ANY, &skip);
+    else if (wk == FL_FOLLOWER) bail = !fast_step<S, FL_FOLLOWER, RM>(kp, i, p, &ls, &role, hint, &myhint);
+    else if (wk == FL_LEADER) bail = !fast_step<S, FL_LEADER, RM>(kp, i, p, &ls, &role, hint, &myhint);
+    else bail = !fast_step<S, FL_ANY, RM>(kp, i, p, &ls, &role, hint, &myhint);
+    bail = bail && !skip;  // a skipped lane is the other instance's
+    if (!bail && !skip) GR_CHECK_STATE(kp.st, p);
+  }
+  wave_finish(kp, i, wave, mine, active, skip, bail, role, myhint, ls, bail_list, counters, list_cap);
+}
+
+// Locate entry x of the 8 lists whose exclusive prefix is start[0..8]: list and offset.
+__device__ inline void list_at(const uint32_t (&start)[9], uint32_t x, uint32_t* l, uint32_t* off) {
+  uint32_t ll = 0;
+#pragma unroll
+  for (uint32_t k = 1; k < 8; ++k) ll = x >= start[k] ? k : ll;
+  uint32_t o = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) o = (k == ll) ? x - start[k] : o;
+  *l = ll;
+  *off = o;
+}
+
+// LISTED (split passes with the steady kernel, R != FL_ANY): a fixed grid walks
+// the waves the steady kernel listed for this instance (wave flags), one wave of
+// the grid per listed wave, grid-stride. Otherwise one workgroup per 256 lanes,
+// every wave checked against its hint.
+template <int S, int R, int RM, bool LISTED>
 __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
                                                                              uint32_t* counters, uint32_t list_cap) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
-  // the workgroup's four wave hints in one scalar load (the set the previous
-  // pass wrote; this pass writes the other one), so no lane waits on a vector
-  // load before its first round
-  const uint32_t hw = kp.hints ? sload_u32(kp.hints + (uint64_t)blockIdx.x * (kBlock / 64)) : 0u;
-  const uint32_t hint = (hw >> (8 * (wave & 3))) & 0xFFu;
-  const int wk = wave_kernel(hint, S);  // FL_ANY: unhinted
-  bool mine = true;
-  bool blk = true;  // this block has waves of this instance
-  if (R != FL_ANY) {  // a split pass (the launcher runs these only then): with
-                      // kp.steady, waves hinted steady are gr_steady_kernel's
-    const uint32_t w0 = blockIdx.x * (kBlock / 64), nw = (kp.n_lanes + 63) / 64;
-    bool any = false;
+  static_assert(!LISTED || R != FL_ANY, "listed waves are the role instances'");
+  if constexpr (LISTED) {
+    // each wave of the grid scans 64 wave flags per load; a listed wave of this
+    // instance's role (an unhinted one is both instances') is stepped over the
+    // lanes its mask leaves
+    const uint8_t* wf = wave_flags(bail_list, list_cap);
+    const uint64_t* wm = wave_masks(bail_list, list_cap);
+    const uint32_t nw = (kp.n_lanes + 63) / 64, lane = threadIdx.x & 63;
+    const uint32_t gw0 = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+    for (uint32_t base = gw0 * 64; base < nw; base += gridDim.x * (kBlock / 64) * 64) {  // wave-uniform
+      const uint32_t f = base + lane < nw ? (uint32_t)wf[base + lane] : 0u;
+      const int k = wave_kernel(f & 0x7Fu, S);
+      uint64_t todo = __ballot((f & WF_LISTED) && (R == FL_FOLLOWER ? k != FL_LEADER : k != FL_FOLLOWER));
+      while (todo) {
+        const uint32_t b = (uint32_t)__ffsll((unsigned long long)todo) - 1;
+        todo &= todo - 1;
+        const uint32_t wave = base + b, hint = (uint32_t)__shfl((int)f, (int)b) & 0x7Fu;
+        const uint64_t m = wm[wave];
+        fast_wave<S, R, RM>(kp, wave * 64 + lane, wave, hint, wave_kernel(hint, S), (m >> lane) & 1ull, bail_list,
+                            counters, list_cap);
+      }
+    }
+  } else {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
+    // the workgroup's four wave hints in one scalar load (the set the previous
+    // pass wrote; this pass writes the other one), so no lane waits on a vector
+    // load before its first round
+    const uint32_t hw = kp.hints ? sload_u32(kp.hints + (uint64_t)blockIdx.x * (kBlock / 64)) : 0u;
+    const uint32_t hint = (hw >> (8 * (wave & 3))) & 0xFFu;
+    const int wk = wave_kernel(hint, S);  // FL_ANY: unhinted
+    bool mine = true;
+    bool blk = true;  // this block has waves of this instance
+    if (R != FL_ANY) {  // a split pass without the steady kernel
+      bool any = false;
 #pragma unroll
-    for (uint32_t w = 0; w < kBlock / 64; ++w) {
-      const uint32_t hx = (hw >> (8 * w)) & 0xFFu;
-      const bool theirs = w0 + w >= nw || (kp.steady && steady_hint<S>(hx));
-      const int k = !theirs ? wave_kernel(hx, S) : R == FL_LEADER ? FL_FOLLOWER : FL_LEADER;
-      any = any || k == R || k == FL_ANY;
+      for (uint32_t w = 0; w < kBlock / 64; ++w) {
+        const int k = wave_kernel((hw >> (8 * w)) & 0xFFu, S);
+        any = any || k == R || k == FL_ANY;
+      }
+      blk = any;  // block-uniform
+      mine = wk == R || wk == FL_ANY;
     }
-    blk = any;  // block-uniform
-    mine = (wk == R || wk == FL_ANY) && !(kp.steady && steady_hint<S>(hint));
+    if (blk) fast_wave<S, R, RM>(kp, i, wave, hint, wk, mine, bail_list, counters, list_cap);
   }
-  if (blk) {
-    LaneStats ls;
-    bool bail = false, skip = false;
-    uint32_t role = 0, myhint = 0;
-    const bool active = mine && i < kp.n_lanes;
-    if (active) {
-      const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-      // leaves ls zero when it bails
-      if (R != FL_ANY)
-        bail = !lean_step<S, R, RM>(kp, i, p, &ls, &role, hint, &myhint, wk == FL_ANY ? R : FL_ANY, &skip);
-      else if (wk == FL_FOLLOWER) bail = !fast_step<S, FL_FOLLOWER, RM>(kp, i, p, &ls, &role, hint, &myhint);
-      else if (wk == FL_LEADER) bail = !fast_step<S, FL_LEADER, RM>(kp, i, p, &ls, &role, hint, &myhint);
-      else bail = !fast_step<S, FL_ANY, RM>(kp, i, p, &ls, &role, hint, &myhint);
-      bail = bail && !skip;  // a skipped lane is the other instance's
-      if (!bail && !skip) GR_CHECK_STATE(kp.st, p);
-    }
-    wave_finish(kp, i, wave, mine, active, skip, bail, role, myhint, ls, bail_list, counters, list_cap);
-  }
-  if (R != FL_ANY && kp.steady) {
+  if (LISTED) {
     // the lanes the steady kernel left (lists 24..31, final: it ran before this
     // launch on the stream), grid-stride; each role instance takes the lanes of
     // its role. No hint is written for them (their waves were the steady kernel's).
     uint32_t start[9];
     start[0] = 0;
 #pragma unroll
-    for (uint32_t l = 0; l < 8; ++l) start[l + 1] = start[l] + counters[(kRetryList0 + l) * kCounterStride];
+    for (uint32_t l = 0; l < 8; ++l)
+      start[l + 1] = start[l] + (uint32_t)__builtin_amdgcn_readfirstlane(counters[(kRetryList0 + l) * kCounterStride]);
     const uint32_t n = start[8];
     LaneStats acc;
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
@@ -188,12 +258,8 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(Step
       bool bail = false;
       uint32_t role = 0, li = 0;
       if (x < n) {
-        uint32_t l = 0;
-#pragma unroll
-        for (uint32_t k = 1; k < 8; ++k) l = x >= start[k] ? k : l;
-        uint32_t off = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) off = (k == l) ? x - start[k] : off;
+        uint32_t l, off;
+        list_at(start, x, &l, &off);
         li = bail_list[(uint64_t)(kRetryList0 + l) * list_cap + off];
         LaneStats ls;
         bool skip = false;
@@ -235,18 +301,28 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
   const uint32_t hw = sload_u32(kp.hints + (uint64_t)blockIdx.x * (kBlock / 64));
   const uint32_t hint = (hw >> (8 * (wave & 3))) & 0xFFu;
-  {
-    const uint32_t w0 = blockIdx.x * (kBlock / 64), nw = (kp.n_lanes + 63) / 64;
-    bool any = false;
-#pragma unroll
-    for (uint32_t w = 0; w < kBlock / 64; ++w) any = any || (w0 + w < nw && steady_hint<S>((hw >> (8 * w)) & 0xFFu));
-    if (!any) return;  // block-uniform
+  const uint32_t nw = (kp.n_lanes + 63) / 64;
+  if (wave >= nw) return;  // wave-uniform
+  if (!steady_hint<S>(hint)) {
+    // not a steady wave: quiesced lanes finish here (QuiescedTick in closed
+    // form), lanes with ticks or a ReadIndex go straight to the tick lists, and
+    // the rest are listed for the role instances (wave flag + lane mask)
+    const bool active = i < kp.n_lanes;
+    const int q = active ? quiet_step<S, RM>(kp, i, i) : QS_DONE;
+    bail_append(q == QS_TICK, kTickList0 + blockIdx.x % 8, bail_list, counters, list_cap, i);
+    const uint64_t rem = __ballot(q == QS_OTHER);
+    if ((threadIdx.x & 63) == 0) {
+      wave_flags(bail_list, list_cap)[wave] = (uint8_t)(rem ? (WF_LISTED | hint) : 0u);
+      if (rem) wave_masks(bail_list, list_cap)[wave] = rem;
+      else kp.hints_out[wave] = 0;  // nothing here to speculate on next pass
+    }
+    return;
   }
-  const bool mine = steady_hint<S>(hint);
+  if ((threadIdx.x & 63) == 0) wave_flags(bail_list, list_cap)[wave] = 0;
   LaneStats ls;
   bool done = false;
   uint32_t myhint = 0, role = 0;
-  const bool active = mine && i < kp.n_lanes;
+  const bool active = i < kp.n_lanes;
   if (active) {
     if constexpr (S == 3) {
       if (steady_leader_hint(hint)) {
@@ -259,7 +335,7 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
   }
   // lanes not finished here (nothing stored) go to FastLane in the role
   // instances that follow (lists 24..31), not straight to the general kernel
-  wave_finish(kp, i, wave, mine, active, false, false, role, myhint, ls, bail_list, counters, list_cap);
+  wave_finish(kp, i, wave, true, active, false, false, role, myhint, ls, bail_list, counters, list_cap);
   bail_append(active && !done, kRetryList0 + blockIdx.x % 8, bail_list, counters, list_cap, i);
 }
 
@@ -329,7 +405,7 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
 #pragma unroll
   for (uint32_t l = 0; l < kGeneralLists; ++l) start[l + 1] = start[l] + counters[l * kCounterStride];
   const uint32_t n = start[kGeneralLists];
-  if (blockIdx.x == 0 && threadIdx.x < kBailLists) next_counters[threadIdx.x * kCounterStride] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < kCounters) next_counters[threadIdx.x * kCounterStride] = 0;
   if (blockIdx.x * kBlock >= n) return;  // uniform per block: nothing to do, no stats row touched
   LaneStats acc;
   for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
@@ -361,10 +437,74 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
   if (kp.stats) block_stats(kp, acc);
 }
 
-// The general kernel's grid: one 256-lane workgroup per CU fills the chip at
-// its occupancy (1 wave per SIMD); never more than the stats block has rows for.
-// Kept small because with no bailed lanes the launch is pure overhead.
+// The general kernel's grid: one 256-lane workgroup per CU fills the chip at its
+// occupancy (256 VGPRs + ~220 AGPRs: 1 wave per SIMD); never more than the stats
+// block has rows for. Kept small because with no bailed lanes the launch is pure
+// overhead. GR_GENERAL_BLOCKS overrides it (A/B runs).
 constexpr uint32_t kGeneralBlocks = 256;
+inline uint32_t general_blocks() {
+  static const uint32_t v = [] {
+    const char* e = getenv("GR_GENERAL_BLOCKS");
+    const long x = e ? strtol(e, nullptr, 10) : 0;
+    return x > 0 ? (uint32_t)x : kGeneralBlocks;
+  }();
+  return v;
+}
+
+// Small passes (at most small_blocks() workgroups, 64k lanes by default) are
+// launch-bound: a 10k x 3 pass spent ~7 us in an empty general-kernel launch
+// and the gaps between kernels. gr_small_kernel does the whole pass in one
+// launch: the lean lane, and in the same wave, for the lanes it hands over, the
+// tick lane and then the general lane. Its register allocation is the general
+// lane's (2 waves per SIMD), which such a grid never needs more than. It also
+// zeroes the next pass's list counters, as the general kernel does.
+constexpr uint32_t kSmallBlocks = 256;
+inline uint32_t small_blocks() {  // GR_SMALL_BLOCKS overrides it (0: never; A/B runs and tests)
+  static const uint32_t v = [] {
+    const char* e = getenv("GR_SMALL_BLOCKS");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : kSmallBlocks;
+  }();
+  return v;
+}
+
+template <int S>
+__global__ __launch_bounds__(kBlock, 1) void gr_small_kernel(StepParams kp, uint32_t* next_counters) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
+  if (blockIdx.x == 0 && threadIdx.x < kCounters) next_counters[threadIdx.x * kCounterStride] = 0;
+  const uint32_t hw = kp.hints ? sload_u32(kp.hints + (uint64_t)blockIdx.x * (kBlock / 64)) : 0u;
+  const uint32_t hint = (hw >> (8 * (wave & 3))) & 0xFFu;
+  const int wk = wave_kernel(hint, S);
+  LaneStats ls;
+  bool bail = false;
+  uint32_t role = 0, myhint = 0, p = 0;
+  const bool active = i < kp.n_lanes;
+  if (active) {
+    p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+    if (wk == FL_FOLLOWER) bail = !fast_step<S, FL_FOLLOWER, RM_ANY>(kp, i, p, &ls, &role, hint, &myhint);
+    else if (wk == FL_LEADER) bail = !fast_step<S, FL_LEADER, RM_ANY>(kp, i, p, &ls, &role, hint, &myhint);
+    else bail = !fast_step<S, FL_ANY, RM_ANY>(kp, i, p, &ls, &role, hint, &myhint);
+    if (!bail) GR_CHECK_STATE(kp.st, p);
+  }
+  if (kp.hints) {  // the wave's next hint, as wave_finish writes it
+    const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane(myhint);
+    const uint64_t same = __ballot(active && myhint == first), act = __ballot(active);
+    if ((threadIdx.x & 63) == 0 && act) kp.hints_out[wave] = (uint8_t)(same == act ? first : 0u);
+  }
+  if (bail) {  // handed over: the tick lane, else the general lane, in this wave
+    LaneStats l2;
+    const bool tickish = kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
+    if (!(tickish && tick_step<S>(kp, i, p, &l2))) {
+      l2 = LaneStats{};
+      Lane<S> L(kp, i, p);
+      L.step(&l2);
+    }
+    GR_CHECK_STATE(kp.st, p);
+    l2.bailed = 1;
+    ls = l2;
+  }
+  if (kp.stats) block_stats(kp, ls);
+}
 
 // Optional per-pass timing: events around the two kernels, recorded on the
 // pass's stream.
@@ -376,27 +516,40 @@ struct PassTiming {
 // The tick kernel's grid: its lanes are at most the active share of a pass.
 constexpr uint32_t kTickBlocks = 1024;
 
+// The role instances' grid when they scan the wave flags: enough waves to fill
+// the chip at their occupancy; with no listed wave each wave reads its flags
+// (one 64-byte load per 64 waves) and leaves.
+constexpr uint32_t kRoleBlocks = 1024;
+
 template <int S, int RM>
 hipError_t launch_fast(const StepParams& kp0, uint32_t blocks, uint32_t* bail_list, uint32_t* cur, uint32_t list_cap,
                        hipStream_t s) {
   StepParams kp = kp0;
-  if (kp.hints && kp.split) {  // the steady lanes, then the two role instances (a large pass)
+  if (kp.hints && kp.split) {  // a large pass: the role instances
     // the steady kernel steps lane i = peer i with compile-time routes
-    kp.steady = RM != RM_ANY && !kp.has_lane_peer ? 1 : 0;
-    if (kp.steady) {
+    if (RM != RM_ANY && !kp.has_lane_peer) {
+      // the steady lanes, then the role instances over the waves it listed and
+      // the lanes it left
       hipLaunchKernelGGL((gr_steady_kernel<S, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
       const hipError_t e0 = hipGetLastError();
       if (e0 != hipSuccess) return e0;
+      const uint32_t rb = blocks < kRoleBlocks ? blocks : kRoleBlocks;
+      hipLaunchKernelGGL((gr_fast_kernel<S, FL_FOLLOWER, RM, true>), dim3(rb), dim3(kBlock), 0, s, kp, bail_list,
+                         cur, list_cap);
+      const hipError_t e1 = hipGetLastError();
+      if (e1 != hipSuccess) return e1;
+      hipLaunchKernelGGL((gr_fast_kernel<S, FL_LEADER, RM, true>), dim3(rb), dim3(kBlock), 0, s, kp, bail_list,
+                         cur, list_cap);
+    } else {
+      hipLaunchKernelGGL((gr_fast_kernel<S, FL_FOLLOWER, RM, false>), dim3(blocks), dim3(kBlock), 0, s, kp,
+                         bail_list, cur, list_cap);
+      const hipError_t err = hipGetLastError();
+      if (err != hipSuccess) return err;
+      hipLaunchKernelGGL((gr_fast_kernel<S, FL_LEADER, RM, false>), dim3(blocks), dim3(kBlock), 0, s, kp,
+                         bail_list, cur, list_cap);
     }
-    hipLaunchKernelGGL((gr_fast_kernel<S, FL_FOLLOWER, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
-                       list_cap);
-    const hipError_t err = hipGetLastError();
-    if (err != hipSuccess) return err;
-    hipLaunchKernelGGL((gr_fast_kernel<S, FL_LEADER, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
-                       list_cap);
   } else {
-    kp.steady = 0;
-    hipLaunchKernelGGL((gr_fast_kernel<S, FL_ANY, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
+    hipLaunchKernelGGL((gr_fast_kernel<S, FL_ANY, RM, false>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
                        list_cap);
   }
   return hipGetLastError();
@@ -407,10 +560,17 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
                          uint32_t parity, hipStream_t s, const PassTiming* t, bool tick_lanes) {
   if (kp.n_lanes == 0) return hipSuccess;
   const uint32_t blocks = (kp.n_lanes + kBlock - 1) / kBlock;
-  uint32_t* cur = counters + (parity & 1) * kBailLists * kCounterStride;
-  uint32_t* nxt = counters + ((parity + 1) & 1) * kBailLists * kCounterStride;
+  uint32_t* cur = counters + (parity & 1) * kCounters * kCounterStride;
+  uint32_t* nxt = counters + ((parity + 1) & 1) * kCounters * kCounterStride;
   hipError_t err;
   if (t && (err = hipEventRecord(t->ev[0], s)) != hipSuccess) return err;
+  if (blocks <= small_blocks()) {  // the whole pass in one launch
+    hipLaunchKernelGGL(gr_small_kernel<S>, dim3(blocks), dim3(kBlock), 0, s, kp, nxt);
+    if ((err = hipGetLastError()) != hipSuccess) return err;
+    if (t && ((err = hipEventRecord(t->ev[1], s)) != hipSuccess || (err = hipEventRecord(t->ev[2], s)) != hipSuccess))
+      return err;
+    return hipSuccess;
+  }
   // the lean instances built for the bound route mode (no route branches); a
   // loopback instance also assumes one-chunk spaces
   const bool loop1 = kp.route_mode == RT_LOOPBACK && kp.in.n_chunks == 1 && kp.out.n_chunks == 1;
@@ -424,7 +584,7 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
     hipLaunchKernelGGL(gr_tick_kernel<S>, dim3(tblocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
     if ((err = hipGetLastError()) != hipSuccess) return err;
   }
-  const uint32_t gblocks = blocks < kGeneralBlocks ? blocks : kGeneralBlocks;
+  const uint32_t gblocks = blocks < general_blocks() ? blocks : general_blocks();
   hipLaunchKernelGGL(gr_step_kernel<S>, dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list,
                      (const uint32_t*)cur, nxt, list_cap);
   if ((err = hipGetLastError()) != hipSuccess) return err;

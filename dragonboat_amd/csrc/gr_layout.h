@@ -509,7 +509,6 @@ struct StepParams {
   uint8_t route_mode;
   uint8_t split;       // follower-hinted waves go to the FL_FOLLOWER instance (gr_kernels.h)
   uint8_t route_wu;    // route_g % 64 == 0: replica_of is wave-uniform
-  uint8_t steady;      // gr_steady_kernel runs in this pass: the role instances skip steady-hinted waves
 };
 
 // Route mode as a compile-time parameter of the lean kernel instances

@@ -310,6 +310,42 @@ struct SteadyFollower : SteadyBase<RM> {
   }
 };
 
+// What the steady kernel did with a lane of a wave whose hint is not steady
+// (gr_kernels.h gr_steady_kernel): finished it, sent it to the tick lists, or
+// left it to the role instances.
+constexpr int QS_DONE = 0, QS_TICK = 1, QS_OTHER = 2;
+
+// QuiescedTick x nq alone (raft.go:431-433: electionTick++ in every state, one
+// item), FastLane's quiesced path (gr_fast.h) in closed form: no message in any
+// in-mailbox, no proposal, no tick or ReadIndex. Quiesced populations carry no
+// role hint (a wave of quiet groups has no input to speculate on), so their
+// lanes would otherwise all go through the role instances.
+template <int S, int RM>
+GF_HD int quiet_step(const StepParams& kp, uint32_t i, uint32_t p) {  // lane i, peer p
+  constexpr bool kOneChunk = RM == RT_LOOPBACK;
+  if (!kp.has_locals) return QS_OTHER;
+  const uint32_t lw = ntld(kp.ln.u32(LR_LWORD)[i]);
+  if (lw & LW_OTHER) return QS_TICK;
+  const uint32_t np = lw & 0xFFFFu, nq = (lw >> LW_QT_SHIFT) & LW_QT_MAX;
+  if (!nq || np) return QS_OTHER;
+  uint32_t gin[S], gout[S];
+  routes_of<S, RM>(kp, i, gin, gout);
+  const uint64_t hdr = ntld(kp.st.u64(SR_HDR)[p]), et = ntld(kp.st.u64(SR_ETICK)[p]);
+  uint32_t any = 0;
+#pragma unroll
+  for (int j = 0; j < S; ++j)
+    any |= gin[j] != NOPOS ? ((uint32_t)ntld(kp.in.template at<kOneChunk>(gin[j]).cnt()) & MB_COUNT) : 0u;
+  if (any) return QS_OTHER;
+  ntst(kp.st.u64(SR_ETICK)[p], (uint64_t)(et + nq));
+  if (h_flags(hdr) & F_ETZ) ntst(kp.st.u64(SR_HDR)[p], hdr & ~((uint64_t)F_ETZ << H_FLAGS_SHIFT));
+#pragma unroll
+  for (int j = 0; j < S; ++j)
+    if (gout[j] != NOPOS) ntst(kp.out.template at<kOneChunk>(gout[j]).cnt(), (uint8_t)0);
+  ntst(kp.ln.u8(LR_RFLAGS)[i], (uint8_t)0);
+  GR_COVER(FAST_QUIESCED);
+  return QS_DONE;
+}
+
 // Kernel-side entry (gr_kernels.h, and the host build of the lane): a wave
 // hinted steady runs the closed-form lane of its role first; any lane it does
 // not finish (nothing stored) runs FastLane; false = hand the lane to the

@@ -6,13 +6,33 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <map>
 #include <vector>
+
 
 #include "gr_fast.h"
 #include "gr_steady.h"
 #include "gr_host.h"
 #include "gr_lane.h"
 #include "gr_tick.h"
+
+#ifdef GR_BAIL_TRACE
+static std::map<int, uint64_t> g_bail_lines;
+void gr::gr_bail_trace(int line) { g_bail_lines[line]++; }
+// (line, count) pairs of the first bail condition per handed-over lane (gr_fast.h GF_BAIL)
+extern "C" uint32_t hl_bail_trace(int32_t* lines, uint64_t* counts, uint32_t cap) {
+  uint32_t k = 0;
+  for (auto& kv : g_bail_lines) {
+    if (k < cap) {
+      lines[k] = kv.first;
+      counts[k] = kv.second;
+    }
+    k++;
+  }
+  g_bail_lines.clear();
+  return k;
+}
+#endif
 
 using namespace gr;
 using namespace gr::host;
@@ -21,6 +41,7 @@ namespace {
 
 static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0, g_tick_lanes = 0, g_steady_lanes = 0;
 static uint32_t g_hint_salt = 0;  // varies the drawn wave hints from call to call
+static bool g_true_hints = false;  // hl_true_hints: every wave gets the device's hint (diagnostics)
 
 template <int S>
 void run_lanes(const StepParams& kp) {
@@ -38,15 +59,25 @@ void run_lanes(const StepParams& kp) {
     // kernels, gr_kernels.h), never a different result.
     const uint32_t w = (i >> 6) * 2654435761u + g_hint_salt;
     uint32_t hint;
-    if ((w >> 7) & 3u) {
-      const uint32_t i0 = i & ~63u;
-      const uint64_t h = kp.st.u64(SR_HDR)[kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i0] : i0];
+    // the hint a lane's header implies (its role as the pass starts)
+    auto hdr_hint = [&](uint32_t x) {
+      const uint64_t h = kp.st.u64(SR_HDR)[kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[x] : x];
       const uint32_t ls0 = (h_flags(h) & F_LSLOT) >> F_LSLOT_SHIFT;
       const uint32_t rh = (h & H_RUN_MASK) == H_RUN_MASK ? WH_RUNS : 0u;
-      hint = h_state(h) == GR_LEADER ? (WH_LEADER | ((h_self(h) & 7u) << WH_SLOT_SHIFT) |
+      return h_state(h) == GR_LEADER ? (WH_LEADER | ((h_self(h) & 7u) << WH_SLOT_SHIFT) |
                                         ((h & H_SYNC_MASK) ? WH_SYNC : 0u) | rh)
              : (h_state(h) == GR_FOLLOWER && ls0) ? (WH_FOLLOWER | ((ls0 - 1) << WH_SLOT_SHIFT) | rh)
                                                   : 0u;
+    };
+    if (g_true_hints) {
+      // as the device: the wave's common hint, 0 when its lanes differ (a
+      // state-based stand-in for the hint the previous pass wrote)
+      const uint32_t i0 = i & ~63u;
+      hint = hdr_hint(i0);
+      for (uint32_t x = i0 + 1; x < i0 + 64 && x < kp.n_lanes && hint; ++x)
+        if (hdr_hint(x) != hint) hint = 0;
+    } else if ((w >> 7) & 3u) {
+      hint = hdr_hint(i & ~63u);
     } else {
       const uint32_t pick = (w >> 13) % (2u + S);
       const uint32_t rh = ((w >> 25) & 1u) ? WH_RUNS : 0u;
@@ -59,9 +90,10 @@ void run_lanes(const StepParams& kp) {
     // unhinted wave through both (each takes the lanes of its role); a small
     // pass runs the FL_ANY instance
     const int fk = wave_kernel(hint, S);
-    const bool split = (g_hint_salt >> 3) & 1u;
+    const bool split = g_true_hints || ((g_hint_salt >> 3) & 1u);
     bool done = false;
     uint32_t sh = 0;
+    int q0 = QS_OTHER;
     if (split && steady_hint<S>(hint)) {
       // a split pass's steady kernel (gr_kernels.h gr_steady_kernel): the closed
       // form only; a lane it does not finish goes to the general lane
@@ -80,6 +112,11 @@ void run_lanes(const StepParams& kp) {
           if (skip) abort();
         }
       }
+    } else if (split && (q0 = quiet_step<S, RM_ANY>(kp, i, p)) != QS_OTHER) {
+      // a split pass's steady kernel on a wave that is not steady: quiesced
+      // lanes in closed form, ticks and ReadIndex straight to the tick lane
+      done = q0 == QS_DONE;
+      g_steady_lanes += done;
     } else if (fk == FL_LEADER) {
       done = fast_step<S, FL_LEADER>(kp, i, p, &ls, nullptr, hint);
     } else if (fk == FL_FOLLOWER) {
@@ -168,10 +205,18 @@ extern "C" int hl_step(uint32_t slots, uint64_t max_entry_size, gr_peer* peers, 
   kp.has_locals = 1;
   kp.has_lane_peer = 1;
   kp.route_mode = RT_TABLE;
+#ifdef GR_HL_SLOTS_35
+  // the sanitizer build (build.py build_sanitized): only the slot counts its
+  // workloads use (tests/san_workload.py), so it compiles in half the time
+  if (S == 3) run_lanes<3>(kp);
+  else if (S == 5) run_lanes<5>(kp);
+  else return GR_EINVAL;
+#else
   if (S == 1) run_lanes<1>(kp);
   else if (S == 3) run_lanes<3>(kp);
   else if (S == 5) run_lanes<5>(kp);
   else run_lanes<GR_SMAX>(kp);
+#endif
   std::vector<gr_message> msgs;
   decode_outbox(obuf.data(), pk, S, &msgs);
   *n_out = msgs.size();
@@ -219,6 +264,10 @@ extern "C" int hl_commit_update(uint32_t slots, gr_peer* peers, uint32_t n_peers
   }
   return rc;
 }
+
+// draw only the hints the device would give, and run split passes (the large-pass
+// schedule), as tools/bail_trace.py wants; 0 restores the test default
+extern "C" void hl_true_hints(int on) { g_true_hints = on != 0; }
 
 // lanes finished by the fast subset / by the general lane since load
 extern "C" void hl_counters(uint64_t* fast, uint64_t* bailed) {

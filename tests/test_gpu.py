@@ -67,6 +67,22 @@ def test_device_resident_path(gpu, placement):
     assert np.all(final["committed"][:777] > 2**32)
 
 
+@pytest.mark.parametrize("mix", [False, True])
+def test_split_pass_churn(gpu, mix, monkeypatch):
+    """Large-pass schedule (StepParams::split) forced on a small population, with
+    BASELINE config 5's leader changes every pass, checked against the oracle
+    after every pass (state, every mailbox, results). mix = False: loopback
+    routes, so the steady kernel runs and the role instances walk its wave lists
+    while churn puts new leaders into follower-hinted waves; mix = True: peers
+    group-major, so every wave holds both roles (unhinted waves through both
+    instances, table routes)."""
+    import devsim
+    monkeypatch.setenv("GR_SPLIT_MIN_LANES", "1")
+    st = {}
+    devsim.run_device(2000, 3, 10, inject_p=0.1, mix=mix, stats=st, seed=11)
+    assert st["injected"] > 0
+
+
 def test_spread_cold_region_on_demand(gpu):
     """Spread exchange: hot region every pass, cold region only on passes whose
     mailboxes hold heartbeats/acks (ticks every third pass); parity every pass."""

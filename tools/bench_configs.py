@@ -28,8 +28,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(name, peers, G, R, passes, warmup, prepare):
-    """prepare(k, eng, n_peers) -> local inputs of pass k (may also reload groups)."""
+def run(name, peers, G, R, passes, warmup, prepare, graph_reps=0):
+    """prepare(k, eng, n_peers) -> local inputs of pass k (may also reload groups).
+    graph_reps > 0: afterwards, two passes captured in a HIP graph (torch.cuda.CUDAGraph
+    over the engine's launches on the capture stream) and replayed graph_reps times:
+    the per-pass time with no CPU launch in it. The local inputs
+    then stay those of the last pass (config 2's proposals are the same every pass)."""
     import torch
     from dragonboat_amd.engine import Engine
     from dragonboat_amd.exchange import Exchange
@@ -64,6 +68,32 @@ def run(name, peers, G, R, passes, warmup, prepare):
             gen += tm["general_ms"]
             bailed += tm["bailed_lanes"]
     st = eng.stats()
+    graph = None
+    if graph_reps:
+        k0 = warmup + passes
+        k0 += k0 & 1  # local spaces ping-pong: the captured pair starts on an even pass
+        if (warmup + passes) & 1:
+            ex.step(eng, spaces, warmup + passes, stream)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        cs = torch.cuda.Stream()
+        cs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.graph(g, stream=cs):
+            for k in range(2):
+                ex.step(eng, spaces, k0 + k, torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        c0 = eng.stats()["leader_commits"]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(graph_reps):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        gms = e0.elapsed_time(e1) / (2 * graph_reps)
+        commits = eng.stats()["leader_commits"] - c0
+        graph = {"passes": 2 * graph_reps, "ms_per_pass": gms, "leader_commits_per_pass": commits / (2 * graph_reps),
+                 "leader_commits_per_s": commits / (2 * graph_reps * gms * 1e-3)}
+        del g
     from dragonboat_amd import abi
     import numpy as np
     res = eng.collect_results(ex.n_peers)  # the last pass's per-lane results
@@ -78,6 +108,8 @@ def run(name, peers, G, R, passes, warmup, prepare):
            "escalations_per_pass": st["escalations"] / passes,
            "msgs_in_per_pass": st["msgs_in"] / passes, "host_s": t_host,
            "last_pass_escalations": reasons}
+    if graph:
+        out["graph"] = graph
     eng.close()
     return out
 
@@ -87,6 +119,7 @@ def main():
     ap.add_argument("--passes", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--only", default="2,3,5")
+    ap.add_argument("--graph-reps", type=int, default=200, help="config 2: replays of a 2-pass HIP graph (0: off)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -98,7 +131,7 @@ def main():
         G, R = 10_000, 3
         peers = P.make_groups(G, R, seed=2)
         res.append(run("2: 10k x 3, uniform proposals", peers, G, R, args.passes, args.warmup,
-                       lambda k, eng, n: P.propose_locals(n, np.arange(G), pass_index=k)))
+                       lambda k, eng, n: P.propose_locals(n, np.arange(G), pass_index=k), graph_reps=args.graph_reps))
     if "3" in want:
         G, R = 100_000, 5
         peers, active = P.config3(G, R)

@@ -27,10 +27,11 @@ def counters(d, kernel_sub):
     return {k: [v[x] for x in sorted(v, key=int)] for k, v in per.items()}
 
 
-# The lean kernel's instances (gr_kernels.h): a split pass runs <S, 2> (followers)
-# then <S, 1> (leaders); a small or host-path pass runs <S, 0>. A device pass's
-# lean-kernel bytes are the sum over the instances it ran.
-ROLE_INSTANCES = ("gr_fast_kernel<3, 2", "gr_fast_kernel<3, 1")  # <S, R, route mode>: substring match
+# The lean kernels of one headline pass (gr_kernels.h, a split pass over
+# loopback routes, RM = 3): the steady kernel, then the role instances <S, 2>
+# (followers) and <S, 1> (leaders) over its wave lists. A device pass's
+# lean-kernel bytes are the sum over the kernels it ran.
+ROLE_INSTANCES = ("gr_steady_kernel<3, 3>", "gr_fast_kernel<3, 2, 3, true>", "gr_fast_kernel<3, 1, 3, true>")
 
 
 def main(o):
@@ -52,7 +53,7 @@ def main(o):
     kf = cal.get("read_u64_bytes_per_unit", 2048.0)
     kw = cal.get("write_u64_bytes_per_unit", 1024.0)
     s["kernels"] = {}
-    for kname in ("gr_fast_kernel", "gr_step_kernel"):
+    for kname in ("gr_fast_kernel", "gr_step_kernel", "gr_tick_kernel"):
         f = counters(os.path.join(o, "fetch"), kname).get("FETCH_SIZE", [])
         w = counters(os.path.join(o, "write"), kname).get("WRITE_SIZE", [])
         f_ss, w_ss = f[3:] or f, w[3:] or w  # steady-state launches (after warm-up)
@@ -89,7 +90,7 @@ def main(o):
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         from dragonboat_amd.build import source_digest
         with open(os.path.join(o, "pmc_latest.json"), "w") as fh:
-            json.dump({"kernel": "gr_fast_kernel<3, *> (the instances of one pass)", "groups": groups, "replicas": 3,
+            json.dump({"kernel": "gr_steady_kernel<3, 3> + gr_fast_kernel<3, {2,1}, 3, true> (the lean kernels of one pass)", "groups": groups, "replicas": 3,
                        "source_digest": source_digest(),
                        "hbm_bytes_per_launch": fk["hbm_bytes_per_launch"],
                        "read_bytes": fk["read_bytes"], "write_bytes": fk["write_bytes"],
