@@ -456,11 +456,25 @@ struct FastLane {
       }
     }
     uint32_t L = 0, nsrc = 0, c = 0, gl = 0, go = NOPOS, cbL = 0;
+    uint32_t fdrop = 0;  // follower: messages of uniform mailboxes at a lower term, dropped
     uint64_t rid = 0;
     if (kFollowerPath && !(kLeaderPath && leader)) {
+      // the term word of every uniform mailbox with messages (the hinted one's is
+      // loaded already): one at a lower term is dropped whole (raft.go:1014-1044),
+      // unless it holds Replicates and checkQuorum asks for a NoOP reply
+      uint32_t ft[S];
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        if (cnt[j]) {
+        const bool have = hf && (uint32_t)j == hL && ghL != NOPOS;
+        ft[j] = have ? fmt : (cnt[j] && !((nonu >> j) & 1u)) ? ntld(min_at(gin[j]).mterm()) : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const bool lower = cnt[j] && !((nonu >> j) & 1u) && ft[j] != 0u && (uint64_t)ft[j] < term;
+        GF_BAIL(lower && !(cbs[j] & MB_RESP) && (flags & GR_F_CHECK_QUORUM));
+        if (lower) {
+          fdrop += cnt[j];
+        } else if (cnt[j]) {
           L = (uint32_t)j;
           c = cnt[j];
           gl = gin[j];
@@ -471,7 +485,7 @@ struct FastLane {
       }
       const uint32_t cc = c < (uint32_t)MK ? c : (uint32_t)MK;
       const bool spec = hf && L == hL;  // the hinted mailbox is the one that sent
-      if (c && !spec) fmt = ntld(min_at(gl).mterm());
+      if (c) fmt = ft[L];
 #pragma unroll
       for (int k = 0; k < MK; ++k) {
         if ((uint32_t)k < cc && !spec) {
@@ -518,13 +532,26 @@ struct FastLane {
     hi0 = hi;
     if (kLeaderPath && leader) {
       GF_BAIL(flags & F_LTT);  // leader transfer in progress
-#pragma unroll
-      for (int j = 0; j < S; ++j)  // uniform accepts (ReplicateResp, flags 0) at the current term
-        GF_BAIL(cnt[j] && (cnt[j] > (uint32_t)MK || !(cbs[j] & MB_RESP) || (uint64_t)lmt[j] != term));
       GF_BAIL(nonu);
+      // a uniform mailbox at a lower term is dropped whole (onMessageTermNotMatched,
+      // raft.go:1014-1044), unless its messages are Replicates and checkQuorum asks
+      // for a NoOP reply; the others must be uniform accepts (ReplicateResp, flags 0)
+      // at the current term
+      uint32_t drop = 0;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const bool lower = cnt[j] && lmt[j] != 0u && (uint64_t)lmt[j] < term;
+        GF_BAIL(lower && !(cbs[j] & MB_RESP) && (flags & GR_F_CHECK_QUORUM));
+        drop |= lower ? 1u << j : 0u;
+        GF_BAIL(!lower && cnt[j] && (cnt[j] > (uint32_t)MK || !(cbs[j] & MB_RESP) || (uint64_t)lmt[j] != term));
+      }
       // messages in node.handleReceivedMessages order: slot, then arrival
 #pragma unroll
       for (int j = 0; j < S; ++j) {
+        if ((drop >> j) & 1u) {
+          nmi += cnt[j];
+          continue;
+        }
 #pragma unroll
         for (int k = 0; k < MK; ++k) {
           if ((uint32_t)k < cnt[j]) {
@@ -538,6 +565,7 @@ struct FastLane {
       // uniform compact Replicates (LogTerm = Term, at most one entry at Term,
       // narrow Commit) from one remote at the current term
       GF_BAIL(nsrc > 1 || c > (uint32_t)MK || nonu || (c && ((cbL & MB_RESP) || (uint64_t)fmt != term)));
+      nmi += fdrop;
       uint32_t oc = 0;
 #pragma unroll
       for (int k = 0; k < MK; ++k) {

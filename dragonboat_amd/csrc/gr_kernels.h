@@ -104,6 +104,9 @@ __device__ inline void bail_append(bool mine, uint32_t list, uint32_t* bail_list
 #ifndef GR_FAST_MIN_WAVES
 #define GR_FAST_MIN_WAVES 1  // waves per SIMD the register allocation must allow (A/B builds)
 #endif
+#ifndef GR_LISTED_MIN_WAVES
+#define GR_LISTED_MIN_WAVES 1  // the role instances over listed waves (A/B builds: 4 and 5 spill)
+#endif
 // Role instances. A large pass (StepParams::split) runs R = FL_FOLLOWER then R =
 // FL_LEADER, each with the other role's code and registers compiled out (66 and
 // 92 VGPRs at S = 3: 7 and 5 waves per SIMD): a wave whose hint (as the pass
@@ -195,25 +198,28 @@ __device__ inline void list_at(const uint32_t (&start)[9], uint32_t x, uint32_t*
 // the grid per listed wave, grid-stride. Otherwise one workgroup per 256 lanes,
 // every wave checked against its hint.
 template <int S, int R, int RM, bool LISTED>
-__global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
+__global__ __launch_bounds__(kBlock, LISTED ? GR_LISTED_MIN_WAVES : GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
                                                                              uint32_t* counters, uint32_t list_cap) {
   static_assert(!LISTED || R != FL_ANY, "listed waves are the role instances'");
   if constexpr (LISTED) {
-    // each wave of the grid scans 64 wave flags per load; a listed wave of this
-    // instance's role (an unhinted one is both instances') is stepped over the
-    // lanes its mask leaves
+    // grid wave g owns waves g, g + W, g + 2W, ... (W = the grid's waves): it
+    // reads 64 of their flags per load (lane l: wave g + W * (r + l)) and steps
+    // the listed ones of this instance's role (an unhinted wave is both
+    // instances') over the lanes their masks leave
     const uint8_t* wf = wave_flags(bail_list, list_cap);
     const uint64_t* wm = wave_masks(bail_list, list_cap);
     const uint32_t nw = (kp.n_lanes + 63) / 64, lane = threadIdx.x & 63;
-    const uint32_t gw0 = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
-    for (uint32_t base = gw0 * 64; base < nw; base += gridDim.x * (kBlock / 64) * 64) {  // wave-uniform
-      const uint32_t f = base + lane < nw ? (uint32_t)wf[base + lane] : 0u;
+    const uint32_t g = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+    const uint32_t W = gridDim.x * (kBlock / 64);
+    for (uint32_t r = 0; g + (uint64_t)W * r < nw; r += 64) {  // wave-uniform
+      const uint64_t idx = g + (uint64_t)W * (r + lane);
+      const uint32_t f = idx < nw ? (uint32_t)wf[idx] : 0u;
       const int k = wave_kernel(f & 0x7Fu, S);
       uint64_t todo = __ballot((f & WF_LISTED) && (R == FL_FOLLOWER ? k != FL_LEADER : k != FL_FOLLOWER));
       while (todo) {
         const uint32_t b = (uint32_t)__ffsll((unsigned long long)todo) - 1;
         todo &= todo - 1;
-        const uint32_t wave = base + b, hint = (uint32_t)__shfl((int)f, (int)b) & 0x7Fu;
+        const uint32_t wave = g + W * (r + b), hint = (uint32_t)__shfl((int)f, (int)b) & 0x7Fu;
         const uint64_t m = wm[wave];
         fast_wave<S, R, RM>(kp, wave * 64 + lane, wave, hint, wave_kernel(hint, S), (m >> lane) & 1ull, bail_list,
                             counters, list_cap);
