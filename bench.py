@@ -482,7 +482,7 @@ def main():
         pipe.step(args.warmup + args.steps + k)
     pipe.synchronize()
     tm = pipe.timing_end()
-    cold_x = pipe.cold_exchanges
+    xbytes = pipe.exchange_bytes_per_pass()
     banks = len(pipe.ex)
     pipe.close()
     commits = st["leader_commits"]
@@ -539,7 +539,7 @@ def main():
                                                                     "all_to_all per pass" if placement == "spread"
                                                                     else "")},
             "escalations": esc,
-            "cold_exchanges": cold_x,
+            "exchange_bytes_per_pass": xbytes,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"lean kernels of one pass (gr_steady_kernel<{S}> + gr_fast_kernel<{S}, role>)",

@@ -595,6 +595,69 @@ int gr_space_cold_used(gr_engine* e, const void* space, uint32_t n_chunks, uint3
   return GR_OK;
 }
 
+uint64_t gr_space_side_bytes(uint32_t n_chunks, uint32_t depth, uint32_t capacity) {
+  if (depth == 0 || depth > GR_C) return 0;
+  return (uint64_t)n_chunks * io::side_chunk_bytes(depth, capacity);
+}
+
+int gr_space_side_pack(void* space, uint32_t n_chunks, uint32_t positions, uint32_t depth, void* side,
+                       uint32_t capacity, void* stream) {
+  if (!space || !side || depth == 0 || depth > GR_C || n_chunks == 0) return GR_EINVAL;
+  const hipStream_t s = (hipStream_t)stream;
+  const SpaceView v = make_view(space, n_chunks, positions, depth);
+  for (uint32_t c = 0; c < n_chunks; ++c)
+    HIPCHK(hipMemsetAsync((uint8_t*)side + (uint64_t)c * io::side_chunk_bytes(depth, capacity), 0, io::kSideHdr, s));
+  hipLaunchKernelGGL(io::side_pack, dim3(io_grid((size_t)n_chunks * v.pc)), dim3(io::kIoBlock), 0, s, v,
+                     (uint8_t*)side, capacity);
+  HIPCHK(hipGetLastError());
+  return GR_OK;
+}
+
+int gr_space_side_unpack(void* space, uint32_t n_chunks, uint32_t positions, uint32_t depth, const void* side,
+                         uint32_t capacity, void* stream) {
+  if (!space || !side || depth == 0 || depth > GR_C || n_chunks == 0) return GR_EINVAL;
+  const hipStream_t s = (hipStream_t)stream;
+  const SpaceView v = make_view(space, n_chunks, positions, depth);
+  if (capacity) {
+    hipLaunchKernelGGL(io::side_unpack, dim3(io_grid((size_t)n_chunks * capacity)), dim3(io::kIoBlock), 0, s, v,
+                       (const uint8_t*)side, capacity);
+    HIPCHK(hipGetLastError());
+  }
+  return GR_OK;
+}
+
+int gr_space_side_pack_host(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
+                            void* side_host, uint32_t capacity) {
+  if (!space_host || !side_host || depth == 0 || depth > GR_C || n_chunks == 0) return GR_EINVAL;
+  const SpaceView v = make_view(space_host, n_chunks, positions, depth);
+  uint8_t* side = (uint8_t*)side_host;
+  for (uint32_t c = 0; c < n_chunks; ++c) {
+    uint32_t* cnt = (uint32_t*)(side + (uint64_t)c * io::side_chunk_bytes(depth, capacity));
+    *cnt = 0;
+    for (uint32_t l = 0; l < v.pc; ++l) {
+      const uint32_t g = c * v.pc + l;
+      if (io::needs_cold(v.at(g).cnt())) io::side_put(v, g, side, capacity, (*cnt)++);
+    }
+  }
+  return GR_OK;
+}
+
+int gr_space_side_unpack_host(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
+                              const void* side_host, uint32_t capacity) {
+  if (!space_host || !side_host || depth == 0 || depth > GR_C || n_chunks == 0) return GR_EINVAL;
+  const SpaceView v = make_view(space_host, n_chunks, positions, depth);
+  const uint8_t* side = (const uint8_t*)side_host;
+  for (uint32_t c = 0; c < n_chunks; ++c) {
+    const uint8_t* h = side + (uint64_t)c * io::side_chunk_bytes(depth, capacity);
+    const uint32_t n = *(const uint32_t*)h;
+    for (uint32_t x = 0; x < n && x < capacity; ++x) {
+      const uint8_t* e = h + io::kSideHdr + (uint64_t)x * io::side_entry_bytes(depth);
+      io::cold_scatter(v.at(c * v.pc + ((const uint32_t*)e)[0]), ((const uint32_t*)e)[1] & MB_COUNT, e);
+    }
+  }
+  return GR_OK;
+}
+
 int gr_space_encode(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
                     const gr_message* msgs, size_t n, const uint32_t* pos_of_msg) {
   if (!space_host || (n && (!msgs || !pos_of_msg)) || depth == 0 || depth > GR_C) return GR_EINVAL;
@@ -620,10 +683,16 @@ int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t position
     for (uint32_t l = 0; l < positions; ++l) {
       const uint32_t g = c * v.pc + l;
       const Mailbox mb = v.at(g);
-      const uint32_t cnt = std::min<uint32_t>(mb.cnt() & MB_COUNT, depth);
+      const uint32_t cb = mb.cnt(), cnt = std::min<uint32_t>(cb & MB_COUNT, depth);
+      const bool lost = !(cb & MB_UNIFORM) && (cb & MB_COLD_LOST);  // cold fields not delivered
       for (uint32_t k = 0; k < cnt; ++k) {
         if (out && n < cap) {
-          out[n] = decode_msg(mb, k);
+          if (lost) {
+            memset(&out[n], 0, sizeof(gr_message));
+            out[n].reject = 0xFF;  // a record whose fields were lost in the exchange
+          } else {
+            out[n] = decode_msg(mb, k);
+          }
           out[n].peer = g;
           out[n].slot = (uint8_t)k;
         }

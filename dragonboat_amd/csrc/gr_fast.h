@@ -532,6 +532,13 @@ struct FastLane {
     hi0 = hi;
     if (kLeaderPath && leader) {
       GF_BAIL(flags & F_LTT);  // leader transfer in progress
+#ifdef GR_BAIL_TRACE
+      if (ok && nonu) {  // diagnostics: the first message type and flags of each non-uniform mailbox
+#pragma unroll
+        for (int j = 0; j < S; ++j)
+          if ((nonu >> j) & 1u) gr_bail_trace(100000 + 1000 * (int)min_at(gin[j]).type(0) + min_at(gin[j]).flags(0));
+      }
+#endif
       GF_BAIL(nonu);
       // a uniform mailbox at a lower term is dropped whole (onMessageTermNotMatched,
       // raft.go:1014-1044), unless its messages are Replicates and checkQuorum asks

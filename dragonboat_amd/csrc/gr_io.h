@@ -305,6 +305,89 @@ __global__ void cold_used(SpaceView v, uint32_t* flag) {
   }
 }
 
+// ---------------------------------------------------------------- side buffers
+// Cross-GPU spaces (exchange.py Pipeline) send the hot region every pass and the
+// cold fields only of the mailboxes that need them (no MB_UNIFORM), compacted
+// into a fixed-capacity side buffer per chunk, so the all-to-all sizes are known
+// without the host reading anything back. Per chunk: a 64-byte header (entry
+// count) and `cap` entries of [u32 position in chunk][u32 count byte] + per
+// message the 50 cold bytes in the cold chunk's field order. A mailbox that does
+// not fit gets MB_COLD_LOST in its (hot) count byte and its reader escalates
+// CAPACITY.
+constexpr uint32_t kSideHdr = 64;
+constexpr uint32_t kColdOff[10] = {0, 2, 6, 10, 14, 18, 22, 26, 34, 42};  // field offsets (x pc) in ck(k)
+constexpr uint32_t kColdSz[10] = {2, 4, 4, 4, 4, 4, 4, 8, 8, 8};
+__host__ __device__ inline uint32_t side_entry_bytes(uint32_t depth) { return (8 + depth * kColdK + 7) & ~7u; }
+__host__ __device__ inline uint64_t side_chunk_bytes(uint32_t depth, uint32_t cap) {
+  return round256(kSideHdr + (uint64_t)cap * side_entry_bytes(depth));
+}
+// Copy the cold fields of the first n messages of mailbox mb into / out of entry e.
+__host__ __device__ inline void cold_gather(const Mailbox& mb, uint32_t n, uint8_t* e) {
+  for (uint32_t k = 0; k < n; ++k)
+    for (uint32_t f = 0; f < 10; ++f) {
+      const uint8_t* src = mb.ck(k) + (uint64_t)kColdOff[f] * mb.pc + (uint64_t)mb.local * kColdSz[f];
+      uint8_t* dst = e + 8 + k * kColdK + kColdOff[f];
+      for (uint32_t b = 0; b < kColdSz[f]; ++b) dst[b] = src[b];
+    }
+}
+__host__ __device__ inline void cold_scatter(const Mailbox& mb, uint32_t n, const uint8_t* e) {
+  for (uint32_t k = 0; k < n; ++k)
+    for (uint32_t f = 0; f < 10; ++f) {
+      uint8_t* dst = mb.ck(k) + (uint64_t)kColdOff[f] * mb.pc + (uint64_t)mb.local * kColdSz[f];
+      const uint8_t* src = e + 8 + k * kColdK + kColdOff[f];
+      for (uint32_t b = 0; b < kColdSz[f]; ++b) dst[b] = src[b];
+    }
+}
+// One position of the pack: entry index idx (or >= cap: lost).
+__host__ __device__ inline void side_put(const SpaceView& v, uint32_t g, uint8_t* side, uint32_t cap, uint32_t idx) {
+  const Mailbox mb = v.at(g);
+  const uint32_t cb = mb.cnt(), c = g / v.pc;
+  if (idx >= cap) {
+    mb.cnt() = (uint8_t)(cb | MB_COLD_LOST);
+    return;
+  }
+  uint8_t* e = side + (uint64_t)c * side_chunk_bytes(v.depth, cap) + kSideHdr + (uint64_t)idx * side_entry_bytes(v.depth);
+  reinterpret_cast<uint32_t*>(e)[0] = g - c * v.pc;
+  reinterpret_cast<uint32_t*>(e)[1] = cb;
+  cold_gather(mb, cb & MB_COUNT, e);
+}
+__host__ __device__ inline bool needs_cold(uint32_t cb) { return (cb & MB_COUNT) && !(cb & MB_UNIFORM); }
+
+// Pack the out space's cold fields into the side buffers (their counts zeroed
+// before): one returning atomic per wave and chunk (a chunk is a multiple of 256
+// positions, so a wave never spans two).
+__global__ void side_pack(SpaceView v, uint8_t* side, uint32_t cap) {
+  const uint64_t n = (uint64_t)v.n_chunks * v.pc;
+  for (uint64_t g0 = (uint64_t)blockIdx.x * kIoBlock; g0 < n; g0 += (uint64_t)gridDim.x * kIoBlock) {
+    const uint64_t g = g0 + threadIdx.x;
+    const bool want = g < n && needs_cold(v.at((uint32_t)g).cnt());
+    const uint64_t bm = __ballot(want);
+    if (!bm) continue;
+    const uint32_t lane = threadIdx.x & 63, first = (uint32_t)__ffsll((unsigned long long)bm) - 1;
+    uint32_t base = 0;
+    if (lane == first) {
+      const uint32_t c = (uint32_t)(g / v.pc);
+      base = atomicAdd(reinterpret_cast<uint32_t*>(side + (uint64_t)c * side_chunk_bytes(v.depth, cap)),
+                       (uint32_t)__popcll(bm));
+    }
+    base = __shfl(base, (int)first);
+    if (want) side_put(v, (uint32_t)g, side, cap, base + (uint32_t)__popcll(bm & ((1ull << lane) - 1)));
+  }
+}
+// Unpack the received side buffers into the in space's cold chunks.
+__global__ void side_unpack(SpaceView v, const uint8_t* side, uint32_t cap) {
+  const uint64_t n = (uint64_t)v.n_chunks * cap;
+  for (uint64_t t = io_tid(); t < n; t += io_stride()) {
+    const uint32_t c = (uint32_t)(t / cap), idx = (uint32_t)(t % cap);
+    const uint8_t* h = side + (uint64_t)c * side_chunk_bytes(v.depth, cap);
+    const uint32_t cnt = *reinterpret_cast<const uint32_t*>(h);
+    if (idx >= cnt) continue;
+    const uint8_t* e = h + kSideHdr + (uint64_t)idx * side_entry_bytes(v.depth);
+    const uint32_t pos = reinterpret_cast<const uint32_t*>(e)[0], cb = reinterpret_cast<const uint32_t*>(e)[1];
+    cold_scatter(v.at(c * v.pc + pos), cb & MB_COUNT, e);
+  }
+}
+
 // Zero the mailbox counts of chunk 0's first `positions` positions (the
 // host-path inbox before encoding): one byte row untiled, the first 64 bytes of
 // each tile with GR_TILE.

@@ -1473,6 +1473,8 @@ struct Lane {
       for (uint32_t k = 0; k < c; ++k) {
         if (item == limit) { *at = item; return 0; }
         if (k == kp.in.depth) { *at = item; return GR_ESC_CAPACITY; }  // overflowed mailbox
+        // its cold fields did not fit the exchange's side buffer (gr_io.h side_pack)
+        if (!(cb & MB_UNIFORM) && (cb & MB_COLD_LOST)) { *at = item; return GR_ESC_CAPACITY; }
         InMsg m;
         read_msg(mb, cb, k, m);
         if (m.type == MT_WIDE) { *at = item; return GR_ESC_WIDE_TERM; }  // terms >= 2^32: host path

@@ -297,6 +297,10 @@ constexpr uint8_t MFL_N1 = 0x20;
 // so they touch neither the per-message tags and terms nor the cold chunk. Only
 // the lean lane writes uniform mailboxes; every other writer stores all fields.
 constexpr uint8_t MB_COUNT = 0x07, MB_UNIFORM = 0x08, MB_RESP = 0x10;
+// On a mailbox without MB_UNIFORM, bit 4 means its cold fields did not fit the
+// exchange's side buffer (gr_io.h side_pack): a reader escalates CAPACITY at its
+// first message instead of reading them (cross-GPU spaces only).
+constexpr uint8_t MB_COLD_LOST = 0x10;
 constexpr uint32_t MB_N1_SHIFT = 5, kUniformMax = 3;
 // A Replicate's Commit travels as a 32-bit offset from its LogIndex when
 // |Commit - LogIndex| < 2^31 (always, unless a follower lags by 2^31 entries);

@@ -233,6 +233,9 @@ struct TickLane {
     }
     const bool leader = state == GR_LEADER;
     GT_BAIL(!leader && state != GR_FOLLOWER);
+#pragma unroll
+    for (int j = 0; j < S; ++j)  // cold fields lost in the exchange (gr_io.h side_pack): general lane
+      GT_BAIL(cnt[j] && !(cbs[j] & MB_UNIFORM) && (cbs[j] & MB_COLD_LOST));
     GT_BAIL((lf & LF_PROPOSE_CC) || nq || np);
     // ---- round 2
     etick = s64(SR_ETICK);

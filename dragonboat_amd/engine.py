@@ -75,6 +75,13 @@ def load_library(path=LIB_PATH):
     lib.gr_space_tile_positions.argtypes = []
     lib.gr_space_cold_used.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p,
                                        c.POINTER(c.c_uint32)]
+    lib.gr_space_side_bytes.restype = c.c_uint64
+    lib.gr_space_side_bytes.argtypes = [c.c_uint32, c.c_uint32, c.c_uint32]
+    for f in ("gr_space_side_pack", "gr_space_side_unpack"):
+        getattr(lib, f).argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_uint32,
+                                    c.c_void_p]
+    for f in ("gr_space_side_pack_host", "gr_space_side_unpack_host"):
+        getattr(lib, f).argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_uint32]
     lib.gr_bind_routes.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32]
     lib.gr_set_locals.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_step_device.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32,
@@ -307,6 +314,20 @@ class Engine:
                                            ctypes.byref(v)), "gr_space_cold_used")
         return bool(v.value)
 
+    def side_bytes(self, n_chunks, depth, capacity):
+        """Bytes of the side buffers of n_chunks chunks (gr_space_side_bytes)."""
+        return int(self.lib.gr_space_side_bytes(n_chunks, depth, capacity))
+
+    def side_pack(self, space_ptr, n_chunks, positions, depth, side_ptr, capacity, stream=0):
+        """Compact the device space's cold fields into the side buffers, on `stream` (no wait)."""
+        _check(self.lib.gr_space_side_pack(space_ptr, n_chunks, positions, depth, side_ptr, capacity, stream),
+               "gr_space_side_pack")
+
+    def side_unpack(self, space_ptr, n_chunks, positions, depth, side_ptr, capacity, stream=0):
+        """Write received side-buffer entries into the device space's cold chunks, on `stream`."""
+        _check(self.lib.gr_space_side_unpack(space_ptr, n_chunks, positions, depth, side_ptr, capacity, stream),
+               "gr_space_side_unpack")
+
     def bind_routes(self, in_pos, out_pos):
         """in_pos/out_pos: uint32 arrays [slots][n_peers] (mailbox positions, 0xFFFFFFFF = none)."""
         in_pos = np.ascontiguousarray(in_pos, np.uint32)
@@ -331,10 +352,12 @@ class Engine:
         return out
 
 
-def decode_space(buf, n_chunks, positions, depth=MAILBOX_DEPTH):
+def decode_space(buf, n_chunks, positions, depth=MAILBOX_DEPTH, lost_ok=False):
     """Decode a host copy of a message space (bytes/uint8 array) into records.
 
-    peer = mailbox position, slot = index within the mailbox."""
+    peer = mailbox position, slot = index within the mailbox. A mailbox whose
+    cold fields were lost in the exchange decodes to records with reject 0xFF:
+    an error unless lost_ok."""
     lib = load_library()
     buf = np.ascontiguousarray(buf, np.uint8)
     n = ctypes.c_size_t()
@@ -344,4 +367,6 @@ def decode_space(buf, n_chunks, positions, depth=MAILBOX_DEPTH):
     if n.value:
         _check(lib.gr_space_decode(buf.ctypes.data, n_chunks, positions, depth, out.ctypes.data, n.value,
                                    ctypes.byref(n)), "decode")
+    if not lost_ok and np.any(out["reject"] == 0xFF):
+        raise RuntimeError("space holds mailboxes whose cold fields were lost in the exchange")
     return out

@@ -17,9 +17,12 @@ their outgoing messages straight into mailbox "spaces" in HBM:
   4 of N chunks for N ≥ 5, and the spaces hold depth-3 mailboxes (the steady
   state's two Replicates per follower per pass plus a heartbeat on a tick; a
   fourth message escalates CAPACITY). The hot region (counts + compact
-  Replicates + non-reject acks, 55 B per mailbox) crosses every pass; the cold
-  region (132 B per mailbox) only when some mailbox holds another kind of
-  message (gr_space_cold_used).
+  Replicates + non-reject acks, 41 B per depth-3 mailbox) crosses every pass;
+  the cold fields cross only for the mailboxes that need them, compacted on the
+  device into a fixed-capacity side buffer per chunk (gr_space_side_pack /
+  _unpack), so the all-to-all sizes are fixed and the host never waits on the
+  device inside the pass loop. A mailbox whose cold fields do not fit escalates
+  CAPACITY at its reader (detected one pass later, never silently lost).
 
 Peers on a rank are laid out replica-major: peer r*G + g is replica r of the
 group (home = (rank - r) % N, index g), so a wave's accesses stay contiguous.
@@ -41,6 +44,7 @@ def count_bytes(hot, n_chunks, hot_chunk, hot_tile, positions):
 
 
 TILE_W = 256  # gr_layout.h kTileW (GR_TILE_SHIFT = 8); Exchange checks it against the library
+SIDE_DIV, SIDE_MIN = 32, 1024  # side-buffer capacity per chunk: positions / SIDE_DIV, at least SIDE_MIN
 
 
 def pad_positions(positions):
@@ -153,16 +157,44 @@ class Exchange:
         assert nbytes == self.n_chunks * cb and 0 < hb < cb
         self.hot_region = self.n_chunks * hb  # hot chunks first, then the cold chunks
         self.hot_tile = eng.hot_tile_bytes(self.depth)  # positions tiled by 64, counts first in a tile
-        self.cold_exchanges = 0
         if self.placement == "spread":  # all_to_all split sizes, bytes per peer rank
             self.hot_splits = ([hb if d in self.dests else 0 for d in range(self.world)],
                                [hb if a in self.srcs else 0 for a in range(self.world)])
-            cold = cb - hb
-            self.cold_splits = ([cold if d in self.dests else 0 for d in range(self.world)],
-                                [cold if a in self.srcs else 0 for a in range(self.world)])
+            # side buffers: the cold fields of up to 1/32 of a chunk's mailboxes
+            # (at least 1024), a fixed size every pass
+            self.side_cap = max(SIDE_MIN, pad_positions(self.positions) // SIDE_DIV)
+            sb = eng.side_bytes(1, self.depth, self.side_cap)
+            self.side_splits = ([sb if d in self.dests else 0 for d in range(self.world)],
+                                [sb if a in self.srcs else 0 for a in range(self.world)])
+            self.side = [torch.zeros(self.n_chunks * sb, dtype=torch.uint8, device=device) for _ in range(2)]
         a = torch.zeros(nbytes, dtype=torch.uint8, device=device)
         b = torch.zeros(nbytes, dtype=torch.uint8, device=device)
         return [a, b]
+
+    def exchange(self, eng, spaces, h):
+        """Spread placement, after a pass on stream handle h: compact the out
+        space's cold fields, move the hot region and the side buffers (fixed
+        sizes), unpack the side buffers into the in space. Returns the pending
+        collective work (empty with one rank or a host backend)."""
+        inp, out = spaces
+        side_out, side_in = self.side
+        eng.side_pack(out.data_ptr(), self.n_chunks, self.positions, self.depth, side_out.data_ptr(),
+                      self.side_cap, h)
+        hr = self.hot_region
+        if self.world == 1:
+            inp[:hr].copy_(out[:hr])
+            side_in.copy_(side_out)
+            work = []
+        else:
+            work = [_all_to_all(inp[:hr], out[:hr], self.hot_splits[1], self.hot_splits[0]),
+                    _all_to_all(side_in, side_out, self.side_splits[1], self.side_splits[0])]
+        return work
+
+    def unpack(self, eng, spaces, h):
+        """Write the received side-buffer entries into the in space (after the
+        exchange's work has completed on stream h)."""
+        eng.side_unpack(spaces[0].data_ptr(), self.n_chunks, self.positions, self.depth, self.side[1].data_ptr(),
+                        self.side_cap, h)
 
     def step(self, eng, spaces, k, stream, events=None):
         """One pass: kernel (optionally bracketed by `events`), then the exchange."""
@@ -178,20 +210,9 @@ class Exchange:
         if events is not None:
             events[1].record(stream)
         if self.placement == "spread":
-            # the hot region always; the cold region only when a mailbox needs it
-            # (every steady-state message is hot-only: 37 B per depth-2 mailbox)
-            hr = self.hot_region
-            parts = [(slice(0, hr), self.hot_splits)]
-            if eng.cold_used(spaces[1].data_ptr(), self.n_chunks, self.positions, self.depth, h):
-                parts.append((slice(hr, None), self.cold_splits))
-                self.cold_exchanges += 1
-            for sl, (out_sp, in_sp) in parts:
-                if self.world > 1:
-                    import torch.distributed as dist
-                    dist.all_to_all_single(spaces[0][sl], spaces[1][sl], output_split_sizes=in_sp,
-                                           input_split_sizes=out_sp)
-                else:
-                    spaces[0][sl].copy_(spaces[1][sl])
+            for w in self.exchange(eng, spaces, h):
+                w.wait()
+            self.unpack(eng, spaces, h)
 
 
 def build_exchange(G, R, S, world, rank, placement, seed=2):
@@ -203,16 +224,15 @@ class Pipeline:
     `banks` independent engines, each with its own spaces and HIP stream, so
     one bank's all-to-all over xGMI overlaps the other bank's pass.
 
-    Per pass k, for every bank b on its stream s_b:
-      wait for bank b's exchange of pass k-1 (the NCCL work handle: a stream
-      wait, not a host wait) -> gr_step_device -> the cold-region check as a
-      device reduction copied into pinned host memory;
-    then, bank by bank, the host reads that flag (the other banks' passes are
-    queued or running meanwhile) and issues the bank's all_to_all_single on
-    s_b with async_op=True: the hot region always, the cold region only when a
-    mailbox needs it. RCCL waits only on s_b, so bank 0's exchange runs beside
-    bank 1's kernel and vice versa. With one rank the exchange is a device copy.
-    `local` placement is one bank whose two spaces ping-pong (no exchange).
+    Per pass k, for every bank b on its stream s_b: wait for bank b's exchange
+    of pass k-1 (the RCCL work handle: a stream wait, not a host wait) -> write
+    its side buffers into the in space -> gr_step_device -> compact the out
+    space's cold fields into the side buffers -> all_to_all_single of the hot
+    region and of the side buffers, async on s_b. Every size is fixed, so the
+    host issues the whole pass without reading anything back from the device.
+    RCCL waits only on s_b, so bank 0's exchange runs beside bank 1's kernel and
+    vice versa. With one rank the exchange is a device copy. `local` placement
+    is one bank whose two spaces ping-pong (no exchange).
     """
 
     def __init__(self, G, R, S, world, rank, placement="spread", banks=None, seed=2):
@@ -224,7 +244,6 @@ class Pipeline:
         self.groups = G
         self.engines, self.spaces, self.streams = [], [], []
         self.work = [[] for _ in self.ex]
-        self.cold_exchanges = 0
 
     @property
     def n_peers(self):
@@ -243,18 +262,6 @@ class Pipeline:
             self.engines.append(eng)
             self.spaces.append(ex.allocate(eng, device))
             self.streams.append(torch.cuda.Stream(device=device))
-        self.flag_host = torch.zeros(len(self.ex), dtype=torch.uint8, pin_memory=True)
-        self.events = [torch.cuda.Event() for _ in self.ex]
-
-    def _cold_flag(self, b):
-        """Device-side: does some mailbox of bank b's out space hold a message with
-        cold fields? (count bytes: nonzero count without MB_UNIFORM.)"""
-        ex, out = self.ex[b], self.spaces[b][1]
-        cnt = count_bytes(out[:ex.hot_region], ex.n_chunks, ex.hot_region // ex.n_chunks, ex.hot_tile,
-                          ex.positions)
-        cold = ((cnt & 7) != 0) & ((cnt & 8) == 0)
-        self.flag_host[b:b + 1].copy_(cold.any().view(1).to(self.flag_host.dtype), non_blocking=True)
-        self.events[b].record()
 
     def step(self, k):
         import torch
@@ -268,28 +275,21 @@ class Pipeline:
                     src, dst = self.spaces[b][k % 2], self.spaces[b][(k + 1) % 2]
                 else:
                     src, dst = self.spaces[b][0], self.spaces[b][1]
+                    ex.unpack(eng, self.spaces[b], s.cuda_stream)
                 eng.step_device(src.data_ptr(), dst.data_ptr(), ex.n_chunks, ex.positions, ex.n_chunks,
                                 ex.positions, ex.n_peers, s.cuda_stream, depth=ex.depth)
                 if ex.placement == "spread":
-                    self._cold_flag(b)
-        if self.placement != "spread":
-            return
-        for b, ex in enumerate(self.ex):
-            s = self.streams[b]
-            self.events[b].synchronize()
-            cold = bool(self.flag_host[b].item())
-            hr = ex.hot_region
-            inp, out = self.spaces[b]
-            parts = [(slice(0, hr), ex.hot_splits)]
-            if cold:
-                parts.append((slice(hr, None), ex.cold_splits))
-                self.cold_exchanges += 1
-            with torch.cuda.stream(s):
-                for sl, (out_sp, in_sp) in parts:
-                    if self.world == 1:
-                        inp[sl].copy_(out[sl])
-                    else:
-                        self.work[b].append(_all_to_all(inp[sl], out[sl], in_sp, out_sp))
+                    self.work[b] = ex.exchange(eng, self.spaces[b], s.cuda_stream)
+
+    def exchange_bytes_per_pass(self):
+        """Bytes this rank sends to other ranks per pass (hot regions + side
+        buffers of the chunks for other ranks; 0 for local placement)."""
+        tot = 0
+        for ex in self.ex:
+            if ex.placement == "spread":
+                tot += sum(n for d, n in zip(range(self.world), ex.hot_splits[0]) if d != self.rank)
+                tot += sum(n for d, n in zip(range(self.world), ex.side_splits[0]) if d != self.rank)
+        return tot
 
     def synchronize(self):
         import torch

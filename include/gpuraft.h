@@ -464,6 +464,27 @@ uint32_t gr_space_tile_positions(void);
  * and waits for it. */
 int gr_space_cold_used(gr_engine* e, const void* space, uint32_t n_chunks, uint32_t positions, uint32_t depth,
                        void* stream, uint32_t* out);
+/* Side buffers: how a space crosses GPUs without the host reading anything back
+ * (dragonboat_amd/exchange.py Pipeline). The hot region travels every pass; the
+ * cold fields travel only for the mailboxes that need them (count byte without
+ * bit 3), compacted by gr_space_side_pack into `capacity` entries per chunk. A
+ * mailbox that does not fit gets bit 4 (MB_COLD_LOST) in its count byte, and the
+ * lane that reads it escalates GR_ESC_CAPACITY at its first message.
+ * gr_space_side_unpack writes received entries into a space's cold chunks. Both
+ * run on `stream` (a hipStream_t) without waiting for it; the _host forms run the
+ * same codec over host memory (tests). gr_space_side_bytes: bytes of the side
+ * buffers of n_chunks chunks (one range per chunk, in chunk order, 0 when depth
+ * is not in 1..GR_C). The reference's role model: per-target message batching
+ * (internal/transport/transport.go:399-476). */
+uint64_t gr_space_side_bytes(uint32_t n_chunks, uint32_t depth, uint32_t capacity);
+int gr_space_side_pack(void* space, uint32_t n_chunks, uint32_t positions, uint32_t depth, void* side,
+                       uint32_t capacity, void* stream);
+int gr_space_side_unpack(void* space, uint32_t n_chunks, uint32_t positions, uint32_t depth, const void* side,
+                         uint32_t capacity, void* stream);
+int gr_space_side_pack_host(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
+                            void* side_host, uint32_t capacity);
+int gr_space_side_unpack_host(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
+                              const void* side_host, uint32_t capacity);
 int gr_bind_routes(gr_engine* e, const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n_peers);
 int gr_set_locals(gr_engine* e, const gr_local_input* locals, size_t n);
 /* Launch one pass on `stream` (a hipStream_t, may be NULL) without syncing.
@@ -474,7 +495,9 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
                    uint32_t depth, uint32_t n_peers, void* stream);
 /* Copy per-peer results of the last device pass for peers [first, first+n). */
 int gr_collect_results(gr_engine* e, uint32_t first, gr_peer_result* out, size_t n);
-/* Decode the messages of a device space into gr_message records (testing). */
+/* Decode the messages of a device space into gr_message records (testing). A
+ * mailbox whose cold fields were lost in the exchange (MB_COLD_LOST) decodes to
+ * records with reject = 0xFF and no other field. */
 int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
                     gr_message* out, size_t cap, size_t* n_out);
 int gr_space_encode(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,

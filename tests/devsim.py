@@ -82,6 +82,10 @@ def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None
             eng.set_locals(loc)
         ex.step(eng, spaces, k, stream)
         torch.cuda.synchronize()
+        if placement == "spread" and stats is not None:  # cold-field entries the side buffers carried
+            sb = len(ex.side[1]) // ex.n_chunks
+            hdr = ex.side[1].cpu().numpy().reshape(ex.n_chunks, sb)[:, :4].copy().view(np.uint32)[:, 0]
+            stats.setdefault("side_entries", []).append(int(hdr.sum()))
         o = pop.step(msgs, loc)
         res = eng.collect_results(n)
         assert not np.any(res["escalation"]), "unexpected escalation on the device path"
@@ -103,8 +107,6 @@ def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None
         assert not bad, f"pass {k}: results {bad[:3]}"
         msgs = want
     final = eng.sync(n)
-    if stats is not None:
-        stats["cold_exchanges"] = getattr(ex, "cold_exchanges", 0)
     eng.close()
     return final
 

@@ -185,14 +185,9 @@ def test_routes_not_affine_fall_back(built):
     assert hostlane_affine_routes(in_pos, out_pos, S) is None
 
 
-class _MockEngine:
-    """The C-ABI's space-size functions (CPU-callable) around a no-op pass: lets
-    Exchange.step's collective run over gloo on CPU tensors."""
-
-    def __init__(self, cold):
-        from dragonboat_amd.engine import load_library
-        self.lib = load_library()
-        self.cold = cold
+class _SideCodec:
+    """The C-ABI's space-size and side-buffer functions (host forms: the same
+    codec the device kernels run) for engines that step on the CPU."""
 
     def space_bytes(self, n, positions, depth):
         return int(self.lib.gr_space_bytes(n, positions, depth))
@@ -206,43 +201,114 @@ class _MockEngine:
     def hot_tile_bytes(self, depth):
         return int(self.lib.gr_space_hot_tile_bytes(depth))
 
+    def side_bytes(self, n_chunks, depth, cap):
+        return int(self.lib.gr_space_side_bytes(n_chunks, depth, cap))
+
+    def side_pack(self, ptr, n_chunks, positions, depth, side_ptr, cap, stream=0):
+        assert self.lib.gr_space_side_pack_host(ptr, n_chunks, positions, depth, side_ptr, cap) == 0
+
+    def side_unpack(self, ptr, n_chunks, positions, depth, side_ptr, cap, stream=0):
+        assert self.lib.gr_space_side_unpack_host(ptr, n_chunks, positions, depth, side_ptr, cap) == 0
+
+
+class _MockEngine(_SideCodec):
+    """A no-op pass: lets Exchange.step's collectives run over gloo on CPU tensors."""
+
+    def __init__(self):
+        from dragonboat_amd.engine import load_library
+        self.lib = load_library()
+
     def step_device(self, *a, **k):
         pass
 
-    def cold_used(self, *a, **k):
-        return self.cold
+
+def _encode_chunks(lib, ex, rank, out):
+    """Messages the 'kernel' of `rank` writes into its out space: per destination
+    chunk, uniform compact Replicates in some mailboxes and heartbeats (cold
+    fields) in others, each message tagged with (rank, destination, position).
+    Returns {dest rank: records with peer = position in chunk}."""
+    import ctypes
+    from dragonboat_amd import abi
+    want = {}
+    msgs, pos = [], []
+    pc = X.pad_positions(ex.positions)
+    for c, d in enumerate(ex.dests):
+        recs = []
+        for q in range(0, ex.positions, 7):
+            m = np.zeros(1, abi.MESSAGE)[0]
+            m["term"] = 5
+            if q % 3:
+                m["type"] = abi.REPLICATE
+                m["log_index"] = 1000 * rank + 10 * d + q
+                m["log_term"] = 5
+                m["commit"] = m["log_index"]
+            else:
+                m["type"] = abi.HEARTBEAT
+                m["commit"] = 7 + q
+                m["hint"] = (rank << 32) | (d << 16) | q
+                m["hint_high"] = q + 1
+            msgs.append(m)
+            pos.append(c * pc + q)
+            r = m.copy()
+            r["peer"] = q
+            recs.append(r)
+        want[d] = recs
+    msgs = np.array(msgs, abi.MESSAGE)
+    pos = np.array(pos, np.uint32)
+    buf = out.numpy()
+    assert lib.gr_space_encode(buf.ctypes.data, ex.n_chunks, ex.positions, ex.depth, msgs.ctypes.data, len(msgs),
+                               pos.ctypes.data) == 0
+    return want
 
 
-def _step_worker(rank, world, port, cold, q):
+def _step_worker(rank, world, port, side_min, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dragonboat_amd.engine import decode_space
 
     class _S:
         cuda_stream = 0
+    X.SIDE_MIN, X.SIDE_DIV = side_min, 1 << 30
     G, R = 40, 3
     ex = X.Exchange(G, R, R, world, rank, "spread")
-    eng = _MockEngine(cold)
+    eng = _MockEngine()
     spaces = ex.allocate(eng, torch.device("cpu"))
-    hr, n = ex.hot_region, ex.n_chunks
-    hb, cb = hr // n, len(spaces[1]) // n
-    out = spaces[1]
-    for c, d in enumerate(ex.dests):  # the kernel's writes: hot + cold part of chunk c (for rank d)
-        out[c * hb:(c + 1) * hb] = rank * 16 + d
-        out[hr + c * (cb - hb):hr + (c + 1) * (cb - hb)] = 128 + rank * 16 + d
+    mine = _encode_chunks(eng.lib, ex, rank, spaces[1])
+    # every rank's messages for every other rank, as the senders encoded them
+    allw = [None] * world
+    dist.all_gather_object(allw, {d: [tuple(int(x) for x in (m["peer"], m["type"], m["log_index"], m["commit"],
+                                                                m["hint"], m["hint_high"])) for m in v]
+                                  for d, v in mine.items()})
     ex.step(eng, spaces, 0, _S())
-    inp, errs = spaces[0], 0
-    for c, a in enumerate(ex.srcs):  # chunk c came from rank a
-        errs += int((inp[c * hb:(c + 1) * hb] != a * 16 + rank).sum())
-        want_cold = 128 + a * 16 + rank if cold else 0
-        errs += int((inp[hr + c * (cb - hb):hr + (c + 1) * (cb - hb)] != want_cold).sum())
-    q.put((rank, errs, ex.cold_exchanges))
+    got = decode_space(spaces[0].numpy().copy(), ex.n_chunks, ex.positions, ex.depth, lost_ok=True)
+    pc = X.pad_positions(ex.positions)
+    errs, lost = 0, 0
+    for c, a in enumerate(ex.srcs):  # in chunk c came from rank a
+        exp = {w[0]: w for w in allw[a][rank]}
+        seen = set()
+        for m in got:
+            if int(m["peer"]) // pc != c:
+                continue
+            qp = int(m["peer"]) % pc
+            if m["reject"] == 0xFF:  # cold fields lost: the count byte says so
+                lost += 1
+                seen.add(qp)
+                continue
+            t = (qp, int(m["type"]), int(m["log_index"]), int(m["commit"]), int(m["hint"]), int(m["hint_high"]))
+            errs += int(exp.get(qp) != t)
+            seen.add(qp)
+        errs += len(set(exp) - seen)
+    q.put((rank, errs, lost))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,cold", [(2, True), (3, False), (5, True)])
-def test_gloo_spread_step_regions(built, world, cold):
-    """Exchange.step over gloo: the hot region of every chunk reaches the rank it
-    was written for; the cold region travels only when gr_space_cold_used says so."""
+@pytest.mark.parametrize("world,side_min", [(2, 1024), (3, 1024), (5, 1024), (3, 2)])
+def test_gloo_spread_step_side_buffers(built, world, side_min):
+    """Exchange.step over gloo: every chunk's hot region reaches the rank it was
+    written for, and the cold fields of its non-uniform mailboxes (heartbeats)
+    arrive through the fixed-size side buffers. With a side capacity of 2 the
+    heartbeats beyond it are not lost silently: their count bytes carry
+    MB_COLD_LOST (a reading lane escalates CAPACITY)."""
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -250,17 +316,20 @@ def test_gloo_spread_step_regions(built, world, cold):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_step_worker, args=(r, world, port, cold, q)) for r in range(world)]
+    procs = [ctx.Process(target=_step_worker, args=(r, world, port, side_min, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
     for p in procs:
         p.join(timeout=60)
     assert all(e == 0 for _, e, _ in res), res
-    assert all(c == int(cold) for _, _, c in res), res
+    if side_min >= 1024:
+        assert all(lost == 0 for _, _, lost in res), res
+    else:
+        assert all(lost > 0 for _, _, lost in res), res
 
 
-class _HostlaneEngine:
+class _HostlaneEngine(_SideCodec):
     """A rank's engine for the CPU rehearsal of config 4: the kernels' lane code
     compiled for the host (hl_step) stepping the rank's replicas, reading and
     writing the same mailbox spaces (gr_space_decode/encode) that Exchange.step
@@ -277,18 +346,6 @@ class _HostlaneEngine:
         for j in range(ex.S):
             for p in np.nonzero(ex.in_pos[j] != X.NOPOS)[0]:
                 self.inv[int(ex.in_pos[j, p])] = (int(p), j)
-
-    def space_bytes(self, n, positions, depth):
-        return int(self.lib.gr_space_bytes(n, positions, depth))
-
-    def chunk_bytes(self, positions, depth):
-        return int(self.lib.gr_space_chunk_bytes(positions, depth))
-
-    def hot_chunk_bytes(self, positions, depth):
-        return int(self.lib.gr_space_hot_chunk_bytes(positions, depth))
-
-    def hot_tile_bytes(self, depth):
-        return int(self.lib.gr_space_hot_tile_bytes(depth))
 
     def step_device(self, in_ptr, out_ptr, in_chunks, in_positions, out_chunks, out_positions, n_peers, stream,
                     depth=3):
@@ -341,7 +398,7 @@ def _raft_worker(rank, world, port, G, passes, q):
     for k in range(passes):
         ex.step(eng, spaces, k, _S())
         states.append(eng.peers.copy())
-    q.put((rank, states, ex.cold_exchanges))
+    q.put((rank, states, 0))
     dist.destroy_process_group()
 
 

@@ -83,14 +83,87 @@ def test_split_pass_churn(gpu, mix, monkeypatch):
     assert st["injected"] > 0
 
 
-def test_spread_cold_region_on_demand(gpu):
-    """Spread exchange: hot region every pass, cold region only on passes whose
-    mailboxes hold heartbeats/acks (ticks every third pass); parity every pass."""
+def test_spread_cold_fields_by_side_buffer(gpu):
+    """Spread exchange: the hot region every pass, the cold fields of the
+    mailboxes that need them (heartbeats and their acks, ticks every third pass)
+    through the device-packed side buffers, with no host read-back; parity every
+    pass."""
     import devsim
     st = {}
     final = devsim.run_device(500, 3, 9, placement="spread", tick_every=3, stats=st)
     assert np.all(final["committed"][:500] > 2**32)
-    assert 0 < st["cold_exchanges"] < 9, st
+    used = [n > 0 for n in st["side_entries"]]
+    assert any(used) and not all(used), st
+
+
+def test_side_buffer_pack_unpack(gpu):
+    """gr_space_side_pack/_unpack on the device equal the host codec: the cold
+    fields of every non-uniform mailbox land in the target space, and the ones
+    beyond the capacity are marked MB_COLD_LOST."""
+    import torch
+    from dragonboat_amd import abi
+    from dragonboat_amd.engine import load_library, decode_space
+    lib = load_library()
+    n_chunks, positions, depth = 2, 4096, 3
+    nb = int(lib.gr_space_bytes(n_chunks, positions, depth))
+    rng = np.random.default_rng(4)
+    msgs, pos = [], []
+    pc = (positions + 255) // 256 * 256
+    for c in range(n_chunks):
+        for q in rng.choice(positions, 900, replace=False):
+            for k in range(int(rng.integers(1, depth + 1))):
+                m = np.zeros(1, abi.MESSAGE)[0]
+                m["term"] = 3
+                m["type"] = abi.HEARTBEAT if rng.random() < 0.6 else abi.REPLICATE
+                m["log_index"] = int(rng.integers(1, 2**40))
+                m["log_term"] = 3
+                m["commit"] = m["log_index"]
+                m["hint"] = int(rng.integers(0, 2**63))
+                m["hint_high"] = q
+                msgs.append(m)
+                pos.append(c * pc + int(q))
+    msgs = np.array(msgs, abi.MESSAGE)
+    order = np.argsort(np.array(pos), kind="stable")
+    msgs, pos = msgs[order], np.array(pos, np.uint32)[order]
+    src = np.zeros(nb, np.uint8)
+    assert lib.gr_space_encode(src.ctypes.data, n_chunks, positions, depth, msgs.ctypes.data, len(msgs),
+                               pos.ctypes.data) == 0
+    for cap in (4096, 100):
+        sb = int(lib.gr_space_side_bytes(n_chunks, depth, cap))
+        d_src = torch.from_numpy(src.copy()).cuda()
+        d_side = torch.zeros(sb, dtype=torch.uint8, device="cuda")
+        assert lib.gr_space_side_pack(d_src.data_ptr(), n_chunks, positions, depth, d_side.data_ptr(), cap, None) == 0
+        # the receiver: the hot region only, then the side buffers
+        hot = int(lib.gr_space_hot_chunk_bytes(positions, depth)) * n_chunks
+        d_dst = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+        d_dst[:hot] = d_src[:hot]
+        assert lib.gr_space_side_unpack(d_dst.data_ptr(), n_chunks, positions, depth, d_side.data_ptr(), cap,
+                                        None) == 0
+        torch.cuda.synchronize()
+        # host codec on the same input
+        h_src, h_side = src.copy(), np.zeros(sb, np.uint8)
+        assert lib.gr_space_side_pack_host(h_src.ctypes.data, n_chunks, positions, depth, h_side.ctypes.data,
+                                           cap) == 0
+        h_dst = np.zeros(nb, np.uint8)
+        h_dst[:hot] = h_src[:hot]
+        assert lib.gr_space_side_unpack_host(h_dst.ctypes.data, n_chunks, positions, depth, h_side.ctypes.data,
+                                             cap) == 0
+        got = decode_space(d_dst.cpu().numpy(), n_chunks, positions, depth, lost_ok=True)
+        want = decode_space(h_dst, n_chunks, positions, depth, lost_ok=True)
+        full = decode_space(src, n_chunks, positions, depth)
+        lost_d, lost_h = got["reject"] == 0xFF, want["reject"] == 0xFF
+        if cap == 4096:
+            assert not lost_d.any() and not lost_h.any()
+            assert np.array_equal(got, full) and np.array_equal(want, full)
+        else:
+            # the same number of mailboxes lost either way (which ones depends on
+            # the order of the device's appends); every delivered one exact
+            n_lost = lambda r: len(set(int(x) for x in r["peer"][r["reject"] == 0xFF]))  # mailboxes
+            assert n_lost(got) == n_lost(want) > 0
+            keep = ~lost_d
+            idx = {(int(m["peer"]), int(m["slot"])): m for m in full}
+            assert all(np.array_equal(np.array([idx[(int(m["peer"]), int(m["slot"]))]]), np.array([m]))
+                       for m in got[keep])
 
 
 def test_bench_runs(gpu):

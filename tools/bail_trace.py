@@ -103,6 +103,9 @@ def main():
     src = open(os.path.join(ROOT, "dragonboat_amd", "csrc", "gr_fast.h")).read().split("\n")
     print("first GF_BAIL per handed-over lane (gr_fast.h line: lanes/pass):")
     for k in np.argsort(-counts[:n].astype(np.int64)):
+        if lines[k] >= 100000:  # (type, flags) of a non-uniform mailbox a leader bailed on
+            print(f"  nonu type {(lines[k] - 100000) // 1000} flags {lines[k] % 1000:#x}: {counts[k] / npass:9.0f}")
+            continue
         print(f"  {lines[k]:4d}: {counts[k] / npass:9.0f}  {src[lines[k] - 1].strip()[:110]}")
     cov = snap() - cov0
     print("general / tick lane branch hits per pass:")
