@@ -109,6 +109,13 @@ class Outbox(ctypes.Structure):
                 ("results", ctypes.c_void_p), ("n_results", ctypes.c_size_t)]
 
 
+class WireUnrouted(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_size_t), ("index", ctypes.c_void_p), ("reason", ctypes.c_void_p)]
+
+
+WIRE_REASONS = ["routed", "no_peer", "nonmember", "snapshot", "type", "runs", "index"]
+
+
 class CInbox(ctypes.Structure):
     _fields_ = [("msgs", ctypes.c_void_p), ("n_msgs", ctypes.c_size_t),
                 ("ext_msgs", ctypes.c_void_p), ("n_ext_msgs", ctypes.c_size_t),
@@ -159,6 +166,7 @@ EXPORTS = [
     "gr_set_locals", "gr_step_device", "gr_step_compact", "gr_step_compact_begin", "gr_step_compact_end", "gr_cinbox_reserve", "gr_release_coutbox",
     "gr_pack_messages", "gr_unpack_messages", "gr_pack_locals",
     "gr_collect_results", "gr_space_decode", "gr_space_encode", "gr_timing_begin", "gr_timing_end",
+    "gr_bind_nodes", "gr_step_wire",
 ]
 
 

@@ -18,6 +18,7 @@
 #include "gr_host.h"
 #include "gr_io.h"
 #include "gr_kernels.h"
+#include "gpuraft_wire.h"
 
 namespace gr {
 
@@ -108,6 +109,11 @@ struct gr_engine {
   Buf d_ext, d_lext;        // gr_step_compact: ext message / local records
   Buf d_oc64, d_off64, d_rx, d_roff;  // compact outbox counts and offsets
   Buf d_outext, d_resext;   // compact outbox ext records
+  Buf d_nodes;              // gr_bind_nodes: (cluster, node) -> slot table
+  Buf d_wrec, d_why, d_unr; // gr_step_wire: routed records, per-message reason, unrouted indices
+  uint32_t nodes_cap = 0;
+  uint8_t* h_unr = nullptr;  // pinned: unrouted indices + reasons
+  size_t h_unr_bytes = 0;
   uint8_t* h_inmsgs = nullptr;   // pinned inbox the caller may fill in place (gr_inbox_reserve)
   uint8_t* h_inlocals = nullptr;
   size_t h_inmsgs_bytes = 0, h_inlocals_bytes = 0;
@@ -411,10 +417,10 @@ void gr_destroy(gr_engine* e) {
                             &e->d_idx, &e->d_skeys, &e->d_sidx, &e->d_win, &e->d_oc, &e->d_off, &e->d_tmp,
                             &e->d_scal, &e->d_outmsgs, &e->d_results, &e->d_peers, &e->d_slots, &e->d_ext,
                             &e->d_lext, &e->d_oc64, &e->d_off64, &e->d_rx, &e->d_roff, &e->d_outext,
-                            &e->d_resext})
+                            &e->d_resext, &e->d_nodes, &e->d_wrec, &e->d_why, &e->d_unr})
     if (b->p) (void)hipFree(b->p);
   for (uint8_t* h : {e->h_outmsgs, e->h_results, e->h_scal, e->h_inmsgs, e->h_inlocals, e->h_inext, e->h_inlext,
-                     e->h_outext, e->h_resext})
+                     e->h_outext, e->h_resext, e->h_unr})
     if (h) (void)hipHostFree(h);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
@@ -704,24 +710,20 @@ int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t position
   return n <= cap || !out ? GR_OK : GR_ECAPACITY;
 }
 
-int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
-  if (!e || !in || !out) return GR_EINVAL;
-  if ((in->n_msgs && !in->msgs) || (in->n_locals && !in->locals)) return GR_EINVAL;
-  if (in->n_msgs + in->n_locals >= 0x80000000ull) return GR_EINVAL;
-  std::lock_guard<std::mutex> guard(e->mu);
-  GR_REFUSE_PENDING(e);
+// The device pass of gr_step over nm gr_message records already in e->d_msgs
+// (copied from the host by gr_step, or routed from decoded wire records by
+// gr_step_wire) and nlc host local inputs. Caller holds e->mu.
+static int step_staged(gr_engine* e, uint32_t nm, const gr_local_input* locals, uint32_t nlc, gr_outbox* out) {
   out->msgs = nullptr;
   out->n_msgs = 0;
   out->results = nullptr;
   out->n_results = 0;
   const uint32_t S = e->S, cap = e->cfg.max_peers;
-  const uint32_t nm = (uint32_t)in->n_msgs, nlc = (uint32_t)in->n_locals;
   if (nm + nlc == 0) return GR_OK;
   const hipStream_t s = e->stream;
   const dim3 blk(io::kIoBlock);
   int r;
   // ---- inbox records -> lanes (gr_io.h)
-  if ((r = grow_device(&e->d_msgs.p, &e->d_msgs.n, (size_t)nm * sizeof(gr_message) + 1))) return r;
   if ((r = grow_device(&e->d_locals.p, &e->d_locals.n, (size_t)nlc * sizeof(gr_local_input) + 1))) return r;
   if ((r = grow_device(&e->d_mark.p, &e->d_mark.n, (size_t)cap * 4))) return r;
   if ((r = grow_device(&e->d_lop.p, &e->d_lop.n, (size_t)cap * 4))) return r;
@@ -732,9 +734,8 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
   uint32_t* scal = (uint32_t*)e->d_scal.p;
   const gr_message* dmsgs = (const gr_message*)e->d_msgs.p;
   const gr_local_input* dloc = (const gr_local_input*)e->d_locals.p;
-  if (nm) HIPCHK(hipMemcpyAsync(e->d_msgs.p, in->msgs, (size_t)nm * sizeof(gr_message), hipMemcpyHostToDevice, s));
   if (nlc)
-    HIPCHK(hipMemcpyAsync(e->d_locals.p, in->locals, (size_t)nlc * sizeof(gr_local_input), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(e->d_locals.p, locals, (size_t)nlc * sizeof(gr_local_input), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(mark, 0, (size_t)cap * 4, s));
   HIPCHK(hipMemsetAsync(scal, 0, 16, s));
   hipLaunchKernelGGL(io::mark_inputs, dim3(io_grid(nm + nlc)), blk, 0, s, dmsgs, nm, dloc, nlc, S, cap, mark,
@@ -828,6 +829,123 @@ int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
   out->results = (gr_peer_result*)e->h_results;
   out->n_results = nl;
   return GR_OK;
+}
+
+int gr_step(gr_engine* e, const gr_inbox* in, gr_outbox* out) {
+  if (!e || !in || !out) return GR_EINVAL;
+  if ((in->n_msgs && !in->msgs) || (in->n_locals && !in->locals)) return GR_EINVAL;
+  if (in->n_msgs + in->n_locals >= 0x80000000ull) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
+  const uint32_t nm = (uint32_t)in->n_msgs;
+  int r;
+  if ((r = grow_device(&e->d_msgs.p, &e->d_msgs.n, (size_t)nm * sizeof(gr_message) + 1))) return r;
+  if (nm)
+    HIPCHK(hipMemcpyAsync(e->d_msgs.p, in->msgs, (size_t)nm * sizeof(gr_message), hipMemcpyHostToDevice, e->stream));
+  return step_staged(e, nm, in->locals, (uint32_t)in->n_locals, out);
+}
+
+// ---------------------------------------------------------------- wire path
+// gr_bind_nodes: the (cluster id, node id) -> engine slot table the wire path
+// routes decoded messages with (open addressing, twice the slots, power of two).
+int gr_bind_nodes(gr_engine* e, const uint64_t* cluster_ids, const uint64_t* node_ids, uint32_t n) {
+  if (!e || (n && (!cluster_ids || !node_ids)) || n > e->cfg.max_peers) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
+  uint32_t tcap = 64;
+  while (tcap < 2 * n) tcap <<= 1;
+  std::vector<io::NodeKey> t(tcap);
+  for (uint32_t p = 0; p < n; ++p) {
+    uint32_t h = io::node_hash(cluster_ids[p], node_ids[p]) & (tcap - 1);
+    while (t[h].peer != NOPOS) {
+      if (t[h].cluster == cluster_ids[p] && t[h].node == node_ids[p]) return GR_EINVAL;  // listed twice
+      h = (h + 1) & (tcap - 1);
+    }
+    t[h].cluster = cluster_ids[p];
+    t[h].node = node_ids[p];
+    t[h].peer = p;
+  }
+  int r;
+  if ((r = grow_device(&e->d_nodes.p, &e->d_nodes.n, (size_t)tcap * sizeof(io::NodeKey)))) return r;
+  HIPCHK(hipMemcpy(e->d_nodes.p, t.data(), (size_t)tcap * sizeof(io::NodeKey), hipMemcpyHostToDevice));
+  e->nodes_cap = tcap;
+  return GR_OK;
+}
+
+extern "C++" template <int S>
+static void launch_route_wire(const grw_message* wm, uint32_t n, const grw_entry* we, uint64_t n_ents,
+                              const io::NodeKey* nodes, uint32_t tcap, StateBase st, gr_message* out,
+                              uint32_t* flag, uint8_t* why, hipStream_t s) {
+  hipLaunchKernelGGL((io::route_wire<S>), dim3(io_grid(n)), dim3(io::kIoBlock), 0, s, wm, n, we, n_ents, nodes, tcap,
+                     st, out, flag, why);
+}
+
+int gr_step_wire(gr_engine* e, const struct grw_message* d_msgs, size_t n_msgs, const struct grw_entry* d_ents,
+                 size_t n_ents, const gr_local_input* locals, size_t n_locals, gr_outbox* out,
+                 gr_wire_unrouted* unrouted) {
+  if (!e || !out || !unrouted || (n_msgs && !d_msgs) || (n_locals && !locals)) return GR_EINVAL;
+  if (n_msgs + n_locals >= 0x80000000ull) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
+  unrouted->n = 0;
+  unrouted->index = nullptr;
+  unrouted->reason = nullptr;
+  if (n_msgs && !e->nodes_cap) return GR_ESTATE;  // gr_bind_nodes first
+  const uint32_t nw = (uint32_t)n_msgs;
+  const hipStream_t s = e->stream;
+  const dim3 blk(io::kIoBlock);
+  int r;
+  if ((r = grow_device(&e->d_msgs.p, &e->d_msgs.n, (size_t)nw * sizeof(gr_message) + 1))) return r;
+  uint32_t nm = 0;
+  if (nw) {
+    // route every decoded message to (slot, sender slot) in a gr_message record,
+    // then keep the routed ones in wire order (their arrival order)
+    if ((r = grow_device(&e->d_wrec.p, &e->d_wrec.n, (size_t)nw * sizeof(gr_message)))) return r;
+    if ((r = grow_device(&e->d_keys.p, &e->d_keys.n, (size_t)nw * 4 + 4))) return r;
+    if ((r = grow_device(&e->d_idx.p, &e->d_idx.n, (size_t)nw * 4 + 4))) return r;
+    if ((r = grow_device(&e->d_why.p, &e->d_why.n, (size_t)nw + 1))) return r;
+    if ((r = grow_device(&e->d_unr.p, &e->d_unr.n, (size_t)nw * 4 + 4))) return r;
+    if ((r = grow_device(&e->d_scal.p, &e->d_scal.n, 16))) return r;
+    if ((r = grow_pinned(&e->h_scal, &e->h_scal_bytes, 16))) return r;
+    uint32_t* flag = (uint32_t*)e->d_keys.p;
+    uint32_t* pos = (uint32_t*)e->d_idx.p;
+    uint32_t* scal = (uint32_t*)e->d_scal.p;
+    switch (e->S) {
+      case 1: launch_route_wire<1>(d_msgs, nw, d_ents, n_ents, (const io::NodeKey*)e->d_nodes.p, e->nodes_cap, e->st,
+                                   (gr_message*)e->d_wrec.p, flag, (uint8_t*)e->d_why.p, s); break;
+      case 3: launch_route_wire<3>(d_msgs, nw, d_ents, n_ents, (const io::NodeKey*)e->d_nodes.p, e->nodes_cap, e->st,
+                                   (gr_message*)e->d_wrec.p, flag, (uint8_t*)e->d_why.p, s); break;
+      case 5: launch_route_wire<5>(d_msgs, nw, d_ents, n_ents, (const io::NodeKey*)e->d_nodes.p, e->nodes_cap, e->st,
+                                   (gr_message*)e->d_wrec.p, flag, (uint8_t*)e->d_why.p, s); break;
+      default: launch_route_wire<GR_SMAX>(d_msgs, nw, d_ents, n_ents, (const io::NodeKey*)e->d_nodes.p,
+                                          e->nodes_cap, e->st, (gr_message*)e->d_wrec.p, flag,
+                                          (uint8_t*)e->d_why.p, s); break;
+    }
+    HIPCHK(hipGetLastError());
+    if ((r = io_scan(e, flag, pos, nw, s))) return r;
+    hipLaunchKernelGGL(io::keep_routed, dim3(io_grid(nw)), blk, 0, s, (const gr_message*)e->d_wrec.p,
+                       (const uint32_t*)flag, (const uint32_t*)pos, nw, (gr_message*)e->d_msgs.p,
+                       (uint32_t*)e->d_unr.p, scal);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(e->h_scal, scal, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    nm = ((uint32_t*)e->h_scal)[0];
+    const uint32_t nu = nw - nm;
+    if (nu) {  // the messages the host steps with the Go code, in wire order, and why
+      if ((r = grow_pinned(&e->h_unr, &e->h_unr_bytes, (size_t)nu * 5))) return r;
+      uint32_t* hidx = (uint32_t*)e->h_unr;
+      uint8_t* hwhy = e->h_unr + (size_t)nu * 4;
+      HIPCHK(hipMemcpyAsync(hidx, e->d_unr.p, (size_t)nu * 4, hipMemcpyDeviceToHost, s));
+      std::vector<uint8_t> allwhy(nw);
+      HIPCHK(hipMemcpyAsync(allwhy.data(), e->d_why.p, nw, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      for (uint32_t k = 0; k < nu; ++k) hwhy[k] = allwhy[hidx[k]];
+      unrouted->n = nu;
+      unrouted->index = hidx;
+      unrouted->reason = hwhy;
+    }
+  }
+  return step_staged(e, nm, locals, (uint32_t)n_locals, out);
 }
 
 // gr_step with compact records (gpuraft.h gr_cmsg / gr_clocal / gr_cresult):

@@ -24,6 +24,7 @@
 // built or read. The codec functions are the same ones the test-only host
 // packer uses (gr_host.h), so the records are bit-identical.
 #pragma once
+#include "gpuraft_wire.h"
 #include "gr_host.h"
 
 namespace gr {
@@ -302,6 +303,118 @@ __global__ void cold_used(SpaceView v, uint32_t* flag) {
     const uint8_t c = v.at((uint32_t)g).cnt();
     const bool cold = (c & MB_COUNT) && !(c & MB_UNIFORM);
     if (__ballot(cold) && (threadIdx.x & 63) == 0) *flag = 1;
+  }
+}
+
+// ---------------------------------------------------------------- wire path
+// gr_step_wire: decoded raftpb.Message records (gpuraft_wire.h grw_message,
+// grw_entry, in HBM from grw_decode_device) become gr_message records on the
+// device: (ClusterID, To) -> engine slot through the gr_bind_nodes table, From
+// -> the sender's remote slot through the slot's RID rows, entries -> their
+// term runs. It replaces the transport's per-message handoff
+// (internal/transport/tcp.go:416-426 -> MessageBatch.Unmarshal,
+// raftpb/raft_optimized.go:1050) and the host packing of gr_message records.
+struct NodeKey {
+  uint64_t cluster = 0, node = 0;
+  uint32_t peer = NOPOS, pad = 0;
+};
+__host__ __device__ inline uint32_t node_hash(uint64_t c, uint64_t n) {
+  uint64_t x = c * 0x9E3779B97F4A7C15ull ^ (n + 0x632BE59BD9B4E019ull + (c << 6) + (c >> 2));
+  x ^= x >> 31;
+  x *= 0xBF58476D1CE4E5B9ull;
+  return (uint32_t)(x ^ (x >> 29));
+}
+// Why a message stays with the host (gpuraft.h gr_wire_reason).
+enum : uint8_t {
+  WR_ROUTED = 0, WR_NO_PEER = 1, WR_NONMEMBER = 2, WR_SNAPSHOT = 3, WR_TYPE = 4, WR_RUNS = 5, WR_INDEX = 6
+};
+
+template <int S>
+__global__ void route_wire(const grw_message* wm, uint32_t n, const grw_entry* we, uint64_t n_ents,
+                           const NodeKey* nodes, uint32_t tcap, StateBase st, gr_message* out, uint32_t* flag,
+                           uint8_t* why) {
+  using Rw = Rows<S>;
+  for (uint32_t i = io_tid(); i < n; i += io_stride()) {
+    const grw_message m = wm[i];
+    uint8_t w = WR_ROUTED;
+    uint32_t peer = NOPOS;
+    for (uint32_t h = node_hash(m.cluster_id, m.to) & (tcap - 1), probe = 0; probe < tcap;
+         h = (h + 1) & (tcap - 1), ++probe) {
+      const NodeKey k = nodes[h];
+      if (k.peer == NOPOS) break;
+      if (k.cluster == m.cluster_id && k.node == m.to) {
+        peer = k.peer;
+        break;
+      }
+    }
+    uint32_t slot = GR_SLOT_NONE;
+    if (peer == NOPOS) {
+      w = WR_NO_PEER;
+    } else {
+      const uint64_t rb = h_rb(st.u64(SR_HDR)[peer]);
+#pragma unroll
+      for (int j = 0; j < S; ++j)
+        if (slot == GR_SLOT_NONE && rb_kind(rb, (uint32_t)j) != GR_SLOT_EMPTY && st.u64(Rw::RID + j)[peer] == m.from)
+          slot = (uint32_t)j;
+      if (slot == GR_SLOT_NONE) w = WR_NONMEMBER;
+    }
+    if (w == WR_ROUTED && m.snapshot_host) w = WR_SNAPSHOT;
+    if (w == WR_ROUTED && (m.type < 0 || m.type > GR_TIMEOUT_NOW)) w = WR_TYPE;
+    gr_message r;
+    memset(&r, 0, sizeof(r));
+    if (w == WR_ROUTED) {
+      // entries -> at most two term runs; a Replicate's entries must be the
+      // consecutive indices LogIndex+1.. (raft.go:485-488), which the records imply
+      uint32_t runs = 0, run2 = 0;
+      uint64_t rt0 = 0, rt1 = 0;
+      bool cc = false, seq = true;
+      if ((uint64_t)m.first_entry + m.n_entries > n_ents) w = WR_RUNS;
+      for (uint32_t k = 0; w == WR_ROUTED && k < m.n_entries; ++k) {
+        const grw_entry en = we[m.first_entry + k];
+        cc = cc || en.type == 1;  // raftpb.ConfigChangeEntry
+        seq = seq && en.index == m.log_index + 1 + k;
+        if (k == 0) {
+          rt0 = en.term;
+          runs = 1;
+        } else if (en.term != (runs == 1 ? rt0 : rt1)) {
+          if (runs == 2) w = WR_RUNS;
+          runs = 2;
+          run2 = k;
+          rt1 = en.term;
+        }
+      }
+      if (w == WR_ROUTED && m.type == GR_REPLICATE && !seq) w = WR_INDEX;
+      r.peer = peer;
+      r.slot = (uint8_t)slot;
+      r.type = (uint8_t)m.type;
+      // a forwarded Propose carrying a config change travels with the reject bit
+      // (gpuraft.h, as Lane::propose forwards it)
+      r.reject = (uint8_t)((m.reject ? 1 : 0) | (m.type == GR_PROPOSE && cc ? 1 : 0));
+      r.n_runs = (uint8_t)runs;
+      r.n_entries = m.n_entries;
+      r.run2_offset = runs == 2 ? run2 : 0;
+      r.term = m.term;
+      r.log_index = m.log_index;
+      r.log_term = m.log_term;
+      r.commit = m.commit;
+      r.hint = m.hint;
+      r.hint_high = m.hint_high;
+      r.run_term[0] = rt0;
+      r.run_term[1] = rt1;
+    }
+    out[i] = r;
+    flag[i] = w == WR_ROUTED ? 1u : 0u;
+    why[i] = w;
+  }
+}
+// Routed records to the front in wire order, unrouted indices after (pos =
+// exclusive scan of flag); *n_routed = their count.
+__global__ void keep_routed(const gr_message* rec, const uint32_t* flag, const uint32_t* pos, uint32_t n,
+                            gr_message* out, uint32_t* unrouted, uint32_t* n_routed) {
+  for (uint32_t i = io_tid(); i < n; i += io_stride()) {
+    if (flag[i]) out[pos[i]] = rec[i];
+    else unrouted[i - pos[i]] = i;
+    if (i == n - 1) *n_routed = pos[i] + flag[i];
   }
 }
 

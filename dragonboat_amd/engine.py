@@ -83,6 +83,9 @@ def load_library(path=LIB_PATH):
     for f in ("gr_space_side_pack_host", "gr_space_side_unpack_host"):
         getattr(lib, f).argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_uint32]
     lib.gr_bind_routes.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32]
+    lib.gr_bind_nodes.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32]
+    lib.gr_step_wire.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t, c.c_void_p,
+                                 c.c_size_t, c.POINTER(abi.Outbox), c.POINTER(abi.WireUnrouted)]
     lib.gr_set_locals.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_step_device.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32,
                                    c.c_uint32, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p]
@@ -213,6 +216,38 @@ class Engine:
             ctypes.memmove(res.ctypes.data, ob.results, ob.n_results * abi.RESULT.itemsize)
         _check(self.lib.gr_release_outbox(self._h, ctypes.byref(ob)), "gr_release_outbox")
         return out, res
+
+    def bind_nodes(self, cluster_ids, node_ids):
+        """gr_bind_nodes: engine slot p is node node_ids[p] of cluster cluster_ids[p]."""
+        cl = np.ascontiguousarray(cluster_ids, np.uint64)
+        nd = np.ascontiguousarray(node_ids, np.uint64)
+        assert len(cl) == len(nd)
+        _check(self.lib.gr_bind_nodes(self._h, cl.ctypes.data if len(cl) else None,
+                                      nd.ctypes.data if len(nd) else None, len(cl)), "gr_bind_nodes")
+
+    def step_wire(self, d_msgs, n_msgs, d_ents, n_ents, locals_=None):
+        """gr_step_wire over decoded wire records already in HBM (device pointers, as
+        grw_decode_device leaves them). Returns (messages, results, unrouted
+        indices, unrouted reasons)."""
+        locals_ = np.zeros(0, abi.LOCAL) if locals_ is None else np.ascontiguousarray(locals_, abi.LOCAL)
+        ob = abi.Outbox()
+        un = abi.WireUnrouted()
+        _check(self.lib.gr_step_wire(self._h, d_msgs, n_msgs, d_ents, n_ents,
+                                     locals_.ctypes.data if len(locals_) else None, len(locals_), ctypes.byref(ob),
+                                     ctypes.byref(un)), "gr_step_wire")
+        idx = np.zeros(un.n, np.uint32)
+        why = np.zeros(un.n, np.uint8)
+        if un.n:
+            ctypes.memmove(idx.ctypes.data, un.index, un.n * 4)
+            ctypes.memmove(why.ctypes.data, un.reason, un.n)
+        out = np.zeros(ob.n_msgs, abi.MESSAGE)
+        res = np.zeros(ob.n_results, abi.RESULT)
+        if ob.n_msgs:
+            ctypes.memmove(out.ctypes.data, ob.msgs, ob.n_msgs * abi.MESSAGE.itemsize)
+        if ob.n_results:
+            ctypes.memmove(res.ctypes.data, ob.results, ob.n_results * abi.RESULT.itemsize)
+        _check(self.lib.gr_release_outbox(self._h, ctypes.byref(ob)), "gr_release_outbox")
+        return out, res, idx, why
 
     def pack_messages(self, msgs):
         """gr_pack_messages: full records -> (compact records, ext records)."""

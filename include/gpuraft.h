@@ -495,6 +495,39 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
                    uint32_t depth, uint32_t n_peers, void* stream);
 /* Copy per-peer results of the last device pass for peers [first, first+n). */
 int gr_collect_results(gr_engine* e, uint32_t first, gr_peer_result* out, size_t n);
+/* The wire path (SURVEY.md §8f-2 feeding the inbox): decoded raftpb.Message
+ * records (gpuraft_wire.h grw_message / grw_entry, device pointers as
+ * grw_decode_device leaves them in HBM) go straight into a gr_step pass, so the
+ * frames are the only bytes that crossed PCIe on the way in. It replaces the
+ * transport handing each message to its node (internal/transport/tcp.go:416-426
+ * -> MessageBatch.Unmarshal raftpb/raft_optimized.go:1050 -> the node's queue)
+ * and the host packing of gr_message records.
+ * gr_bind_nodes: engine slot p is node node_ids[p] of cluster cluster_ids[p]
+ * (n <= max_peers, every pair once). gr_step_wire routes every message by
+ * (ClusterID, To) to its slot and by From to the sender's remote slot, turns its
+ * entries into term runs, and runs gr_step's pass over the routed ones in wire
+ * order (their arrival order) plus the host's local inputs. The messages it
+ * cannot route stay with the host, listed in `unrouted` (engine-owned pinned
+ * arrays valid until the next call): wire index and gr_wire_reason. */
+enum gr_wire_reason {
+  GR_WIRE_ROUTED = 0, GR_WIRE_NO_PEER = 1,    /* no slot holds (ClusterID, To) */
+  GR_WIRE_NONMEMBER = 2,                       /* From is not a member (Peer.Handle, peer.go:200-209) */
+  GR_WIRE_SNAPSHOT = 3,                        /* a non-zero Snapshot (InstallSnapshot: host) */
+  GR_WIRE_TYPE = 4,                            /* not a type the engine steps */
+  GR_WIRE_RUNS = 5,                            /* entries span more than two term runs */
+  GR_WIRE_INDEX = 6                            /* a Replicate whose entries are not LogIndex+1.. */
+};
+typedef struct gr_wire_unrouted {
+  size_t n;
+  const uint32_t* index;  /* into the decoded message array */
+  const uint8_t* reason;  /* gr_wire_reason */
+} gr_wire_unrouted;
+struct grw_message;
+struct grw_entry;
+int gr_bind_nodes(gr_engine* e, const uint64_t* cluster_ids, const uint64_t* node_ids, uint32_t n);
+int gr_step_wire(gr_engine* e, const struct grw_message* d_msgs, size_t n_msgs, const struct grw_entry* d_ents,
+                 size_t n_ents, const gr_local_input* locals, size_t n_locals, gr_outbox* out,
+                 gr_wire_unrouted* unrouted);
 /* Decode the messages of a device space into gr_message records (testing). A
  * mailbox whose cold fields were lost in the exchange (MB_COLD_LOST) decodes to
  * records with reject = 0xFF and no other field. */

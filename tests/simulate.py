@@ -117,6 +117,36 @@ class GpuCompactHalvesBackend(GpuCompactBackend):
     halves = True
 
 
+class GpuWireBackend(GpuBackend):
+    """The wire path (gr_step_wire): the inbox records become MessageBatch frames
+    (tests/wirefeed.py, the senders' transports), the frames are the only inbox
+    bytes uploaded, libgrwire decodes them in HBM, and the engine routes the
+    decoded records straight into the pass. Every message must route (the
+    populations' messages are all between members)."""
+    cluster_of = None  # slot -> cluster id; default: replica-major groups (slot % G) + 1
+
+    def __init__(self, peers, slots, max_entry_size=abi.MAX_ENTRY_SIZE):
+        super().__init__(peers, slots, max_entry_size=max_entry_size)
+        import wirefeed
+        n = len(peers)
+        cl = self.cluster_of
+        if cl is None:
+            G = n // slots if slots and n % slots == 0 else n
+            cl = (np.arange(n) % G) + 1
+        self.feed = wirefeed.WireFeed(peers, cl)
+        self.eng.bind_nodes(cl, np.asarray(peers["node_id"], np.uint64))
+
+    def step(self, msgs, loc):
+        dm, nm, de, ne, keep = self.feed.decode(msgs)
+        out, res, idx, why = self.eng.step_wire(dm, nm, de, ne, loc)
+        assert len(idx) == 0, [abi.WIRE_REASONS[w] for w in why[:4]]
+        return out, res
+
+    def close(self):
+        self.feed.close()
+        super().close()
+
+
 def res_esc_free(res, n):
     """Peers that did not escalate this pass (their device state is the pass's)."""
     ok = np.ones(n, bool)
