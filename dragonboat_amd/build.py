@@ -95,7 +95,11 @@ def _hip_lib(out, srcs, deps, extra=(), force=False, scratch_check=True):
         return out
     odir = out + ".o.d"
     os.makedirs(odir, exist_ok=True)
+    # the lean lane's message loop (gr_fast.h: slots x messages, each able to
+    # broadcast) must unroll fully, or its per-slot arrays become scratch: the
+    # default pragma-unroll size limit (16K) is just below what S = 3 needs
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *extra,
+             "-mllvm", "-pragma-unroll-threshold=100000",
              "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
     objs = [os.path.join(odir, os.path.basename(s) + ".o") for s in srcs]
     with ThreadPoolExecutor(JOBS) as ex:

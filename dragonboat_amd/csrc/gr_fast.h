@@ -28,13 +28,15 @@ namespace gr {
 // (branch-light, no early exits: keeps the exec-mask nesting shallow) and
 // hands over at the end. Nothing but uncounted message bodies is stored
 // before `ok` is checked.
+// GF_BAIL re-reads `ok` after evaluating its condition: a condition that bails
+// itself (below_newest inside term_of) must not be overwritten by the outer one.
 #ifdef GR_BAIL_TRACE
 // Diagnostic host build of the lane code only (tools/bail_trace.py): counts, per
 // source line, the first steady-state condition that handed a lane over.
 void gr_bail_trace(int line);
-#define GF_BAIL(c) (ok = ok && !((c) ? (gr_bail_trace(__LINE__), true) : false))
+#define GF_BAIL(c) (ok = ok ? !((c) ? (gr_bail_trace(__LINE__), true) : false) && ok : false)
 #else
-#define GF_BAIL(c) (ok = ok && !(c))
+#define GF_BAIL(c) (ok = ok ? !(c) && ok : false)
 #endif
 
 // Lane roles a lean-lane instance is built for (gr_kernels.h launches one
@@ -100,7 +102,10 @@ struct FastLane {
   // emission
   uint32_t gout[S];
   uint32_t outc[S];
-  uint32_t n1out = 0;    // leader: bit 4j + k = out Replicate k of slot j carries an entry
+  uint32_t n1out = 0;    // leader: bit 8j + k = out Replicate k of slot j carries an entry
+  uint32_t fullout = 0;  // leader: bit 8j + k = out Replicate k of slot j is a full record (not compact)
+  uint64_t eub = 0;      // entry-size bound (a leader's multi-entry sends)
+  const uint64_t max_entry;  // StepParams::max_entry_size, read once
   uint32_t rejout = 0;   // follower: bit k = out ReplicateResp k is a reject (not uniform: tags written)
   uint32_t nmo = 0, nmi = 0, nent = 0;
   uint32_t lslot_out = 0;  // F_LSLOT after the pass (the wave hint)
@@ -109,7 +114,8 @@ struct FastLane {
   uint64_t append_from = 0;
   uint32_t prop_result = 0;
 
-  GF_HD FastLane(const StepParams& k, uint32_t lane, uint32_t peer) : kp(k), i(lane), p(peer) {}
+  GF_HD FastLane(const StepParams& k, uint32_t lane, uint32_t peer, uint64_t max_entry_size)
+      : max_entry(max_entry_size), kp(k), i(lane), p(peer) {}
 
   GF_HD uint64_t& s64(uint32_t row) const { return kp.st.u64(row)[p]; }
   GF_HD uint8_t& s8(uint32_t row) const { return kp.st.u8(row)[p]; }
@@ -134,20 +140,31 @@ struct FastLane {
     nruns++;
     pushed = true;
   }
-  // raft.send (raft.go:457-461) of a Replicate into slot j. The lean lane sends
-  // only what a uniform mailbox carries (a compact Replicate: LogTerm = Term, at
-  // most one entry at Term, narrow Commit); anything else is the general lane's.
+  // raft.send (raft.go:457-461) of a Replicate into slot j, as Lane::emit writes
+  // it: a compact Replicate (LogTerm = Term, at most one entry at Term) travels
+  // in the hot fields only (a uniform mailbox when all are compact); any other
+  // (a multi-entry catch-up, a LogTerm from the newest run's older term) also
+  // writes its tag, term, entry count, LogTerm and run term.
   GF_HD void emit_replicate(int j, uint64_t log_index, uint64_t log_term, uint32_t n, uint64_t rt0) {
-    GF_BAIL(gout[j] == NOPOS || outc[j] >= kp.out.depth || outc[j] >= kUniformMax);
-    GF_BAIL(wide_term(term, 0, 0, 0));  // GR_ESC_WIDE_TERM in the general lane
+    GF_BAIL(gout[j] == NOPOS || outc[j] >= kp.out.depth);
+    GF_BAIL(wide_term(term, log_term, n ? rt0 : 0, 0));  // GR_ESC_WIDE_TERM in the general lane
     uint32_t cd;
-    GF_BAIL(!commit_delta(committed, log_index, &cd) || log_term != term || (n && rt0 != term));  // n <= 1 here
+    GF_BAIL(!commit_delta(committed, log_index, &cd));  // a wide Commit: the general lane writes it
     if (!ok) return;
+    const bool compact = log_term == term && (n == 0 || (n == 1 && rt0 == term));
     const Mailbox mb = mout_at(gout[j]);
     const uint32_t c = outc[j];
-    n1out |= (n ? 1u : 0u) << (4 * j + c);  // MB_N1 bits: finish_out
+    n1out |= (n ? 1u : 0u) << (8 * j + c);  // MB_N1 bits: finish_out
     ntst(mb.u64(c, MF_LOG_INDEX), (uint64_t)(log_index));
     ntst(mb.t32(c, MT_CDELTA), (uint32_t)(cd));
+    if (!compact) {
+      fullout |= 1u << (8 * j + c);
+      ntst(mb.tag(c), (uint16_t)(GR_REPLICATE | ((uint32_t)((n ? 1u : 0u) << MFL_RUNS_SHIFT) << 8)));
+      ntst(mb.t32(c, MT_TERM), (uint32_t)term);
+      ntst(mb.n(c), n);
+      ntst(mb.t32(c, MT_LOG_TERM), (uint32_t)log_term);
+      if (n) ntst(mb.t32(c, MT_RT0), (uint32_t)rt0);
+    }
     outc[j] = c + 1;
     nmo++;
   }
@@ -166,22 +183,28 @@ struct FastLane {
   }
 
   // The count byte of out mailbox j, and the tags and terms its messages need:
-  // a leader's compact Replicates and a follower's accepts make a uniform mailbox
-  // (MB_UNIFORM, the term word, the entry bits); a follower's mailbox with a
-  // reject gets every tag and term.
+  // a leader's compact Replicates (at most kUniformMax) and a follower's accepts
+  // make a uniform mailbox (MB_UNIFORM, the term word, the entry bits); otherwise
+  // every message gets its tag and term (a leader's compact ones as MFL_COMPACT
+  // records, read_msg's form; its full records have theirs already).
   GF_HD void finish_out(int j, bool lead) {
     const uint32_t c = outc[j];
     uint32_t cb = c;
     if (c) {
       const Mailbox mb = mout_at(gout[j]);
-      if (lead || !rejout) {
-        cb |= MB_UNIFORM | (lead ? 0u : (uint32_t)MB_RESP) | (lead ? ((n1out >> (4 * j)) & 7u) << MB_N1_SHIFT : 0u);
+      const uint32_t fo = (fullout >> (8 * j)) & 0xFFu, n1 = (n1out >> (8 * j)) & 0xFFu;
+      if (lead ? (fo == 0 && c <= kUniformMax) : !rejout) {
+        cb |= MB_UNIFORM | (lead ? 0u : (uint32_t)MB_RESP) | (lead ? (n1 & 7u) << MB_N1_SHIFT : 0u);
         ntst(mb.mterm(), (uint32_t)term);
       } else {
 #pragma unroll
         for (uint32_t k = 0; k < (uint32_t)GR_C; ++k) {
-          if (k < c) {
-            ntst(mb.tag(k), (uint16_t)(GR_REPLICATE_RESP | (((rejout >> k) & 1u) ? (uint32_t)MFL_REJECT << 8 : 0u)));
+          if (k < c && !(lead && ((fo >> k) & 1u))) {
+            const uint32_t tg = lead ? GR_REPLICATE | ((uint32_t)(MFL_COMPACT | (((n1 >> k) & 1u)
+                                                                                ? MFL_N1 | (1u << MFL_RUNS_SHIFT)
+                                                                                : 0u)) << 8)
+                                     : GR_REPLICATE_RESP | (((rejout >> k) & 1u) ? (uint32_t)MFL_REJECT << 8 : 0u);
+            ntst(mb.tag(k), (uint16_t)tg);
             ntst(mb.t32(k, MT_TERM), (uint32_t)term);
           }
         }
@@ -234,9 +257,13 @@ struct FastLane {
       // nx <= rsn covers entries in an older run and nx <= firstIndex-1
       // (InstallSnapshot path): with H_GE_LO, nx > rsn implies nx > firstIndex-1
       GF_BAIL(nruns == 0 || below_newest(nx - 1));  // nx <= rsn
-      GF_BAIL(hi - nx + 1 > 1);         // several entries: MaxEntrySize check
+      const uint64_t cnt = hi - nx + 1;  // entries nx..hi, all in the newest run
+      // limitSize (entryutils.go:50-63) keeps all iff their sum fits (Lane::send_replicate)
+      // (cnt > max / eub as cnt * eub > max: exact while both are below 2^32; a
+      // bound of 4 GiB or more goes to the general lane)
+      GF_BAIL(cnt > 1 && (eub == 0 || (eub >> 32) != 0 || cnt > 0xFFFFFFFFull || cnt * eub > max_entry));
       GF_BAIL(rst(j) != GR_REPLICATE_ST && rst(j) != GR_RETRY);
-      n = 1;
+      n = (uint32_t)cnt;
       if (rst(j) == GR_REPLICATE_ST) {  // remote.progress, remote.go:120-128
         next[j] = hi + 1;
         mdirty |= 1u << j;
@@ -247,16 +274,27 @@ struct FastLane {
     }
     emit_replicate(j, nx - 1, lt, n, rtn);
   }
-  GF_HD void broadcast() {  // raft.go:534-546: voters (not self), then observers
-#pragma unroll
-    for (int j = 0; j < S; ++j)
-      if (rkind(j) == GR_SLOT_VOTER && (uint32_t)j != self) send_replicate(j);
+  GF_HD void broadcast_kind(uint32_t ob) {
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      if (rkind(j) == GR_SLOT_OBSERVER) {
-        GF_BAIL((uint32_t)j == self);
+      const bool v = rkind(j) == GR_SLOT_VOTER && (uint32_t)j != self;
+      const bool o = rkind(j) == GR_SLOT_OBSERVER;
+      if (ob ? o : v) {
+        GF_BAIL(ob && (uint32_t)j == self);
         send_replicate(j);
       }
+    }
+  }
+  GF_HD void broadcast() {  // raft.go:534-546: voters (not self), then observers
+    // one copy of send_replicate per slot: the voters / observers loop stays
+    // rolled (code size: this is inlined at every message); S = 1 unrolls it
+    // (rolled, its lane object does not stay in registers)
+    if constexpr (S == 1) {
+      broadcast_kind(0);
+      broadcast_kind(1);
+    } else {
+#pragma unroll 1
+      for (uint32_t ob = 0; ob < 2; ++ob) broadcast_kind(ob);
     }
   }
   // remote.tryUpdate (remote.go:108-118)
@@ -430,12 +468,13 @@ struct FastLane {
       return false;
     }
     const uint32_t np = lw & 0xFFFFu;
-    const uint32_t nq = (lw >> LW_QT_SHIFT) & LW_QT_MAX;
+    const uint32_t nq = (lw & LW_OTHER) ? 0u : (lw >> LW_QT_SHIFT) & LW_QT_MAX;
     uint64_t etick = 0;
     if (nq) etick = ntld(s64(SR_ETICK));
     // ---- round 2 (only where the hint did not match): leader remotes and messages
     if (kLeaderPath && leader) {
       rbw = h_rb(hdr) & ((1ull << (5 * S)) - 1);
+      eub = ntld(s64(SR_ENTRY_UB));
       // remote rows: stale ones (sync bits) from lastIndex, the rest loaded unless the hint did
       const uint64_t sb = kSync ? hdr : 0;
 #pragma unroll
@@ -539,7 +578,26 @@ struct FastLane {
           if ((nonu >> j) & 1u) gr_bail_trace(100000 + 1000 * (int)min_at(gin[j]).type(0) + min_at(gin[j]).flags(0));
       }
 #endif
-      GF_BAIL(nonu);
+      // a non-uniform mailbox (an old leader's Replicates after an election) is
+      // dropped whole when every message in it has a lower term (with checkQuorum,
+      // which may ask for a NoOP reply, the check below hands it over)
+      uint32_t ndrop = 0;
+      if (nonu) {
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          if ((nonu >> j) & 1u) {
+            GF_BAIL(cnt[j] > (uint32_t)MK || (cbs[j] & MB_COLD_LOST));
+            bool low = true;
+#pragma unroll
+            for (int k = 0; k < MK; ++k) {  // (a slot past the count reads a stale word, unused)
+              const uint32_t tm = ntld(min_at(gin[j]).t32(k, MT_TERM));
+              low = low && ((uint32_t)k >= cnt[j] || (tm != 0u && (uint64_t)tm < term));
+            }
+            GF_BAIL(!low);
+            ndrop |= 1u << j;
+          }
+        }
+      }
       // a uniform mailbox at a lower term is dropped whole (onMessageTermNotMatched,
       // raft.go:1014-1044), unless its messages are Replicates and checkQuorum asks
       // for a NoOP reply; the others must be uniform accepts (ReplicateResp, flags 0)
@@ -547,23 +605,26 @@ struct FastLane {
       uint32_t drop = 0;
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        const bool lower = cnt[j] && lmt[j] != 0u && (uint64_t)lmt[j] < term;
+        const bool lower = ((ndrop >> j) & 1u) || (cnt[j] && !((nonu >> j) & 1u) && lmt[j] != 0u && (uint64_t)lmt[j] < term);
         GF_BAIL(lower && !(cbs[j] & MB_RESP) && (flags & GR_F_CHECK_QUORUM));
         drop |= lower ? 1u << j : 0u;
         GF_BAIL(!lower && cnt[j] && (cnt[j] > (uint32_t)MK || !(cbs[j] & MB_RESP) || (uint64_t)lmt[j] != term));
       }
-      // messages in node.handleReceivedMessages order: slot, then arrival
+      // messages in node.handleReceivedMessages order: slot, then arrival; the
+      // position loop stays rolled (its slot is wave-uniform), so the message
+      // code is inlined once per slot, not once per slot and position
 #pragma unroll
-      for (int j = 0; j < S; ++j) {
-        if ((drop >> j) & 1u) {
-          nmi += cnt[j];
-          continue;
-        }
+      for (int j = 0; j < S; ++j) nmi += cnt[j];
+#pragma unroll 1
+      for (uint32_t q = 0; q < (uint32_t)(S * MK); ++q) {
+        const uint32_t qj = q / MK, qk = q % MK;
 #pragma unroll
-        for (int k = 0; k < MK; ++k) {
-          if ((uint32_t)k < cnt[j]) {
-            nmi++;
-            if (rkind(j) != GR_SLOT_EMPTY) replicate_resp(j, lidx[j][k]);
+        for (int j = 0; j < S; ++j) {
+          if ((uint32_t)j == qj && !((drop >> j) & 1u) && qk < cnt[j] && rkind(j) != GR_SLOT_EMPTY) {
+            uint64_t x = lidx[j][0];
+#pragma unroll
+            for (int k = 1; k < MK; ++k) x = qk == (uint32_t)k ? lidx[j][k] : x;
+            replicate_resp(j, x);
           }
         }
       }
@@ -571,15 +632,49 @@ struct FastLane {
     } else if (kFollowerPath) {
       // uniform compact Replicates (LogTerm = Term, at most one entry at Term,
       // narrow Commit) from one remote at the current term
-      GF_BAIL(nsrc > 1 || c > (uint32_t)MK || nonu || (c && ((cbL & MB_RESP) || (uint64_t)fmt != term)));
+      // the source's mailbox may hold full records (a leader's catch-up of several
+      // entries, or a LogTerm below its term: emit_replicate, Lane::emit); any
+      // other mailbox with messages must be uniform
+      const bool fullL = c && ((nonu >> L) & 1u);
+      GF_BAIL(nsrc > 1 || c > (uint32_t)MK || (nonu & ~(fullL ? 1u << L : 0u)) ||
+              (c && !fullL && ((cbL & MB_RESP) || (uint64_t)fmt != term)));
+      uint32_t ftag[MK], fterm[MK], fn[MK], flt[MK], frt[MK];
+      uint64_t fcw[MK];
+#pragma unroll
+      for (int k = 0; k < MK; ++k) {
+        ftag[k] = 0; fterm[k] = 0; fn[k] = 0; flt[k] = 0; frt[k] = 0; fcw[k] = 0;
+        if (fullL && (uint32_t)k < c) {  // read_msg's fields (gr_lane.h), one round
+          const Mailbox mb = min_at(gl);
+          ftag[k] = ntld(mb.tag(k));
+          fterm[k] = ntld(mb.t32(k, MT_TERM));
+          fn[k] = ntld(mb.n(k));
+          flt[k] = ntld(mb.t32(k, MT_LOG_TERM));
+          frt[k] = ntld(mb.t32(k, MT_RT0));
+          fcw[k] = ntld(mb.u64(k, MF_COMMIT));
+        }
+      }
       nmi += fdrop;
       uint32_t oc = 0;
 #pragma unroll
       for (int k = 0; k < MK; ++k) {
         if ((uint32_t)k < c) {
           nmi++;
-          const uint32_t n1 = (cbL >> (MB_N1_SHIFT + k)) & 1u;
-          replicate(fidx[k], term, commit_of(fcd[k], fidx[k]), n1, term, go, &oc);
+          if (fullL) {
+            const uint32_t fl = ftag[k] >> 8, runs = (fl >> MFL_RUNS_SHIFT) & 3u;
+            // Replicates at the current term with at most one term run; a reject,
+            // another type or two runs are the general lane's
+            GF_BAIL((ftag[k] & 0xFFu) != GR_REPLICATE || (fl & MFL_REJECT) || runs > 1 || (uint64_t)fterm[k] != term);
+            const bool cpt = fl & MFL_COMPACT;
+            const uint32_t n = cpt ? ((fl & MFL_N1) ? 1u : 0u) : fn[k];
+            GF_BAIL(!cpt && (n ? runs != 1 : runs != 0));
+            const uint64_t lt = cpt ? term : (uint64_t)flt[k];
+            const uint64_t rt = cpt ? term : (uint64_t)frt[k];
+            const uint64_t cm = (!cpt && (fl & MFL_WIDE_COMMIT)) ? fcw[k] : commit_of(fcd[k], fidx[k]);
+            replicate(fidx[k], lt, cm, n, n ? rt : 0, go, &oc);
+          } else {
+            const uint32_t n1 = (cbL >> (MB_N1_SHIFT + k)) & 1u;
+            replicate(fidx[k], term, commit_of(fcd[k], fidx[k]), n1, term, go, &oc);
+          }
         }
       }
 #pragma unroll
@@ -742,7 +837,7 @@ template <int S, int R = FL_ANY, int RM = RM_ANY>
 GF_HD bool lean_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, uint32_t* state = nullptr,
                      uint32_t hint = 0, uint32_t* hint_out = nullptr, int take = FL_ANY,
                      bool* skipped = nullptr) {
-  FastLane<S, R, RM> L(kp, i, p);
+  FastLane<S, R, RM> L(kp, i, p, kp.max_entry_size);
   const bool done = L.step(ls, hint, take);
   if (state) *state = L.state;
   if (hint_out) *hint_out = L.role_hint();

@@ -25,7 +25,7 @@ constexpr uint32_t kSplitMinLanes = 1u << 18;  // StepParams::split: role instan
 
 // Per-workgroup partial counters: row b of the stats block belongs to workgroup
 // b of whichever kernel runs (uncontended adds, no return value waited for).
-__device__ inline uint32_t wave_sum(uint32_t v) {
+__device__ inline __attribute__((always_inline)) uint32_t wave_sum(uint32_t v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
@@ -33,7 +33,7 @@ __device__ inline uint32_t wave_sum(uint32_t v) {
 // Each wave adds its own sums: the nine totals are wave-uniform after the
 // butterfly, lane k adds total k with a non-returning atomic. No LDS and no
 // barrier, so a wave never waits for the rest of its workgroup to finish.
-__device__ inline void block_stats(const StepParams& kp, const LaneStats& ls) {
+__device__ inline __attribute__((always_inline)) void block_stats(const StepParams& kp, const LaneStats& ls) {
   constexpr int N = 9;
   // one named field at a time: a register array indexed in a loop was put in scratch
   const uint32_t f0 = wave_sum(ls.leader_commit), f1 = wave_sum(ls.follower_commit),
@@ -89,7 +89,7 @@ __host__ __device__ inline uint64_t* wave_masks(uint32_t* bail_list, uint32_t ca
 
 // One wave's appends to bail list `list`: one returning atomic for the wave,
 // the wave's lanes contiguous and ascending.
-__device__ inline void bail_append(bool mine, uint32_t list, uint32_t* bail_list, uint32_t* counters,
+__device__ inline __attribute__((always_inline)) void bail_append(bool mine, uint32_t list, uint32_t* bail_list, uint32_t* counters,
                                    uint32_t list_cap, uint32_t i) {
   const uint64_t bm = __ballot(mine);
   if (!bm) return;
@@ -120,7 +120,7 @@ __device__ inline void bail_append(bool mine, uint32_t list, uint32_t* bail_list
 // mostly empty launch).
 // A wave-uniform 32-bit load through the scalar cache (constant address
 // space: s_load_dword). Only for data no wave of the running kernel writes.
-__device__ inline uint32_t sload_u32(const uint8_t* p) {
+__device__ inline __attribute__((always_inline)) uint32_t sload_u32(const uint8_t* p) {
   typedef const __attribute__((address_space(4))) uint32_t cu32;
   return *(cu32*)(uintptr_t)p;
 }
@@ -133,7 +133,7 @@ __device__ inline uint32_t sload_u32(const uint8_t* p) {
 // or a ReadIndex into 16..23, the tick kernel's: the later kernels walk their
 // lists in order, so their waves hold one kind of lane and diverge less), and
 // the stats.
-__device__ inline void wave_finish(const StepParams& kp, uint32_t i, uint32_t wave, bool mine, bool active,
+__device__ inline __attribute__((always_inline)) void wave_finish(const StepParams& kp, uint32_t i, uint32_t wave, bool mine, bool active,
                                    bool skip, bool bail, uint32_t role, uint32_t myhint, const LaneStats& ls,
                                    uint32_t* bail_list, uint32_t* counters, uint32_t list_cap) {
   if (kp.hints) {
@@ -161,7 +161,7 @@ __device__ inline void wave_finish(const StepParams& kp, uint32_t i, uint32_t wa
 // pass started is `hint` (wk = wave_kernel(hint)); mine = the wave is this
 // instance's. Steps the lane, then the wave's hint, bail lists and stats.
 template <int S, int R, int RM>
-__device__ inline void fast_wave(const StepParams& kp, uint32_t i, uint32_t wave, uint32_t hint, int wk, bool mine,
+__device__ inline __attribute__((always_inline)) void fast_wave(const StepParams& kp, uint32_t i, uint32_t wave, uint32_t hint, int wk, bool mine,
                                  uint32_t* bail_list, uint32_t* counters, uint32_t list_cap) {
   LaneStats ls;
   bool bail = false, skip = false;
@@ -182,7 +182,7 @@ __device__ inline void fast_wave(const StepParams& kp, uint32_t i, uint32_t wave
 }
 
 // Locate entry x of the 8 lists whose exclusive prefix is start[0..8]: list and offset.
-__device__ inline void list_at(const uint32_t (&start)[9], uint32_t x, uint32_t* l, uint32_t* off) {
+__device__ inline __attribute__((always_inline)) void list_at(const uint32_t (&start)[9], uint32_t x, uint32_t* l, uint32_t* off) {
   uint32_t ll = 0;
 #pragma unroll
   for (uint32_t k = 1; k < 8; ++k) ll = x >= start[k] ? k : ll;

@@ -248,11 +248,19 @@ constexpr uint8_t LF_PROPOSE_CC = 0x02;
 // of 13): bits 0-15 the ProposeEntries count, bits 17-24 the QuiescedTick
 // count, bit 16 set when there is anything else (ReadIndex, config change,
 // ticks, or a count that does not fit), which the lean lane hands over.
+// With bit 16 set, bit 26 (LW_TICKONLY) says the word still holds everything
+// the tick lane takes (gr_tick.h: no proposal, no QuiescedTick, no config
+// change): the Tick count in bits 17-24 and the ReadIndex flag in bit 25, so
+// that lane reads one word instead of four rows.
 constexpr uint32_t LW_OTHER = 0x10000u;
 constexpr uint32_t LW_QT_SHIFT = 17, LW_QT_MAX = 0xFFu;
+constexpr uint32_t LW_TICK_SHIFT = 17, LW_TICK_MAX = 0xFFu, LW_RI = 1u << 25, LW_TICKONLY = 1u << 26;
 __host__ __device__ inline uint32_t local_word(uint32_t ticks, uint32_t qticks, uint32_t propose, uint32_t lflags) {
   const bool other = ticks || lflags || propose > 0xFFFFu || qticks > LW_QT_MAX;
-  return other ? LW_OTHER : (propose | (qticks << LW_QT_SHIFT));
+  if (!other) return propose | (qticks << LW_QT_SHIFT);
+  if (!qticks && !propose && !(lflags & ~(uint32_t)LF_READ_INDEX) && ticks <= LW_TICK_MAX)
+    return LW_OTHER | LW_TICKONLY | (ticks << LW_TICK_SHIFT) | ((lflags & LF_READ_INDEX) ? LW_RI : 0u);
+  return LW_OTHER;
 }
 // Device-internal bits of the header's flags byte (never visible in gr_peer.flags:
 // gr_host.h masks them; GR_F_* use bits 0-2). They let the lean lane test one

@@ -27,7 +27,7 @@
 namespace gr {
 
 #define GT_HD __host__ __device__ inline __attribute__((always_inline))
-#define GT_BAIL(c) (ok = ok && !(c))
+#define GT_BAIL(c) (ok = ok ? !(c) && ok : false)
 
 GT_HD uint32_t gt_popc8(uint32_t x) {
   x &= 0xFFu;
@@ -215,12 +215,22 @@ struct TickLane {
     uint32_t lf = 0, nt = 0, nq = 0, np = 0;
     uint64_t rclo = 0, rchi = 0;
     if (kp.has_locals) {
-      lf = kp.ln.u8(LR_LFLAGS)[i];
-      nt = kp.ln.u32(LR_TICKS)[i];
-      nq = kp.ln.u32(LR_QTICKS)[i];
-      np = kp.ln.u32(LR_PROPOSE)[i];
-      rclo = kp.ln.u64(LR_RI_LO)[i];
-      rchi = kp.ln.u64(LR_RI_HI)[i];
+      // the packed word holds the whole input when it is ticks and a ReadIndex
+      // only (LW_TICKONLY): one row instead of four (gr_layout.h)
+      const uint32_t lw = kp.ln.u32(LR_LWORD)[i];
+      if (lw & LW_TICKONLY) {
+        nt = (lw >> LW_TICK_SHIFT) & LW_TICK_MAX;
+        lf = (lw & LW_RI) ? LF_READ_INDEX : 0u;
+      } else {
+        lf = kp.ln.u8(LR_LFLAGS)[i];
+        nt = kp.ln.u32(LR_TICKS)[i];
+        nq = kp.ln.u32(LR_QTICKS)[i];
+        np = kp.ln.u32(LR_PROPOSE)[i];
+      }
+      if (lf & LF_READ_INDEX) {
+        rclo = kp.ln.u64(LR_RI_LO)[i];
+        rchi = kp.ln.u64(LR_RI_HI)[i];
+      }
     }
     uint32_t gin[S], cnt[S], cbs[S];
 #pragma unroll
@@ -240,7 +250,7 @@ struct TickLane {
     // ---- round 2
     etick = s64(SR_ETICK);
     uint64_t retimeout = 0;
-    if (nruns) {  // the newest run: always the last row (right-aligned window)
+    if (nruns && leader && (lf & LF_READ_INDEX)) {  // the newest run (the last row): read_index's term test
       rsn = s64(SR_RUN_START + GR_K - 1);
       rtn = s64(SR_RUN_TERM + GR_K - 1);
     }
@@ -275,13 +285,16 @@ struct TickLane {
         ract[j] = rb_active(rb, j);
         rkind[j] = rb_kind(rb, j);
       }
+      // the FIFO's live entries only (entries at or past the count are never
+      // read: parity and the host compare the first read_index_count)
 #pragma unroll
       for (int q = 0; q < GR_Q; ++q) {
-        rii[q] = s64(Rw::RI_INDEX + q);
-        rilo[q] = s64(Rw::RI_LO + q);
-        rihi[q] = s64(Rw::RI_HI + q);
-        rifrom |= (uint32_t)s8(Rw::B_RIFROM + q) << (8 * q);
-        riack |= (uint32_t)s8(Rw::B_RIACK + q) << (8 * q);
+        const bool live = (uint32_t)q < ric;
+        rii[q] = live ? s64(Rw::RI_INDEX + q) : 0;
+        rilo[q] = live ? s64(Rw::RI_LO + q) : 0;
+        rihi[q] = live ? s64(Rw::RI_HI + q) : 0;
+        rifrom |= live ? (uint32_t)s8(Rw::B_RIFROM + q) << (8 * q) : 0u;
+        riack |= live ? (uint32_t)s8(Rw::B_RIACK + q) << (8 * q) : 0u;
       }
     } else {
       retimeout = s64(SR_RETIMEOUT);
@@ -400,11 +413,13 @@ struct TickLane {
       if (fifo_dirty) {
 #pragma unroll
         for (int q = 0; q < GR_Q; ++q) {
-          s64(Rw::RI_INDEX + q) = rii[q];
-          s64(Rw::RI_LO + q) = rilo[q];
-          s64(Rw::RI_HI + q) = rihi[q];
-          s8(Rw::B_RIFROM + q) = (uint8_t)(rifrom >> (8 * q));
-          s8(Rw::B_RIACK + q) = (uint8_t)(riack >> (8 * q));
+          if ((uint32_t)q < ric) {  // the live entries after the pass
+            s64(Rw::RI_INDEX + q) = rii[q];
+            s64(Rw::RI_LO + q) = rilo[q];
+            s64(Rw::RI_HI + q) = rihi[q];
+            s8(Rw::B_RIFROM + q) = (uint8_t)(rifrom >> (8 * q));
+            s8(Rw::B_RIACK + q) = (uint8_t)(riack >> (8 * q));
+          }
         }
       }
     }
