@@ -589,9 +589,11 @@ struct FastLane {
             GF_BAIL(cnt[j] > (uint32_t)MK || (cbs[j] & MB_COLD_LOST));
             bool low = true;
 #pragma unroll
-            for (int k = 0; k < MK; ++k) {  // (a slot past the count reads a stale word, unused)
-              const uint32_t tm = ntld(min_at(gin[j]).t32(k, MT_TERM));
-              low = low && ((uint32_t)k >= cnt[j] || (tm != 0u && (uint64_t)tm < term));
+            for (int k = 0; k < MK; ++k) {  // (a slot past the count reads stale words, unused)
+              // an MT_WIDE record (a term past 32 bits, gr_host.h encode_msg) has no term word
+              const Mailbox mb = min_at(gin[j]);
+              const uint32_t ty = ntld(mb.type(k)), tm = ntld(mb.t32(k, MT_TERM));
+              low = low && ((uint32_t)k >= cnt[j] || (ty != MT_WIDE && tm != 0u && (uint64_t)tm < term));
             }
             GF_BAIL(!low);
             ndrop |= 1u << j;
