@@ -191,8 +191,15 @@ extern "C" int hl_step(uint32_t slots, uint64_t max_entry_size, gr_peer* peers, 
       ln.out_pos()[(size_t)j * ln.lcap + l] = pk.out_pos[(size_t)j * nl + l];
     }
   }
-  std::vector<uint64_t> ibuf((space_total_bytes(1, pk.in_positions) + 7) / 8, 0);
+  // device mailboxes hold the previous pass's words wherever this pass writes
+  // none (encode_msg skips an MT_WIDE record's fields): fill the inbox with a
+  // pattern and zero only the count bytes, so a read of an unwritten word shows
+  std::vector<uint64_t> ibuf((space_total_bytes(1, pk.in_positions) + 7) / 8, 0x5A5A5A5A5A5A5A5Aull);
   std::vector<uint64_t> obuf((space_total_bytes(1, pk.out_positions) + 7) / 8, 0);
+  {
+    const SpaceView v = make_view(ibuf.data(), 1, pk.in_positions);
+    for (uint32_t g = 0; g < pk.in_positions; ++g) v.at(g).cnt() = 0;
+  }
   encode_inbox(in, pk, ibuf.data());
   StepParams kp;
   memset(&kp, 0, sizeof(kp));
