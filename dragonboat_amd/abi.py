@@ -166,7 +166,7 @@ EXPORTS = [
     "gr_set_locals", "gr_step_device", "gr_step_compact", "gr_step_compact_begin", "gr_step_compact_end", "gr_cinbox_reserve", "gr_release_coutbox",
     "gr_pack_messages", "gr_unpack_messages", "gr_pack_locals",
     "gr_collect_results", "gr_space_decode", "gr_space_encode", "gr_timing_begin", "gr_timing_end",
-    "gr_bind_nodes", "gr_step_wire",
+    "gr_bind_nodes", "gr_step_wire", "gr_step_wire_compact",
 ]
 
 

@@ -713,11 +713,19 @@ int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t position
 // The device pass of gr_step over nm gr_message records already in e->d_msgs
 // (copied from the host by gr_step, or routed from decoded wire records by
 // gr_step_wire) and nlc host local inputs. Caller holds e->mu.
-static int step_staged(gr_engine* e, uint32_t nm, const gr_local_input* locals, uint32_t nlc, gr_outbox* out) {
-  out->msgs = nullptr;
-  out->n_msgs = 0;
-  out->results = nullptr;
-  out->n_results = 0;
+static int pack_out_compact(gr_engine* e, uint32_t nl, const SpaceView& vout, gr_coutbox* out, PhaseClock* cl);
+
+// gr_step's device pipeline from inbox records in HBM (e->d_msgs); the outbox as
+// full records (out) or, with cout, as compact records (gr_step_wire_compact)
+static int step_staged(gr_engine* e, uint32_t nm, const gr_local_input* locals, uint32_t nlc, gr_outbox* out,
+                       gr_coutbox* cout = nullptr) {
+  if (out) {
+    out->msgs = nullptr;
+    out->n_msgs = 0;
+    out->results = nullptr;
+    out->n_results = 0;
+  }
+  if (cout) memset(cout, 0, sizeof(*cout));
   const uint32_t S = e->S, cap = e->cfg.max_peers;
   if (nm + nlc == 0) return GR_OK;
   const hipStream_t s = e->stream;
@@ -795,6 +803,10 @@ static int step_staged(gr_engine* e, uint32_t nm, const gr_local_input* locals, 
   e->passes++;
   e->locals_set = false;    // the lane rows now hold this pass's compact locals
   e->routes_bound = false;  // and RT_IDENTITY replaced the bound routes
+  if (cout) {
+    PhaseClock clk;
+    return pack_out_compact(e, nl, vout, cout, &clk);
+  }
   // ---- outbox mailboxes + lane results -> records
   if ((r = grow_device(&e->d_oc.p, &e->d_oc.n, (size_t)nl * 4))) return r;
   if ((r = grow_device(&e->d_off.p, &e->d_off.n, (size_t)nl * 4))) return r;
@@ -880,13 +892,12 @@ static void launch_route_wire(const grw_message* wm, uint32_t n, const grw_entry
                      st, out, flag, why);
 }
 
-int gr_step_wire(gr_engine* e, const struct grw_message* d_msgs, size_t n_msgs, const struct grw_entry* d_ents,
-                 size_t n_ents, const gr_local_input* locals, size_t n_locals, gr_outbox* out,
-                 gr_wire_unrouted* unrouted) {
-  if (!e || !out || !unrouted || (n_msgs && !d_msgs) || (n_locals && !locals)) return GR_EINVAL;
-  if (n_msgs + n_locals >= 0x80000000ull) return GR_EINVAL;
-  std::lock_guard<std::mutex> guard(e->mu);
-  GR_REFUSE_PENDING(e);
+// The wire path's routing half (gr_step_wire, gr_step_wire_compact): decoded
+// records -> routed gr_message records in e->d_msgs (*nm of them), the rest
+// listed in *unrouted. Called with e->mu held.
+static int wire_route(gr_engine* e, const struct grw_message* d_msgs, size_t n_msgs, const struct grw_entry* d_ents,
+                      size_t n_ents, gr_wire_unrouted* unrouted, uint32_t* nm_out) {
+  *nm_out = 0;
   unrouted->n = 0;
   unrouted->index = nullptr;
   unrouted->reason = nullptr;
@@ -945,7 +956,101 @@ int gr_step_wire(gr_engine* e, const struct grw_message* d_msgs, size_t n_msgs, 
       unrouted->reason = hwhy;
     }
   }
+  *nm_out = nm;
+  return GR_OK;
+}
+
+int gr_step_wire(gr_engine* e, const struct grw_message* d_msgs, size_t n_msgs, const struct grw_entry* d_ents,
+                 size_t n_ents, const gr_local_input* locals, size_t n_locals, gr_outbox* out,
+                 gr_wire_unrouted* unrouted) {
+  if (!e || !out || !unrouted || (n_msgs && !d_msgs) || (n_locals && !locals)) return GR_EINVAL;
+  if (n_msgs + n_locals >= 0x80000000ull) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
+  uint32_t nm;
+  int r;
+  if ((r = wire_route(e, d_msgs, n_msgs, d_ents, n_ents, unrouted, &nm))) return r;
   return step_staged(e, nm, locals, (uint32_t)n_locals, out);
+}
+
+int gr_step_wire_compact(gr_engine* e, const struct grw_message* d_msgs, size_t n_msgs,
+                         const struct grw_entry* d_ents, size_t n_ents, const gr_local_input* locals,
+                         size_t n_locals, gr_coutbox* out, gr_wire_unrouted* unrouted) {
+  if (!e || !out || !unrouted || (n_msgs && !d_msgs) || (n_locals && !locals)) return GR_EINVAL;
+  if (n_msgs + n_locals >= 0x80000000ull) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
+  uint32_t nm;
+  int r;
+  if ((r = wire_route(e, d_msgs, n_msgs, d_ents, n_ents, unrouted, &nm))) return r;
+  return step_staged(e, nm, locals, (uint32_t)n_locals, nullptr, out);
+}
+
+// The outbox mailboxes and lane results of the pass just launched, as compact
+// records (+ ext records where they do not fit), downloaded into engine-owned
+// pinned memory: gr_step_compact_end and gr_step_wire_compact.
+static int pack_out_compact(gr_engine* e, uint32_t nl, const SpaceView& vout, gr_coutbox* out, PhaseClock* cl) {
+  PhaseClock& clk = *cl;
+  const uint32_t S = e->S;
+  const hipStream_t s = e->stream;
+  const dim3 blk(io::kIoBlock);
+  int r;
+  uint32_t* scal = (uint32_t*)e->d_scal.p;
+  uint32_t* peer_of_lane = e->ln.u32(LR_LANE_PEER);
+  // ---- outbox mailboxes + lane results -> compact records (+ ext)
+  if ((r = grow_device(&e->d_oc64.p, &e->d_oc64.n, (size_t)nl * 8))) return r;
+  if ((r = grow_device(&e->d_off64.p, &e->d_off64.n, (size_t)nl * 8))) return r;
+  if ((r = grow_device(&e->d_rx.p, &e->d_rx.n, (size_t)nl * 4))) return r;
+  if ((r = grow_device(&e->d_roff.p, &e->d_roff.n, (size_t)nl * 4))) return r;
+  if ((r = grow_device(&e->d_results.p, &e->d_results.n, (size_t)nl * sizeof(gr_cresult)))) return r;
+  uint64_t* oc = (uint64_t*)e->d_oc64.p;
+  uint64_t* off = (uint64_t*)e->d_off64.p;
+  uint32_t* rx = (uint32_t*)e->d_rx.p;
+  uint32_t* roff = (uint32_t*)e->d_roff.p;
+  hipLaunchKernelGGL(io::out_counts_c, dim3(io_grid(nl)), blk, 0, s, vout, e->ln, nl, S, oc, rx);
+  HIPCHK(hipGetLastError());
+  if ((r = io_scan64(e, oc, off, nl, s))) return r;
+  if ((r = io_scan(e, rx, roff, nl, s))) return r;
+  hipLaunchKernelGGL(io::finish_total_c, dim3(1), dim3(64), 0, s, (const uint64_t*)oc, (const uint64_t*)off,
+                     (const uint32_t*)rx, (const uint32_t*)roff, nl, scal + 1);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->h_scal + 4, scal + 1, 12, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  clk.mark("mailboxes+pass+counts");
+  const uint32_t total = ((uint32_t*)e->h_scal)[1], text = ((uint32_t*)e->h_scal)[2], rext = ((uint32_t*)e->h_scal)[3];
+  const size_t mbytes = (size_t)total * sizeof(gr_cmsg), xbytes = (size_t)text * sizeof(gr_message);
+  const size_t rbytes = (size_t)nl * sizeof(gr_cresult), rxbytes = (size_t)rext * sizeof(gr_peer_result);
+  if ((r = grow_device(&e->d_outmsgs.p, &e->d_outmsgs.n, mbytes + 1))) return r;
+  if ((r = grow_device(&e->d_outext.p, &e->d_outext.n, xbytes + 1))) return r;
+  if ((r = grow_device(&e->d_resext.p, &e->d_resext.n, rxbytes + 1))) return r;
+  if ((r = grow_pinned(&e->h_outmsgs, &e->h_outmsgs_bytes, mbytes + 1))) return r;
+  if ((r = grow_pinned(&e->h_outext, &e->h_outext_bytes, xbytes + 1))) return r;
+  if ((r = grow_pinned(&e->h_results, &e->h_results_bytes, rbytes))) return r;
+  if ((r = grow_pinned(&e->h_resext, &e->h_resext_bytes, rxbytes + 1))) return r;
+  hipLaunchKernelGGL(io::pack_results_c, dim3(io_grid(nl)), blk, 0, s, e->ln, e->st, (const uint32_t*)peer_of_lane,
+                     nl, (const uint32_t*)roff, (gr_cresult*)e->d_results.p, (gr_peer_result*)e->d_resext.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->h_results, e->d_results.p, rbytes, hipMemcpyDeviceToHost, s));
+  if (rext) HIPCHK(hipMemcpyAsync(e->h_resext, e->d_resext.p, rxbytes, hipMemcpyDeviceToHost, s));
+  if (total) {
+    hipLaunchKernelGGL(io::pack_outbox_c, dim3(io_grid(nl)), blk, 0, s, vout, nl, S, (const uint64_t*)off,
+                       (const uint32_t*)peer_of_lane, (gr_cmsg*)e->d_outmsgs.p, (gr_message*)e->d_outext.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(e->h_outmsgs, e->d_outmsgs.p, mbytes, hipMemcpyDeviceToHost, s));
+    if (text) HIPCHK(hipMemcpyAsync(e->h_outext, e->d_outext.p, xbytes, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  clk.mark("pack+download");
+  clk.report();
+  out->msgs = total ? (gr_cmsg*)e->h_outmsgs : nullptr;
+  out->n_msgs = total;
+  out->ext_msgs = text ? (gr_message*)e->h_outext : nullptr;
+  out->n_ext_msgs = text;
+  out->results = (gr_cresult*)e->h_results;
+  out->n_results = nl;
+  out->ext_results = rext ? (gr_peer_result*)e->h_resext : nullptr;
+  out->n_ext_results = rext;
+  return GR_OK;
 }
 
 // gr_step with compact records (gpuraft.h gr_cmsg / gr_clocal / gr_cresult):
@@ -1097,59 +1202,7 @@ int gr_step_compact_end(gr_engine* e, gr_coutbox* out) {
   e->passes++;
   e->locals_set = false;
   e->routes_bound = false;
-  // ---- outbox mailboxes + lane results -> compact records (+ ext)
-  if ((r = grow_device(&e->d_oc64.p, &e->d_oc64.n, (size_t)nl * 8))) return r;
-  if ((r = grow_device(&e->d_off64.p, &e->d_off64.n, (size_t)nl * 8))) return r;
-  if ((r = grow_device(&e->d_rx.p, &e->d_rx.n, (size_t)nl * 4))) return r;
-  if ((r = grow_device(&e->d_roff.p, &e->d_roff.n, (size_t)nl * 4))) return r;
-  if ((r = grow_device(&e->d_results.p, &e->d_results.n, (size_t)nl * sizeof(gr_cresult)))) return r;
-  uint64_t* oc = (uint64_t*)e->d_oc64.p;
-  uint64_t* off = (uint64_t*)e->d_off64.p;
-  uint32_t* rx = (uint32_t*)e->d_rx.p;
-  uint32_t* roff = (uint32_t*)e->d_roff.p;
-  hipLaunchKernelGGL(io::out_counts_c, dim3(io_grid(nl)), blk, 0, s, vout, e->ln, nl, S, oc, rx);
-  HIPCHK(hipGetLastError());
-  if ((r = io_scan64(e, oc, off, nl, s))) return r;
-  if ((r = io_scan(e, rx, roff, nl, s))) return r;
-  hipLaunchKernelGGL(io::finish_total_c, dim3(1), dim3(64), 0, s, (const uint64_t*)oc, (const uint64_t*)off,
-                     (const uint32_t*)rx, (const uint32_t*)roff, nl, scal + 1);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(e->h_scal + 4, scal + 1, 12, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  clk.mark("mailboxes+pass+counts");
-  const uint32_t total = ((uint32_t*)e->h_scal)[1], text = ((uint32_t*)e->h_scal)[2], rext = ((uint32_t*)e->h_scal)[3];
-  const size_t mbytes = (size_t)total * sizeof(gr_cmsg), xbytes = (size_t)text * sizeof(gr_message);
-  const size_t rbytes = (size_t)nl * sizeof(gr_cresult), rxbytes = (size_t)rext * sizeof(gr_peer_result);
-  if ((r = grow_device(&e->d_outmsgs.p, &e->d_outmsgs.n, mbytes + 1))) return r;
-  if ((r = grow_device(&e->d_outext.p, &e->d_outext.n, xbytes + 1))) return r;
-  if ((r = grow_device(&e->d_resext.p, &e->d_resext.n, rxbytes + 1))) return r;
-  if ((r = grow_pinned(&e->h_outmsgs, &e->h_outmsgs_bytes, mbytes + 1))) return r;
-  if ((r = grow_pinned(&e->h_outext, &e->h_outext_bytes, xbytes + 1))) return r;
-  if ((r = grow_pinned(&e->h_results, &e->h_results_bytes, rbytes))) return r;
-  if ((r = grow_pinned(&e->h_resext, &e->h_resext_bytes, rxbytes + 1))) return r;
-  hipLaunchKernelGGL(io::pack_results_c, dim3(io_grid(nl)), blk, 0, s, e->ln, e->st, (const uint32_t*)peer_of_lane,
-                     nl, (const uint32_t*)roff, (gr_cresult*)e->d_results.p, (gr_peer_result*)e->d_resext.p);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(e->h_results, e->d_results.p, rbytes, hipMemcpyDeviceToHost, s));
-  if (rext) HIPCHK(hipMemcpyAsync(e->h_resext, e->d_resext.p, rxbytes, hipMemcpyDeviceToHost, s));
-  if (total) {
-    hipLaunchKernelGGL(io::pack_outbox_c, dim3(io_grid(nl)), blk, 0, s, vout, nl, S, (const uint64_t*)off,
-                       (const uint32_t*)peer_of_lane, (gr_cmsg*)e->d_outmsgs.p, (gr_message*)e->d_outext.p);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(e->h_outmsgs, e->d_outmsgs.p, mbytes, hipMemcpyDeviceToHost, s));
-    if (text) HIPCHK(hipMemcpyAsync(e->h_outext, e->d_outext.p, xbytes, hipMemcpyDeviceToHost, s));
-  }
-  HIPCHK(hipStreamSynchronize(s));
-  clk.mark("pack+download");
-  clk.report();
-  out->msgs = total ? (gr_cmsg*)e->h_outmsgs : nullptr;
-  out->n_msgs = total;
-  out->ext_msgs = text ? (gr_message*)e->h_outext : nullptr;
-  out->n_ext_msgs = text;
-  out->results = (gr_cresult*)e->h_results;
-  out->n_results = nl;
-  out->ext_results = rext ? (gr_peer_result*)e->h_resext : nullptr;
-  out->n_ext_results = rext;
+  if ((r = pack_out_compact(e, nl, vout, out, &clk))) return r;
   return GR_OK;
 }
 

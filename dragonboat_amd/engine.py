@@ -86,6 +86,8 @@ def load_library(path=LIB_PATH):
     lib.gr_bind_nodes.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32]
     lib.gr_step_wire.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t, c.c_void_p,
                                  c.c_size_t, c.POINTER(abi.Outbox), c.POINTER(abi.WireUnrouted)]
+    lib.gr_step_wire_compact.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t, c.c_void_p,
+                                         c.c_size_t, c.POINTER(abi.COutbox), c.POINTER(abi.WireUnrouted)]
     lib.gr_set_locals.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
     lib.gr_step_device.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32,
                                    c.c_uint32, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p]
@@ -225,21 +227,25 @@ class Engine:
         _check(self.lib.gr_bind_nodes(self._h, cl.ctypes.data if len(cl) else None,
                                       nd.ctypes.data if len(nd) else None, len(cl)), "gr_bind_nodes")
 
-    def step_wire(self, d_msgs, n_msgs, d_ents, n_ents, locals_=None):
+    def step_wire(self, d_msgs, n_msgs, d_ents, n_ents, locals_=None, compact=False):
         """gr_step_wire over decoded wire records already in HBM (device pointers, as
         grw_decode_device leaves them). Returns (messages, results, unrouted
-        indices, unrouted reasons)."""
+        indices, unrouted reasons); with compact=True gr_step_wire_compact, whose
+        outbox is returned as step_compact returns it: ((cmsgs, ext msgs, cresults,
+        ext results), unrouted indices, unrouted reasons)."""
         locals_ = np.zeros(0, abi.LOCAL) if locals_ is None else np.ascontiguousarray(locals_, abi.LOCAL)
-        ob = abi.Outbox()
+        ob = abi.COutbox() if compact else abi.Outbox()
         un = abi.WireUnrouted()
-        _check(self.lib.gr_step_wire(self._h, d_msgs, n_msgs, d_ents, n_ents,
-                                     locals_.ctypes.data if len(locals_) else None, len(locals_), ctypes.byref(ob),
-                                     ctypes.byref(un)), "gr_step_wire")
+        fn = self.lib.gr_step_wire_compact if compact else self.lib.gr_step_wire
+        _check(fn(self._h, d_msgs, n_msgs, d_ents, n_ents, locals_.ctypes.data if len(locals_) else None,
+                  len(locals_), ctypes.byref(ob), ctypes.byref(un)), fn.__name__)
         idx = np.zeros(un.n, np.uint32)
         why = np.zeros(un.n, np.uint8)
         if un.n:
             ctypes.memmove(idx.ctypes.data, un.index, un.n * 4)
             ctypes.memmove(why.ctypes.data, un.reason, un.n)
+        if compact:
+            return self._take_coutbox(ob), idx, why
         out = np.zeros(ob.n_msgs, abi.MESSAGE)
         res = np.zeros(ob.n_results, abi.RESULT)
         if ob.n_msgs:
@@ -290,6 +296,10 @@ class Engine:
             _check(self.lib.gr_step_compact_end(self._h, ctypes.byref(ob)), "gr_step_compact_end")
         else:
             _check(self.lib.gr_step_compact(self._h, ctypes.byref(ib), ctypes.byref(ob)), "gr_step_compact")
+        return self._take_coutbox(ob)
+
+    def _take_coutbox(self, ob):
+        """(cmsgs, ext msgs, cresults, ext results) copied out of a gr_coutbox, released."""
         out = []
         for ptr, n, dt in ((ob.msgs, ob.n_msgs, abi.CMSG), (ob.ext_msgs, ob.n_ext_msgs, abi.MESSAGE),
                            (ob.results, ob.n_results, abi.CRESULT), (ob.ext_results, ob.n_ext_results, abi.RESULT)):

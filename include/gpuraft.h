@@ -528,6 +528,12 @@ int gr_bind_nodes(gr_engine* e, const uint64_t* cluster_ids, const uint64_t* nod
 int gr_step_wire(gr_engine* e, const struct grw_message* d_msgs, size_t n_msgs, const struct grw_entry* d_ents,
                  size_t n_ents, const gr_local_input* locals, size_t n_locals, gr_outbox* out,
                  gr_wire_unrouted* unrouted);
+/* gr_step_wire with the outbox and results as compact records (gr_coutbox, as
+ * gr_step_compact returns them: 24-B gr_cmsg / 40-B gr_cresult, full records as
+ * ext only where they do not fit); release with gr_release_coutbox. */
+int gr_step_wire_compact(gr_engine* e, const struct grw_message* d_msgs, size_t n_msgs,
+                         const struct grw_entry* d_ents, size_t n_ents, const gr_local_input* locals,
+                         size_t n_locals, gr_coutbox* out, gr_wire_unrouted* unrouted);
 /* Decode the messages of a device space into gr_message records (testing). A
  * mailbox whose cold fields were lost in the exchange (MB_COLD_LOST) decodes to
  * records with reject = 0xFF and no other field. */

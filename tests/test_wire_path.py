@@ -106,3 +106,41 @@ def test_wire_unrouted_reasons(gpu):
     assert np.array_equal(eng.sync(R * G), ref.sync(R * G))
     eng.close()
     ref.close()
+
+
+def test_wire_compact_outbox(gpu):
+    """gr_step_wire_compact returns exactly what gr_step_compact returns for the
+    same messages and locals (compact records, ext records, compact results)."""
+    import torch
+    import wirefeed
+    from dragonboat_amd.engine import Engine
+    from oracle.pyoracle import OraclePopulation
+    G, R = 300, 3
+    peers = P.make_groups(G, R, seed=4)
+    topo = P.Topology(G, R)
+    cl = (np.arange(R * G) % G) + 1
+    pop = OraclePopulation(peers, R)
+    o = pop.step(np.zeros(0, abi.MESSAGE), P.propose_locals(R * G, np.arange(G), pass_index=0))
+    msgs = topo.route_messages(o["msgs"])
+    feed = wirefeed.WireFeed(peers, cl)
+    d_m, nm, d_e, ne, keep = feed.decode(msgs)
+    loc = P.propose_locals(R * G, np.arange(G), pass_index=1)
+    loc["ticks"][::7] = 1
+    eng = Engine(R * G, R)
+    eng.load(peers)
+    eng.bind_nodes(cl, peers["node_id"])
+    got, idx, why = eng.step_wire(d_m, nm, d_e, ne, loc, compact=True)
+    feed.close()
+    assert len(idx) == 0
+    ref = Engine(R * G, R)
+    ref.load(peers)
+    cm, xm = ref.pack_messages(msgs)
+    cloc, xloc = ref.pack_locals(loc)
+    want = ref.step_compact(cm, xm, cloc, xloc)
+    for a, b in zip(got, want):
+        assert a.dtype == b.dtype and np.array_equal(a, b)
+    assert len(got[0]) > 0
+    assert np.array_equal(eng.sync(R * G), ref.sync(R * G))
+    eng.close()
+    ref.close()
+    del keep, torch

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--groups", type=int, default=1_000_000)
     ap.add_argument("--passes", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--compact", action="store_true", help="gr_step_wire_compact (24-B outbox records)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -65,15 +66,20 @@ def main():
             # the C-ABI call a Go step worker makes; its outbox is engine-owned pinned
             # memory the caller reads in place (the copy into numpy below is untimed)
             import ctypes
-            ob, un = abi.Outbox(), abi.WireUnrouted()
+            ob, un = (abi.COutbox() if a.compact else abi.Outbox()), abi.WireUnrouted()
             loc_c = np.ascontiguousarray(loc, abi.LOCAL)
-            rc = eng.lib.gr_step_wire(eng._h, d_msgs.data_ptr(), nm, d_ents.data_ptr(), ne, loc_c.ctypes.data,
-                                      len(loc_c), ctypes.byref(ob), ctypes.byref(un))
+            fn = eng.lib.gr_step_wire_compact if a.compact else eng.lib.gr_step_wire
+            rc = fn(eng._h, d_msgs.data_ptr(), nm, d_ents.data_ptr(), ne, loc_c.ctypes.data, len(loc_c),
+                    ctypes.byref(ob), ctypes.byref(un))
             t3w = time.perf_counter()
             assert rc == 0 and un.n == 0, (rc, un.n)
-            out = np.zeros(ob.n_msgs, abi.MESSAGE)
-            ctypes.memmove(out.ctypes.data, ob.msgs, ob.n_msgs * abi.MESSAGE.itemsize)
-            eng.lib.gr_release_outbox(eng._h, ctypes.byref(ob))
+            if a.compact:  # the next pass's inbox: the compact records expanded (untimed)
+                cm, xm, _, _ = eng._take_coutbox(ob)
+                out = eng.unpack_messages(cm, xm)
+            else:
+                out = np.zeros(ob.n_msgs, abi.MESSAGE)
+                ctypes.memmove(out.ctypes.data, ob.msgs, ob.n_msgs * abi.MESSAGE.itemsize)
+                eng.lib.gr_release_outbox(eng._h, ctypes.byref(ob))
         else:
             t1 = t2 = time.perf_counter()
             out, res = eng.step(msgs, loc)
@@ -91,9 +97,11 @@ def main():
     eng.close()
     p = a.passes
     print(json.dumps({
-        "path": "gr_step_wire: MessageBatch frames uploaded, decoded in HBM (grw_decode_device), routed into "
-                "the step pass; outbox gr_message records + results downloaded into engine-owned pinned memory "
-                "(the caller reads them in place; copying them out is not timed)",
+        "path": ("gr_step_wire_compact" if a.compact else "gr_step_wire") +
+                ": MessageBatch frames uploaded, decoded in HBM (grw_decode_device), routed into the step pass; "
+                "outbox " + ("compact gr_cmsg/gr_cresult" if a.compact else "gr_message/gr_peer_result") +
+                " records downloaded into engine-owned pinned memory (the caller reads them in place; copying "
+                "them out is not timed)",
         "groups": G, "replicas": R, "passes": p,
         "ms_per_pass": (t_up + t_dec + t_step) / p * 1e3,
         "upload_ms": t_up / p * 1e3, "decode_ms": t_dec / p * 1e3, "route_step_download_ms": t_step / p * 1e3,
