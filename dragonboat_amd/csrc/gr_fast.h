@@ -104,7 +104,6 @@ struct FastLane {
   uint32_t outc[S];
   uint32_t n1out = 0;    // leader: bit 8j + k = out Replicate k of slot j carries an entry
   uint32_t fullout = 0;  // leader: bit 8j + k = out Replicate k of slot j is a full record (not compact)
-  uint64_t eub = 0;      // entry-size bound (a leader's multi-entry sends)
   const uint64_t max_entry;  // StepParams::max_entry_size, read once
   uint32_t rejout = 0;   // follower: bit k = out ReplicateResp k is a reject (not uniform: tags written)
   uint32_t nmo = 0, nmi = 0, nent = 0;
@@ -261,7 +260,10 @@ struct FastLane {
       // limitSize (entryutils.go:50-63) keeps all iff their sum fits (Lane::send_replicate)
       // (cnt > max / eub as cnt * eub > max: exact while both are below 2^32; a
       // bound of 4 GiB or more goes to the general lane)
-      GF_BAIL(cnt > 1 && (eub == 0 || (eub >> 32) != 0 || cnt > 0xFFFFFFFFull || cnt * eub > max_entry));
+      if (cnt > 1) {  // the entry-size bound row, loaded only for a lagging remote
+        const uint64_t eub = ntld(s64(SR_ENTRY_UB));
+        GF_BAIL(eub == 0 || (eub >> 32) != 0 || cnt > 0xFFFFFFFFull || cnt * eub > max_entry);
+      }
       GF_BAIL(rst(j) != GR_REPLICATE_ST && rst(j) != GR_RETRY);
       n = (uint32_t)cnt;
       if (rst(j) == GR_REPLICATE_ST) {  // remote.progress, remote.go:120-128
@@ -474,7 +476,6 @@ struct FastLane {
     // ---- round 2 (only where the hint did not match): leader remotes and messages
     if (kLeaderPath && leader) {
       rbw = h_rb(hdr) & ((1ull << (5 * S)) - 1);
-      eub = ntld(s64(SR_ENTRY_UB));
       // remote rows: stale ones (sync bits) from lastIndex, the rest loaded unless the hint did
       const uint64_t sb = kSync ? hdr : 0;
 #pragma unroll
@@ -612,21 +613,18 @@ struct FastLane {
         drop |= lower ? 1u << j : 0u;
         GF_BAIL(!lower && cnt[j] && (cnt[j] > (uint32_t)MK || !(cbs[j] & MB_RESP) || (uint64_t)lmt[j] != term));
       }
-      // messages in node.handleReceivedMessages order: slot, then arrival; the
-      // position loop stays rolled (its slot is wave-uniform), so the message
-      // code is inlined once per slot, not once per slot and position
+      // messages in node.handleReceivedMessages order: slot, then arrival
 #pragma unroll
-      for (int j = 0; j < S; ++j) nmi += cnt[j];
-#pragma unroll 1
-      for (uint32_t q = 0; q < (uint32_t)(S * MK); ++q) {
-        const uint32_t qj = q / MK, qk = q % MK;
+      for (int j = 0; j < S; ++j) {
+        if ((drop >> j) & 1u) {
+          nmi += cnt[j];
+          continue;
+        }
 #pragma unroll
-        for (int j = 0; j < S; ++j) {
-          if ((uint32_t)j == qj && !((drop >> j) & 1u) && qk < cnt[j] && rkind(j) != GR_SLOT_EMPTY) {
-            uint64_t x = lidx[j][0];
-#pragma unroll
-            for (int k = 1; k < MK; ++k) x = qk == (uint32_t)k ? lidx[j][k] : x;
-            replicate_resp(j, x);
+        for (int k = 0; k < MK; ++k) {
+          if ((uint32_t)k < cnt[j]) {
+            nmi++;
+            if (rkind(j) != GR_SLOT_EMPTY) replicate_resp(j, lidx[j][k]);
           }
         }
       }
