@@ -19,9 +19,9 @@ per pass (dragonboat_amd/exchange.py).
 Roofline accounting: `achieved` = the algorithmic bytes one
 launch must move at this engine's encoding, over the lean kernels' HIP-event
 duration. The unit is one group-round; its bytes are counted field by field
-from the steady lanes' loads and stores (gr_steady.h; 412 B at R = 3: leader
-94 B loaded + 92 B stored, each follower 66 + 47 B), and a launch processes one
-group-round per leader commit. PMC confirms it (traffic ~421 B/round).
+from the steady lanes' loads and stores (gr_steady.h; 332 B at R = 3: leader
+78 B loaded + 68 B stored, each follower 54 + 39 B), and a launch processes one
+group-round per leader commit. PMC checks it (`traffic`).
 SURVEY.md §8d's canonical count at reference field widths, B_round(R) =
 (R-1)(69+65+138) + 8R + 48 = 616 B at R = 3, is reported beside it as
 `canonical_achieved`/`canonical_frac`: it counts bytes the kernels never move,
@@ -56,20 +56,22 @@ def b_round(R):
 B_RESP, B_EMIT, B_MATCH0, B_ENTRY = 69, 65, 122, 16
 
 # Bytes one steady group-round moves at this engine's encoding (gr_steady.h,
-# loopback routes, R = 3), load by load and store by store:
+# loopback routes, R = 3), load by load and store by store. The
+# two messages of each steady mailbox travel shared (gr_layout.h MB_SHARED:
+# message 0's hot fields only):
 #   leader   loads  hdr, term, committed, lastIndex 32 + locals word 4
-#                   + 2 ack mailboxes x (count 1 + term word 4 + 2 LogIndex 16)
-#                   + 2 follower match rows 16                          =  94
+#                   + 2 ack mailboxes x (count 1 + term word 4 + LogIndex 8)
+#                   + 2 follower match rows 16                          =  78
 #            stores committed 8 + lastIndex 8 + 2 match rows 16
-#                   + 2 out mailboxes x (2 x (LogIndex 8 + Commit offset 4)
-#                   + term word 4 + count 1) + proposal result 1 + flags 1 =  92
+#                   + 2 out mailboxes x (LogIndex 8 + Commit offset 4
+#                   + term word 4 + count 1) + proposal result 1 + flags 1 =  68
 #   follower loads  core 32 + locals word 4 + 2 count bytes + term word 4
-#                   + 2 LogIndex 16 + 2 Commit offsets 8                 =  66
-#            stores committed 8 + lastIndex 8 + ack mailbox (2 LogIndex 16
+#                   + LogIndex 8 + Commit offset 4                       =  54
+#            stores committed 8 + lastIndex 8 + ack mailbox (LogIndex 8
 #                   + term word 4 + count 1) + other count 1
-#                   + append_from 8 + flags 1                            =  47
-# = 94 + 92 + 2 x (66 + 47) = 412 B per group-round.
-ENCODED_ROUND_BYTES = {3: 412}
+#                   + append_from 8 + flags 1                            =  39
+# = 78 + 68 + 2 x (54 + 39) = 332 B per group-round.
+ENCODED_ROUND_BYTES = {3: 332}
 
 
 def reference_width_bytes(st, groups, R, passes):
@@ -96,7 +98,8 @@ def parse():
                     help="engines per rank whose exchanges overlap each other's passes (spread default 2)")
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
     ap.add_argument("--cpu-groups", type=int, default=20000)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="T of the CPU baseline (0: nproc, BASELINE.md)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="T of the CPU baseline (0: nproc capped by affinity and the cgroup quota)")
     ap.add_argument("--cpu-seconds", type=float, default=40.0, help="CPU baseline time budget (all legs)")
     ap.add_argument("--host-path", choices=["on", "off"], default="on",
                     help="also time gr_step with host records (N=1, rank 0)")
@@ -174,6 +177,21 @@ def cgroup_cpu_max():
         return None
 
 
+def effective_cpus(info):
+    """CPUs the baseline's threads can actually use: the affinity set, capped by
+    the cgroup quota (cpu.max "quota period" -> ceil(quota / period))."""
+    n = info.get("affinity_cpus") or info.get("nproc") or 1
+    q = info.get("cgroup_cpu_max")
+    if q:
+        parts = q.split()
+        if len(parts) == 2 and parts[0] != "max":
+            try:
+                n = min(n, max(1, -(-int(parts[0]) // int(parts[1]))))
+            except ValueError:
+                pass
+    return n
+
+
 def thread_row(nproc):
     """Thread counts of the scaling row: powers of two up to nproc, and nproc."""
     row, t = [], 1
@@ -194,6 +212,12 @@ def cpu_baseline(args, R):
     info = cpu_info()
     info["cgroup_cpu_max"] = cgroup_cpu_max()
     nproc = info["nproc"] or 1
+    eff = effective_cpus(info)
+    info["effective_cpus"] = eff
+    # the thread row runs up to BASELINE.md's T = nproc; the reported value is the
+    # row's best (the strongest CPU number), and `cores` the CPUs those threads
+    # could actually use: the threads, capped by the affinity set and the cgroup
+    # quota (more threads than that only time-slice the quota's CPU time)
     T = args.cpu_threads or nproc
     G = args.cpu_groups
     budget = args.cpu_seconds
@@ -205,15 +229,20 @@ def cpu_baseline(args, R):
     for t in row:
         c, _, n = _oracle_rate(P.make_groups(G, R, seed=2), P.Topology(G, R), R, steady(G), t, per)
         scaling.append({"threads": t, "commits_per_s": c, "passes": n})
-    at_T = scaling[-1]
     best = max(scaling, key=lambda x: x["commits_per_s"])
-    out = {"value": at_T["commits_per_s"], "unit": "commit-index updates/s", "cores": T, "kind": "port",
-           "sample": f"config 4 shape: {G} groups x {R} replicas, {at_T['passes']} passes, oracle raft step "
-                     f"timed (message routing and persistence excluded), T = {T} threads (nproc)",
+    bt = best["threads"]
+    out = {"value": best["commits_per_s"], "unit": "commit-index updates/s", "cores": min(bt, eff),
+           "threads": bt, "kind": "port",
+           "sample": f"config 4 shape: {G} groups x {R} replicas, {best['passes']} passes, oracle raft step "
+                     f"timed (message routing and persistence excluded), best of the thread row 1..{T}: "
+                     f"{bt} threads on {min(bt, eff)} effective CPUs (nproc {nproc}, cgroup quota "
+                     f"{info['cgroup_cpu_max']})",
+           "at_nproc": scaling[-1],
            "one_thread": {"value": scaling[0]["commits_per_s"], "passes": scaling[0]["passes"]},
            "best": best, "thread_scaling": scaling,
-           "note": "T = nproc per BASELINE.md; the box's cgroup quota (cgroup_cpu_max) caps the CPU time the "
-                   "threads get, so the row peaks below nproc ('best')",
+           "note": "value = the best point of the thread row (1, 2, 4, ... nproc threads); cores = that row's "
+                   "threads capped by the affinity set and the cgroup quota (cgroup_cpu_max, ceil(quota/period) "
+                   "CPUs): the CPU time the threads can actually get; nproc and effective_cpus are beside it",
            "label": "C++ restatement of reference Go step (oracle/raft_oracle.hpp), not Go",
            **info}
     T = best["threads"]  # the other configs at the row's best thread count

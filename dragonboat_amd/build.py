@@ -70,7 +70,7 @@ def _run(cmd):
 # lean lane made a 1M x 3 pass 6x slower (0.82 vs 0.13 ms) and moved 3 GB of
 # scratch traffic per launch. The compiler's resource remarks are checked at
 # build time, so such a build fails instead of shipping.
-NO_SCRATCH_KERNELS = ("gr_fast_kernel",)
+NO_SCRATCH_KERNELS = ("gr_fast_kernel", "gr_roles_kernel")
 RESOURCE_REMARKS = "-Rpass-analysis=kernel-resource-usage"
 
 

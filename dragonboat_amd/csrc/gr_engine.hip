@@ -658,7 +658,7 @@ int gr_space_side_unpack_host(void* space_host, uint32_t n_chunks, uint32_t posi
     const uint32_t n = *(const uint32_t*)h;
     for (uint32_t x = 0; x < n && x < capacity; ++x) {
       const uint8_t* e = h + io::kSideHdr + (uint64_t)x * io::side_entry_bytes(depth);
-      io::cold_scatter(v.at(c * v.pc + ((const uint32_t*)e)[0]), ((const uint32_t*)e)[1] & MB_COUNT, e);
+      io::cold_scatter(v.at(c * v.pc + ((const uint32_t*)e)[0]), mb_n(((const uint32_t*)e)[1]), e);
     }
   }
   return GR_OK;
@@ -672,7 +672,7 @@ int gr_space_encode(void* space_host, uint32_t n_chunks, uint32_t positions, uin
     const uint32_t g = pos_of_msg[k];
     if (g / v.pc >= n_chunks || g % v.pc >= positions) return GR_ERANGE;
     const Mailbox mb = v.at(g);
-    const uint8_t c = mb.cnt() & MB_COUNT;
+    const uint8_t c = (uint8_t)mb_n(mb.cnt());
     if (c >= depth) return GR_ECAPACITY;
     encode_msg(mb, c, msgs[k]);
     mb.cnt() = (uint8_t)(c + 1);
@@ -689,7 +689,7 @@ int gr_space_decode(const void* space_host, uint32_t n_chunks, uint32_t position
     for (uint32_t l = 0; l < positions; ++l) {
       const uint32_t g = c * v.pc + l;
       const Mailbox mb = v.at(g);
-      const uint32_t cb = mb.cnt(), cnt = std::min<uint32_t>(cb & MB_COUNT, depth);
+      const uint32_t cb = mb.cnt(), cnt = std::min<uint32_t>(mb_n(cb), depth);
       const bool lost = !(cb & MB_UNIFORM) && (cb & MB_COLD_LOST);  // cold fields not delivered
       for (uint32_t k = 0; k < cnt; ++k) {
         if (out && n < cap) {
@@ -1135,7 +1135,12 @@ int gr_step_compact_end(gr_engine* e, gr_coutbox* out) {
   if (!e->cpend.on) return GR_EINVAL;  // no pass was begun
   const gr_engine::CPending pend = e->cpend;
   e->cpend.on = false;
-  e->pending.store(false, std::memory_order_release);
+  // `pending` stays set until this call returns (every path): the pass below
+  // still uses the lane rows, bail lists and scratch the flag protects
+  struct ClearPending {
+    std::atomic<bool>& f;
+    ~ClearPending() { f.store(false, std::memory_order_release); }
+  } clear_pending{e->pending};
   memset(out, 0, sizeof(*out));
   PhaseClock clk;
   const uint32_t S = e->S, cap = e->cfg.max_peers;
@@ -1374,6 +1379,7 @@ int gr_stats_reset(gr_engine* e) {
 
 int gr_bind_routes(gr_engine* e, const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n_peers) {
   if (!e || !in_pos || !out_pos || n_peers > e->cfg.max_peers) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(e->mu);  // against a concurrent compact _begin/_end
   GR_REFUSE_PENDING(e);
   HIPCHK(hipDeviceSynchronize());
   std::vector<uint32_t> base(2 * GR_SMAX * GR_SMAX, NOPOS);
@@ -1438,6 +1444,9 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
                    uint32_t n_peers, void* stream) {
   if (!e || !in_space || !out_space || n_peers > e->cfg.max_peers || depth == 0 || depth > GR_C)
     return GR_EINVAL;
+  // the mutex orders this pass after a compact _begin/_end on another thread
+  // (uncontended: one lock per pass)
+  std::lock_guard<std::mutex> guard(e->mu);
   GR_REFUSE_PENDING(e);  // the pending compact pass owns the lane rows and bail lists
   StepParams kp = base_params(e);
   kp.has_locals = e->locals_set ? 1 : 0;

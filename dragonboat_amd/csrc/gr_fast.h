@@ -398,9 +398,9 @@ struct FastLane {
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       const uint32_t b = gin[j] != NOPOS ? (uint32_t)ntld(min_at(gin[j]).cnt()) : 0u;
-      cnt[j] = b & MB_COUNT;
+      cnt[j] = mb_n(b);
       cbs[j] = b;
-      nonu |= ((b & MB_COUNT) && !(b & MB_UNIFORM)) ? (1u << j) : 0u;
+      nonu |= (mb_n(b) && !(b & MB_UNIFORM)) ? (1u << j) : 0u;
     }
     // leader: the term word and LogIndexes of every in-mailbox (ReplicateResp accepts)
     uint32_t lmt[S];
@@ -495,6 +495,11 @@ struct FastLane {
         }
       }
     }
+    if (kLeaderPath && leader) {
+#pragma unroll
+      for (int j = 0; j < S; ++j)  // a shared ack pair (MB_SHARED): message 1 = message 0 + 1
+        if (mb_shared(cbs[j])) lidx[j][1] = lidx[j][0] + 1;
+    }
     uint32_t L = 0, nsrc = 0, c = 0, gl = 0, go = NOPOS, cbL = 0;
     uint32_t fdrop = 0;  // follower: messages of uniform mailboxes at a lower term, dropped
     uint64_t rid = 0;
@@ -533,6 +538,10 @@ struct FastLane {
           fidx[k] = ntld(mb.u64(k, MF_LOG_INDEX));
           fcd[k] = ntld(mb.t32(k, MT_CDELTA));
         }
+      }
+      if (mb_shared(cbL)) {  // a shared Replicate pair (MB_SHARED): message 0's fields
+        fidx[1] = fidx[0];
+        fcd[1] = fcd[0];
       }
       // electionTick = 0 and leaderID = remote_id(L) are usually already so
       // (F_ETZ, F_LSLOT): then neither is loaded nor rewritten
@@ -636,8 +645,11 @@ struct FastLane {
       // entries, or a LogTerm below its term: emit_replicate, Lane::emit); any
       // other mailbox with messages must be uniform
       const bool fullL = c && ((nonu >> L) & 1u);
+      // a full-record mailbox whose cold fields were not delivered (MB_COLD_LOST,
+      // gr_space_side_pack) holds a previous pass's words there: CAPACITY in the
+      // general lane, as the leader path above and Lane::run do
       GF_BAIL(nsrc > 1 || c > (uint32_t)MK || (nonu & ~(fullL ? 1u << L : 0u)) ||
-              (c && !fullL && ((cbL & MB_RESP) || (uint64_t)fmt != term)));
+              (fullL && (cbL & MB_COLD_LOST)) || (c && !fullL && ((cbL & MB_RESP) || (uint64_t)fmt != term)));
       uint32_t ftag[MK], fterm[MK], fn[MK], flt[MK], frt[MK];
       uint64_t fcw[MK];
 #pragma unroll

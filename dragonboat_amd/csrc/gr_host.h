@@ -30,6 +30,14 @@ __host__ __device__ inline uint64_t header_of(const gr_peer& g, uint32_t S) {
           << (5 * j);
   uint64_t h = h_make(g.state, g.self_slot, n, gelo, flags, g.read_index_count, rb);
   if (has_run_bits((int)S) && n) h |= run_bits(n, g.run_start[n - 1], g.run_term[n - 1], g.term, g.committed);
+  // a leader's sync bits where the record's rows already hold the values they
+  // imply (gr_layout.h): a loaded steady leader starts as FastLane leaves one
+  // (the rows are written too, so the bits only let the lanes skip them)
+  if (has_sync_bits((int)S) && g.state == GR_LEADER) {
+    for (uint32_t j = 0; j < S; ++j)
+      if (g.remotes[j].next == g.last_index + 1) h |= 1ull << (H_NX_SHIFT + j);
+    if (g.self_slot < S && g.remotes[g.self_slot].match == g.last_index) h |= 1ull << H_MS_BIT;
+  }
   return h;
 }
 __host__ __device__ inline void set_header(gr_peer& g, uint32_t S, uint64_t h) {
@@ -223,11 +231,11 @@ __host__ __device__ inline gr_message decode_msg(const Mailbox& mb, uint32_t k) 
   switch (m.type) {
     case GR_REPLICATE:
       if (fl & MFL_COMPACT) {  // gr_layout.h: LogTerm = Term, <= 1 entry at Term, narrow Commit
-        m.log_index = mb.u64(k, MF_LOG_INDEX);
+        m.log_index = mb.log_index_at(k, cb);  // a shared mailbox: message 0's
         m.n_entries = (fl & MFL_N1) ? 1u : 0u;
         m.n_runs = m.n_entries ? 1u : 0u;
         m.log_term = m.term;
-        m.commit = commit_of(mb.t32(k, MT_CDELTA), m.log_index);
+        m.commit = commit_of(mb.cdelta_at(k, cb), m.log_index);
         if (m.n_entries) m.run_term[0] = m.term;
         break;
       }
@@ -242,7 +250,7 @@ __host__ __device__ inline gr_message decode_msg(const Mailbox& mb, uint32_t k) 
       }
       break;
     case GR_REPLICATE_RESP:  // the device writes Hint only on a reject
-      m.log_index = mb.u64(k, MF_LOG_INDEX);
+      m.log_index = mb.log_index_at(k, cb);  // a shared mailbox: message 0's + k
       if (m.reject) m.hint = mb.u64(k, MF_HINT);
       break;
     case GR_HEARTBEAT:
@@ -586,7 +594,7 @@ inline void decode_outbox(const void* space, const PackedInbox& pk, uint32_t S, 
   for (uint32_t l = 0; l < nl; ++l) {
     for (uint32_t j = 0; j < S; ++j) {
       const Mailbox mb = v.at(j * nl + l);
-      const uint32_t c = std::min<uint32_t>(mb.cnt() & MB_COUNT, GR_C);
+      const uint32_t c = std::min<uint32_t>(mb_n(mb.cnt()), GR_C);
       for (uint32_t k = 0; k < c; ++k) {
         gr_message m = decode_msg(mb, k);
         m.peer = pk.peers[l];

@@ -120,7 +120,7 @@ __global__ void out_counts(SpaceView out, uint32_t nl, uint32_t S, uint32_t* oc)
   for (uint32_t l = io_tid(); l < nl; l += io_stride()) {
     uint32_t c = 0;
     for (uint32_t j = 0; j < S; ++j) {
-      const uint32_t x = out.at(j * nl + l).cnt() & MB_COUNT;
+      const uint32_t x = mb_n(out.at(j * nl + l).cnt());
       c += x < (uint32_t)GR_C ? x : (uint32_t)GR_C;
     }
     oc[l] = c;
@@ -138,7 +138,7 @@ __global__ void pack_outbox(SpaceView out, uint32_t nl, uint32_t S, const uint32
     const uint32_t peer = peer_of_lane[l];
     for (uint32_t j = 0; j < S; ++j) {
       const Mailbox mb = out.at(j * nl + l);
-      const uint32_t x = mb.cnt() & MB_COUNT;
+      const uint32_t x = mb_n(mb.cnt());
       const uint32_t c = x < (uint32_t)GR_C ? x : (uint32_t)GR_C;
       for (uint32_t k = 0; k < c; ++k) {
         gr_message m = host::decode_msg(mb, k);
@@ -233,7 +233,7 @@ __global__ void out_counts_c(SpaceView out, LaneBase L, uint32_t nl, uint32_t S,
     uint32_t c = 0, e = 0;
     for (uint32_t j = 0; j < S; ++j) {
       const Mailbox mb = out.at(j * nl + l);
-      const uint32_t x = mb.cnt() & MB_COUNT;
+      const uint32_t x = mb_n(mb.cnt());
       const uint32_t cnt = x < (uint32_t)GR_C ? x : (uint32_t)GR_C;
       c += cnt;
       for (uint32_t k = 0; k < cnt; ++k) {
@@ -263,7 +263,7 @@ __global__ void pack_outbox_c(SpaceView out, uint32_t nl, uint32_t S, const uint
     const uint32_t peer = peer_of_lane[l];
     for (uint32_t j = 0; j < S; ++j) {
       const Mailbox mb = out.at(j * nl + l);
-      const uint32_t x = mb.cnt() & MB_COUNT;
+      const uint32_t x = mb_n(mb.cnt());
       const uint32_t c = x < (uint32_t)GR_C ? x : (uint32_t)GR_C;
       for (uint32_t k = 0; k < c; ++k) {
         gr_message m = host::decode_msg(mb, k);
@@ -301,7 +301,7 @@ __global__ void cold_used(SpaceView v, uint32_t* flag) {
   const uint64_t n = (uint64_t)v.n_chunks * v.pc;
   for (uint64_t g = io_tid(); g < n; g += io_stride()) {
     const uint8_t c = v.at((uint32_t)g).cnt();
-    const bool cold = (c & MB_COUNT) && !(c & MB_UNIFORM);
+    const bool cold = mb_n(c) && !(c & MB_UNIFORM);
     if (__ballot(cold) && (threadIdx.x & 63) == 0) *flag = 1;
   }
 }
@@ -462,9 +462,9 @@ __host__ __device__ inline void side_put(const SpaceView& v, uint32_t g, uint8_t
   uint8_t* e = side + (uint64_t)c * side_chunk_bytes(v.depth, cap) + kSideHdr + (uint64_t)idx * side_entry_bytes(v.depth);
   reinterpret_cast<uint32_t*>(e)[0] = g - c * v.pc;
   reinterpret_cast<uint32_t*>(e)[1] = cb;
-  cold_gather(mb, cb & MB_COUNT, e);
+  cold_gather(mb, mb_n(cb), e);
 }
-__host__ __device__ inline bool needs_cold(uint32_t cb) { return (cb & MB_COUNT) && !(cb & MB_UNIFORM); }
+__host__ __device__ inline bool needs_cold(uint32_t cb) { return mb_n(cb) && !(cb & MB_UNIFORM); }
 
 // Pack the out space's cold fields into the side buffers (their counts zeroed
 // before): one returning atomic per wave and chunk (a chunk is a multiple of 256
@@ -497,7 +497,7 @@ __global__ void side_unpack(SpaceView v, const uint8_t* side, uint32_t cap) {
     if (idx >= cnt) continue;
     const uint8_t* e = h + kSideHdr + (uint64_t)idx * side_entry_bytes(v.depth);
     const uint32_t pos = reinterpret_cast<const uint32_t*>(e)[0], cb = reinterpret_cast<const uint32_t*>(e)[1];
-    cold_scatter(v.at(c * v.pc + pos), cb & MB_COUNT, e);
+    cold_scatter(v.at(c * v.pc + pos), mb_n(cb), e);
   }
 }
 

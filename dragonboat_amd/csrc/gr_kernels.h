@@ -33,7 +33,8 @@ __device__ inline __attribute__((always_inline)) uint32_t wave_sum(uint32_t v) {
 // Each wave adds its own sums: the nine totals are wave-uniform after the
 // butterfly, lane k adds total k with a non-returning atomic. No LDS and no
 // barrier, so a wave never waits for the rest of its workgroup to finish.
-__device__ inline __attribute__((always_inline)) void block_stats(const StepParams& kp, const LaneStats& ls) {
+__device__ inline __attribute__((always_inline)) void block_stats(const StepParams& kp, const LaneStats& ls,
+                                                                  uint32_t bid = blockIdx.x) {
   constexpr int N = 9;
   // one named field at a time: a register array indexed in a loop was put in scratch
   const uint32_t f0 = wave_sum(ls.leader_commit), f1 = wave_sum(ls.follower_commit),
@@ -49,7 +50,7 @@ __device__ inline __attribute__((always_inline)) void block_stats(const StepPara
     uint32_t f = 0;
 #pragma unroll
     for (uint32_t x = 0; x < (uint32_t)N; ++x) f = k == x ? field[x] : f;
-    if (v) atomicAdd((unsigned long long*)(kp.stats + (uint64_t)blockIdx.x * NSTAT + f), (unsigned long long)v);
+    if (v) atomicAdd((unsigned long long*)(kp.stats + (uint64_t)bid * NSTAT + f), (unsigned long long)v);
   }
 }
 
@@ -75,6 +76,11 @@ __device__ inline __attribute__((always_inline)) void block_stats(const StepPara
 constexpr uint32_t kBailLists = 32, kGeneralLists = 16, kTickList0 = 16, kRetryList0 = 24, kCounters = kBailLists,
                    kCounterStride = 64;  // counters 256 B apart
 constexpr uint32_t WF_LISTED = 0x80;     // wave flag: the role instances step this wave's masked lanes
+// Word 1 of counter 0's 256-B slot: nonzero when a split pass's steady kernel
+// listed some wave for the role instances (a plain store, no atomic); with it
+// zero and the retry lists empty the role instances return at once. Cleared for
+// the next pass with the counters.
+constexpr uint32_t kListedWord = 1;
 __host__ __device__ inline uint64_t wave_flag_words(uint32_t cap) { return ((uint64_t)cap / 64 + 64) / 4 * 2; }
 // u32 words of the list storage: kBailLists lane lists of cap, the wave flags, the wave masks (u64)
 __host__ __device__ inline uint64_t bail_words(uint32_t cap) {
@@ -135,7 +141,8 @@ __device__ inline __attribute__((always_inline)) uint32_t sload_u32(const uint8_
 // the stats.
 __device__ inline __attribute__((always_inline)) void wave_finish(const StepParams& kp, uint32_t i, uint32_t wave, bool mine, bool active,
                                    bool skip, bool bail, uint32_t role, uint32_t myhint, const LaneStats& ls,
-                                   uint32_t* bail_list, uint32_t* counters, uint32_t list_cap) {
+                                   uint32_t* bail_list, uint32_t* counters, uint32_t list_cap,
+                                   uint32_t bid = blockIdx.x) {
   if (kp.hints) {
     // over the lanes that are this kernel's (mine), written by the first of them
     const uint64_t mm = __ballot(mine);
@@ -152,9 +159,9 @@ __device__ inline __attribute__((always_inline)) void wave_finish(const StepPara
 #pragma unroll
   for (uint32_t side = 0; side < 3; ++side) {
     const bool m = bail && (side == 2 ? tickish : !tickish && lead == (side == 1));
-    bail_append(m, (blockIdx.x % 8) + side * 8, bail_list, counters, list_cap, i);
+    bail_append(m, (bid % 8) + side * 8, bail_list, counters, list_cap, i);
   }
-  if (kp.stats) block_stats(kp, ls);
+  if (kp.stats) block_stats(kp, ls, bid);
 }
 
 // One wave of a lean-kernel instance: lane i of wave `wave`, whose hint as the
@@ -162,7 +169,8 @@ __device__ inline __attribute__((always_inline)) void wave_finish(const StepPara
 // instance's. Steps the lane, then the wave's hint, bail lists and stats.
 template <int S, int R, int RM>
 __device__ inline __attribute__((always_inline)) void fast_wave(const StepParams& kp, uint32_t i, uint32_t wave, uint32_t hint, int wk, bool mine,
-                                 uint32_t* bail_list, uint32_t* counters, uint32_t list_cap) {
+                                 uint32_t* bail_list, uint32_t* counters, uint32_t list_cap,
+                                 uint32_t bid = blockIdx.x) {
   LaneStats ls;
   bool bail = false, skip = false;
   uint32_t role = 0, myhint = 0;
@@ -178,7 +186,7 @@ __device__ inline __attribute__((always_inline)) void fast_wave(const StepParams
     bail = bail && !skip;  // a skipped lane is the other instance's
     if (!bail && !skip) GR_CHECK_STATE(kp.st, p);
   }
-  wave_finish(kp, i, wave, mine, active, skip, bail, role, myhint, ls, bail_list, counters, list_cap);
+  wave_finish(kp, i, wave, mine, active, skip, bail, role, myhint, ls, bail_list, counters, list_cap, bid);
 }
 
 // Locate entry x of the 8 lists whose exclusive prefix is start[0..8]: list and offset.
@@ -193,15 +201,25 @@ __device__ inline __attribute__((always_inline)) void list_at(const uint32_t (&s
   *off = o;
 }
 
-// LISTED (split passes with the steady kernel, R != FL_ANY): a fixed grid walks
-// the waves the steady kernel listed for this instance (wave flags), one wave of
-// the grid per listed wave, grid-stride. Otherwise one workgroup per 256 lanes,
-// every wave checked against its hint.
-template <int S, int R, int RM, bool LISTED>
-__global__ __launch_bounds__(kBlock, LISTED ? GR_LISTED_MIN_WAVES : GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
-                                                                             uint32_t* counters, uint32_t list_cap) {
-  static_assert(!LISTED || R != FL_ANY, "listed waves are the role instances'");
-  if constexpr (LISTED) {
+// The role instances of a split pass with the steady kernel (R != FL_ANY): a
+// fixed grid of nblk workgroups (this one is bid) walks the waves the steady
+// kernel listed for this instance (wave flags), one wave of the grid per listed
+// wave, grid-stride, then the lanes it left for FastLane (retry lists).
+template <int S, int R, int RM>
+__device__ inline __attribute__((always_inline)) void roles_listed(const StepParams& kp, uint32_t* bail_list,
+                                                                   uint32_t* counters, uint32_t list_cap,
+                                                                   uint32_t bid, uint32_t nblk) {
+  static_assert(R != FL_ANY, "listed waves are the role instances'");
+  // nothing listed and no retry lane (the steady state): return before any
+  // flag is read (wave-uniform scalar loads of words the steady kernel wrote)
+  uint32_t start[9];
+  start[0] = 0;
+#pragma unroll
+  for (uint32_t l = 0; l < 8; ++l)
+    start[l + 1] = start[l] + (uint32_t)__builtin_amdgcn_readfirstlane(counters[(kRetryList0 + l) * kCounterStride]);
+  const uint32_t n = start[8];
+  if (!__builtin_amdgcn_readfirstlane(counters[kListedWord]) && n == 0) return;
+  {
     // grid wave g owns waves g, g + W, g + 2W, ... (W = the grid's waves): it
     // reads 64 of their flags per load (lane l: wave g + W * (r + l)) and steps
     // the listed ones of this instance's role (an unhinted wave is both
@@ -209,8 +227,8 @@ __global__ __launch_bounds__(kBlock, LISTED ? GR_LISTED_MIN_WAVES : GR_FAST_MIN_
     const uint8_t* wf = wave_flags(bail_list, list_cap);
     const uint64_t* wm = wave_masks(bail_list, list_cap);
     const uint32_t nw = (kp.n_lanes + 63) / 64, lane = threadIdx.x & 63;
-    const uint32_t g = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
-    const uint32_t W = gridDim.x * (kBlock / 64);
+    const uint32_t g = (uint32_t)__builtin_amdgcn_readfirstlane(bid * (kBlock / 64) + (threadIdx.x >> 6));
+    const uint32_t W = nblk * (kBlock / 64);
     for (uint32_t r = 0; g + (uint64_t)W * r < nw; r += 64) {  // wave-uniform
       const uint64_t idx = g + (uint64_t)W * (r + lane);
       const uint32_t f = idx < nw ? (uint32_t)wf[idx] : 0u;
@@ -222,9 +240,58 @@ __global__ __launch_bounds__(kBlock, LISTED ? GR_LISTED_MIN_WAVES : GR_FAST_MIN_
         const uint32_t wave = g + W * (r + b), hint = (uint32_t)__shfl((int)f, (int)b) & 0x7Fu;
         const uint64_t m = wm[wave];
         fast_wave<S, R, RM>(kp, wave * 64 + lane, wave, hint, wave_kernel(hint, S), (m >> lane) & 1ull, bail_list,
-                            counters, list_cap);
+                            counters, list_cap, bid);
       }
     }
+  }
+  // the lanes the steady kernel left (lists 24..31, final: it ran before this
+  // launch on the stream), grid-stride; each role instance takes the lanes of
+  // its role. No hint is written for them (their waves were the steady kernel's).
+  LaneStats acc;
+  for (uint32_t base = bid * kBlock; base < n; base += nblk * kBlock) {
+    const uint32_t x = base + threadIdx.x;
+    bool bail = false;
+    uint32_t role = 0, li = 0;
+    if (x < n) {
+      uint32_t l, off;
+      list_at(start, x, &l, &off);
+      li = bail_list[(uint64_t)(kRetryList0 + l) * list_cap + off];
+      LaneStats ls;
+      bool skip = false;
+      uint32_t h = 0;
+      bail = !lean_step<S, R, RM>(kp, li, li, &ls, &role, 0u, &h, R, &skip);
+      bail = bail && !skip;
+      if (!bail && !skip) {
+        GR_CHECK_STATE(kp.st, li);
+        acc.leader_commit += ls.leader_commit;
+        acc.follower_commit += ls.follower_commit;
+        acc.msgs_in += ls.msgs_in;
+        acc.msgs_out += ls.msgs_out;
+        acc.leader_in += ls.leader_in;
+        acc.leader_out += ls.leader_out;
+        acc.entries += ls.entries;
+      }
+    }
+    const bool lead = role == GR_LEADER;
+    const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[li] & LW_OTHER);
+#pragma unroll
+    for (uint32_t side = 0; side < 3; ++side) {
+      const bool m = bail && (side == 2 ? tickish : !tickish && lead == (side == 1));
+      bail_append(m, (bid % 8) + side * 8, bail_list, counters, list_cap, li);
+    }
+  }
+  if (kp.stats && n > bid * kBlock) block_stats(kp, acc, bid);
+}
+
+// LISTED (split passes with the steady kernel, R != FL_ANY): roles_listed over
+// the whole grid. Otherwise one workgroup per 256 lanes, every wave checked
+// against its hint.
+template <int S, int R, int RM, bool LISTED>
+__global__ __launch_bounds__(kBlock, LISTED ? GR_LISTED_MIN_WAVES : GR_FAST_MIN_WAVES) void gr_fast_kernel(StepParams kp, uint32_t* bail_list,
+                                                                             uint32_t* counters, uint32_t list_cap) {
+  static_assert(!LISTED || R != FL_ANY, "listed waves are the role instances'");
+  if constexpr (LISTED) {
+    roles_listed<S, R, RM>(kp, bail_list, counters, list_cap, blockIdx.x, gridDim.x);
   } else {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
@@ -248,51 +315,18 @@ __global__ __launch_bounds__(kBlock, LISTED ? GR_LISTED_MIN_WAVES : GR_FAST_MIN_
     }
     if (blk) fast_wave<S, R, RM>(kp, i, wave, hint, wk, mine, bail_list, counters, list_cap);
   }
-  if (LISTED) {
-    // the lanes the steady kernel left (lists 24..31, final: it ran before this
-    // launch on the stream), grid-stride; each role instance takes the lanes of
-    // its role. No hint is written for them (their waves were the steady kernel's).
-    uint32_t start[9];
-    start[0] = 0;
-#pragma unroll
-    for (uint32_t l = 0; l < 8; ++l)
-      start[l + 1] = start[l] + (uint32_t)__builtin_amdgcn_readfirstlane(counters[(kRetryList0 + l) * kCounterStride]);
-    const uint32_t n = start[8];
-    LaneStats acc;
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-      const uint32_t x = base + threadIdx.x;
-      bool bail = false;
-      uint32_t role = 0, li = 0;
-      if (x < n) {
-        uint32_t l, off;
-        list_at(start, x, &l, &off);
-        li = bail_list[(uint64_t)(kRetryList0 + l) * list_cap + off];
-        LaneStats ls;
-        bool skip = false;
-        uint32_t h = 0;
-        bail = !lean_step<S, R, RM>(kp, li, li, &ls, &role, 0u, &h, R, &skip);
-        bail = bail && !skip;
-        if (!bail && !skip) {
-          GR_CHECK_STATE(kp.st, li);
-          acc.leader_commit += ls.leader_commit;
-          acc.follower_commit += ls.follower_commit;
-          acc.msgs_in += ls.msgs_in;
-          acc.msgs_out += ls.msgs_out;
-          acc.leader_in += ls.leader_in;
-          acc.leader_out += ls.leader_out;
-          acc.entries += ls.entries;
-        }
-      }
-      const bool lead = role == GR_LEADER;
-      const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[li] & LW_OTHER);
-#pragma unroll
-      for (uint32_t side = 0; side < 3; ++side) {
-        const bool m = bail && (side == 2 ? tickish : !tickish && lead == (side == 1));
-        bail_append(m, (blockIdx.x % 8) + side * 8, bail_list, counters, list_cap, li);
-      }
-    }
-    if (kp.stats && n > blockIdx.x * kBlock) block_stats(kp, acc);
-  }
+}
+
+// Both role instances of a split pass in one launch (GR_ROLES_MERGED=1, A/B):
+// workgroups [0, half) are the follower instance, [half, 2 half) the leader
+// instance. The two never touch the same lane (FastLane `take`), so they may
+// run side by side; the register allocation is the larger of the two.
+template <int S, int RM>
+__global__ __launch_bounds__(kBlock, GR_LISTED_MIN_WAVES) void gr_roles_kernel(StepParams kp, uint32_t* bail_list,
+                                                                                uint32_t* counters, uint32_t list_cap) {
+  const uint32_t half = gridDim.x / 2;
+  if (blockIdx.x < half) roles_listed<S, FL_FOLLOWER, RM>(kp, bail_list, counters, list_cap, blockIdx.x, half);
+  else roles_listed<S, FL_LEADER, RM>(kp, bail_list, counters, list_cap, blockIdx.x - half, half);
 }
 
 // The steady lanes (gr_steady.h) of a split pass, in a kernel of their own so
@@ -319,8 +353,12 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
     const uint64_t rem = __ballot(q == QS_OTHER);
     if ((threadIdx.x & 63) == 0) {
       wave_flags(bail_list, list_cap)[wave] = (uint8_t)(rem ? (WF_LISTED | hint) : 0u);
-      if (rem) wave_masks(bail_list, list_cap)[wave] = rem;
-      else kp.hints_out[wave] = 0;  // nothing here to speculate on next pass
+      if (rem) {
+        wave_masks(bail_list, list_cap)[wave] = rem;
+        counters[kListedWord] = 1u;  // the role instances have work (idempotent store)
+      } else {
+        kp.hints_out[wave] = 0;  // nothing here to speculate on next pass
+      }
     }
     return;
   }
@@ -412,6 +450,7 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
   for (uint32_t l = 0; l < kGeneralLists; ++l) start[l + 1] = start[l] + counters[l * kCounterStride];
   const uint32_t n = start[kGeneralLists];
   if (blockIdx.x == 0 && threadIdx.x < kCounters) next_counters[threadIdx.x * kCounterStride] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == kCounters) next_counters[kListedWord] = 0;
   if (blockIdx.x * kBlock >= n) return;  // uniform per block: nothing to do, no stats row touched
   LaneStats acc;
   for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
@@ -478,6 +517,7 @@ __global__ __launch_bounds__(kBlock, 1) void gr_small_kernel(StepParams kp, uint
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
   if (blockIdx.x == 0 && threadIdx.x < kCounters) next_counters[threadIdx.x * kCounterStride] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == kCounters) next_counters[kListedWord] = 0;
   const uint32_t hw = kp.hints ? sload_u32(kp.hints + (uint64_t)blockIdx.x * (kBlock / 64)) : 0u;
   const uint32_t hint = (hw >> (8 * (wave & 3))) & 0xFFu;
   const int wk = wave_kernel(hint, S);
@@ -526,6 +566,14 @@ constexpr uint32_t kTickBlocks = 1024;
 // the chip at their occupancy; with no listed wave each wave reads its flags
 // (one 64-byte load per 64 waves) and leaves.
 constexpr uint32_t kRoleBlocks = 1024;
+// GR_ROLES_MERGED=1: both role instances in one launch (gr_roles_kernel; A/B runs)
+inline bool roles_merged() {
+  static const bool v = [] {
+    const char* e = getenv("GR_ROLES_MERGED");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 
 template <int S, int RM>
 hipError_t launch_fast(const StepParams& kp0, uint32_t blocks, uint32_t* bail_list, uint32_t* cur, uint32_t list_cap,
@@ -540,6 +588,10 @@ hipError_t launch_fast(const StepParams& kp0, uint32_t blocks, uint32_t* bail_li
       const hipError_t e0 = hipGetLastError();
       if (e0 != hipSuccess) return e0;
       const uint32_t rb = blocks < kRoleBlocks ? blocks : kRoleBlocks;
+      if (roles_merged()) {
+        hipLaunchKernelGGL((gr_roles_kernel<S, RM>), dim3(2 * rb), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
+        return hipGetLastError();
+      }
       hipLaunchKernelGGL((gr_fast_kernel<S, FL_FOLLOWER, RM, true>), dim3(rb), dim3(kBlock), 0, s, kp, bail_list,
                          cur, list_cap);
       const hipError_t e1 = hipGetLastError();

@@ -1172,11 +1172,11 @@ struct Lane {
     m.log_index = 0; m.log_term = 0; m.commit = 0; m.hint = 0; m.hint_high = 0; m.rt0 = 0; m.rt1 = 0;
     switch (m.type) {
       case GR_REPLICATE:
-        m.log_index = mb.u64(k, MF_LOG_INDEX);
+        m.log_index = mb.log_index_at(k, cb);  // a shared mailbox: message 0's
         if (m.flags & MFL_COMPACT) {  // LogTerm = Term, <= 1 entry at Term, narrow Commit
           m.n = (m.flags & MFL_N1) ? 1u : 0u;
           m.log_term = m.term;
-          m.commit = commit_of(mb.t32(k, MT_CDELTA), m.log_index);
+          m.commit = commit_of(mb.cdelta_at(k, cb), m.log_index);
           m.rt0 = m.n ? m.term : 0;
           break;
         }
@@ -1193,7 +1193,7 @@ struct Lane {
         }
         break;
       case GR_REPLICATE_RESP:
-        m.log_index = mb.u64(k, MF_LOG_INDEX);
+        m.log_index = mb.log_index_at(k, cb);  // a shared mailbox: message 0's + k
         if (m.flags & MFL_REJECT) m.hint = mb.u64(k, MF_HINT);
         break;
       case GR_HEARTBEAT:
@@ -1468,7 +1468,7 @@ struct Lane {
       const uint32_t g = in_gpos(j);
       if (g == NOPOS) continue;
       const Mailbox mb = kp.in.at(g);
-      const uint32_t cb = mb.cnt(), c = cb & MB_COUNT;
+      const uint32_t cb = mb.cnt(), c = mb_n(cb);
 #pragma unroll 1
       for (uint32_t k = 0; k < c; ++k) {
         if (item == limit) { *at = item; return 0; }

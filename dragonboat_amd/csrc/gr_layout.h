@@ -305,6 +305,20 @@ constexpr uint8_t MFL_N1 = 0x20;
 // so they touch neither the per-message tags and terms nor the cold chunk. Only
 // the lean lane writes uniform mailboxes; every other writer stores all fields.
 constexpr uint8_t MB_COUNT = 0x07, MB_UNIFORM = 0x08, MB_RESP = 0x10;
+// Shared uniform mailboxes (MB_UNIFORM | MB_SHARED; the count is then bits 0-1):
+// the steady state's two messages per mailbox repeat each other's hot fields, so
+// only message 0's are stored. Compact Replicates: every message has message
+// 0's LogIndex and Commit offset (a commit broadcast and the proposal after it,
+// both at the leader's old lastIndex: makeReplicateMessage, raft.go:474-498);
+// accepts: message k has LogIndex = message 0's + k (the acks of those two
+// Replicates, LogIndex + entries, raft.go:971-974). A shared Replicate mailbox
+// stores 12 bytes less per extra message, a shared ack mailbox 8. Readers take
+// the count from mb_n and the fields from Mailbox::log_index_at / cdelta_at.
+constexpr uint8_t MB_SHARED = 0x04;
+__host__ __device__ inline uint32_t mb_n(uint32_t cb) { return (cb & MB_UNIFORM) ? (cb & 3u) : (cb & MB_COUNT); }
+__host__ __device__ inline bool mb_shared(uint32_t cb) {
+  return (cb & (MB_UNIFORM | MB_SHARED)) == (MB_UNIFORM | MB_SHARED);
+}
 // On a mailbox without MB_UNIFORM, bit 4 means its cold fields did not fit the
 // exchange's side buffer (gr_io.h side_pack): a reader escalates CAPACITY at its
 // first message instead of reading them (cross-GPU spaces only).
@@ -419,6 +433,15 @@ struct Mailbox {
   }
   __host__ __device__ inline uint32_t term_at(uint32_t k, uint32_t cb) const {
     return (cb & MB_UNIFORM) ? mterm() : t32(k, MT_TERM);
+  }
+  // LogIndex and Commit offset of message k given the count byte (shared
+  // mailboxes: derived from message 0's, which is all they store)
+  __host__ __device__ inline uint64_t log_index_at(uint32_t k, uint32_t cb) const {
+    if (k && mb_shared(cb)) return u64(0, MF_LOG_INDEX) + ((cb & MB_RESP) ? (uint64_t)k : 0ull);
+    return u64(k, MF_LOG_INDEX);
+  }
+  __host__ __device__ inline uint32_t cdelta_at(uint32_t k, uint32_t cb) const {
+    return t32(k && mb_shared(cb) ? 0u : k, MT_CDELTA);
   }
   __host__ __device__ static inline uint32_t uniform_tag(uint32_t cb, uint32_t k) {
     if (cb & MB_RESP) return GR_REPLICATE_RESP;  // flags 0: an accept

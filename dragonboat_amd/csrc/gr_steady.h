@@ -110,8 +110,15 @@ struct SteadyLeader : SteadyBase<RM> {
       cb[j] = in ? (uint32_t)ntld(mb.cnt()) : 0u;
       mt[j] = in ? ntld(mb.mterm()) : 0u;
       x[j][0] = in ? ntld(mb.u64(0, MF_LOG_INDEX)) : 0ull;
-      x[j][1] = in ? ntld(mb.u64(1, MF_LOG_INDEX)) : 0ull;
       m[j] = (uint32_t)j != hself ? ntld(B::s64(Rw::MATCH + j)) : hi0;
+    }
+    // a second ack: shared mailboxes (MB_SHARED, the steady state) imply it from
+    // the first; only an unshared pair loads it, in a second round
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      x[j][1] = x[j][0] + 1;
+      if (gin[j] != NOPOS && mb_n(cb[j]) >= 2 && !mb_shared(cb[j]))
+        x[j][1] = ntld(B::min_at(gin[j]).u64(1, MF_LOG_INDEX));
     }
     // ---- preconditions (see the header comment)
     const uint32_t self = h_self(hdr), flags = h_flags(hdr);
@@ -124,7 +131,7 @@ struct SteadyLeader : SteadyBase<RM> {
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       ok = ok && rb_kind(rb, j) == GR_SLOT_VOTER && h_nx(hdr, j);
-      const uint32_t c = cb[j] & MB_COUNT;
+      const uint32_t c = mb_n(cb[j]);
       nmi += c;
       if ((uint32_t)j != hself) {
         ok = ok && rb_state(rb, j) == GR_REPLICATE_ST && rb_active(rb, j);
@@ -143,7 +150,7 @@ struct SteadyLeader : SteadyBase<RM> {
     for (int j = 0; j < S; ++j) {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
-        const bool upd = (uint32_t)j != hself && (uint32_t)k < (cb[j] & MB_COUNT) && m[j] < x[j][k];
+        const bool upd = (uint32_t)j != hself && (uint32_t)k < mb_n(cb[j]) && m[j] < x[j][k];
         m[j] = upd ? x[j][k] : m[j];
         mdirty |= upd ? 1u << j : 0u;
         const uint64_t q = B::umax(B::umin(m[0], m[1]), B::umin(B::umax(m[0], m[1]), m[2]));  // sortMatchValues, R = 3
@@ -155,7 +162,9 @@ struct SteadyLeader : SteadyBase<RM> {
       }
     }
     const uint32_t nout = ncb + np;  // messages per follower mailbox
-    ok = ok && nout <= kUniformMax && nout <= kp.out.depth;
+    // the closed form keeps two commit broadcasts (bc0, bc1): a third one (staggered
+    // acks, e.g. A acks 10, 11 and B acks 12 over committed 9) is FastLane's
+    ok = ok && ncb <= 2 && nout <= kUniformMax && nout <= kp.out.depth;
     uint32_t cd0 = 0, cd1 = 0, cdp = 0;
     ok = ok && (ncb < 1 || commit_delta(bc0, hi0, &cd0)) && (ncb < 2 || commit_delta(bc1, hi0, &cd1)) &&
          (np == 0 || commit_delta(c, hi0, &cdp));
@@ -171,7 +180,11 @@ struct SteadyLeader : SteadyBase<RM> {
       if ((mdirty >> j) & 1u) ntst(B::s64(Rw::MATCH + j), m[j]);
     // match[self] = lastIndex and every next = lastIndex + 1 again: the sync bits
     // hold, the header is unchanged
-    const uint32_t nb = nout | MB_UNIFORM | (np ? 1u << (MB_N1_SHIFT + ncb) : 0u);
+    // one commit broadcast and the proposal: both carry LogIndex = the old
+    // lastIndex and Commit = c, a shared mailbox (gr_layout.h MB_SHARED) stores
+    // message 0's fields only
+    const bool shared = ncb == 1 && np == 1;
+    const uint32_t nb = nout | MB_UNIFORM | (shared ? MB_SHARED : 0u) | (np ? 1u << (MB_N1_SHIFT + ncb) : 0u);
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       if (gout[j] == NOPOS) continue;
@@ -189,7 +202,7 @@ struct SteadyLeader : SteadyBase<RM> {
         ntst(mb.u64(1, MF_LOG_INDEX), hi0);
         ntst(mb.t32(1, MT_CDELTA), cd1);
       }
-      if (np) {
+      if (np && !shared) {
         ntst(mb.u64(ncb, MF_LOG_INDEX), hi0);
         ntst(mb.t32(ncb, MT_CDELTA), cdp);
       }
@@ -208,7 +221,7 @@ struct SteadyLeader : SteadyBase<RM> {
     ls->leader_out = nmo;
     ls->entries = 0;
     *hint_out = (nmi || np) ? (WH_STEADY_LEADER | (self << WH_SLOT_SHIFT)) : 0u;  // FastLane::role_hint
-    GR_COVER(FAST_LEADER);
+    GR_COVER(STEADY_LEADER);
     return true;
   }
 };
@@ -236,7 +249,7 @@ struct SteadyFollower : SteadyBase<RM> {
     for (int j = 0; j < S; ++j) {
       const bool in = gin[j] != NOPOS;
       const uint32_t b = in ? (uint32_t)ntld(B::min_at(gin[j]).cnt()) : 0u;
-      other |= (uint32_t)j != hL ? (b & MB_COUNT) : 0u;
+      other |= (uint32_t)j != hL ? mb_n(b) : 0u;
       gL = (uint32_t)j == hL ? gin[j] : gL;
       oL = (uint32_t)j == hL ? gout[j] : oL;
     }
@@ -245,14 +258,19 @@ struct SteadyFollower : SteadyBase<RM> {
     const uint32_t fmt = gL != NOPOS ? ntld(mb.mterm()) : 0u;
     uint64_t li[2];
     uint32_t cd[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      li[k] = gL != NOPOS ? ntld(mb.u64(k, MF_LOG_INDEX)) : 0ull;
-      cd[k] = gL != NOPOS ? ntld(mb.t32(k, MT_CDELTA)) : 0u;
+    li[0] = gL != NOPOS ? ntld(mb.u64(0, MF_LOG_INDEX)) : 0ull;
+    cd[0] = gL != NOPOS ? ntld(mb.t32(0, MT_CDELTA)) : 0u;
+    // a shared mailbox (MB_SHARED, the steady state) repeats message 0's fields;
+    // only an unshared pair loads the second, in a second round
+    li[1] = li[0];
+    cd[1] = cd[0];
+    if (gL != NOPOS && mb_n(cbL) >= 2 && !mb_shared(cbL)) {
+      li[1] = ntld(mb.u64(1, MF_LOG_INDEX));
+      cd[1] = ntld(mb.t32(1, MT_CDELTA));
     }
     // ---- preconditions
     const uint32_t flags = h_flags(hdr);
-    const uint32_t c = cbL & MB_COUNT;
+    const uint32_t c = mb_n(cbL);
     bool ok = h_state(hdr) == GR_FOLLOWER && !(hdr & H_SYNC_MASK) && (hdr & H_RUN_MASK) == H_RUN_MASK &&
               h_nruns(hdr) >= 1 && h_gelo(hdr) && (flags & F_ETZ) && ((flags & F_LSLOT) >> F_LSLOT_SHIFT) == hL + 1 &&
               lw == 0 && other == 0 && !wide_term(term, 0, 0, 0);
@@ -289,10 +307,13 @@ struct SteadyFollower : SteadyBase<RM> {
         ntst(mo.cnt(), (uint8_t)0);
         continue;
       }
+      // two consecutive accepts (the acks of a commit broadcast and the proposal
+      // after it) make a shared mailbox: LogIndex of message 0 only
+      const bool shared = c == 2 && out[1] == out[0] + 1;
       ntst(mo.u64(0, MF_LOG_INDEX), out[0]);
-      if (c > 1) ntst(mo.u64(1, MF_LOG_INDEX), out[1]);
+      if (c > 1 && !shared) ntst(mo.u64(1, MF_LOG_INDEX), out[1]);
       ntst(mo.mterm(), (uint32_t)term);
-      ntst(mo.cnt(), (uint8_t)(c | MB_UNIFORM | MB_RESP));
+      ntst(mo.cnt(), (uint8_t)(c | MB_UNIFORM | MB_RESP | (shared ? MB_SHARED : 0u)));
     }
     if (append_from) kp.ln.u64(LR_APPEND_FROM)[i] = append_from;
     ntst(kp.ln.u8(LR_RFLAGS)[i], (uint8_t)(append_from ? RF_APPEND : 0));
@@ -305,7 +326,7 @@ struct SteadyFollower : SteadyBase<RM> {
     ls->leader_out = 0;
     ls->entries = nent;
     *hint_out = c ? (WH_FOLLOWER | WH_RUNS | (hL << WH_SLOT_SHIFT)) : 0u;  // FastLane::role_hint
-    GR_COVER(FAST_FOLLOWER);
+    GR_COVER(STEADY_FOLLOWER);
     return true;
   }
 };
@@ -334,7 +355,7 @@ GF_HD int quiet_step(const StepParams& kp, uint32_t i, uint32_t p) {  // lane i,
   uint32_t any = 0;
 #pragma unroll
   for (int j = 0; j < S; ++j)
-    any |= gin[j] != NOPOS ? ((uint32_t)ntld(kp.in.template at<kOneChunk>(gin[j]).cnt()) & MB_COUNT) : 0u;
+    any |= gin[j] != NOPOS ? mb_n((uint32_t)ntld(kp.in.template at<kOneChunk>(gin[j]).cnt())) : 0u;
   if (any) return QS_OTHER;
   ntst(kp.st.u64(SR_ETICK)[p], (uint64_t)(et + nq));
   if (h_flags(hdr) & F_ETZ) ntst(kp.st.u64(SR_HDR)[p], hdr & ~((uint64_t)F_ETZ << H_FLAGS_SHIFT));
@@ -342,7 +363,7 @@ GF_HD int quiet_step(const StepParams& kp, uint32_t i, uint32_t p) {  // lane i,
   for (int j = 0; j < S; ++j)
     if (gout[j] != NOPOS) ntst(kp.out.template at<kOneChunk>(gout[j]).cnt(), (uint8_t)0);
   ntst(kp.ln.u8(LR_RFLAGS)[i], (uint8_t)0);
-  GR_COVER(FAST_QUIESCED);
+  GR_COVER(QUIET_STEP);
   return QS_DONE;
 }
 

@@ -239,7 +239,7 @@ struct TickLane {
       gout[j] = route_of(kp, 1, j, i);
       outc[j] = 0;
       cbs[j] = gin[j] != NOPOS ? (uint32_t)kp.in.at(gin[j]).cnt() : 0u;
-      cnt[j] = cbs[j] & MB_COUNT;
+      cnt[j] = mb_n(cbs[j]);
     }
     const bool leader = state == GR_LEADER;
     GT_BAIL(!leader && state != GR_FOLLOWER);

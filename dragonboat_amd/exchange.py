@@ -126,7 +126,9 @@ def spread_peers(G, R, N, rank, seed=2, **kw):
 class Exchange:
     """Spaces + routes for one rank; `step` launches one pass and exchanges."""
 
-    def __init__(self, G, R, S, world, rank, placement, seed=2):
+    def __init__(self, G, R, S, world, rank, placement, seed=2, exchange=None):
+        """exchange=True keeps the one-rank spread exchange (copy + side buffers)
+        that a one-rank run otherwise skips (tests of the N > 1 code on one GPU)."""
         self.G, self.R, self.S = G, R, S
         self.world, self.rank, self.placement = world, rank, placement
         self.n_peers = R * G
@@ -147,6 +149,13 @@ class Exchange:
             self.depth = 3  # two Replicates (or acks) + a heartbeat (or its ack) per pass
         else:
             raise ValueError(placement)
+        # one rank: every mailbox is the rank's own, at the same position on both
+        # sides (the one chunk's sender and receiver positions coincide), so the
+        # exchange is no copy at all: the two spaces ping-pong as in local placement
+        self.pingpong = placement == "local" or (world == 1 and not exchange)
+        if placement == "spread" and world == 1:
+            assert self.n_chunks == 1 and np.array_equal(np.sort(self.in_pos[self.in_pos != NOPOS]),
+                                                         np.sort(self.out_pos[self.out_pos != NOPOS]))
 
     def allocate(self, eng, device):
         import torch
@@ -157,7 +166,7 @@ class Exchange:
         assert nbytes == self.n_chunks * cb and 0 < hb < cb
         self.hot_region = self.n_chunks * hb  # hot chunks first, then the cold chunks
         self.hot_tile = eng.hot_tile_bytes(self.depth)  # positions tiled by 64, counts first in a tile
-        if self.placement == "spread":  # all_to_all split sizes, bytes per peer rank
+        if not self.pingpong:  # all_to_all split sizes, bytes per peer rank
             self.hot_splits = ([hb if d in self.dests else 0 for d in range(self.world)],
                                [hb if a in self.srcs else 0 for a in range(self.world)])
             # side buffers: the cold fields of up to 1/32 of a chunk's mailboxes
@@ -175,7 +184,9 @@ class Exchange:
         """Spread placement, after a pass on stream handle h: compact the out
         space's cold fields, move the hot region and the side buffers (fixed
         sizes), unpack the side buffers into the in space. Returns the pending
-        collective work (empty with one rank or a host backend)."""
+        collective work (empty with one rank or a host backend). The copies and
+        collectives run on torch's current stream, which the caller makes the
+        stream of h (Exchange.step, Pipeline.step)."""
         inp, out = spaces
         side_out, side_in = self.side
         eng.side_pack(out.data_ptr(), self.n_chunks, self.positions, self.depth, side_out.data_ptr(),
@@ -199,7 +210,7 @@ class Exchange:
     def step(self, eng, spaces, k, stream, events=None):
         """One pass: kernel (optionally bracketed by `events`), then the exchange."""
         h = stream.cuda_stream
-        if self.placement == "local":
+        if self.pingpong:
             src, dst = spaces[k % 2], spaces[(k + 1) % 2]
         else:
             src, dst = spaces[0], spaces[1]
@@ -209,9 +220,13 @@ class Exchange:
                         self.n_chunks, self.positions, self.n_peers, h, depth=self.depth)
         if events is not None:
             events[1].record(stream)
-        if self.placement == "spread":
-            for w in self.exchange(eng, spaces, h):
-                w.wait()
+        if not self.pingpong:
+            import torch
+            # exchange() copies (one rank) and issues RCCL on torch's current
+            # stream: make that the pass's stream, so they follow the pack
+            with torch.cuda.stream(stream):
+                for w in self.exchange(eng, spaces, h):
+                    w.wait()
             self.unpack(eng, spaces, h)
 
 
@@ -235,12 +250,16 @@ class Pipeline:
     is one bank whose two spaces ping-pong (no exchange).
     """
 
-    def __init__(self, G, R, S, world, rank, placement="spread", banks=None, seed=2):
-        if banks is None:
-            banks = 2 if placement == "spread" and G >= 128 else 1
-        sizes = [G // banks + (1 if b < G % banks else 0) for b in range(banks)]
+    def __init__(self, G, R, S, world, rank, placement="spread", banks=None, seed=2, exchange=None):
+        if banks is None:  # banks overlap one another's exchange: only with one to overlap
+            banks = 2 if placement == "spread" and world > 1 and G >= 128 else 1
+        # bank sizes a multiple of 64 but the last: a wave's lanes then share a
+        # replica block (StepParams::route_wu, scalar route arithmetic)
+        base = (G // banks) // 64 * 64 if G // banks >= 64 else G // banks
+        sizes = [base] * (banks - 1) + [G - base * (banks - 1)]
         self.R, self.S, self.world, self.rank, self.placement = R, S, world, rank, placement
-        self.ex = [Exchange(Gb, R, S, world, rank, placement, seed=seed + 7919 * b) for b, Gb in enumerate(sizes)]
+        self.ex = [Exchange(Gb, R, S, world, rank, placement, seed=seed + 7919 * b, exchange=exchange)
+                   for b, Gb in enumerate(sizes)]
         self.groups = G
         self.engines, self.spaces, self.streams = [], [], []
         self.work = [[] for _ in self.ex]
@@ -271,14 +290,14 @@ class Pipeline:
                 for w in self.work[b]:
                     w.wait()  # s waits for this bank's previous exchange
                 self.work[b] = []
-                if ex.placement == "local":
+                if ex.pingpong:
                     src, dst = self.spaces[b][k % 2], self.spaces[b][(k + 1) % 2]
                 else:
                     src, dst = self.spaces[b][0], self.spaces[b][1]
                     ex.unpack(eng, self.spaces[b], s.cuda_stream)
                 eng.step_device(src.data_ptr(), dst.data_ptr(), ex.n_chunks, ex.positions, ex.n_chunks,
                                 ex.positions, ex.n_peers, s.cuda_stream, depth=ex.depth)
-                if ex.placement == "spread":
+                if not ex.pingpong:
                     self.work[b] = ex.exchange(eng, self.spaces[b], s.cuda_stream)
 
     def exchange_bytes_per_pass(self):
@@ -286,7 +305,7 @@ class Pipeline:
         buffers of the chunks for other ranks; 0 for local placement)."""
         tot = 0
         for ex in self.ex:
-            if ex.placement == "spread":
+            if not ex.pingpong:
                 tot += sum(n for d, n in zip(range(self.world), ex.hot_splits[0]) if d != self.rank)
                 tot += sum(n for d, n in zip(range(self.world), ex.side_splits[0]) if d != self.rank)
         return tot

@@ -177,12 +177,65 @@ def targeted(backend):
     return got
 
 
+def quiesced(backend, G=256, passes=6, seed=13):
+    """A quiesced population (QuiescedTick only) between steady passes: the lean
+    lane's quiesced path and, on split passes, the steady kernel's quiet_step."""
+    R = 3
+    peers = P.make_groups(G, R, seed=seed)
+    topo = P.Topology(G, R)
+
+    def lf(k):
+        if k % 3 == 2:
+            return P.propose_locals(R * G, np.arange(G), pass_index=k)
+        return P.propose_locals(R * G, [], pass_index=k, quiesced=1 + k % 2)
+    return SIM.simulate(backend, peers, topo, passes, lf)
+
+
+def device_battery(lib_path):
+    """The device-resident split schedule (devsim.DeviceLockstep, split forced on
+    a small population): the steady kernel's closed-form leader and follower
+    lanes and quiet_step, the role instances, staggered acks, churn; oracle
+    every pass. Returns the stats of each run."""
+    import os
+    import devsim
+    out = {}
+    old = os.environ.get("GR_SPLIT_MIN_LANES")
+    os.environ["GR_SPLIT_MIN_LANES"] = "1"  # read at gr_create
+    try:
+        G, R = 1024, 3
+        topo = P.Topology(G, R)
+        rng = np.random.default_rng(17)
+        ls = devsim.DeviceLockstep(P.make_groups(G, R, seed=17), G, R, lib_path=lib_path)
+        try:
+            for k in range(15):
+                if k in (11, 13):
+                    cur = ls.export()
+                    ch = P.inject_leader_change(cur, topo, 0.2, rng)
+                    ls.inject(ch, cur[ch])
+                if 3 <= k <= 9:  # quiesced passes; once the messages die out, waves lose
+                    # their hints (FastLane's quiesced path) and the steady kernel's quiet_step runs
+                    loc = P.propose_locals(R * G, [], pass_index=k, quiesced=1)
+                else:
+                    loc = P.propose_locals(R * G, P.current_leaders(ls.export(), topo), pass_index=k)
+                ls.step(loc)
+            out["device_split"] = dict(ls.stats)
+        finally:
+            ls.close()
+    finally:
+        if old is None:
+            os.environ.pop("GR_SPLIT_MIN_LANES", None)
+        else:
+            os.environ["GR_SPLIT_MIN_LANES"] = old
+    return out
+
+
 def battery(backend):
     """Everything above plus the blind-spot and network workloads (small sizes)."""
     class Req:  # the tests' fixture lookup, satisfied by the caller
         def getfixturevalue(self, name):
             return None
-    out = {"fuzz": fuzz(backend)["esc_reasons"], "targeted": targeted(backend)}
+    out = {"fuzz": fuzz(backend)["esc_reasons"], "targeted": targeted(backend),
+           "quiesced": quiesced(backend)["commits"]}
     be = "gpu" if backend is SIM.GpuBackend else "cpu"
     req = Req()
     for R, obs in [(2, 1), (3, 2)]:

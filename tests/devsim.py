@@ -29,7 +29,8 @@ def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None
     and followers; the routes are then plain tables (local placement only)."""
     import torch
     S = R
-    ex = Exchange(G, R, S, 1, 0, placement, seed=seed)
+    # spread on one rank: keep the exchange (copy + side buffers) under test
+    ex = Exchange(G, R, S, 1, 0, placement, seed=seed, exchange=placement == "spread")
     n = ex.n_peers
     # perm[x] = engine peer of replica-major peer x (identity unless mix)
     perm = np.arange(n)
@@ -111,7 +112,7 @@ def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None
     return final
 
 
-def route(out, ex, G, R, perm=None):
+def route(out, ex, G, R, perm=None):  # (ex: unused, the layout is replica-major)
     """Outbox records (sender peer, target slot) -> inbox records (receiver, sender slot),
     using the placement's peer layout (replica-major in both placements on one rank,
     engine peer perm[x] for replica-major peer x when given)."""
@@ -129,3 +130,146 @@ def route(out, ex, G, R, perm=None):
     nxt["slot"] = r.astype(np.uint8)
     order = np.lexsort((np.arange(len(nxt)), nxt["slot"], nxt["peer"]))
     return nxt[order]
+
+
+class DeviceLockstep:
+    """The device-resident split schedule (gr_step_device over loopback mailbox
+    spaces: the steady kernel, the role instances, the tick and general kernels,
+    exactly what bench.py and tools/bench_configs.py time) stepped pass by pass
+    beside the oracle on identical inputs. After every pass it checks every
+    peer's state, every mailbox of the space the next pass reads, every result
+    and every escalation against the oracle (the escalation protocol of
+    simulate.Lockstep: escalated groups are compared at their prefix and
+    reloaded from the oracle's full pass).
+
+    The next pass's inbox is the space the kernels wrote, untouched, unless the
+    host has to change it: a group escalated (the space holds only its device
+    prefix; the oracle's full outbox is encoded in its place, as the host's
+    messages would be) or `drop_fn` drops messages (the network's loss, config
+    3's HeartbeatResp drops): then the whole space is re-encoded from the
+    oracle's delivered messages (gr_space_encode) and uploaded."""
+
+    def __init__(self, peers, G, R, lib_path=None, threads=16):
+        import torch
+        from dragonboat_amd import populations as P
+        self.G, self.R, self.S = G, R, R
+        self.n = R * G
+        assert len(peers) == self.n
+        self.topo = P.Topology(G, R)
+        self.in_pos, self.out_pos = self.topo.loopback_routes(self.S)
+        self.positions = self.n * self.S
+        self.depth = abi.GR_C
+        self.eng = Engine(self.n, self.S, lib_path=lib_path)
+        self.eng.load(peers)
+        self.eng.bind_routes(self.in_pos, self.out_pos)
+        nb = self.eng.space_bytes(1, self.positions, self.depth)
+        self.spaces = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        self.stream = torch.cuda.current_stream()
+        self.pop = OraclePopulation(peers, self.S)
+        self.inv = self._inverse()
+        self.msgs = np.zeros(0, abi.MESSAGE)  # the oracle's view of the next inbox
+        self.threads = threads
+        self.k = 0
+        self.stats = {"escalations": 0, "esc_reasons": {}, "reencoded": 0, "commits": 0, "ready": 0,
+                      "msgs": 0, "injected": 0}
+
+    def _inverse(self):
+        """mailbox position -> (receiving peer, sender slot), as arrays."""
+        peer = np.full(self.positions, -1, np.int64)
+        slot = np.full(self.positions, -1, np.int64)
+        for j in range(self.S):
+            ok = self.in_pos[j] != 0xFFFFFFFF
+            p = np.nonzero(ok)[0]
+            peer[self.in_pos[j, ok].astype(np.int64)] = p
+            slot[self.in_pos[j, ok].astype(np.int64)] = j
+        return peer, slot
+
+    def export(self):
+        return self.pop.export()
+
+    def inject(self, idx, recs):
+        """Host-side state edits on both sides (config 5's leader changes)."""
+        idx = np.asarray(idx, np.int64)
+        if len(idx):
+            self.pop.reload(idx, recs)
+            self.eng.load_peers(idx.astype(np.uint32), recs)
+            self.stats["injected"] += len(idx)
+
+    def _encode(self, msgs, space):
+        """Write inbox records (receiver peer, sender slot) into a device space."""
+        from dragonboat_amd.engine import load_library
+        lib = self.eng.lib
+        buf = np.zeros(self.eng.space_bytes(1, self.positions, self.depth), np.uint8)
+        pos = self.in_pos[msgs["slot"].astype(np.int64), msgs["peer"].astype(np.int64)].astype(np.uint32)
+        assert np.all(pos != 0xFFFFFFFF)
+        order = np.argsort(pos, kind="stable")  # arrival order kept inside a mailbox
+        m, pos = np.ascontiguousarray(msgs[order]), np.ascontiguousarray(pos[order])
+        rc = lib.gr_space_encode(buf.ctypes.data, 1, self.positions, self.depth, m.ctypes.data if len(m) else None,
+                                 len(m), pos.ctypes.data if len(pos) else None)
+        assert rc == 0, rc
+        import torch
+        space.copy_(torch.from_numpy(buf))
+
+    def override_inbox(self, msgs):
+        """Replace the next pass's inbox (both sides) with inbox records."""
+        msgs = np.asarray(msgs, abi.MESSAGE)
+        self._encode(msgs, self.spaces[self.k % 2])
+        self.msgs = msgs
+
+    def step(self, loc, drop_fn=None):
+        import torch
+        k = self.k
+        loc = np.asarray(loc, abi.LOCAL)
+        self.eng.set_locals(loc)
+        dev0 = self.eng.sync(self.n)
+        src, dst = self.spaces[k % 2], self.spaces[(k + 1) % 2]
+        self.eng.step_device(src.data_ptr(), dst.data_ptr(), 1, self.positions, 1, self.positions, self.n,
+                             self.stream.cuda_stream, depth=self.depth)
+        torch.cuda.synchronize()
+        res = self.eng.collect_results(self.n)
+        lim = parity.limits_from(res, self.n)
+        o = self.pop.step(self.msgs, loc, lim, dev_before=dev0, threads=self.threads)
+        dev = self.eng.sync(self.n)
+        bad = parity.compare_states(dev, o["mid"], self.S)
+        assert not bad, f"pass {k}: state {bad[:3]}"
+        got = decode_space(dst.cpu().numpy(), 1, self.positions, self.depth)
+        pos = got["peer"].astype(np.int64)
+        got["peer"] = self.inv[0][pos].astype(np.uint32)
+        got["slot"] = self.inv[1][pos].astype(np.uint8)
+        want_prefix = self._route(parity.prefix_msgs(o, lim))
+        bad = parity.compare_msgs(got, want_prefix)
+        assert not bad, f"pass {k}: mailboxes {bad[:3]}"
+        bad = parity.compare_results(res, o["results"])
+        assert not bad, f"pass {k}: results {bad[:3]}"
+        bad = parity.check_escalations(res, o["esc_mask"])
+        assert not bad, f"pass {k}: unjustified escalations {bad[:3]}"
+        esc = res[res["escalation"] != 0]
+        st = self.stats
+        st["escalations"] += len(esc)
+        for r in esc:
+            nm = abi.ESC_NAMES[r["escalation"]]
+            st["esc_reasons"][nm] = st["esc_reasons"].get(nm, 0) + 1
+        st["commits"] += int(np.sum(dev["committed"] > dev0["committed"]))
+        st["ready"] += int(res["n_ready"].sum())
+        st["msgs"] += len(got)
+        full = self.pop.export()
+        assert self.pop.representable().all(), "a peer outgrew its gr_peer record"
+        nxt = self._route(o["msgs"])
+        n_full = len(nxt)
+        if drop_fn is not None:
+            nxt = drop_fn(k, nxt)
+        if len(esc) or len(nxt) != n_full:
+            if len(esc):  # the host ran their suffix: reload them from the oracle
+                idx = esc["peer"].astype(np.int64)
+                self.eng.load_peers(idx.astype(np.uint32), full[idx])
+            self._encode(nxt, dst)
+            st["reencoded"] += 1
+        self.msgs = nxt
+        self.k += 1
+        return res
+
+    def _route(self, out):
+        return route(out, self, self.G, self.R)
+
+    def close(self):
+        self.eng.close()

@@ -53,6 +53,9 @@ def test_coverage_gpu(gpu):
         before = np.zeros(len(names), np.uint64)
         assert lib.gr_coverage_read(before.ctypes.data_as(ctypes.c_void_p), len(names)) == len(names)
         out = CW.battery(SIM.GpuBackend)
+        # the device-resident split schedule (steady kernel, quiet_step, role
+        # instances): gr_step never launches it
+        out["device"] = CW.device_battery(build.COVER_LIB)
         after = np.zeros(len(names), np.uint64)
         lib.gr_coverage_read(after.ctypes.data_as(ctypes.c_void_p), len(names))
     finally:

@@ -502,12 +502,13 @@ def test_compact_log_moves_first_index(built, gpu):
     eng.close()
 
 
-@pytest.mark.parametrize("banks", [1, 2])
-def test_pipeline_spread_banks(gpu, banks):
-    """bench.py's N > 1 path at N = 1 (exchange = device copy): the banked spread
-    pipeline (dragonboat_amd.exchange.Pipeline: one engine and HIP stream per
-    bank, exchanges issued per bank after a device-side cold check) equals an
-    oracle run of every bank's groups after every pass."""
+@pytest.mark.parametrize("banks,exchange", [(1, False), (1, True), (2, True)])
+def test_pipeline_spread_banks(gpu, banks, exchange):
+    """The banked spread pipeline (dragonboat_amd.exchange.Pipeline: one engine
+    and HIP stream per bank) at N = 1 equals an oracle run of every bank's groups
+    after every pass: with the one-rank ping-pong (exchange=False, what bench.py
+    runs at N = 1) and with the N > 1 exchange code kept (exchange=True: device
+    copy of the hot region, side-buffer pack/unpack)."""
     import torch
     from dragonboat_amd import abi
     from dragonboat_amd.engine import Engine
@@ -515,7 +516,7 @@ def test_pipeline_spread_banks(gpu, banks):
     from oracle.pyoracle import OraclePopulation
     import parity
     G, R, K = 900, 3, 5
-    pipe = Pipeline(G, R, R, 1, 0, "spread", banks=banks)
+    pipe = Pipeline(G, R, R, 1, 0, "spread", banks=banks, exchange=exchange)
     pipe.setup(Engine, torch.device("cuda", 0), 0)
     pops = [OraclePopulation(ex.peers, R) for ex in pipe.ex]
     msgs = [np.zeros(0, abi.MESSAGE) for _ in pipe.ex]

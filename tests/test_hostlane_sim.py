@@ -121,3 +121,52 @@ def test_config1_single_group(built):
     pass for 300 passes, committed traced against the oracle every pass."""
     st = _run(1, 300, seed=1)
     assert st["escalations"] == 0 and st["commits"] >= 290 * 3 - 10
+
+
+def staggered_acks(G, R=3, seed=21):
+    """Leaders three entries past committed with both followers' match at
+    committed; follower 1 acks committed+1 and +2, follower 2 acks committed+3:
+    three commit advances in one pass (the closed-form steady leader
+    keeps two commit broadcasts and must hand this lane to FastLane)."""
+    peers = P.make_groups(G, R, seed=seed)
+    L = peers[:G]
+    c = L["committed"].copy()
+    for r in range(R):
+        peers[r * G:(r + 1) * G]["last_index"] = c + np.uint64(3)
+    L["remotes"]["next"][:, :R] = (c + np.uint64(4))[:, None]
+    L["remotes"]["match"][:, 0] = c + np.uint64(3)  # self
+    msgs = np.zeros(3 * G, abi.MESSAGE)
+    for k, (slot, d) in enumerate(((1, 1), (1, 2), (2, 3))):
+        m = msgs[k * G:(k + 1) * G]
+        m["peer"] = np.arange(G, dtype=np.uint32)
+        m["slot"] = slot
+        m["type"] = abi.REPLICATE_RESP
+        m["term"] = L["term"]
+        m["log_index"] = c + np.uint64(d)
+    order = np.lexsort((np.arange(len(msgs)), msgs["slot"], msgs["peer"]))
+    return peers, msgs[order]
+
+
+def test_steady_leader_staggered_acks(built):
+    """Three commit advances in one pass on steady leaders (sync bits set at load,
+    the device hint), with the device's hints and the split schedule: every
+    lane, state and message equal to the oracle."""
+    from oracle.pyoracle import hostlane_lib, hostlane_steady_lanes
+    G, R = 128, 3
+    peers, msgs = staggered_acks(G, R)
+    hl = hostlane_lib()
+    hl.hl_true_hints(1)
+    try:
+        ls = SIM.Lockstep(SIM.HostlaneBackend, peers, R)
+        s0 = hostlane_steady_lanes()
+        out, res = ls.step(msgs, np.zeros(0, abi.LOCAL))
+        assert not np.any(res["escalation"])
+        # the leaders committed all three (the median reached committed + 3)
+        st = ls.export()
+        assert np.all(st["committed"][:G] == peers["committed"][:G] + np.uint64(3))
+        # three commit broadcasts per follower this pass
+        assert len(out[(out["peer"] < G) & (out["type"] == abi.REPLICATE)]) == 3 * 2 * G
+        ls.close()
+        assert hostlane_steady_lanes() >= s0
+    finally:
+        hl.hl_true_hints(0)
