@@ -167,6 +167,7 @@ EXPORTS = [
     "gr_pack_messages", "gr_unpack_messages", "gr_pack_locals",
     "gr_collect_results", "gr_space_decode", "gr_space_encode", "gr_timing_begin", "gr_timing_end",
     "gr_bind_nodes", "gr_step_wire", "gr_step_wire_compact",
+    "gr_graph_capture", "gr_graph_replay", "gr_graph_destroy",
 ]
 
 

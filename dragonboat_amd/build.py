@@ -18,7 +18,7 @@ CSRC = os.path.join(ROOT, "dragonboat_amd", "csrc")
 ENGINE_SRC = [os.path.join(CSRC, "gr_engine.hip")] + [os.path.join(CSRC, f"gr_kernels_s{s}.hip") for s in (1, 3, 5, 8)]
 ENGINE_DEPS = ENGINE_SRC + [os.path.join(CSRC, f)
                             for f in ("gr_lane.h", "gr_layout.h", "gr_host.h", "gr_fast.h", "gr_steady.h", "gr_tick.h", "gr_io.h",
-                                      "gr_cover.h", "gr_kernels.h")] + \
+                                      "gr_cover.h", "gr_kernels.h", "gr_scan.h")] + \
     [os.path.join(ROOT, "include", "gpuraft.h")]
 JOBS = max(1, min(8, os.cpu_count() or 1))
 ENGINE_LIB = os.path.join(ROOT, "dragonboat_amd", "_build", "libgpuraft.so")
@@ -27,7 +27,8 @@ ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
 KAT_BIN = os.path.join(ROOT, "oracle", "_build", "kat_tests")
 HOSTLANE_LIB = os.path.join(ROOT, "tests", "_build", "libhostlane.so")
 WIRE_SRC = os.path.join(ROOT, "dragonboat_amd", "csrc", "gr_wire.hip")
-WIRE_DEPS = [WIRE_SRC, os.path.join(ROOT, "include", "gpuraft_wire.h"), os.path.join(ROOT, "include", "gpuraft.h")]
+WIRE_DEPS = [WIRE_SRC, os.path.join(ROOT, "include", "gpuraft_wire.h"), os.path.join(ROOT, "include", "gpuraft.h"),
+             os.path.join(CSRC, "gr_scan.h")]
 WIRE_LIB = os.path.join(ROOT, "dragonboat_amd", "_build", "libgrwire.so")
 WIRE_ORACLE_LIB = os.path.join(ROOT, "oracle", "_build", "liboraclewire.so")
 HBM_CALIB = os.path.join(ROOT, "tools", "hbm_calib")
@@ -197,7 +198,7 @@ def build_wire(force=False):
     os.makedirs(os.path.dirname(WIRE_LIB), exist_ok=True)
     if force or _stale(WIRE_LIB, WIRE_DEPS):
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-I" + os.path.join(ROOT, "include"), WIRE_SRC, "-o", WIRE_LIB])
+              "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, WIRE_SRC, "-o", WIRE_LIB])
     return WIRE_LIB
 
 

@@ -13,7 +13,6 @@
 #include <new>
 #include <vector>
 
-#include <rocprim/rocprim.hpp>  // device-wide scan and radix sort of the boundary passes (gr_io.h)
 
 #include "gr_host.h"
 #include "gr_io.h"
@@ -77,6 +76,9 @@ struct gr_engine {
   // gr_step_device passes of at least this many lanes run the role instances
   // (StepParams::split); GR_SPLIT_MIN_LANES at gr_create overrides it (tests)
   uint32_t split_min = kSplitMinLanes;
+  // passes of at most this many workgroups run fused (gr_small_kernel);
+  // GR_SMALL_BLOCKS at gr_create overrides it (0: never; tests and A/B runs)
+  uint32_t small_blocks = kSmallBlocks;
   uint8_t* hints = nullptr;      // 2 x [hint_stride(cap)] wave hints of the device-resident path (gr_layout.h WH_*):
                                  // one set read by a pass, the other written for the next
   uint64_t hint_flip = 0;
@@ -102,7 +104,8 @@ struct gr_engine {
   Buf d_mark, d_lop;        // [max_peers] input flags, lane of peer
   Buf d_keys, d_idx, d_skeys, d_sidx;  // mailbox sort
   Buf d_win, d_oc, d_off;   // [lanes]
-  Buf d_tmp;                // rocprim scratch
+  Buf d_tmp;                // scan tile sums (io_scan)
+  Buf d_kcnt, d_kbase;      // sort_keys: records per mailbox and their exclusive scan
   Buf d_scal;               // lane count, error, outbox total
   Buf d_outmsgs, d_results; // packed outbox
   Buf d_peers, d_slots;     // gr_peer records of a load/sync, slot list
@@ -203,6 +206,7 @@ StepParams base_params(gr_engine* e) {
   kp.ln = e->ln;
   kp.stats = e->stats;
   kp.max_entry_size = e->cfg.max_entry_size;
+  kp.small_blocks = e->small_blocks;
   return kp;
 }
 
@@ -288,40 +292,45 @@ int transfer(gr_engine* e, const uint32_t* slots, uint32_t first, size_t n, gr_p
   return GR_OK;
 }
 
-// Exclusive sum of n u32 on `s` (rocprim), scratch grown on demand.
+// Exclusive sum of n values on `s` (gr_scan.h), the tile sums in e->d_tmp.
+template <class T>
+int io_scan_t(gr_engine* e, const T* in, T* out, uint32_t n, hipStream_t s) {
+  if (n == 0) return GR_OK;
+  const int r = grow_device(&e->d_tmp.p, &e->d_tmp.n, (size_t)scan::scan_tiles_of(n) * sizeof(T));
+  if (r) return r;
+  HIPCHK(scan::exclusive_scan<T>(in, out, n, (T*)e->d_tmp.p, s));
+  return GR_OK;
+}
 int io_scan(gr_engine* e, const uint32_t* in, uint32_t* out, uint32_t n, hipStream_t s) {
-  size_t tb = 0;
-  HIPCHK(rocprim::exclusive_scan(nullptr, tb, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
-  const int r = grow_device(&e->d_tmp.p, &e->d_tmp.n, tb);
-  if (r) return r;
-  tb = e->d_tmp.n;
-  HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tb, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
-  return GR_OK;
+  return io_scan_t<uint32_t>(e, in, out, n, s);
 }
-
 int io_scan64(gr_engine* e, const uint64_t* in, uint64_t* out, uint32_t n, hipStream_t s) {
-  size_t tb = 0;
-  HIPCHK(rocprim::exclusive_scan(nullptr, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
-  const int r = grow_device(&e->d_tmp.p, &e->d_tmp.n, tb);
-  if (r) return r;
-  tb = e->d_tmp.n;
-  HIPCHK(rocprim::exclusive_scan(e->d_tmp.p, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
-  return GR_OK;
+  return io_scan_t<uint64_t>(e, in, out, n, s);
 }
 
-// Stable radix sort of the inbox's mailbox keys (slot-major j*nl + lane), so
-// arrival order inside a mailbox survives; sorted keys/indexes in d_skeys/d_sidx.
+// Stable sort of the inbox's mailbox keys (slot-major j*nl + lane, each below
+// `positions`), so arrival order inside a mailbox survives: a counting sort
+// (gr_io.h key_count, key_scatter, key_order); sorted keys/indexes in
+// d_skeys/d_sidx. d_idx holds each record's slot in its mailbox meanwhile.
 int sort_keys(gr_engine* e, uint32_t nm, uint32_t positions, hipStream_t s) {
-  uint32_t bits = 1;
-  while (bits < 32 && (1ull << bits) < positions) ++bits;
-  size_t tb = 0;
-  HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, (uint32_t*)e->d_keys.p, (uint32_t*)e->d_skeys.p,
-                                   (uint32_t*)e->d_idx.p, (uint32_t*)e->d_sidx.p, (size_t)nm, 0, bits, s));
-  const int r = grow_device(&e->d_tmp.p, &e->d_tmp.n, tb);
-  if (r) return r;
-  tb = e->d_tmp.n;
-  HIPCHK(rocprim::radix_sort_pairs(e->d_tmp.p, tb, (uint32_t*)e->d_keys.p, (uint32_t*)e->d_skeys.p,
-                                   (uint32_t*)e->d_idx.p, (uint32_t*)e->d_sidx.p, (size_t)nm, 0, bits, s));
+  int r;
+  if ((r = grow_device(&e->d_kcnt.p, &e->d_kcnt.n, (size_t)positions * 4 + 4))) return r;
+  if ((r = grow_device(&e->d_kbase.p, &e->d_kbase.n, (size_t)positions * 4 + 4))) return r;
+  uint32_t* cnt = (uint32_t*)e->d_kcnt.p;
+  uint32_t* base = (uint32_t*)e->d_kbase.p;
+  HIPCHK(hipMemsetAsync(cnt, 0, (size_t)positions * 4, s));
+  const dim3 blk(io::kIoBlock);
+  hipLaunchKernelGGL(io::key_count, dim3(io_grid(nm)), blk, 0, s, (const uint32_t*)e->d_keys.p, nm, cnt,
+                     (uint32_t*)e->d_idx.p);
+  HIPCHK(hipGetLastError());
+  if ((r = io_scan(e, cnt, base, positions, s))) return r;
+  hipLaunchKernelGGL(io::key_scatter, dim3(io_grid(nm)), blk, 0, s, (const uint32_t*)e->d_keys.p,
+                     (const uint32_t*)e->d_idx.p, nm, (const uint32_t*)base, (uint32_t*)e->d_skeys.p,
+                     (uint32_t*)e->d_sidx.p);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(io::key_order, dim3(io_grid(positions)), blk, 0, s, (const uint32_t*)cnt,
+                     (const uint32_t*)base, positions, (uint32_t*)e->d_sidx.p);
+  HIPCHK(hipGetLastError());
   return GR_OK;
 }
 
@@ -374,6 +383,7 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
     const long v = strtol(sm, nullptr, 10);
     if (v > 0) e->split_min = (uint32_t)v;
   }
+  if (const char* sb = getenv("GR_SMALL_BLOCKS")) e->small_blocks = (uint32_t)strtoul(sb, nullptr, 10);
   void *ds = nullptr, *dl = nullptr;
   if (hipMalloc(&ds, sb) != hipSuccess || hipMalloc(&dl, lb) != hipSuccess ||
       hipMalloc((void**)&e->stats, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
@@ -417,7 +427,7 @@ void gr_destroy(gr_engine* e) {
                             &e->d_idx, &e->d_skeys, &e->d_sidx, &e->d_win, &e->d_oc, &e->d_off, &e->d_tmp,
                             &e->d_scal, &e->d_outmsgs, &e->d_results, &e->d_peers, &e->d_slots, &e->d_ext,
                             &e->d_lext, &e->d_oc64, &e->d_off64, &e->d_rx, &e->d_roff, &e->d_outext,
-                            &e->d_resext, &e->d_nodes, &e->d_wrec, &e->d_why, &e->d_unr})
+                            &e->d_resext, &e->d_nodes, &e->d_wrec, &e->d_why, &e->d_unr, &e->d_kcnt, &e->d_kbase})
     if (b->p) (void)hipFree(b->p);
   for (uint8_t* h : {e->h_outmsgs, e->h_results, e->h_scal, e->h_inmsgs, e->h_inlocals, e->h_inext, e->h_inlext,
                      e->h_outext, e->h_resext, e->h_unr})
@@ -1439,15 +1449,10 @@ int gr_set_locals(gr_engine* e, const gr_local_input* locals, size_t n) {
   return GR_OK;
 }
 
-int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t in_chunks,
-                   uint32_t in_positions, uint32_t out_chunks, uint32_t out_positions, uint32_t depth,
-                   uint32_t n_peers, void* stream) {
-  if (!e || !in_space || !out_space || n_peers > e->cfg.max_peers || depth == 0 || depth > GR_C)
-    return GR_EINVAL;
-  // the mutex orders this pass after a compact _begin/_end on another thread
-  // (uncontended: one lock per pass)
-  std::lock_guard<std::mutex> guard(e->mu);
-  GR_REFUSE_PENDING(e);  // the pending compact pass owns the lane rows and bail lists
+// One device-resident pass, enqueued on `stream` (e->mu held by the caller).
+static int step_device_locked(gr_engine* e, const void* in_space, void* out_space, uint32_t in_chunks,
+                              uint32_t in_positions, uint32_t out_chunks, uint32_t out_positions, uint32_t depth,
+                              uint32_t n_peers, void* stream) {
   StepParams kp = base_params(e);
   kp.has_locals = e->locals_set ? 1 : 0;
   kp.has_lane_peer = 0;
@@ -1470,6 +1475,79 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
                       next_timing(e), kp.has_locals && e->locals_other));
   e->passes++;
   return GR_OK;
+}
+
+int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t in_chunks,
+                   uint32_t in_positions, uint32_t out_chunks, uint32_t out_positions, uint32_t depth,
+                   uint32_t n_peers, void* stream) {
+  if (!e || !in_space || !out_space || n_peers > e->cfg.max_peers || depth == 0 || depth > GR_C)
+    return GR_EINVAL;
+  // the mutex orders this pass after a compact _begin/_end on another thread
+  // (uncontended: one lock per pass)
+  std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);  // the pending compact pass owns the lane rows and bail lists
+  return step_device_locked(e, in_space, out_space, in_chunks, in_positions, out_chunks, out_positions, depth,
+                            n_peers, stream);
+}
+
+// A captured sequence of device-resident passes (gpuraft.h gr_graph_*).
+struct gr_graph {
+  gr_engine* e = nullptr;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  uint32_t n_passes = 0;
+};
+
+int gr_graph_capture(gr_engine* e, void* space_a, void* space_b, uint32_t n_chunks, uint32_t positions,
+                     uint32_t depth, uint32_t n_peers, uint32_t n_passes, gr_graph** out) {
+  if (!e || !space_a || !space_b || !out || n_peers > e->cfg.max_peers || depth == 0 || depth > GR_C ||
+      n_passes == 0 || (n_passes & 1))
+    return GR_EINVAL;
+  *out = nullptr;
+  std::lock_guard<std::mutex> guard(e->mu);
+  GR_REFUSE_PENDING(e);
+  if (e->timing) return GR_ESTATE;  // per-pass timing events are not captured
+  HIPCHK(hipDeviceSynchronize());   // nothing of the engine in flight while the parities are read
+  hipStream_t cs = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  gr_graph* g = new gr_graph();
+  g->e = e;
+  g->n_passes = n_passes;
+  int r = GR_OK;
+  if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) r = GR_EDEVICE;
+  // pass k reads space k % 2 and writes the other; the launch and hint parities
+  // advance by n_passes (even), so every replay starts where the capture did
+  for (uint32_t k = 0; k < n_passes && r == GR_OK; ++k)
+    r = step_device_locked(e, (k & 1) ? space_b : space_a, (k & 1) ? space_a : space_b, n_chunks, positions,
+                           n_chunks, positions, depth, n_peers, cs);
+  hipGraph_t graph = nullptr;
+  const hipError_t ce = hipStreamEndCapture(cs, &graph);  // ends the capture on every path
+  if (r == GR_OK && (ce != hipSuccess || !graph)) r = GR_EDEVICE;
+  if (r == GR_OK && hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0) != hipSuccess) r = GR_EDEVICE;
+  g->graph = graph;
+  (void)hipStreamDestroy(cs);
+  if (r != GR_OK) {
+    gr_graph_destroy(g);
+    return r;
+  }
+  *out = g;
+  return GR_OK;
+}
+
+int gr_graph_replay(gr_graph* g, void* stream) {
+  if (!g || !g->exec) return GR_EINVAL;
+  std::lock_guard<std::mutex> guard(g->e->mu);
+  GR_REFUSE_PENDING(g->e);
+  HIPCHK(hipGraphLaunch(g->exec, (hipStream_t)stream));
+  g->e->passes += g->n_passes;
+  return GR_OK;
+}
+
+void gr_graph_destroy(gr_graph* g) {
+  if (!g) return;
+  if (g->exec) (void)hipGraphExecDestroy(g->exec);
+  if (g->graph) (void)hipGraphDestroy(g->graph);
+  delete g;
 }
 
 int gr_collect_results(gr_engine* e, uint32_t first, gr_peer_result* out, size_t n) {

@@ -11,8 +11,9 @@
 //           -> exclusive scan of the flags: lane_of_peer, nl (lanes = peers
 //              with input, ascending, as node.go's step worker visits them)
 //           -> lane_peers (peer_of_lane into LR_LANE_PEER)
-//           -> msg_keys + stable radix sort by mailbox (slot-major position
-//              j*nl + lane): arrival order inside a mailbox survives
+//           -> msg_keys + stable counting sort by mailbox (slot-major position
+//              j*nl + lane; key_count, scan, key_scatter, key_order): arrival
+//              order inside a mailbox survives
 //           -> encode_sorted (SoA mailbox fields, the count byte; more than
 //              GR_C messages mark the mailbox overflowed, as the host packer did)
 //           -> local_winner + fill_locals (one gr_local_input per lane, the
@@ -26,6 +27,7 @@
 #pragma once
 #include "gpuraft_wire.h"
 #include "gr_host.h"
+#include "gr_scan.h"
 
 namespace gr {
 namespace io {
@@ -76,6 +78,64 @@ __global__ void msg_keys(const gr_message* msgs, uint32_t n, const uint32_t* lan
   for (uint32_t k = io_tid(); k < n; k += io_stride()) {
     keys[k] = (uint32_t)msgs[k].slot * nl + lane_of_peer[msgs[k].peer];
     idx[k] = k;
+  }
+}
+
+// ---- the stable sort of the inbox's mailbox keys (bounded: key < positions),
+// hand-written as a counting sort: count the records of every mailbox (each
+// record takes a slot of its mailbox), scan the counts, scatter, then restore
+// arrival order inside each mailbox (record index ascending; mailboxes hold a
+// few records, more than GR_C overflow and escalate anyway).
+__global__ void key_count(const uint32_t* keys, uint32_t n, uint32_t* cnt, uint32_t* slot) {
+  for (uint32_t k = io_tid(); k < n; k += io_stride()) slot[k] = atomicAdd(cnt + keys[k], 1u);
+}
+__global__ void key_scatter(const uint32_t* keys, const uint32_t* slot, uint32_t n, const uint32_t* base,
+                            uint32_t* skeys, uint32_t* sidx) {
+  for (uint32_t k = io_tid(); k < n; k += io_stride()) {
+    const uint32_t key = keys[k], at = base[key] + slot[k];
+    skeys[at] = key;
+    sidx[at] = k;  // msg_keys' idx[k] = k
+  }
+}
+// Arrival order inside mailbox `key`: its record indexes ascending (insertion
+// sort; a mailbox with more records than fit in registers uses a heap sort in
+// place, an input the engine escalates CAPACITY for anyway).
+__global__ void key_order(const uint32_t* cnt, const uint32_t* base, uint32_t nkeys, uint32_t* sidx) {
+  for (uint32_t key = io_tid(); key < nkeys; key += io_stride()) {
+    const uint32_t c = cnt[key];
+    if (c < 2) continue;
+    uint32_t* a = sidx + base[key];
+    if (c <= 16) {
+      for (uint32_t i = 1; i < c; ++i) {
+        const uint32_t x = a[i];
+        uint32_t j = i;
+        while (j > 0 && a[j - 1] > x) {
+          a[j] = a[j - 1];
+          --j;
+        }
+        a[j] = x;
+      }
+      continue;
+    }
+    // heap sort (max-heap, then repeated extraction)
+    auto sift = [&](uint32_t root, uint32_t end) {
+      while (2 * root + 1 < end) {
+        uint32_t ch = 2 * root + 1;
+        if (ch + 1 < end && a[ch] < a[ch + 1]) ++ch;
+        if (a[root] >= a[ch]) return;
+        const uint32_t t = a[root];
+        a[root] = a[ch];
+        a[ch] = t;
+        root = ch;
+      }
+    };
+    for (uint32_t r = c / 2; r-- > 0;) sift(r, c);
+    for (uint32_t end = c - 1; end > 0; --end) {
+      const uint32_t t = a[0];
+      a[0] = a[end];
+      a[end] = t;
+      sift(0, end);
+    }
   }
 }
 
@@ -424,32 +484,29 @@ __global__ void keep_routed(const gr_message* rec, const uint32_t* flag, const u
 // into a fixed-capacity side buffer per chunk, so the all-to-all sizes are known
 // without the host reading anything back. Per chunk: a 64-byte header (entry
 // count) and `cap` entries of [u32 position in chunk][u32 count byte] + per
-// message the 50 cold bytes in the cold chunk's field order. A mailbox that does
+// message the 56 used bytes of its cold record (gr_layout.h Mailbox). A mailbox that does
 // not fit gets MB_COLD_LOST in its (hot) count byte and its reader escalates
 // CAPACITY.
 constexpr uint32_t kSideHdr = 64;
-constexpr uint32_t kColdOff[10] = {0, 2, 6, 10, 14, 18, 22, 26, 34, 42};  // field offsets (x pc) in ck(k)
-constexpr uint32_t kColdSz[10] = {2, 4, 4, 4, 4, 4, 4, 8, 8, 8};
-__host__ __device__ inline uint32_t side_entry_bytes(uint32_t depth) { return (8 + depth * kColdK + 7) & ~7u; }
+__host__ __device__ inline uint32_t side_entry_bytes(uint32_t depth) { return 8 + depth * kColdUsed; }
 __host__ __device__ inline uint64_t side_chunk_bytes(uint32_t depth, uint32_t cap) {
   return round256(kSideHdr + (uint64_t)cap * side_entry_bytes(depth));
 }
-// Copy the cold fields of the first n messages of mailbox mb into / out of entry e.
+// Copy the cold records (their kColdUsed bytes, 8-byte words) of the first n
+// messages of mailbox mb into / out of entry e.
 __host__ __device__ inline void cold_gather(const Mailbox& mb, uint32_t n, uint8_t* e) {
-  for (uint32_t k = 0; k < n; ++k)
-    for (uint32_t f = 0; f < 10; ++f) {
-      const uint8_t* src = mb.ck(k) + (uint64_t)kColdOff[f] * mb.pc + (uint64_t)mb.local * kColdSz[f];
-      uint8_t* dst = e + 8 + k * kColdK + kColdOff[f];
-      for (uint32_t b = 0; b < kColdSz[f]; ++b) dst[b] = src[b];
-    }
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(mb.rec(k));
+    uint64_t* dst = reinterpret_cast<uint64_t*>(e + 8 + k * kColdUsed);
+    for (uint32_t w = 0; w < kColdUsed / 8; ++w) dst[w] = src[w];
+  }
 }
 __host__ __device__ inline void cold_scatter(const Mailbox& mb, uint32_t n, const uint8_t* e) {
-  for (uint32_t k = 0; k < n; ++k)
-    for (uint32_t f = 0; f < 10; ++f) {
-      uint8_t* dst = mb.ck(k) + (uint64_t)kColdOff[f] * mb.pc + (uint64_t)mb.local * kColdSz[f];
-      const uint8_t* src = e + 8 + k * kColdK + kColdOff[f];
-      for (uint32_t b = 0; b < kColdSz[f]; ++b) dst[b] = src[b];
-    }
+  for (uint32_t k = 0; k < n; ++k) {
+    uint64_t* dst = reinterpret_cast<uint64_t*>(mb.rec(k));
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(e + 8 + k * kColdUsed);
+    for (uint32_t w = 0; w < kColdUsed / 8; ++w) dst[w] = src[w];
+  }
 }
 // One position of the pack: entry index idx (or >= cap: lost).
 __host__ __device__ inline void side_put(const SpaceView& v, uint32_t g, uint8_t* side, uint32_t cap, uint32_t idx) {

@@ -496,21 +496,14 @@ inline uint32_t general_blocks() {
   return v;
 }
 
-// Small passes (at most small_blocks() workgroups, 64k lanes by default) are
+// Small passes (at most StepParams::small_blocks workgroups, 64k lanes by default) are
 // launch-bound: a 10k x 3 pass spent ~7 us in an empty general-kernel launch
 // and the gaps between kernels. gr_small_kernel does the whole pass in one
 // launch: the lean lane, and in the same wave, for the lanes it hands over, the
 // tick lane and then the general lane. Its register allocation is the general
 // lane's (2 waves per SIMD), which such a grid never needs more than. It also
 // zeroes the next pass's list counters, as the general kernel does.
-constexpr uint32_t kSmallBlocks = 256;
-inline uint32_t small_blocks() {  // GR_SMALL_BLOCKS overrides it (0: never; A/B runs and tests)
-  static const uint32_t v = [] {
-    const char* e = getenv("GR_SMALL_BLOCKS");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : kSmallBlocks;
-  }();
-  return v;
-}
+constexpr uint32_t kSmallBlocks = 256;  // StepParams::small_blocks default (gr_engine.hip)
 
 template <int S>
 __global__ __launch_bounds__(kBlock, 1) void gr_small_kernel(StepParams kp, uint32_t* next_counters) {
@@ -607,8 +600,10 @@ hipError_t launch_fast(const StepParams& kp0, uint32_t blocks, uint32_t* bail_li
                          bail_list, cur, list_cap);
     }
   } else {
-    hipLaunchKernelGGL((gr_fast_kernel<S, FL_ANY, RM, false>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur,
-                       list_cap);
+    // a mid-size pass (more workgroups than a fused small pass, fewer lanes than
+    // a split one): the route-generic instance (one fewer instance per route mode)
+    hipLaunchKernelGGL((gr_fast_kernel<S, FL_ANY, RM_ANY, false>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list,
+                       cur, list_cap);
   }
   return hipGetLastError();
 }
@@ -622,7 +617,7 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   uint32_t* nxt = counters + ((parity + 1) & 1) * kCounters * kCounterStride;
   hipError_t err;
   if (t && (err = hipEventRecord(t->ev[0], s)) != hipSuccess) return err;
-  if (blocks <= small_blocks()) {  // the whole pass in one launch
+  if (blocks <= kp.small_blocks) {  // the whole pass in one launch
     hipLaunchKernelGGL(gr_small_kernel<S>, dim3(blocks), dim3(kBlock), 0, s, kp, nxt);
     if ((err = hipGetLastError()) != hipSuccess) return err;
     if (t && ((err = hipEventRecord(t->ev[1], s)) != hipSuccess || (err = hipEventRecord(t->ev[2], s)) != hipSuccess))

@@ -346,7 +346,12 @@ __host__ __device__ inline uint32_t space_pad_positions(uint32_t positions) {
 }
 constexpr uint32_t kHotH = 5;    // bytes per position, hot chunk header: count + term word
 constexpr uint32_t kHotK = 12;   // bytes per position per message, hot chunk: Commit offset + LogIndex
-constexpr uint32_t kColdK = 50;  // ... cold chunk: tag, term and the rest
+// ... cold chunk: one 64-byte record per position and message (the fields of
+// gr_layout.h Mailbox, 56 bytes used). The cold fields belong to the irregular
+// traffic (heartbeats and their acks, rejects, full Replicates), whose lanes are
+// scattered over the chunk: a record keeps a message's cold fields in one line
+// instead of one line per field (10 with the field-major layout it replaced).
+constexpr uint32_t kColdK = 64, kColdUsed = 56;
 __host__ __device__ inline uint64_t round256(uint64_t b) { return (b + 255u) & ~(uint64_t)255u; }
 // A space's mailbox depth (1..GR_C) fixes its chunk sizes: spaces that cross
 // xGMI use the depth the steady state needs (2).
@@ -399,32 +404,30 @@ struct Mailbox {
   uint32_t local;
   uint32_t pc;
   // hot:  [count u8][term word u32], then per message [Commit offset u32][LogIndex u64]
-  // cold: per message [tag u16][term u32][n u32][run2 u32][log term u32][rt0 u32][rt1 u32]
-  //       [Commit u64][Hint u64][HintHigh u64]     (each field x pc positions)
+  //       (each field x pc positions)
+  // cold: per message, a 64-byte record per position (message-major):
+  //       [tag u16][pad u16][term u32][n u32][run2 u32][log term u32][rt0 u32][rt1 u32][pad u32]
+  //       [Commit u64][Hint u64][HintHigh u64][pad u64]
   __host__ __device__ inline uint8_t* hk(uint32_t k) const { return hot + (kHotH + (uint64_t)k * kHotK) * pc; }
-  __host__ __device__ inline uint8_t* ck(uint32_t k) const { return cold + (uint64_t)k * kColdK * pc; }
+  __host__ __device__ inline uint8_t* rec(uint32_t k) const { return cold + ((uint64_t)k * pc + local) * kColdK; }
   __host__ __device__ inline uint8_t& cnt() const { return hot[local]; }
   __host__ __device__ inline uint32_t& mterm() const { return reinterpret_cast<uint32_t*>(hot + pc)[local]; }
-  __host__ __device__ inline uint8_t& type(uint32_t k) const { return ck(k)[2 * local]; }
-  __host__ __device__ inline uint8_t& flags(uint32_t k) const { return ck(k)[2 * local + 1]; }
+  __host__ __device__ inline uint8_t& type(uint32_t k) const { return rec(k)[0]; }
+  __host__ __device__ inline uint8_t& flags(uint32_t k) const { return rec(k)[1]; }
   // type | flags << 8 in one access (little-endian)
-  __host__ __device__ inline uint16_t& tag(uint32_t k) const { return reinterpret_cast<uint16_t*>(ck(k))[local]; }
-  __host__ __device__ inline uint32_t& n(uint32_t k) const {
-    return reinterpret_cast<uint32_t*>(ck(k) + 6ull * pc)[local];
-  }
-  __host__ __device__ inline uint32_t& run2(uint32_t k) const {
-    return reinterpret_cast<uint32_t*>(ck(k) + 10ull * pc)[local];
-  }
+  __host__ __device__ inline uint16_t& tag(uint32_t k) const { return *reinterpret_cast<uint16_t*>(rec(k)); }
+  __host__ __device__ inline uint32_t& n(uint32_t k) const { return reinterpret_cast<uint32_t*>(rec(k))[2]; }
+  __host__ __device__ inline uint32_t& run2(uint32_t k) const { return reinterpret_cast<uint32_t*>(rec(k))[3]; }
   __host__ __device__ inline uint32_t& t32(uint32_t k, uint32_t f) const {
     if (f == MT_CDELTA) return reinterpret_cast<uint32_t*>(hk(k))[local];
-    if (f == MT_TERM) return reinterpret_cast<uint32_t*>(ck(k) + 2ull * pc)[local];
-    // MT_LOG_TERM, MT_RT0, MT_RT1: cold words at 14, 18, 22
-    return reinterpret_cast<uint32_t*>(ck(k) + (14ull + 4ull * (f - MT_LOG_TERM)) * pc)[local];
+    if (f == MT_TERM) return reinterpret_cast<uint32_t*>(rec(k))[1];
+    // MT_LOG_TERM, MT_RT0, MT_RT1: record words 4, 5, 6
+    return reinterpret_cast<uint32_t*>(rec(k))[4 + (f - MT_LOG_TERM)];
   }
   __host__ __device__ inline uint64_t& u64(uint32_t k, uint32_t f) const {
     if (f == MF_LOG_INDEX) return reinterpret_cast<uint64_t*>(hk(k) + 4ull * pc)[local];
-    // MF_COMMIT, MF_HINT, MF_HINT_HIGH
-    return reinterpret_cast<uint64_t*>(ck(k) + (26ull + 8ull * (f - MF_COMMIT)) * pc)[local];
+    // MF_COMMIT, MF_HINT, MF_HINT_HIGH: record u64 words 4, 5, 6
+    return reinterpret_cast<uint64_t*>(rec(k))[4 + (f - MF_COMMIT)];
   }
   // Tag and term of message k given the mailbox's count byte `cb` (MB_UNIFORM:
   // rebuilt from the count byte and the term word, else the stored fields).
@@ -544,6 +547,9 @@ struct StepParams {
   uint8_t route_mode;
   uint8_t split;       // follower-hinted waves go to the FL_FOLLOWER instance (gr_kernels.h)
   uint8_t route_wu;    // route_g % 64 == 0: replica_of is wave-uniform
+  // host-side launch choice (gr_kernels.h launch): passes of at most this many
+  // workgroups run as one fused kernel (gr_small_kernel)
+  uint32_t small_blocks;
 };
 
 // Route mode as a compile-time parameter of the lean kernel instances

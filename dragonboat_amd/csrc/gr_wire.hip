@@ -37,10 +37,9 @@
 #include <mutex>
 #include <new>
 
-#include <rocprim/rocprim.hpp>
-
 #include "gpuraft.h"
 #include "gpuraft_wire.h"
+#include "gr_scan.h"  // hand-written exclusive scan (shared with the engine)
 
 namespace grw {
 
@@ -1238,11 +1237,10 @@ static int grow(grw_ctx::Buf& b, size_t bytes) {
 
 template <class T>
 static int scan_excl(grw_ctx* c, const T* in, T* out, size_t n) {
-  size_t tb = 0;
-  HIPCHK(rocprim::exclusive_scan(nullptr, tb, in, out, (T)0, n, rocprim::plus<T>(), c->stream));
-  if (int r = grow(c->tmp, tb)) return r;
-  tb = c->tmp.n;
-  HIPCHK(rocprim::exclusive_scan(c->tmp.p, tb, in, out, (T)0, n, rocprim::plus<T>(), c->stream));
+  if (n == 0) return GR_OK;
+  if (n >= 0xFFFFFFFFull) return GR_EINVAL;
+  if (int r = grow(c->tmp, (size_t)gr::scan::scan_tiles_of(n) * sizeof(T))) return r;
+  HIPCHK(gr::scan::exclusive_scan<T>(in, out, (uint32_t)n, (T*)c->tmp.p, c->stream));
   return GR_OK;
 }
 

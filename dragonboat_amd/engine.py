@@ -92,6 +92,11 @@ def load_library(path=LIB_PATH):
     lib.gr_step_device.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32,
                                    c.c_uint32, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p]
     lib.gr_collect_results.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p, c.c_size_t]
+    lib.gr_graph_capture.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32,
+                                     c.c_uint32, c.c_uint32, c.POINTER(c.c_void_p)]
+    lib.gr_graph_replay.argtypes = [c.c_void_p, c.c_void_p]
+    lib.gr_graph_destroy.argtypes = [c.c_void_p]
+    lib.gr_graph_destroy.restype = None
     lib.gr_space_decode.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_size_t,
                                     c.POINTER(c.c_size_t)]
     lib.gr_space_encode.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_size_t,
@@ -389,6 +394,20 @@ class Engine:
                     n_peers, stream=0, depth=MAILBOX_DEPTH):
         _check(self.lib.gr_step_device(self._h, in_ptr, out_ptr, in_chunks, in_positions, out_chunks,
                                        out_positions, depth, n_peers, stream), "gr_step_device")
+
+    def graph_capture(self, space_a, space_b, n_chunks, positions, n_peers, n_passes=2, depth=MAILBOX_DEPTH):
+        """gr_graph_capture: n_passes (even) device passes over the ping-pong spaces
+        (device pointers) recorded into a HIP graph; returns the graph handle."""
+        g = ctypes.c_void_p()
+        _check(self.lib.gr_graph_capture(self._h, space_a, space_b, n_chunks, positions, depth, n_peers, n_passes,
+                                         ctypes.byref(g)), "gr_graph_capture")
+        return g
+
+    def graph_replay(self, g, stream=0):
+        _check(self.lib.gr_graph_replay(g, stream), "gr_graph_replay")
+
+    def graph_destroy(self, g):
+        self.lib.gr_graph_destroy(g)
 
     def collect_results(self, n=None, first=0):
         n = self.max_peers - first if n is None else n

@@ -493,6 +493,22 @@ int gr_set_locals(gr_engine* e, const gr_local_input* locals, size_t n);
 int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t in_chunks,
                    uint32_t in_positions, uint32_t out_chunks, uint32_t out_positions,
                    uint32_t depth, uint32_t n_peers, void* stream);
+/* Graph mode (launch-bound small passes, e.g. BASELINE config 2):
+ * gr_graph_capture records n_passes (even) device-resident passes over two
+ * ping-pong spaces (pass k reads space_a when k is even, space_b when odd, and
+ * writes the other) into a HIP graph with the engine's current routes and bound
+ * local inputs; gr_graph_replay launches the whole sequence on `stream` with one
+ * call, so a step worker that advances the same bound groups every tick
+ * (execengine.go:453-465's per-group stepNode loop) pays one launch per
+ * n_passes passes. Replays continue from the state the previous pass left (n_passes is
+ * even, so every replay starts in space_a); gr_step_device calls may be mixed
+ * in. Capture refuses while per-pass timing is on (GR_ESTATE); the spaces,
+ * routes and locals must stay as captured until gr_graph_destroy. */
+typedef struct gr_graph gr_graph;
+int gr_graph_capture(gr_engine* e, void* space_a, void* space_b, uint32_t n_chunks, uint32_t positions,
+                     uint32_t depth, uint32_t n_peers, uint32_t n_passes, gr_graph** out);
+int gr_graph_replay(gr_graph* g, void* stream);
+void gr_graph_destroy(gr_graph* g);
 /* Copy per-peer results of the last device pass for peers [first, first+n). */
 int gr_collect_results(gr_engine* e, uint32_t first, gr_peer_result* out, size_t n);
 /* The wire path (SURVEY.md §8f-2 feeding the inbox): decoded raftpb.Message

@@ -199,8 +199,9 @@ def device_battery(lib_path):
     import os
     import devsim
     out = {}
-    old = os.environ.get("GR_SPLIT_MIN_LANES")
-    os.environ["GR_SPLIT_MIN_LANES"] = "1"  # read at gr_create
+    saved = {k: os.environ.get(k) for k in ("GR_SPLIT_MIN_LANES", "GR_SMALL_BLOCKS")}
+    os.environ["GR_SPLIT_MIN_LANES"] = "1"  # both read at gr_create
+    os.environ["GR_SMALL_BLOCKS"] = "0"     # not the fused small-pass kernel
     try:
         G, R = 1024, 3
         topo = P.Topology(G, R)
@@ -222,10 +223,11 @@ def device_battery(lib_path):
         finally:
             ls.close()
     finally:
-        if old is None:
-            os.environ.pop("GR_SPLIT_MIN_LANES", None)
-        else:
-            os.environ["GR_SPLIT_MIN_LANES"] = old
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     return out
 
 

@@ -86,6 +86,7 @@ def test_device_steady_leader_staggered_acks(gpu, monkeypatch):
     hands the lane to FastLane; state and mailboxes equal the
     oracle."""
     monkeypatch.setenv("GR_SPLIT_MIN_LANES", "1")
+    monkeypatch.setenv("GR_SMALL_BLOCKS", "0")  # the split schedule, not the fused small-pass kernel
     G, R = 2048, 3
     ls = devsim.DeviceLockstep(P.make_groups(G, R, seed=21), G, R)
     try:
@@ -113,5 +114,55 @@ def test_device_steady_leader_staggered_acks(gpu, monkeypatch):
         ls.override_inbox(msgs[np.lexsort((np.arange(3 * G), msgs["slot"], msgs["peer"]))])
         ls.step(P.propose_locals(R * G, [], pass_index=9))
         assert np.all(ls.export()["committed"][:G] == c + np.uint64(3))
+    finally:
+        ls.close()
+
+
+@pytest.mark.parametrize("G,split", [(10_000, False), (4096, True)])
+def test_graph_replay_matches_oracle(gpu, monkeypatch, G, split):
+    """Graph mode (gr_graph_capture / gr_graph_replay): two passes captured once,
+    replayed three times through the C-ABI, then one more pass by
+    gr_step_device: after every replay the state and the space the next pass
+    reads equal the oracle's after the same number of passes. G = 10k is
+    BASELINE config 2 (the fused small-pass kernel); the split schedule is forced
+    on 4096 groups (steady kernel, role instances, general kernel in the graph)."""
+    import torch
+    from dragonboat_amd.engine import decode_space
+    from oracle.pyoracle import OraclePopulation
+    import parity
+    if split:
+        monkeypatch.setenv("GR_SPLIT_MIN_LANES", "1")
+        monkeypatch.setenv("GR_SMALL_BLOCKS", "0")
+    R = 3
+    ls = devsim.DeviceLockstep(P.make_groups(G, R, seed=8), G, R)
+    try:
+        loc = P.propose_locals(R * G, np.arange(G), pass_index=0)
+        ls.eng.set_locals(loc)
+        a, b = ls.spaces
+        g = ls.eng.graph_capture(a.data_ptr(), b.data_ptr(), 1, ls.positions, ls.n, n_passes=2, depth=ls.depth)
+        pop = ls.pop
+        msgs = np.zeros(0, abi.MESSAGE)
+        try:
+            for rep in range(3):
+                ls.eng.graph_replay(g, torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                for _ in range(2):
+                    o = pop.step(msgs, loc)
+                    msgs = ls._route(o["msgs"])
+                bad = parity.compare_states(ls.eng.sync(ls.n), pop.export(), R)
+                assert not bad, (rep, bad[:3])
+                got = decode_space(a.cpu().numpy(), 1, ls.positions, ls.depth)
+                pos = got["peer"].astype(np.int64)
+                got["peer"] = ls.inv[0][pos].astype(np.uint32)
+                got["slot"] = ls.inv[1][pos].astype(np.uint8)
+                bad = parity.compare_msgs(got, msgs)
+                assert not bad, (rep, bad[:3])
+        finally:
+            ls.eng.graph_destroy(g)
+        # a plain pass after the replays continues from their state (space a)
+        ls.msgs = msgs
+        ls.k = 0
+        ls.step(loc)
+        assert ls.stats["escalations"] == 0
     finally:
         ls.close()

@@ -78,6 +78,7 @@ def test_split_pass_churn(gpu, mix, monkeypatch):
     instances, table routes)."""
     import devsim
     monkeypatch.setenv("GR_SPLIT_MIN_LANES", "1")
+    monkeypatch.setenv("GR_SMALL_BLOCKS", "0")  # not the fused small-pass kernel
     st = {}
     devsim.run_device(2000, 3, 10, inject_p=0.1, mix=mix, stats=st, seed=11)
     assert st["injected"] > 0

@@ -30,10 +30,10 @@ sys.path.insert(0, ROOT)
 
 def run(name, peers, G, R, passes, warmup, prepare, graph_reps=0):
     """prepare(k, eng, n_peers) -> local inputs of pass k (may also reload groups).
-    graph_reps > 0: afterwards, two passes captured in a HIP graph (torch.cuda.CUDAGraph
-    over the engine's launches on the capture stream) and replayed graph_reps times:
-    the per-pass time with no CPU launch in it. The local inputs
-    then stay those of the last pass (config 2's proposals are the same every pass)."""
+    graph_reps > 0: afterwards, two passes captured with the library's graph mode
+    (gr_graph_capture) and replayed graph_reps times (gr_graph_replay): the per-pass
+    time with no CPU launch in it. The local inputs then stay
+    those of the last pass (config 2's proposals are the same every pass)."""
     import torch
     from dragonboat_amd.engine import Engine
     from dragonboat_amd.exchange import Exchange
@@ -70,30 +70,28 @@ def run(name, peers, G, R, passes, warmup, prepare, graph_reps=0):
     st = eng.stats()
     graph = None
     if graph_reps:
-        k0 = warmup + passes
-        k0 += k0 & 1  # local spaces ping-pong: the captured pair starts on an even pass
-        if (warmup + passes) & 1:
+        # the library's graph mode (gr_graph_capture / gr_graph_replay): two passes
+        # captured once over the ping-pong spaces, replayed graph_reps times
+        if (warmup + passes) & 1:  # the captured pair starts in space 0
             ex.step(eng, spaces, warmup + passes, stream)
         torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        cs = torch.cuda.Stream()
-        cs.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.graph(g, stream=cs):
-            for k in range(2):
-                ex.step(eng, spaces, k0 + k, torch.cuda.current_stream())
+        g = eng.graph_capture(spaces[0].data_ptr(), spaces[1].data_ptr(), ex.n_chunks, ex.positions, ex.n_peers,
+                              n_passes=2, depth=ex.depth)
+        eng.graph_replay(g, stream.cuda_stream)  # warm
         torch.cuda.synchronize()
         c0 = eng.stats()["leader_commits"]
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(graph_reps):
-            g.replay()
+            eng.graph_replay(g, stream.cuda_stream)
         e1.record()
         torch.cuda.synchronize()
+        eng.graph_destroy(g)
         gms = e0.elapsed_time(e1) / (2 * graph_reps)
         commits = eng.stats()["leader_commits"] - c0
-        graph = {"passes": 2 * graph_reps, "ms_per_pass": gms, "leader_commits_per_pass": commits / (2 * graph_reps),
+        graph = {"api": "gr_graph_capture/gr_graph_replay", "passes": 2 * graph_reps, "ms_per_pass": gms,
+                 "leader_commits_per_pass": commits / (2 * graph_reps),
                  "leader_commits_per_s": commits / (2 * graph_reps * gms * 1e-3)}
-        del g
     from dragonboat_amd import abi
     import numpy as np
     res = eng.collect_results(ex.n_peers)  # the last pass's per-lane results
