@@ -61,8 +61,8 @@ __device__ inline __attribute__((always_inline)) void block_stats(const StepPara
 // appends over 16 counters 256 B apart keeps them from serialising when every
 // wave bails a few lanes (one shared counter: 105 us instead of 37 us on
 // config 3); no barrier, so waves of steady-state populations retire freely.
-// Lists 0..7 followers, 8..15 leaders (the general kernel's), 16..23 lanes with
-// ticks or a ReadIndex (LW_OTHER), which the tick kernel takes first.
+// Lists 0..7 followers, 8..15 leaders (the general kernel's); 16..23 unused
+// (the tick lists are below).
 // Lists 24..31: lanes a split pass's steady kernel did not finish, which the
 // role instances step with FastLane before anything goes to the general kernel.
 // After the lane lists' storage: one flag byte and one lane mask per wave, the
@@ -73,7 +73,16 @@ __device__ inline __attribute__((always_inline)) void block_stats(const StepPara
 // rewritten every split pass, so no counter or atomic is involved: the role
 // instances scan the flags, 64 waves per load, instead of launching one
 // workgroup per 256 lanes, most of which would find nothing to do.
-constexpr uint32_t kBailLists = 32, kGeneralLists = 16, kTickList0 = 16, kRetryList0 = 24, kCounters = kBailLists,
+// The tick lists (lanes with ticks or a ReadIndex for the tick kernel) are
+// kTickLists shorter lists after the wave masks: a lane of 256-lane block b (or
+// retry entry x of block x / 256) goes to list b % kTickLists, so a list never
+// holds more than tick_cap lanes. Config 3 appends from every one of its ~7.8k
+// waves (10% of its groups are active, scattered); one returning atomic word
+// saturates near 90 appends per us (MI355X_MICROARCH.md, "dequeue"), so 8 list
+// counters made those appends most of the steady kernel's time.
+constexpr uint32_t kTickLists = 64;
+constexpr uint32_t kBailLists = 32, kGeneralLists = 16, kRetryList0 = 24,
+                   kTickCounter0 = kBailLists, kCounters = kBailLists + kTickLists,
                    kCounterStride = 64;  // counters 256 B apart
 constexpr uint32_t WF_LISTED = 0x80;     // wave flag: the role instances step this wave's masked lanes
 // Word 1 of counter 0's 256-B slot: nonzero when a split pass's steady kernel
@@ -82,10 +91,18 @@ constexpr uint32_t WF_LISTED = 0x80;     // wave flag: the role instances step t
 // the next pass with the counters.
 constexpr uint32_t kListedWord = 1;
 __host__ __device__ inline uint64_t wave_flag_words(uint32_t cap) { return ((uint64_t)cap / 64 + 64) / 4 * 2; }
-// u32 words of the list storage: kBailLists lane lists of cap, the wave flags, the wave masks (u64)
-__host__ __device__ inline uint64_t bail_words(uint32_t cap) {
+// Lanes one tick list can receive: the lanes of every kTickLists-th block, from
+// the steady kernel and the listed role waves (keyed by lane), plus as many
+// retry entries (keyed by entry index): twice one key's bound.
+__host__ __device__ inline uint64_t tick_cap(uint32_t cap) {
+  return 2 * (((uint64_t)(cap + 255) / 256 + kTickLists - 1) / kTickLists * 256);
+}
+__host__ __device__ inline uint64_t tick_off(uint32_t cap) {
   return (uint64_t)kBailLists * cap + wave_flag_words(cap) + 2 * ((uint64_t)cap / 64 + 1);
 }
+// u32 words of the list storage: kBailLists lane lists of cap, the wave flags,
+// the wave masks (u64), the kTickLists tick lists of tick_cap
+__host__ __device__ inline uint64_t bail_words(uint32_t cap) { return tick_off(cap) + kTickLists * tick_cap(cap); }
 __host__ __device__ inline uint8_t* wave_flags(uint32_t* bail_list, uint32_t cap) {
   return (uint8_t*)(bail_list + (uint64_t)kBailLists * cap);
 }
@@ -105,6 +122,23 @@ __device__ inline __attribute__((always_inline)) void bail_append(bool mine, uin
   if (lane == first) base = atomicAdd(counters + list * kCounterStride, (uint32_t)__popcll(bm));
   base = __shfl(base, (int)first);
   if (mine) bail_list[(uint64_t)list * list_cap + base + (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
+}
+
+// One wave's appends to the tick list of lanes with key `key` (a lane or retry
+// entry index; key >> 8, its 256-lane block, is the same for the wave's lanes).
+__device__ inline __attribute__((always_inline)) void tick_append(bool mine, uint32_t key, uint32_t* bail_list,
+                                                                  uint32_t* counters, uint32_t list_cap, uint32_t i) {
+  const uint64_t bm = __ballot(mine);
+  if (!bm) return;
+  const uint32_t l = ((uint32_t)__builtin_amdgcn_readfirstlane(key) >> 8) % kTickLists;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t first = (uint32_t)__ffsll((unsigned long long)bm) - 1;
+  uint32_t base = 0;
+  if (lane == first) base = atomicAdd(counters + (kTickCounter0 + l) * kCounterStride, (uint32_t)__popcll(bm));
+  base = __shfl(base, (int)first);
+  if (mine)
+    bail_list[tick_off(list_cap) + (uint64_t)l * tick_cap(list_cap) + base +
+              (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
 }
 
 #ifndef GR_FAST_MIN_WAVES
@@ -136,7 +170,7 @@ __device__ inline __attribute__((always_inline)) uint32_t sload_u32(const uint8_
 // stepped here, else 0; written by each instance that stepped a lane of the
 // wave, both write 0 when an unhinted wave's lanes split between them), the
 // bail lists (followers into lists 0..7, leaders into 8..15, lanes with ticks
-// or a ReadIndex into 16..23, the tick kernel's: the later kernels walk their
+// or a ReadIndex into the tick lists (tick_append): the later kernels walk their
 // lists in order, so their waves hold one kind of lane and diverge less), and
 // the stats.
 __device__ inline __attribute__((always_inline)) void wave_finish(const StepParams& kp, uint32_t i, uint32_t wave, bool mine, bool active,
@@ -157,10 +191,11 @@ __device__ inline __attribute__((always_inline)) void wave_finish(const StepPara
   const bool lead = role == GR_LEADER;
   const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
 #pragma unroll
-  for (uint32_t side = 0; side < 3; ++side) {
-    const bool m = bail && (side == 2 ? tickish : !tickish && lead == (side == 1));
+  for (uint32_t side = 0; side < 2; ++side) {
+    const bool m = bail && !tickish && lead == (side == 1);
     bail_append(m, (bid % 8) + side * 8, bail_list, counters, list_cap, i);
   }
+  tick_append(tickish, wave * 64, bail_list, counters, list_cap, i);  // the wave's lanes share a block
   if (kp.stats) block_stats(kp, ls, bid);
 }
 
@@ -275,10 +310,11 @@ __device__ inline __attribute__((always_inline)) void roles_listed(const StepPar
     const bool lead = role == GR_LEADER;
     const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[li] & LW_OTHER);
 #pragma unroll
-    for (uint32_t side = 0; side < 3; ++side) {
-      const bool m = bail && (side == 2 ? tickish : !tickish && lead == (side == 1));
+    for (uint32_t side = 0; side < 2; ++side) {
+      const bool m = bail && !tickish && lead == (side == 1);
       bail_append(m, (bid % 8) + side * 8, bail_list, counters, list_cap, li);
     }
+    tick_append(tickish, base, bail_list, counters, list_cap, li);  // keyed by the entry's block
   }
   if (kp.stats && n > bid * kBlock) block_stats(kp, acc, bid);
 }
@@ -349,7 +385,7 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
     // the rest are listed for the role instances (wave flag + lane mask)
     const bool active = i < kp.n_lanes;
     const int q = active ? quiet_step<S, RM>(kp, i, i) : QS_DONE;
-    bail_append(q == QS_TICK, kTickList0 + blockIdx.x % 8, bail_list, counters, list_cap, i);
+    tick_append(q == QS_TICK, i, bail_list, counters, list_cap, i);
     const uint64_t rem = __ballot(q == QS_OTHER);
     if ((threadIdx.x & 63) == 0) {
       wave_flags(bail_list, list_cap)[wave] = (uint8_t)(rem ? (WF_LISTED | hint) : 0u);
@@ -384,7 +420,7 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
 }
 
 // Pass 2a: the heartbeat/ReadIndex/tick lane (gr_tick.h) over the lanes pass 1
-// handed over with ticks or a ReadIndex (lists 16..23), in a kernel of its own so
+// handed over with ticks or a ReadIndex (the tick lists), in a kernel of its own so
 // its register budget (and occupancy) is its own; what it cannot finish goes to
 // the general lists. Launched only when some lane may carry LW_OTHER.
 #ifndef GR_TICK_MIN_WAVES
@@ -393,25 +429,34 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
 template <int S>
 __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(StepParams kp, uint32_t* bail_list,
                                                                              uint32_t* counters, uint32_t list_cap) {
-  uint32_t start[9];
-  start[0] = 0;
+  // the lists' exclusive prefix (one wave scans the kTickLists counters)
+  __shared__ uint32_t tstart[kTickLists + 1];
+  if (threadIdx.x < kTickLists) {
+    const uint32_t c = counters[(kTickCounter0 + threadIdx.x) * kCounterStride];
+    uint32_t incl = c;
 #pragma unroll
-  for (uint32_t l = 0; l < 8; ++l) start[l + 1] = start[l] + counters[(kTickList0 + l) * kCounterStride];
-  const uint32_t n = start[8];
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d);
+      if (threadIdx.x >= d) incl += y;
+    }
+    tstart[threadIdx.x + 1] = incl;
+    if (threadIdx.x == 0) tstart[0] = 0;
+  }
+  __syncthreads();
+  const uint32_t n = tstart[kTickLists];
   if (blockIdx.x * kBlock >= n) return;
+  const uint32_t* tl = bail_list + tick_off(list_cap);
+  const uint64_t tc = tick_cap(list_cap);
   LaneStats acc;
   for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
     const uint32_t x = base + threadIdx.x;
     bool hand = false;
     uint32_t i = 0;
     if (x < n) {
-      uint32_t l = 0;
+      uint32_t l = 0;  // the last list whose start is at or below x (binary search)
 #pragma unroll
-      for (uint32_t k = 1; k < 8; ++k) l = x >= start[k] ? k : l;
-      uint32_t off = 0;
-#pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) off = (k == l) ? x - start[k] : off;
-      i = bail_list[(uint64_t)(kTickList0 + l) * list_cap + off];
+      for (uint32_t step = kTickLists / 2; step > 0; step >>= 1) l = tstart[l + step] <= x ? l + step : l;
+      i = tl[(uint64_t)l * tc + (x - tstart[l])];
       const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
       LaneStats ls;
       if (tick_step<S>(kp, i, p, &ls)) {

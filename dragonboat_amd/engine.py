@@ -92,11 +92,12 @@ def load_library(path=LIB_PATH):
     lib.gr_step_device.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32,
                                    c.c_uint32, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p]
     lib.gr_collect_results.argtypes = [c.c_void_p, c.c_uint32, c.c_void_p, c.c_size_t]
-    lib.gr_graph_capture.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32,
-                                     c.c_uint32, c.c_uint32, c.POINTER(c.c_void_p)]
-    lib.gr_graph_replay.argtypes = [c.c_void_p, c.c_void_p]
-    lib.gr_graph_destroy.argtypes = [c.c_void_p]
-    lib.gr_graph_destroy.restype = None
+    if hasattr(lib, "gr_graph_capture"):  # (older builds loaded for A/B runs lack graph mode)
+        lib.gr_graph_capture.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32,
+                                         c.c_uint32, c.c_uint32, c.POINTER(c.c_void_p)]
+        lib.gr_graph_replay.argtypes = [c.c_void_p, c.c_void_p]
+        lib.gr_graph_destroy.argtypes = [c.c_void_p]
+        lib.gr_graph_destroy.restype = None
     lib.gr_space_decode.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_size_t,
                                     c.POINTER(c.c_size_t)]
     lib.gr_space_encode.argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_size_t,
