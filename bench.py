@@ -19,8 +19,8 @@ per pass (dragonboat_amd/exchange.py).
 Roofline accounting: `achieved` = the algorithmic bytes one
 launch must move at this engine's encoding, over the lean kernels' HIP-event
 duration. The unit is one group-round; its bytes are counted field by field
-from the steady lanes' loads and stores (gr_steady.h; 332 B at R = 3: leader
-78 B loaded + 68 B stored, each follower 54 + 39 B), and a launch processes one
+from the steady lanes' loads and stores (gr_steady.h; 300 B at R = 3: leader
+62 B loaded + 52 B stored, each follower 54 + 39 B), and a launch processes one
 group-round per leader commit. PMC checks it (`traffic`).
 SURVEY.md §8d's canonical count at reference field widths, B_round(R) =
 (R-1)(69+65+138) + 8R + 48 = 616 B at R = 3, is reported beside it as
@@ -61,17 +61,17 @@ B_RESP, B_EMIT, B_MATCH0, B_ENTRY = 69, 65, 122, 16
 # message 0's hot fields only):
 #   leader   loads  hdr, term, committed, lastIndex 32 + locals word 4
 #                   + 2 ack mailboxes x (count 1 + term word 4 + LogIndex 8)
-#                   + 2 follower match rows 16                          =  78
-#            stores committed 8 + lastIndex 8 + 2 match rows 16
+#                   (match rows: header bits H_MP, gr_layout.h)          =  62
+#            stores committed 8 + lastIndex 8
 #                   + 2 out mailboxes x (LogIndex 8 + Commit offset 4
-#                   + term word 4 + count 1) + proposal result 1 + flags 1 =  68
+#                   + term word 4 + count 1) + proposal result 1 + flags 1 =  52
 #   follower loads  core 32 + locals word 4 + 2 count bytes + term word 4
 #                   + LogIndex 8 + Commit offset 4                       =  54
 #            stores committed 8 + lastIndex 8 + ack mailbox (LogIndex 8
 #                   + term word 4 + count 1) + other count 1
 #                   + append_from 8 + flags 1                            =  39
-# = 78 + 68 + 2 x (54 + 39) = 332 B per group-round.
-ENCODED_ROUND_BYTES = {3: 332}
+# = 62 + 52 + 2 x (54 + 39) = 300 B per group-round.
+ENCODED_ROUND_BYTES = {3: 300}
 
 
 def reference_width_bytes(st, groups, R, passes):

@@ -408,7 +408,7 @@ struct FastLane {
     if (hl) {  // speculative: match/next (those a synced wave needs), the term word and LogIndexes
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        if (!hsync || (uint32_t)j != hself) {
+        if (!hsync) {  // a synced wave's MATCH rows are all stale (H_MS, H_MP)
           match[j] = ntld(s64(Rw::MATCH + j));
           have_m |= 1u << j;
         }
@@ -481,6 +481,7 @@ struct FastLane {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         if (h_ms(sb) && (uint32_t)j == self) match[j] = hi;
+        else if (h_mp(sb, (uint32_t)j) && (uint32_t)j != self) match[j] = hi - 1;
         else if (!((have_m >> j) & 1u)) match[j] = ntld(s64(Rw::MATCH + j));
         if (h_nx(sb, (uint32_t)j)) next[j] = hi + 1;
         else if (!((have_n >> j) & 1u)) next[j] = ntld(s64(Rw::NEXT + j));
@@ -715,21 +716,26 @@ struct FastLane {
       // sync bits: a row in sync with the final lastIndex is not stored (its bit
       // says so); a row that leaves sync, or changed, is
       uint64_t sbits = 0;
-      bool all_nx = true, own_ms = false;
+      bool all_nx = true, own_ms = false, all_mp = true;
 #pragma unroll
       for (int j = 0; j < S; ++j) {
+        const bool me = (uint32_t)j == self;
         const bool nx_now = kSync && next[j] == hi + 1;
-        const bool ms_now = kSync && (uint32_t)j == self && match[j] == hi;
+        const bool ms_now = kSync && me && match[j] == hi;
+        const bool mp_now = kSync && !me && hi >= 1 && match[j] == hi - 1;
         const bool dj = (mdirty >> j) & 1u;
-        if ((dj || (kSync && h_ms(hdr) && (uint32_t)j == self)) && !ms_now)
-          ntst(s64(Rw::MATCH + j), (uint64_t)(match[j]));
+        const bool m_stale = kSync && (me ? h_ms(hdr) : h_mp(hdr, (uint32_t)j));
+        if ((dj || m_stale) && !(me ? ms_now : mp_now)) ntst(s64(Rw::MATCH + j), (uint64_t)(match[j]));
         if ((dj || (kSync && h_nx(hdr, (uint32_t)j))) && !nx_now) ntst(s64(Rw::NEXT + j), (uint64_t)(next[j]));
         sbits |= (nx_now ? 1ull : 0ull) << (H_NX_SHIFT + j);
         sbits |= (ms_now ? 1ull : 0ull) << H_MS_BIT;
+        sbits |= (mp_now ? 1ull : 0ull) << (H_MP_SHIFT + j);
         own_ms = own_ms || ms_now;
         if (rkind(j) != GR_SLOT_EMPTY && !nx_now) all_nx = false;
+        if (rkind(j) != GR_SLOT_EMPTY && !me && !mp_now) all_mp = false;
       }
-      synced = kSync && own_ms && all_nx;
+      // WH_SYNC (the wave hint): every member's NEXT and MATCH row is stale
+      synced = kSync && own_ms && all_nx && all_mp;
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         if ((sdirty >> j) & 1u) {

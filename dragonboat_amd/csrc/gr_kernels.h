@@ -165,6 +165,18 @@ __device__ inline __attribute__((always_inline)) uint32_t sload_u32(const uint8_
   return *(cu32*)(uintptr_t)p;
 }
 
+// The wave's hint for the next pass (WH_*): h when every lane of `act` stepped
+// here (done) with hint h or with hint 0 (no input this pass: a wildcard, so an
+// idle lane or a padding slot does not cost its wave the speculation), and at
+// least one with h; else 0.
+__device__ inline __attribute__((always_inline)) uint32_t wave_hint(bool done, uint32_t myhint, uint64_t act) {
+  const uint64_t nz = __ballot(done && myhint != 0);
+  if (!nz) return 0u;
+  const uint32_t h = (uint32_t)__shfl((int)myhint, (int)__ffsll((unsigned long long)nz) - 1);
+  const uint64_t ok = __ballot(done && (myhint == h || myhint == 0));
+  return ok == act ? h : 0u;
+}
+
 // Per-wave bookkeeping shared by the lean and steady kernels: the next pass's
 // hint of this wave (its lanes' common role hint when every active lane was
 // stepped here, else 0; written by each instance that stepped a lane of the
@@ -181,10 +193,11 @@ __device__ inline __attribute__((always_inline)) void wave_finish(const StepPara
     // over the lanes that are this kernel's (mine), written by the first of them
     const uint64_t mm = __ballot(mine);
     if (mine) {
+      // the lanes' common role hint; a lane with no input (hint 0, done) takes
+      // any hint (wave_hint), a lane left to the other instance blocks it
       const bool done = active && !skip;
-      const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane(myhint);
-      const uint64_t same = __ballot(done && myhint == first), act = __ballot(i < kp.n_lanes), dn = __ballot(done);
-      const uint32_t nh = same == act ? first : 0u;
+      const uint64_t act = __ballot(i < kp.n_lanes), dn = __ballot(done);
+      const uint32_t nh = wave_hint(done, myhint, act);
       if ((threadIdx.x & 63) == (uint32_t)__ffsll((unsigned long long)mm) - 1 && dn) kp.hints_out[wave] = (uint8_t)nh;
     }
   }
@@ -571,9 +584,9 @@ __global__ __launch_bounds__(kBlock, 1) void gr_small_kernel(StepParams kp, uint
     if (!bail) GR_CHECK_STATE(kp.st, p);
   }
   if (kp.hints) {  // the wave's next hint, as wave_finish writes it
-    const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane(myhint);
-    const uint64_t same = __ballot(active && myhint == first), act = __ballot(active);
-    if ((threadIdx.x & 63) == 0 && act) kp.hints_out[wave] = (uint8_t)(same == act ? first : 0u);
+    const uint64_t act = __ballot(active);
+    const uint32_t nh = wave_hint(active, myhint, act);
+    if ((threadIdx.x & 63) == 0 && act) kp.hints_out[wave] = (uint8_t)nh;
   }
   if (bail) {  // handed over: the tick lane, else the general lane, in this wave
     LaneStats l2;

@@ -174,7 +174,9 @@ struct Lane {
       const uint64_t sb = has_sync_bits(S) ? hdr0 : 0;  // stale rows: values from lastIndex as loaded
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        match[j] = (h_ms(sb) && (uint32_t)j == h_self(hdr0)) ? hi_ld : s64(R::MATCH + j);
+        match[j] = (h_ms(sb) && (uint32_t)j == h_self(hdr0))  ? hi_ld
+                   : (h_mp(sb, (uint32_t)j) && (uint32_t)j != h_self(hdr0)) ? hi_ld - 1
+                                                                          : s64(R::MATCH + j);
         next[j] = h_nx(sb, (uint32_t)j) ? hi_ld + 1 : s64(R::NEXT + j);
       }
     }
@@ -491,8 +493,28 @@ struct Lane {
   }
 
   // ---------------------------------------------------------------- emission
-  GR_HD uint32_t out_gpos(uint32_t j) const { return route_of(kp, 1, j, i); }
-  GR_HD uint32_t in_gpos(uint32_t j) const { return route_of(kp, 0, j, i); }
+  // routes, mailbox count bytes and local inputs, read once per pass in the
+  // first load round (preload): the message and local-input loops then start
+  // without a dependent load round per slot
+  uint32_t gin_[S], gout_[S], pcb_[S];
+  uint32_t plf_ = 0, pnt_ = 0, pnq_ = 0, pnp_ = 0;
+  GR_HD void preload() {
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      gin_[j] = route_of(kp, 0, (uint32_t)j, i);
+      gout_[j] = route_of(kp, 1, (uint32_t)j, i);
+    }
+#pragma unroll
+    for (int j = 0; j < S; ++j) pcb_[j] = gin_[j] != NOPOS ? (uint32_t)kp.in.at(gin_[j]).cnt() : 0u;
+    if (kp.has_locals) {
+      plf_ = kp.ln.u8(LR_LFLAGS)[i];
+      pnt_ = kp.ln.u32(LR_TICKS)[i];
+      pnq_ = kp.ln.u32(LR_QTICKS)[i];
+      pnp_ = kp.ln.u32(LR_PROPOSE)[i];
+    }
+  }
+  GR_HD uint32_t out_gpos(uint32_t j) const { return sel(gout_, j); }
+  GR_HD uint32_t in_gpos(uint32_t j) const { return sel(gin_, j); }
   // raft.send (raft.go:457-461): From is implied by the mailbox; Term is
   // r.term unless the type is a request (finalizeMessageTerm :444-455).
   GR_HD int emit(uint32_t j, const OutMsg& m) {
@@ -1468,7 +1490,7 @@ struct Lane {
       const uint32_t g = in_gpos(j);
       if (g == NOPOS) continue;
       const Mailbox mb = kp.in.at(g);
-      const uint32_t cb = mb.cnt(), c = mb_n(cb);
+      const uint32_t cb = sel(pcb_, j), c = mb_n(cb);
 #pragma unroll 1
       for (uint32_t k = 0; k < c; ++k) {
         if (item == limit) { *at = item; return 0; }
@@ -1485,9 +1507,7 @@ struct Lane {
       }
     }
     if (kp.has_locals) {
-      const uint8_t lf = kp.ln.u8(LR_LFLAGS)[i];
-      const uint32_t nt = kp.ln.u32(LR_TICKS)[i], nq = kp.ln.u32(LR_QTICKS)[i],
-                     np = kp.ln.u32(LR_PROPOSE)[i];
+      const uint32_t lf = plf_, nt = pnt_, nq = pnq_, np = pnp_;
       if (lf & LF_READ_INDEX) {
         if (item == limit) { *at = item; return 0; }
         need(G_CORE);
@@ -1539,6 +1559,7 @@ struct Lane {
     GR_COVER(GENERAL_LANE);
     uint32_t at = 0, limit = 0xFFFFFFFFu;
     int esc = 0;
+    preload();
 #pragma unroll 1
     for (int attempt = 0; attempt < 2; ++attempt) {  // one call site keeps run() inlined
       begin();

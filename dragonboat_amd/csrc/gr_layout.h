@@ -116,11 +116,17 @@ __host__ __device__ inline uint64_t h_make(uint32_t state, uint32_t self, uint32
 // rows per pass. Every other writer of lastIndex or of the remote rows first
 // materialises the rows and clears the bits (Lane::store); the tick lane only
 // reads them; host conversion resolves them (host::resolve_sync).
-constexpr uint32_t H_NX_SHIFT = 56, H_MS_BIT = 59;
-constexpr uint64_t H_SYNC_MASK = (7ull << H_NX_SHIFT) | (1ull << H_MS_BIT);
+// H_MP_SHIFT + j (round 4) says match[j] == lastIndex - 1 for a slot j other
+// than self, and its MATCH row is stale: after a steady pass every follower has
+// acknowledged the previous entry and the leader has appended one more
+// (remote.tryUpdate, raft.go:1205-1227, then appendEntries :643-654), so a
+// steady leader loads and stores none of its MATCH rows either.
+constexpr uint32_t H_NX_SHIFT = 56, H_MS_BIT = 59, H_MP_SHIFT = 40;
+constexpr uint64_t H_SYNC_MASK = (7ull << H_NX_SHIFT) | (1ull << H_MS_BIT) | (7ull << H_MP_SHIFT);
 __host__ __device__ constexpr bool has_sync_bits(int S) { return S <= 3; }
 __host__ __device__ inline bool h_nx(uint64_t h, uint32_t j) { return (h >> (H_NX_SHIFT + j)) & 1u; }
 __host__ __device__ inline bool h_ms(uint64_t h) { return (h >> H_MS_BIT) & 1u; }
+__host__ __device__ inline bool h_mp(uint64_t h, uint32_t j) { return (h >> (H_MP_SHIFT + j)) & 1u; }
 // Run bits (S <= 6; above rb and the sync bits): H_RTT says the window's newest
 // run has the current term, H_RLC that it starts at or below committed. Both
 // hold in steady state (the leader's term's run began before the commit point),

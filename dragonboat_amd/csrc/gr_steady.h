@@ -110,7 +110,7 @@ struct SteadyLeader : SteadyBase<RM> {
       cb[j] = in ? (uint32_t)ntld(mb.cnt()) : 0u;
       mt[j] = in ? ntld(mb.mterm()) : 0u;
       x[j][0] = in ? ntld(mb.u64(0, MF_LOG_INDEX)) : 0ull;
-      m[j] = (uint32_t)j != hself ? ntld(B::s64(Rw::MATCH + j)) : hi0;
+      m[j] = (uint32_t)j != hself ? hi0 - 1 : hi0;  // H_MP / H_MS (checked below): no MATCH row loaded
     }
     // a second ack: shared mailboxes (MB_SHARED, the steady state) imply it from
     // the first; only an unshared pair loads it, in a second round
@@ -134,7 +134,7 @@ struct SteadyLeader : SteadyBase<RM> {
       const uint32_t c = mb_n(cb[j]);
       nmi += c;
       if ((uint32_t)j != hself) {
-        ok = ok && rb_state(rb, j) == GR_REPLICATE_ST && rb_active(rb, j);
+        ok = ok && h_mp(hdr, j) && rb_state(rb, j) == GR_REPLICATE_ST && rb_active(rb, j);
         ok = ok && (c == 0 || ((cb[j] & MB_UNIFORM) && (cb[j] & MB_RESP) && c <= 2 && (uint64_t)mt[j] == term));
         ok = ok && (c < 1 || x[j][0] <= hi0) && (c < 2 || x[j][1] <= hi0);
       } else {
@@ -145,14 +145,12 @@ struct SteadyLeader : SteadyBase<RM> {
     uint64_t c = committed0;
     uint64_t bc0 = 0, bc1 = 0;  // the Commit of the first / second commit broadcast
     uint32_t ncb = 0;
-    uint32_t mdirty = 0;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const bool upd = (uint32_t)j != hself && (uint32_t)k < mb_n(cb[j]) && m[j] < x[j][k];
         m[j] = upd ? x[j][k] : m[j];
-        mdirty |= upd ? 1u << j : 0u;
         const uint64_t q = B::umax(B::umin(m[0], m[1]), B::umin(B::umax(m[0], m[1]), m[2]));  // sortMatchValues, R = 3
         const bool adv = upd && q > c;
         bc0 = adv && ncb == 0 ? q : bc0;
@@ -175,11 +173,18 @@ struct SteadyLeader : SteadyBase<RM> {
     const uint64_t hi = hi0 + np;  // the proposal's entry (no new run: the newest one is at term)
     if (c != committed0) ntst(B::s64(SR_COMMITTED), c);
     if (np) ntst(B::s64(SR_LAST_INDEX), hi);
+    // match[self] = lastIndex and every next = lastIndex + 1 again (H_MS, H_NX
+    // hold); a follower's match is lastIndex - 1 again when it acked the newest
+    // entry before this pass's proposal (H_MP holds, nothing stored), else its
+    // row is written and its bit cleared
+    uint64_t nh = hdr;
 #pragma unroll
-    for (int j = 0; j < S; ++j)
-      if ((mdirty >> j) & 1u) ntst(B::s64(Rw::MATCH + j), m[j]);
-    // match[self] = lastIndex and every next = lastIndex + 1 again: the sync bits
-    // hold, the header is unchanged
+    for (int j = 0; j < S; ++j) {
+      if ((uint32_t)j == hself || m[j] == hi - 1) continue;
+      ntst(B::s64(Rw::MATCH + j), m[j]);
+      nh &= ~(1ull << (H_MP_SHIFT + j));
+    }
+    if (nh != hdr) ntst(B::s64(SR_HDR), nh);
     // one commit broadcast and the proposal: both carry LogIndex = the old
     // lastIndex and Commit = c, a shared mailbox (gr_layout.h MB_SHARED) stores
     // message 0's fields only
@@ -220,7 +225,8 @@ struct SteadyLeader : SteadyBase<RM> {
     ls->leader_in = nmi;
     ls->leader_out = nmo;
     ls->entries = 0;
-    *hint_out = (nmi || np) ? (WH_STEADY_LEADER | (self << WH_SLOT_SHIFT)) : 0u;  // FastLane::role_hint
+    // FastLane::role_hint: WH_SYNC only while every member row is stale
+    *hint_out = (nmi || np) ? ((nh == hdr ? WH_STEADY_LEADER : (WH_LEADER | WH_RUNS)) | (self << WH_SLOT_SHIFT)) : 0u;
     GR_COVER(STEADY_LEADER);
     return true;
   }

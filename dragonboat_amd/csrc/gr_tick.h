@@ -279,8 +279,11 @@ struct TickLane {
       const uint64_t rb = h_rb(hdr);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        // H_MS: the self slot's MATCH row is stale, its match is lastIndex
-        match[j] = (has_sync_bits(S) && h_ms(hdr) && (uint32_t)j == self) ? hi : s64(Rw::MATCH + j);
+        // H_MS: the self slot's MATCH row is stale, its match is lastIndex;
+        // H_MP: another slot's is lastIndex - 1
+        match[j] = (has_sync_bits(S) && h_ms(hdr) && (uint32_t)j == self)                ? hi
+                   : (has_sync_bits(S) && h_mp(hdr, (uint32_t)j) && (uint32_t)j != self) ? hi - 1
+                                                                                         : s64(Rw::MATCH + j);
         rst[j] = rb_state(rb, j);
         ract[j] = rb_active(rb, j);
         rkind[j] = rb_kind(rb, j);

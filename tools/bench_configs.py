@@ -118,6 +118,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--only", default="2,3,5")
     ap.add_argument("--graph-reps", type=int, default=200, help="config 2: replays of a 2-pass HIP graph (0: off)")
+    ap.add_argument("--groups2", type=int, default=10_000, help="config 2's group count (A/B of the layout)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -126,9 +127,9 @@ def main():
     res = []
     want = set(args.only.split(","))
     if "2" in want:
-        G, R = 10_000, 3
+        G, R = args.groups2, 3
         peers = P.make_groups(G, R, seed=2)
-        res.append(run("2: 10k x 3, uniform proposals", peers, G, R, args.passes, args.warmup,
+        res.append(run(f"2: {G} x 3, uniform proposals", peers, G, R, args.passes, args.warmup,
                        lambda k, eng, n: P.propose_locals(n, np.arange(G), pass_index=k), graph_reps=args.graph_reps))
     if "3" in want:
         G, R = 100_000, 5
