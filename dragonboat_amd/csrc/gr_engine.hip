@@ -11,6 +11,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <string>
 #include <vector>
 
 
@@ -93,6 +94,11 @@ struct gr_engine {
   bool locals_set = false;
   bool locals_other = false;  // some bound local input has ticks / a ReadIndex / oversized counts (LW_OTHER)
   uint64_t passes = 0;
+  // GR_WAVE_CLOCK=<path> at gr_create (profiling): the general kernel records
+  // each wave's span; gr_destroy writes the last pass's records to <path>
+  uint64_t* wclock = nullptr;
+  uint8_t bin_general = 1;  // StepParams::bin_general (GR_BIN_GENERAL=0 at gr_create: off, A/B runs)
+  std::string wclock_path;
 
   // gr_step buffers (gr_io.h), grown on demand and reused
   struct Buf {
@@ -207,6 +213,8 @@ StepParams base_params(gr_engine* e) {
   kp.stats = e->stats;
   kp.max_entry_size = e->cfg.max_entry_size;
   kp.small_blocks = e->small_blocks;
+  kp.wclock = e->wclock;
+  kp.bin_general = e->bin_general;
   return kp;
 }
 
@@ -384,6 +392,12 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
     if (v > 0) e->split_min = (uint32_t)v;
   }
   if (const char* sb = getenv("GR_SMALL_BLOCKS")) e->small_blocks = (uint32_t)strtoul(sb, nullptr, 10);
+  if (const char* bg = getenv("GR_BIN_GENERAL")) e->bin_general = bg[0] == '1';
+  if (const char* wc = getenv("GR_WAVE_CLOCK")) {
+    if (hipMalloc((void**)&e->wclock, (size_t)kGeneralWaveSlots * kWaveClockWords * 8) == hipSuccess &&
+        hipMemset(e->wclock, 0, (size_t)kGeneralWaveSlots * kWaveClockWords * 8) == hipSuccess)
+      e->wclock_path = wc;
+  }
   void *ds = nullptr, *dl = nullptr;
   if (hipMalloc(&ds, sb) != hipSuccess || hipMalloc(&dl, lb) != hipSuccess ||
       hipMalloc((void**)&e->stats, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
@@ -422,6 +436,17 @@ void gr_destroy(gr_engine* e) {
   if (e->counters) (void)hipFree(e->counters);
   if (e->route_base) (void)hipFree(e->route_base);
   if (e->hints) (void)hipFree(e->hints);
+  if (e->wclock) {
+    std::vector<uint64_t> h((size_t)kGeneralWaveSlots * kWaveClockWords);
+    if (!e->wclock_path.empty() && hipStreamSynchronize(e->stream) == hipSuccess &&
+        hipMemcpy(h.data(), e->wclock, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      if (FILE* f = fopen(e->wclock_path.c_str(), "wb")) {
+        fwrite(h.data(), 8, h.size(), f);
+        fclose(f);
+      }
+    }
+    (void)hipFree(e->wclock);
+  }
   free_timings(e);
   for (gr_engine::Buf* b : {&e->d_in, &e->d_out, &e->d_msgs, &e->d_locals, &e->d_mark, &e->d_lop, &e->d_keys,
                             &e->d_idx, &e->d_skeys, &e->d_sidx, &e->d_win, &e->d_oc, &e->d_off, &e->d_tmp,

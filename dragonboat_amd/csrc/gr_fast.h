@@ -481,7 +481,7 @@ struct FastLane {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         if (h_ms(sb) && (uint32_t)j == self) match[j] = hi;
-        else if (h_mp(sb, (uint32_t)j) && (uint32_t)j != self) match[j] = hi - 1;
+        else if (h_mp(sb, (uint32_t)j) && (uint32_t)j != self) match[j] = hi - 2;
         else if (!((have_m >> j) & 1u)) match[j] = ntld(s64(Rw::MATCH + j));
         if (h_nx(sb, (uint32_t)j)) next[j] = hi + 1;
         else if (!((have_n >> j) & 1u)) next[j] = ntld(s64(Rw::NEXT + j));
@@ -722,7 +722,7 @@ struct FastLane {
         const bool me = (uint32_t)j == self;
         const bool nx_now = kSync && next[j] == hi + 1;
         const bool ms_now = kSync && me && match[j] == hi;
-        const bool mp_now = kSync && !me && hi >= 1 && match[j] == hi - 1;
+        const bool mp_now = kSync && !me && hi >= 2 && match[j] == hi - 2;
         const bool dj = (mdirty >> j) & 1u;
         const bool m_stale = kSync && (me ? h_ms(hdr) : h_mp(hdr, (uint32_t)j));
         if ((dj || m_stale) && !(me ? ms_now : mp_now)) ntst(s64(Rw::MATCH + j), (uint64_t)(match[j]));

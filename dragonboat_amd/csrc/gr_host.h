@@ -36,7 +36,7 @@ __host__ __device__ inline uint64_t header_of(const gr_peer& g, uint32_t S) {
   if (has_sync_bits((int)S) && g.state == GR_LEADER) {
     for (uint32_t j = 0; j < S; ++j) {
       if (g.remotes[j].next == g.last_index + 1) h |= 1ull << (H_NX_SHIFT + j);
-      if (j != g.self_slot && g.last_index >= 1 && g.remotes[j].match == g.last_index - 1)
+      if (j != g.self_slot && g.last_index >= 2 && g.remotes[j].match == g.last_index - 2)
         h |= 1ull << (H_MP_SHIFT + j);
     }
     if (g.self_slot < S && g.remotes[g.self_slot].match == g.last_index) h |= 1ull << H_MS_BIT;
@@ -63,7 +63,7 @@ __host__ __device__ inline void resolve_sync(gr_peer& g, uint32_t S, uint64_t h)
   if (!has_sync_bits((int)S)) return;  // wider groups: those header bits are remote state
   for (uint32_t j = 0; j < S; ++j) {
     if (h_nx(h, j)) g.remotes[j].next = g.last_index + 1;
-    if (h_mp(h, j) && j != g.self_slot) g.remotes[j].match = g.last_index - 1;
+    if (h_mp(h, j) && j != g.self_slot) g.remotes[j].match = g.last_index - 2;
   }
   if (h_ms(h) && g.self_slot < S) g.remotes[g.self_slot].match = g.last_index;
 }

@@ -61,9 +61,12 @@ __device__ inline __attribute__((always_inline)) void block_stats(const StepPara
 // appends over 16 counters 256 B apart keeps them from serialising when every
 // wave bails a few lanes (one shared counter: 105 us instead of 37 us on
 // config 3); no barrier, so waves of steady-state populations retire freely.
-// Lists 0..7 followers, 8..15 leaders (the general kernel's); 16..23 unused
-// (the tick lists are below).
-// Lists 24..31: lanes a split pass's steady kernel did not finish, which the
+// Lists 0..31 are the general kernel's, keyed by handler class (general_bin:
+// list = class x 2 + workgroup parity), so that kernel, walking them in order,
+// runs waves of one class (fewer divergent handler paths per wave); with
+// StepParams::bin_general off, by role and workgroup (followers 0..15, leaders
+// 16..31). The tick lists are below.
+// Lists 32..39: lanes a split pass's steady kernel did not finish, which the
 // role instances step with FastLane before anything goes to the general kernel.
 // After the lane lists' storage: one flag byte and one lane mask per wave, the
 // waves a split pass's steady kernel leaves to the role instances (flag =
@@ -81,7 +84,7 @@ __device__ inline __attribute__((always_inline)) void block_stats(const StepPara
 // saturates near 90 appends per us (MI355X_MICROARCH.md, "dequeue"), so 8 list
 // counters made those appends most of the steady kernel's time.
 constexpr uint32_t kTickLists = 64;
-constexpr uint32_t kBailLists = 32, kGeneralLists = 16, kRetryList0 = 24,
+constexpr uint32_t kBailLists = 40, kGeneralLists = 32, kRetryList0 = 32,
                    kTickCounter0 = kBailLists, kCounters = kBailLists + kTickLists,
                    kCounterStride = 64;  // counters 256 B apart
 constexpr uint32_t WF_LISTED = 0x80;     // wave flag: the role instances step this wave's masked lanes
@@ -141,6 +144,54 @@ __device__ inline __attribute__((always_inline)) void tick_append(bool mine, uin
               (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
 }
 
+// The general kernel's lane classes (StepParams::bin_general): role, whether a
+// message from a higher or a lower term waits (a step-down or a term adoption,
+// or a stale message to drop), and whether a mailbox holds full records (rejects,
+// catch-up Replicates, heartbeats) rather than uniform steady traffic. Its loads
+// are the ones the lane that handed the lane over has just made (L2-resident).
+constexpr uint32_t kGeneralBins = 16;
+template <int S>
+__device__ inline __attribute__((always_inline)) uint32_t general_bin(const StepParams& kp, uint32_t i, uint32_t p) {
+  const uint64_t hdr = kp.st.u64(SR_HDR)[p], term = kp.st.u64(SR_TERM)[p];
+  bool higher = false, lower = false, full = false;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const uint32_t g = route_of(kp, 0, j, i);
+    if (g == NOPOS) continue;
+    const Mailbox mb = kp.in.at(g);
+    const uint32_t cb = mb.cnt();
+    if (!mb_n(cb)) continue;
+    const uint64_t t = mb.term_at(0, cb);
+    higher = higher || t > term;
+    lower = lower || t < term;
+    full = full || !(cb & MB_UNIFORM);
+  }
+  const uint32_t st = h_state(hdr) == GR_LEADER ? 0u : 1u;
+  return st * 8 + (higher ? 4u : 0u) + (lower ? 2u : 0u) + (full ? 1u : 0u);
+}
+
+// Hand lane i (peer p) to the general kernel: one append per class present in
+// the wave (bin_general), else by role and workgroup (lead: a leader lane).
+template <int S>
+__device__ inline __attribute__((always_inline)) void general_append(const StepParams& kp, bool mine, bool lead, uint32_t i,
+                                                                     uint32_t p, uint32_t bid, uint32_t* bail_list,
+                                                                     uint32_t* counters, uint32_t list_cap) {
+  uint64_t bm = __ballot(mine);
+  if (!bm) return;
+  uint32_t key = 0;
+  if (kp.bin_general) {
+    if (mine) key = general_bin<S>(kp, i, p) * 2 + (bid & 1u);
+  } else {
+    key = (lead ? kGeneralLists / 2 : 0u) + bid % (kGeneralLists / 2);
+  }
+  while (bm) {  // wave-uniform
+    const uint32_t k = (uint32_t)__shfl((int)key, __ffsll((unsigned long long)bm) - 1);
+    const bool mm = mine && key == k;
+    bail_append(mm, k, bail_list, counters, list_cap, i);
+    bm &= ~__ballot(mm);
+  }
+}
+
 #ifndef GR_FAST_MIN_WAVES
 #define GR_FAST_MIN_WAVES 1  // waves per SIMD the register allocation must allow (A/B builds)
 #endif
@@ -185,6 +236,7 @@ __device__ inline __attribute__((always_inline)) uint32_t wave_hint(bool done, u
 // or a ReadIndex into the tick lists (tick_append): the later kernels walk their
 // lists in order, so their waves hold one kind of lane and diverge less), and
 // the stats.
+template <int S>
 __device__ inline __attribute__((always_inline)) void wave_finish(const StepParams& kp, uint32_t i, uint32_t wave, bool mine, bool active,
                                    bool skip, bool bail, uint32_t role, uint32_t myhint, const LaneStats& ls,
                                    uint32_t* bail_list, uint32_t* counters, uint32_t list_cap,
@@ -203,11 +255,8 @@ __device__ inline __attribute__((always_inline)) void wave_finish(const StepPara
   }
   const bool lead = role == GR_LEADER;
   const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
-#pragma unroll
-  for (uint32_t side = 0; side < 2; ++side) {
-    const bool m = bail && !tickish && lead == (side == 1);
-    bail_append(m, (bid % 8) + side * 8, bail_list, counters, list_cap, i);
-  }
+  const uint32_t p = bail && !tickish && kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+  general_append<S>(kp, bail && !tickish, lead, i, p, bid, bail_list, counters, list_cap);
   tick_append(tickish, wave * 64, bail_list, counters, list_cap, i);  // the wave's lanes share a block
   if (kp.stats) block_stats(kp, ls, bid);
 }
@@ -234,7 +283,7 @@ __device__ inline __attribute__((always_inline)) void fast_wave(const StepParams
     bail = bail && !skip;  // a skipped lane is the other instance's
     if (!bail && !skip) GR_CHECK_STATE(kp.st, p);
   }
-  wave_finish(kp, i, wave, mine, active, skip, bail, role, myhint, ls, bail_list, counters, list_cap, bid);
+  wave_finish<S>(kp, i, wave, mine, active, skip, bail, role, myhint, ls, bail_list, counters, list_cap, bid);
 }
 
 // Locate entry x of the 8 lists whose exclusive prefix is start[0..8]: list and offset.
@@ -322,11 +371,7 @@ __device__ inline __attribute__((always_inline)) void roles_listed(const StepPar
     }
     const bool lead = role == GR_LEADER;
     const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[li] & LW_OTHER);
-#pragma unroll
-    for (uint32_t side = 0; side < 2; ++side) {
-      const bool m = bail && !tickish && lead == (side == 1);
-      bail_append(m, (bid % 8) + side * 8, bail_list, counters, list_cap, li);
-    }
+    general_append<S>(kp, bail && !tickish, lead, li, li, bid, bail_list, counters, list_cap);
     tick_append(tickish, base, bail_list, counters, list_cap, li);  // keyed by the entry's block
   }
   if (kp.stats && n > bid * kBlock) block_stats(kp, acc, bid);
@@ -428,7 +473,7 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
   }
   // lanes not finished here (nothing stored) go to FastLane in the role
   // instances that follow (lists 24..31), not straight to the general kernel
-  wave_finish(kp, i, wave, true, active, false, false, role, myhint, ls, bail_list, counters, list_cap);
+  wave_finish<S>(kp, i, wave, true, active, false, false, role, myhint, ls, bail_list, counters, list_cap);
   bail_append(active && !done, kRetryList0 + blockIdx.x % 8, bail_list, counters, list_cap, i);
 }
 
@@ -487,7 +532,8 @@ __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(Step
         hand = true;  // the general lane steps it
       }
     }
-    bail_append(hand, blockIdx.x % 8, bail_list, counters, list_cap, i);
+    general_append<S>(kp, hand, false, i, hand && kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i, blockIdx.x,
+                      bail_list, counters, list_cap);
   }
   if (kp.stats) block_stats(kp, acc);
 }
@@ -510,9 +556,12 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
   if (blockIdx.x == 0 && threadIdx.x < kCounters) next_counters[threadIdx.x * kCounterStride] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters) next_counters[kListedWord] = 0;
   if (blockIdx.x * kBlock >= n) return;  // uniform per block: nothing to do, no stats row touched
+  const uint64_t t0 = kp.wclock ? wall_clock64() : 0;
   LaneStats acc;
+  uint64_t tph[3] = {0, 0, 0};  // GR_WAVE_CLOCK: the first round's phase marks
   for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
     const uint32_t x = base + threadIdx.x;
+    uint32_t i = 0;
     if (x < n) {
       uint32_t l = 0;
 #pragma unroll
@@ -520,12 +569,19 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
       uint32_t off = 0;
 #pragma unroll
       for (uint32_t k = 0; k < kGeneralLists; ++k) off = (k == l) ? x - start[k] : off;
-      const uint32_t i = bail_list[(uint64_t)l * list_cap + off];
+      i = bail_list[(uint64_t)l * list_cap + off];
+    }
+    if (x < n) {
       const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
       LaneStats ls;
       Lane<S> L(kp, i, p);
       L.step(&ls);
       GR_CHECK_STATE(kp.st, p);
+      if (!tph[0]) {
+        tph[0] = L.tclk[0];
+        tph[1] = L.tclk[1];
+        tph[2] = L.tclk[2];
+      }
       acc.leader_commit += ls.leader_commit;
       acc.follower_commit += ls.follower_commit;
       acc.escalated += ls.escalated;
@@ -537,6 +593,32 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
       acc.bailed += 1;
     }
   }
+  if (kp.wclock) {  // profiling: this wave's span and what it stepped
+    const uint64_t t1 = wall_clock64();
+    const uint32_t nl = wave_sum(acc.bailed), nm = wave_sum(acc.msgs_in), ne = wave_sum(acc.escalated),
+                   nli = wave_sum(acc.leader_in);
+    const uint32_t w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0) {
+      uint64_t* r = kp.wclock + (uint64_t)w * kWaveClockWords;
+      r[0] = t0;
+      r[1] = t1;
+      r[2] = nl;
+      r[3] = nm;
+      r[4] = ne;
+      r[5] = nli;
+    }
+    // the phase marks of the wave's first round (any active lane's: the wave runs them together)
+    const uint64_t any = __ballot(tph[0] != 0);
+    if (any) {
+      const int src = __ffsll((unsigned long long)any) - 1;
+      const uint64_t a = __shfl(tph[0], src), b = __shfl(tph[1], src), c = __shfl(tph[2], src);
+      if ((threadIdx.x & 63) == 0) {
+        uint64_t* r = kp.wclock + (uint64_t)w * kWaveClockWords;
+        r[6] = a;
+        r[7] = ((b - a) << 32) | (c - b);
+      }
+    }
+  }
   if (kp.stats) block_stats(kp, acc);
 }
 
@@ -545,6 +627,7 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
 // block has rows for. Kept small because with no bailed lanes the launch is pure
 // overhead. GR_GENERAL_BLOCKS overrides it (A/B runs).
 constexpr uint32_t kGeneralBlocks = 256;
+constexpr uint32_t kGeneralWaveSlots = 4096;  // GR_WAVE_CLOCK records: the general grid's waves at most
 inline uint32_t general_blocks() {
   static const uint32_t v = [] {
     const char* e = getenv("GR_GENERAL_BLOCKS");
@@ -695,7 +778,11 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
     hipLaunchKernelGGL(gr_tick_kernel<S>, dim3(tblocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
     if ((err = hipGetLastError()) != hipSuccess) return err;
   }
-  const uint32_t gblocks = blocks < general_blocks() ? blocks : general_blocks();
+  uint32_t gblocks = blocks < general_blocks() ? blocks : general_blocks();
+  if (kp.wclock && gblocks > kGeneralWaveSlots / (kBlock / 64)) gblocks = kGeneralWaveSlots / (kBlock / 64);
+  if (kp.wclock &&
+      (err = hipMemsetAsync(kp.wclock, 0, (size_t)gblocks * (kBlock / 64) * kWaveClockWords * 8, s)) != hipSuccess)
+    return err;
   hipLaunchKernelGGL(gr_step_kernel<S>, dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list,
                      (const uint32_t*)cur, nxt, list_cap);
   if ((err = hipGetLastError()) != hipSuccess) return err;

@@ -114,6 +114,7 @@ struct Lane {
   uint64_t imk = 0, isv = 0;  // inMemory.markerIndex, savedTo
 
   // outputs of this pass
+  uint64_t tclk[3] = {0, 0, 0};  // GR_WAVE_CLOCK phase marks (device builds): loads, run, store done
   uint32_t outcnt = 0;  // 3 bits per slot
   uint64_t outu = 0;    // 5 bits per slot: not uniform, ReplicateResp kind, MB_N1 of messages 0..2
   uint32_t rtrc = 0, prop_result = 0;
@@ -175,7 +176,7 @@ struct Lane {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         match[j] = (h_ms(sb) && (uint32_t)j == h_self(hdr0))  ? hi_ld
-                   : (h_mp(sb, (uint32_t)j) && (uint32_t)j != h_self(hdr0)) ? hi_ld - 1
+                   : (h_mp(sb, (uint32_t)j) && (uint32_t)j != h_self(hdr0)) ? hi_ld - 2
                                                                           : s64(R::MATCH + j);
         next[j] = h_nx(sb, (uint32_t)j) ? hi_ld + 1 : s64(R::NEXT + j);
       }
@@ -1566,12 +1567,15 @@ struct Lane {
       // the groups nearly every handed-over lane reads, in one round of loads
       // instead of one dependent round per group as the handlers reach them
       need(G_CORE | G_WIN | G_REM | G_ETICK | G_LID);
+      if (attempt == 0) tclk[0] = lane_clock(kp);
       const int e = run(limit, &at);
+      if (attempt == 0) tclk[1] = lane_clock(kp);
       if (!e) break;
       esc = e;  // second attempt re-runs the prefix and cannot escalate
       limit = at;
     }
     store();
+    tclk[2] = lane_clock(kp);
 #pragma unroll 1
     for (uint32_t j = 0; j < (uint32_t)S; ++j) {  // every routed mailbox is rewritten each pass
       const uint32_t g = out_gpos(j);

@@ -116,10 +116,12 @@ __host__ __device__ inline uint64_t h_make(uint32_t state, uint32_t self, uint32
 // rows per pass. Every other writer of lastIndex or of the remote rows first
 // materialises the rows and clears the bits (Lane::store); the tick lane only
 // reads them; host conversion resolves them (host::resolve_sync).
-// H_MP_SHIFT + j (round 4) says match[j] == lastIndex - 1 for a slot j other
-// than self, and its MATCH row is stale: after a steady pass every follower has
-// acknowledged the previous entry and the leader has appended one more
-// (remote.tryUpdate, raft.go:1205-1227, then appendEntries :643-654), so a
+// H_MP_SHIFT + j (round 4) says match[j] == lastIndex - 2 for a slot j other
+// than self, and its MATCH row is stale. In the pipelined steady state a pass's
+// acks are for the entry proposed two passes earlier (a Replicate crosses one
+// pass boundary to the follower, its ack another back), so after the acks
+// (remote.tryUpdate, raft.go:1205-1227) and this pass's proposal
+// (appendEntries :643-654) every follower's match is lastIndex - 2 again: a
 // steady leader loads and stores none of its MATCH rows either.
 constexpr uint32_t H_NX_SHIFT = 56, H_MS_BIT = 59, H_MP_SHIFT = 40;
 constexpr uint64_t H_SYNC_MASK = (7ull << H_NX_SHIFT) | (1ull << H_MS_BIT) | (7ull << H_MP_SHIFT);
@@ -556,7 +558,24 @@ struct StepParams {
   // host-side launch choice (gr_kernels.h launch): passes of at most this many
   // workgroups run as one fused kernel (gr_small_kernel)
   uint32_t small_blocks;
+  // GR_WAVE_CLOCK (profiling, gr_engine.hip): per general-kernel wave a record of
+  // kWaveClockWords u64 (start and end clock, lanes, messages in, escalations,
+  // leader messages), or nullptr
+  uint64_t* wclock;
+  // lanes handed to the general kernel go to lists keyed by handler class
+  // (gr_kernels.h general_bin) instead of by role and workgroup
+  uint8_t bin_general;
 };
+constexpr uint32_t kWaveClockWords = 8;
+// The wave's clock for GR_WAVE_CLOCK phase marks (0 when off, and in host builds).
+__host__ __device__ inline uint64_t lane_clock(const StepParams& kp) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return kp.wclock ? wall_clock64() : 0ull;
+#else
+  (void)kp;
+  return 0ull;
+#endif
+}
 
 // Route mode as a compile-time parameter of the lean kernel instances
 // (gr_kernels.h): RM_ANY reads StepParams::route_mode at run time; an instance

@@ -110,7 +110,7 @@ struct SteadyLeader : SteadyBase<RM> {
       cb[j] = in ? (uint32_t)ntld(mb.cnt()) : 0u;
       mt[j] = in ? ntld(mb.mterm()) : 0u;
       x[j][0] = in ? ntld(mb.u64(0, MF_LOG_INDEX)) : 0ull;
-      m[j] = (uint32_t)j != hself ? hi0 - 1 : hi0;  // H_MP / H_MS (checked below): no MATCH row loaded
+      m[j] = (uint32_t)j != hself ? hi0 - 2 : hi0;  // H_MP / H_MS (checked below): no MATCH row loaded
     }
     // a second ack: shared mailboxes (MB_SHARED, the steady state) imply it from
     // the first; only an unshared pair loads it, in a second round
@@ -174,13 +174,13 @@ struct SteadyLeader : SteadyBase<RM> {
     if (c != committed0) ntst(B::s64(SR_COMMITTED), c);
     if (np) ntst(B::s64(SR_LAST_INDEX), hi);
     // match[self] = lastIndex and every next = lastIndex + 1 again (H_MS, H_NX
-    // hold); a follower's match is lastIndex - 1 again when it acked the newest
-    // entry before this pass's proposal (H_MP holds, nothing stored), else its
-    // row is written and its bit cleared
+    // hold); a follower's match is lastIndex - 2 again when its acks were for the
+    // entry two proposals back (H_MP holds, nothing stored), else its row is
+    // written and its bit cleared
     uint64_t nh = hdr;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      if ((uint32_t)j == hself || m[j] == hi - 1) continue;
+      if ((uint32_t)j == hself || m[j] == hi - 2) continue;
       ntst(B::s64(Rw::MATCH + j), m[j]);
       nh &= ~(1ull << (H_MP_SHIFT + j));
     }

@@ -280,9 +280,9 @@ struct TickLane {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         // H_MS: the self slot's MATCH row is stale, its match is lastIndex;
-        // H_MP: another slot's is lastIndex - 1
+        // H_MP: another slot's is lastIndex - 2
         match[j] = (has_sync_bits(S) && h_ms(hdr) && (uint32_t)j == self)                ? hi
-                   : (has_sync_bits(S) && h_mp(hdr, (uint32_t)j) && (uint32_t)j != self) ? hi - 1
+                   : (has_sync_bits(S) && h_mp(hdr, (uint32_t)j) && (uint32_t)j != self) ? hi - 2
                                                                                          : s64(Rw::MATCH + j);
         rst[j] = rb_state(rb, j);
         ract[j] = rb_active(rb, j);

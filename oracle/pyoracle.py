@@ -63,6 +63,7 @@ def hostlane_lib():
         lib.hl_counters.restype = None
         lib.hl_tick_lanes.restype = c.c_uint64
         lib.hl_steady_lanes.restype = c.c_uint64
+        lib.hl_steady_leaders.restype = c.c_uint64
         lib.hl_detect_affine.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32, c.c_void_p,
                                          c.POINTER(c.c_uint32)]
         lib.hl_detect_affine.restype = c.c_int
@@ -214,6 +215,11 @@ def hostlane_tick_lanes():
 def hostlane_steady_lanes():
     """Lanes the emulated steady kernel (gr_steady.h closed forms) finished since load."""
     return int(hostlane_lib().hl_steady_lanes())
+
+
+def hostlane_steady_leaders():
+    """Leader lanes the emulated steady kernel's SteadyLeader finished since load."""
+    return int(hostlane_lib().hl_steady_leaders())
 
 
 def hostlane_affine_routes(in_pos, out_pos, slots):

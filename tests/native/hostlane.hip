@@ -39,7 +39,7 @@ using namespace gr::host;
 
 namespace {
 
-static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0, g_tick_lanes = 0, g_steady_lanes = 0;
+static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0, g_tick_lanes = 0, g_steady_lanes = 0, g_steady_leaders = 0;
 static uint32_t g_hint_salt = 0;  // varies the drawn wave hints from call to call
 static bool g_true_hints = false;  // hl_true_hints: every wave gets the device's hint (diagnostics)
 
@@ -98,7 +98,10 @@ void run_lanes(const StepParams& kp) {
       // a split pass's steady kernel (gr_kernels.h gr_steady_kernel): the closed
       // form only; a lane it does not finish goes to the general lane
       if constexpr (S == 3) {
-        if (steady_leader_hint(hint)) done = SteadyLeader<S, RM_ANY>(kp, i, p).step(&ls, hint, &sh);
+        if (steady_leader_hint(hint)) {
+          done = SteadyLeader<S, RM_ANY>(kp, i, p).step(&ls, hint, &sh);
+          g_steady_leaders += done;
+        }
       }
       if (steady_follower_hint(hint)) done = SteadyFollower<S, RM_ANY>(kp, i, p).step(&ls, hint, &sh);
       g_steady_lanes += done;
@@ -287,6 +290,7 @@ extern "C" uint64_t hl_tick_lanes() { return g_tick_lanes; }
 
 // lanes the split pass's steady kernel emulation finished (gr_steady.h)
 extern "C" uint64_t hl_steady_lanes() { return g_steady_lanes; }
+extern "C" uint64_t hl_steady_leaders() { return g_steady_leaders; }
 
 // gr_bind_routes' affine-route detection, for the CPU tests
 extern "C" int hl_detect_affine(const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n, uint32_t S,

@@ -170,3 +170,30 @@ def test_steady_leader_staggered_acks(built):
         assert hostlane_steady_lanes() >= s0
     finally:
         hl.hl_true_hints(0)
+
+
+def test_steady_leaders_stay_closed_form(built):
+    """BASELINE config 2/4 steady state with the device's hints: after the first
+    passes set the sync bits (H_NX, H_MS, H_MP: match = lastIndex - 2 in the
+    pipelined steady state), every leader pass is the closed form SteadyLeader
+    (gr_steady.h), with no MATCH row loaded, and parity holds every pass. Guards the
+    header bits' steady-state values: a wrong one keeps every test green but sends
+    the headline's leaders through FastLane."""
+    from oracle.pyoracle import hostlane_lib, hostlane_steady_leaders
+    G, R, passes, warm = 128, 3, 10, 4
+    hl = hostlane_lib()
+    hl.hl_true_hints(1)
+    try:
+        counts = []
+
+        def lf(k):
+            counts.append(hostlane_steady_leaders())
+            return P.propose_locals(R * G, np.arange(G), pass_index=k)
+        peers = P.make_groups(G, R, seed=11)
+        st = SIM.simulate(SIM.HostlaneBackend, peers, P.Topology(G, R), passes, lf)
+        counts.append(hostlane_steady_leaders())
+        assert st["escalations"] == 0
+        per_pass = np.diff(counts)[warm:]
+        assert np.all(per_pass == G), per_pass
+    finally:
+        hl.hl_true_hints(0)

@@ -26,3 +26,12 @@ import json
 d=json.loads(open('gpurun_out/exp_bench.json').read().strip().splitlines()[-1])
 print('bench', d['value'], d['ms_per_step'], d['roofline'])
 "
+GR_WAVE_CLOCK=gpurun_out/wc5.bin timeout -k 10 200 python -u tools/bench_configs.py --passes 6 --only 5 > gpurun_out/exp_wc5.json 2> gpurun_out/exp_wc5.err || { tail -5 gpurun_out/exp_wc5.err; exit 1; }
+python tools/wave_clock.py gpurun_out/wc5.bin
+GR_BIN_GENERAL=1 GR_WAVE_CLOCK=gpurun_out/wc5b.bin timeout -k 10 200 python -u tools/bench_configs.py --passes 6 --only 5 > gpurun_out/exp_wc5b.json 2> gpurun_out/exp_wc5b.err || { tail -5 gpurun_out/exp_wc5b.err; exit 1; }
+python tools/wave_clock.py gpurun_out/wc5b.bin
+python -c "
+import json
+for f in ('exp_wc5', 'exp_wc5b'):
+    d=json.loads(open('gpurun_out/%s.json' % f).read().strip().splitlines()[-1]); print(f, '%.1f us' % (d['device_ms_per_pass']*1e3), 'fast %.1f gen %.1f bailed %d' % (d['fast_ms']*1e3, d['general_ms']*1e3, d['bailed_lanes_per_pass']))
+"
