@@ -74,15 +74,16 @@ RESULT = np.dtype([
 ])
 # Compact boundary records (gr_step_compact)
 CM_REJECT, CM_ENTRY, CM_LOG_TERM, CM_COMMIT, CM_HINT, CM_EXT = 0x01, 0x02, 0x04, 0x08, 0x10, 0x80
+CM_ENTRY2, CM_PAIR = 0x20, 0x40  # a record standing for two messages (gpuraft.h GR_CM_PAIR)
 CL_CONFIG_CHANGE, CL_EXT = 0x01, 0x80
 CR_EXT = 0x80
 CMSG = np.dtype([("peer", u32), ("type", u8), ("slot", u8), ("flags", u8), ("pad", u8), ("term", u32),
                  ("aux", u32), ("log_index", u64)])
 CLOCAL = np.dtype([("peer", u32), ("propose_entries", u32), ("ticks", np.uint16), ("quiesced_ticks", u8),
                    ("flags", u8), ("ext", u32), ("rand", u64)])
-CRESULT = np.dtype([("peer", u32), ("escalation", u8), ("propose_result", u8), ("flags", u8), ("pad", u8),
-                    ("esc_item", u32), ("ext", u32), ("committed", u64), ("last_index", u64), ("save_from", u64)])
-assert CMSG.itemsize == 24 and CLOCAL.itemsize == 24 and CRESULT.itemsize == 40
+CRESULT = np.dtype([("peer", u32), ("escalation", u8), ("propose_result", u8), ("flags", u8), ("save_count", u8),
+                    ("aux", u32), ("commit_lag", u32), ("last_index", u64)])
+assert CMSG.itemsize == 24 and CLOCAL.itemsize == 24 and CRESULT.itemsize == 24
 UPDATE_COMMIT = np.dtype([("stable_log_to", u64), ("stable_log_term", u64), ("applied_to", u64)])
 SIZES = {"gr_peer": 664, "gr_message": 80, "gr_local_input": 48, "gr_peer_result": 168,
          "gr_remote": 32, "gr_read_status": 32}
@@ -164,7 +165,7 @@ EXPORTS = [
     "gr_space_side_bytes", "gr_space_side_pack", "gr_space_side_unpack", "gr_space_side_pack_host",
     "gr_space_side_unpack_host", "gr_bind_routes",
     "gr_set_locals", "gr_step_device", "gr_step_compact", "gr_step_compact_begin", "gr_step_compact_end", "gr_cinbox_reserve", "gr_release_coutbox",
-    "gr_pack_messages", "gr_unpack_messages", "gr_pack_locals",
+    "gr_pack_messages", "gr_unpack_messages", "gr_cmsg_count", "gr_pair_messages", "gr_pack_locals",
     "gr_collect_results", "gr_space_decode", "gr_space_encode", "gr_timing_begin", "gr_timing_end",
     "gr_bind_nodes", "gr_step_wire", "gr_step_wire_compact",
     "gr_graph_capture", "gr_graph_replay", "gr_graph_destroy",

@@ -1042,7 +1042,7 @@ static int pack_out_compact(gr_engine* e, uint32_t nl, const SpaceView& vout, gr
   uint64_t* off = (uint64_t*)e->d_off64.p;
   uint32_t* rx = (uint32_t*)e->d_rx.p;
   uint32_t* roff = (uint32_t*)e->d_roff.p;
-  hipLaunchKernelGGL(io::out_counts_c, dim3(io_grid(nl)), blk, 0, s, vout, e->ln, nl, S, oc, rx);
+  hipLaunchKernelGGL(io::out_counts_c, dim3(io_grid(nl)), blk, 0, s, vout, e->ln, e->st, nl, S, oc, rx);
   HIPCHK(hipGetLastError());
   if ((r = io_scan64(e, oc, off, nl, s))) return r;
   if ((r = io_scan(e, rx, roff, nl, s))) return r;
@@ -1298,10 +1298,33 @@ int gr_pack_messages(const gr_message* in, size_t n, gr_cmsg* out, gr_message* e
 
 int gr_unpack_messages(const gr_cmsg* in, size_t n, const gr_message* ext, size_t n_ext, gr_message* out) {
   if (n && (!in || !out)) return GR_EINVAL;
+  size_t o = 0;
   for (size_t k = 0; k < n; ++k) {
     if ((in[k].flags & GR_CM_EXT) && (!ext || in[k].aux >= n_ext)) return GR_EINVAL;
-    out[k] = host::expand_cmsg(in[k], ext);
+    for (uint32_t q = 0; q < host::cmsg_n(in[k]); ++q) out[o++] = host::expand_cmsg(in[k], ext, q);
   }
+  return GR_OK;
+}
+
+size_t gr_cmsg_count(const gr_cmsg* in, size_t n) {
+  size_t t = 0;
+  for (size_t k = 0; in && k < n; ++k) t += host::cmsg_n(in[k]);
+  return t;
+}
+
+int gr_pair_messages(gr_cmsg* c, size_t n, size_t* n_out) {
+  if ((n && !c) || !n_out) return GR_EINVAL;
+  size_t o = 0;
+  for (size_t k = 0; k < n;) {
+    gr_cmsg pr;
+    if (k + 1 < n && host::pair_of(c[k], c[k + 1], &pr)) {
+      c[o++] = pr;
+      k += 2;
+    } else {
+      c[o++] = c[k++];
+    }
+  }
+  *n_out = o;
   return GR_OK;
 }
 

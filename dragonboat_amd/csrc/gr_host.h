@@ -480,24 +480,47 @@ __host__ __device__ inline bool cmsg_of(const gr_message& m, gr_cmsg* c) {
   c->flags = fl;
   return true;
 }
-// The full record of a compact one (not GR_CM_EXT).
-__host__ __device__ inline gr_message msg_of(const gr_cmsg& c) {
+// Messages a compact record stands for: two for a GR_CM_PAIR record.
+__host__ __device__ inline uint32_t cmsg_n(const gr_cmsg& c) {
+  return (c.flags & (GR_CM_PAIR | GR_CM_EXT)) == GR_CM_PAIR ? 2u : 1u;
+}
+// Message k (0, or 1 of a pair) of a compact record (not GR_CM_EXT) in full.
+__host__ __device__ inline gr_message msg_of(const gr_cmsg& c, uint32_t k = 0) {
   gr_message m{};
   m.peer = c.peer;
   m.type = c.type;
   m.slot = c.slot;
   m.reject = (c.flags & GR_CM_REJECT) ? 1 : 0;
   m.term = c.term;
-  m.log_index = c.log_index;
+  // a pair's second accept acknowledges one index more; its second Replicate
+  // repeats LogIndex (gpuraft.h GR_CM_PAIR)
+  m.log_index = c.log_index + (k && c.type == GR_REPLICATE_RESP ? 1u : 0u);
   if (c.flags & GR_CM_LOG_TERM) m.log_term = m.term;
-  if (c.flags & GR_CM_COMMIT) m.commit = commit_of(c.aux, m.log_index);
-  if (c.flags & GR_CM_HINT) m.hint = commit_of(c.aux, m.log_index);
-  if (c.flags & GR_CM_ENTRY) {
+  if (c.flags & GR_CM_COMMIT) m.commit = commit_of(c.aux, c.log_index);
+  if (c.flags & GR_CM_HINT) m.hint = commit_of(c.aux, c.log_index);
+  if (c.flags & (k ? GR_CM_ENTRY2 : GR_CM_ENTRY)) {
     m.n_entries = 1;
     m.n_runs = 1;
     m.run_term[0] = m.term;
   }
   return m;
+}
+// The pair record of two consecutive compact records of one mailbox, or false
+// when GR_CM_PAIR cannot carry them (gpuraft.h).
+__host__ __device__ inline bool pair_of(const gr_cmsg& a, const gr_cmsg& b, gr_cmsg* out) {
+  if (((a.flags | b.flags) & (GR_CM_EXT | GR_CM_PAIR | GR_CM_ENTRY2)) || a.peer != b.peer || a.slot != b.slot ||
+      a.type != b.type || a.term != b.term || a.aux != b.aux)
+    return false;
+  if (a.type == GR_REPLICATE) {
+    if (b.log_index != a.log_index || (a.flags & ~GR_CM_ENTRY) != (b.flags & ~GR_CM_ENTRY)) return false;
+  } else if (a.type == GR_REPLICATE_RESP) {
+    if ((a.flags & GR_CM_REJECT) || a.flags != b.flags || b.log_index != a.log_index + 1) return false;
+  } else {
+    return false;
+  }
+  *out = a;
+  out->flags = (uint8_t)(a.flags | GR_CM_PAIR | ((b.flags & GR_CM_ENTRY) ? GR_CM_ENTRY2 : 0));
+  return true;
 }
 __host__ __device__ inline int validate_cmsg(const gr_cmsg& c, const gr_message* ext, uint32_t n_ext, uint32_t S,
                                              uint32_t cap) {
@@ -508,12 +531,15 @@ __host__ __device__ inline int validate_cmsg(const gr_cmsg& c, const gr_message*
     if (m.peer != c.peer || m.slot != c.slot || m.type != c.type) return GR_EINVAL;
     return validate_msg(m, S, cap);
   }
-  if (c.flags & 0x60) return GR_EINVAL;
+  if ((c.flags & GR_CM_ENTRY2) && !(c.flags & GR_CM_PAIR)) return GR_EINVAL;
+  if ((c.flags & GR_CM_PAIR) && !(c.type == GR_REPLICATE ||
+                                  (c.type == GR_REPLICATE_RESP && !(c.flags & (GR_CM_REJECT | GR_CM_ENTRY2)))))
+    return GR_EINVAL;
   if ((c.flags & GR_CM_COMMIT) && (c.flags & GR_CM_HINT)) return GR_EINVAL;
   return GR_OK;
 }
-__host__ __device__ inline gr_message expand_cmsg(const gr_cmsg& c, const gr_message* ext) {
-  return (c.flags & GR_CM_EXT) ? ext[c.aux] : msg_of(c);
+__host__ __device__ inline gr_message expand_cmsg(const gr_cmsg& c, const gr_message* ext, uint32_t k = 0) {
+  return (c.flags & GR_CM_EXT) ? ext[c.aux] : msg_of(c, k);
 }
 __host__ __device__ inline bool clocal_of(const gr_local_input& x, gr_clocal* c) {
   c->peer = x.peer;
@@ -546,16 +572,20 @@ __host__ __device__ inline bool validate_clocal(const gr_clocal& c, const gr_loc
 __host__ __device__ inline bool result_needs_ext(uint8_t rf) {
   return (rf & (RF_READY | RF_FORWARDED | RF_HARDSTATE)) != 0;
 }
-__host__ __device__ inline gr_cresult cresult_of(const gr_peer_result& r) {
-  gr_cresult c{};
-  c.peer = r.peer;
-  c.escalation = r.escalation;
-  c.propose_result = r.propose_result;
-  c.esc_item = r.esc_item;
-  c.committed = r.committed;
-  c.last_index = r.last_index;
-  c.save_from = r.save_from;
-  return c;
+// The compact result (gpuraft.h gr_cresult); false when it needs the full
+// record (an escalation, or an index range the relative fields cannot carry).
+__host__ __device__ inline bool cresult_of(const gr_peer_result& r, gr_cresult* c) {
+  *c = gr_cresult{};
+  c->peer = r.peer;
+  c->escalation = r.escalation;
+  c->propose_result = r.propose_result;
+  c->aux = r.esc_item;
+  c->last_index = r.last_index;
+  const uint64_t lag = r.last_index - r.committed, save = r.save_from ? r.last_index - r.save_from + 1 : 0;
+  c->commit_lag = (uint32_t)lag;
+  c->save_count = (uint8_t)save;
+  return !r.escalation && r.committed <= r.last_index && !(lag >> 32) && r.save_from <= r.last_index + 1 &&
+         save <= 0xFFu;
 }
 
 inline uint64_t space_total_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth = GR_C) {

@@ -256,18 +256,33 @@ __global__ void msg_keys_c(const gr_cmsg* msgs, uint32_t n, const uint32_t* lane
   }
 }
 
-// encode_sorted over compact records (expanded in registers).
+// encode_sorted over compact records (expanded in registers). A GR_CM_PAIR
+// record is two messages: a record's first message lands after the messages of
+// the mailbox's earlier records.
 __global__ void encode_sorted_c(CInbox in, const uint32_t* skeys, const uint32_t* sidx, SpaceView v) {
   const uint32_t n = in.n_msgs;
   for (uint32_t s = io_tid(); s < n; s += io_stride()) {
     const uint32_t key = skeys[s];
-    uint32_t r = 0;
-    while (r <= (uint32_t)GR_C && r < s && skeys[s - r - 1] == key) ++r;
+    uint32_t nrec = 0, r = 0;  // earlier records of the mailbox, their messages (counted up to overflow)
+    while (r <= (uint32_t)GR_C && nrec < s && skeys[s - nrec - 1] == key) {
+      r += host::cmsg_n(in.msgs[sidx[s - nrec - 1]]);
+      ++nrec;
+    }
     const Mailbox mb = v.at(key);
-    if (r < (uint32_t)GR_C) host::encode_msg(mb, r, host::expand_cmsg(in.msgs[sidx[s]], in.ext));
+    const gr_cmsg c = in.msgs[sidx[s]];
+    const uint32_t nm = host::cmsg_n(c);
+    for (uint32_t q = 0; q < nm; ++q)
+      if (r + q < (uint32_t)GR_C) host::encode_msg(mb, r + q, host::expand_cmsg(c, in.ext, q));
     if (s + 1 == n || skeys[s + 1] != key)
-      mb.cnt() = r < (uint32_t)GR_C ? host::count_byte(mb, r + 1, [&](uint32_t q) {
-        return host::expand_cmsg(in.msgs[sidx[s - r + q]], in.ext);
+      mb.cnt() = r + nm <= (uint32_t)GR_C ? host::count_byte(mb, r + nm, [&](uint32_t q) {
+        uint32_t x = s - nrec;  // the mailbox's first record
+        for (;;) {
+          const gr_cmsg& cx = in.msgs[sidx[x]];
+          const uint32_t k = host::cmsg_n(cx);
+          if (q < k) return host::expand_cmsg(cx, in.ext, q);
+          q -= k;
+          ++x;
+        }
       }) : (uint8_t)(GR_C + 1);
   }
 }
@@ -285,24 +300,51 @@ __global__ void fill_locals_c(CInbox in, const uint32_t* win, uint32_t nl, LaneB
   }
 }
 
-// Per lane: messages (high word) and those needing an ext record (low word) in
-// one u64, so one scan gives both output offsets; rx = 1 when the result needs
-// the full record.
-__global__ void out_counts_c(SpaceView out, LaneBase L, uint32_t nl, uint32_t S, uint64_t* oc, uint32_t* rx) {
-  for (uint32_t l = io_tid(); l < nl; l += io_stride()) {
-    uint32_t c = 0, e = 0;
-    for (uint32_t j = 0; j < S; ++j) {
-      const Mailbox mb = out.at(j * nl + l);
-      const uint32_t x = mb_n(mb.cnt());
-      const uint32_t cnt = x < (uint32_t)GR_C ? x : (uint32_t)GR_C;
-      c += cnt;
-      for (uint32_t k = 0; k < cnt; ++k) {
-        gr_cmsg cm;
-        if (!host::cmsg_of(host::decode_msg(mb, k), &cm)) ++e;
+// The compact records of one out mailbox, in order (a pair of messages that
+// GR_CM_PAIR carries is one record; a message that fits no compact form is an
+// ext record): rec(compact record, full message or nullptr).
+template <class Rec>
+__device__ inline void mailbox_records(const Mailbox& mb, uint32_t peer, uint32_t slot, Rec rec) {
+  const uint32_t x = mb_n(mb.cnt());
+  const uint32_t c = x < (uint32_t)GR_C ? x : (uint32_t)GR_C;
+  for (uint32_t k = 0; k < c;) {
+    gr_message m = host::decode_msg(mb, k);
+    m.peer = peer;
+    m.slot = (uint8_t)slot;
+    gr_cmsg cm;
+    const bool fits = host::cmsg_of(m, &cm);
+    if (fits && k + 1 < c) {
+      gr_message m2 = host::decode_msg(mb, k + 1);
+      m2.peer = peer;
+      m2.slot = (uint8_t)slot;
+      gr_cmsg c2, pr;
+      if (host::cmsg_of(m2, &c2) && host::pair_of(cm, c2, &pr)) {
+        rec(pr, (const gr_message*)nullptr);
+        k += 2;
+        continue;
       }
     }
+    rec(cm, fits ? (const gr_message*)nullptr : &m);
+    ++k;
+  }
+}
+
+// Per lane: records (high word) and those needing an ext record (low word) in
+// one u64, so one scan gives both output offsets; rx = 1 when the result needs
+// the full record.
+__global__ void out_counts_c(SpaceView out, LaneBase L, StateBase st, uint32_t nl, uint32_t S, uint64_t* oc,
+                             uint32_t* rx) {
+  for (uint32_t l = io_tid(); l < nl; l += io_stride()) {
+    uint32_t c = 0, e = 0;
+    for (uint32_t j = 0; j < S; ++j)
+      mailbox_records(out.at(j * nl + l), 0u, j, [&](const gr_cmsg&, const gr_message* full) {
+        ++c;
+        e += full ? 1u : 0u;
+      });
     oc[l] = ((uint64_t)c << 32) | e;
-    rx[l] = host::result_needs_ext(L.u8(LR_RFLAGS)[l]) ? 1u : 0u;
+    gr_cresult cr;
+    rx[l] = host::result_needs_ext(L.u8(LR_RFLAGS)[l]) || !host::cresult_of(host::make_result(L, st, l, 0), &cr)
+                ? 1u : 0u;
   }
 }
 
@@ -321,23 +363,15 @@ __global__ void pack_outbox_c(SpaceView out, uint32_t nl, uint32_t S, const uint
   for (uint32_t l = io_tid(); l < nl; l += io_stride()) {
     uint32_t o = (uint32_t)(off[l] >> 32), eo = (uint32_t)off[l];
     const uint32_t peer = peer_of_lane[l];
-    for (uint32_t j = 0; j < S; ++j) {
-      const Mailbox mb = out.at(j * nl + l);
-      const uint32_t x = mb_n(mb.cnt());
-      const uint32_t c = x < (uint32_t)GR_C ? x : (uint32_t)GR_C;
-      for (uint32_t k = 0; k < c; ++k) {
-        gr_message m = host::decode_msg(mb, k);
-        m.peer = peer;
-        m.slot = (uint8_t)j;
-        gr_cmsg cm;
-        if (!host::cmsg_of(m, &cm)) {
+    for (uint32_t j = 0; j < S; ++j)
+      mailbox_records(out.at(j * nl + l), peer, j, [&](gr_cmsg cm, const gr_message* full) {
+        if (full) {
           cm.flags = GR_CM_EXT;
           cm.aux = eo;
-          ext[eo++] = m;
+          ext[eo++] = *full;
         }
         rec[o++] = cm;
-      }
-    }
+      });
   }
 }
 
@@ -345,10 +379,11 @@ __global__ void pack_results_c(LaneBase L, StateBase st, const uint32_t* peer_of
                                const uint32_t* roff, gr_cresult* out, gr_peer_result* ext) {
   for (uint32_t l = io_tid(); l < nl; l += io_stride()) {
     const gr_peer_result pr = host::make_result(L, st, l, peer_of_lane[l]);
-    gr_cresult c = host::cresult_of(pr);
-    if (host::result_needs_ext(L.u8(LR_RFLAGS)[l])) {
+    gr_cresult c;
+    // the same test as out_counts_c's rx
+    if (!host::cresult_of(pr, &c) || host::result_needs_ext(L.u8(LR_RFLAGS)[l])) {
       c.flags = GR_CR_EXT;
-      c.ext = roff[l];
+      c.aux = roff[l];
       ext[roff[l]] = pr;
     }
     out[l] = c;

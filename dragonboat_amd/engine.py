@@ -56,6 +56,9 @@ def load_library(path=LIB_PATH):
     lib.gr_release_coutbox.argtypes = [c.c_void_p, c.POINTER(abi.COutbox)]
     lib.gr_pack_messages.argtypes = [c.c_void_p, c.c_size_t, c.c_void_p, c.c_void_p, c.POINTER(c.c_size_t)]
     lib.gr_unpack_messages.argtypes = [c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t, c.c_void_p]
+    lib.gr_cmsg_count.argtypes = [c.c_void_p, c.c_size_t]
+    lib.gr_cmsg_count.restype = c.c_size_t
+    lib.gr_pair_messages.argtypes = [c.c_void_p, c.c_size_t, c.POINTER(c.c_size_t)]
     lib.gr_pack_locals.argtypes = [c.c_void_p, c.c_size_t, c.c_void_p, c.c_void_p, c.POINTER(c.c_size_t)]
     lib.gr_commit_update.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p]
     lib.gr_step.argtypes = [c.c_void_p, c.POINTER(abi.Inbox), c.POINTER(abi.Outbox)]
@@ -272,10 +275,19 @@ class Engine:
                                          ctypes.byref(nx)), "gr_pack_messages")
         return c, ext[:nx.value].copy()
 
+    def pair_messages(self, c):
+        """gr_pair_messages: compact records with every pair GR_CM_PAIR carries merged."""
+        c = np.array(c, abi.CMSG)
+        n = ctypes.c_size_t()
+        _check(self.lib.gr_pair_messages(c.ctypes.data if len(c) else None, len(c), ctypes.byref(n)),
+               "gr_pair_messages")
+        return c[:n.value].copy()
+
     def unpack_messages(self, c, ext):
+        """gr_unpack_messages: compact (and ext) records -> full records (a pair record -> two)."""
         c = np.ascontiguousarray(c, abi.CMSG)
         ext = np.ascontiguousarray(ext, abi.MESSAGE)
-        out = np.zeros(len(c), abi.MESSAGE)
+        out = np.zeros(int(self.lib.gr_cmsg_count(c.ctypes.data if len(c) else None, len(c))), abi.MESSAGE)
         _check(self.lib.gr_unpack_messages(c.ctypes.data if len(c) else None, len(c),
                                            ext.ctypes.data if len(ext) else None, len(ext),
                                            out.ctypes.data if len(out) else None), "gr_unpack_messages")

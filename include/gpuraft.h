@@ -317,11 +317,12 @@ int gr_release_outbox(gr_engine* e, gr_outbox* out);
 
 /*
  * Compact records: the same pass as gr_step with the steady state's messages in
- * 24 bytes instead of 80 and results in 40 instead of 168, so a 1M-group pass
- * moves ~0.5 GB over PCIe instead of ~2 GB. A record that does not fit its
- * compact form points into an "ext" array of full records (GR_*_EXT); order is
- * always the compact array's. gr_pack_messages / gr_unpack_messages convert on
- * the host (what a cgo caller's packer does).
+ * 24 bytes instead of 80, two of them per record where they repeat each other
+ * (GR_CM_PAIR), and results in 24 bytes instead of 168, so a 1M-group pass moves
+ * ~0.29 GB over PCIe instead of ~2 GB. A record that does not fit its compact
+ * form points into an "ext" array of full records (GR_*_EXT); order is always
+ * the compact array's. gr_pack_messages / gr_pair_messages / gr_unpack_messages
+ * convert on the host (what a cgo caller's packer does).
  *
  * gr_cmsg: Term < 2^32; LogTerm, Commit, Hint and the entries follow from the
  * flags (fields not listed are 0): GR_CM_ENTRY = one entry at Term
@@ -336,6 +337,15 @@ int gr_release_outbox(gr_engine* e, gr_outbox* out);
 #define GR_CM_LOG_TERM 0x04
 #define GR_CM_COMMIT 0x08
 #define GR_CM_HINT 0x10
+/* GR_CM_PAIR: the record stands for two consecutive messages of one mailbox
+ * (same peer, slot, type and term), the steady state's usual pair: two
+ * Replicates with the same LogIndex, LogTerm and Commit (a commit broadcast and
+ * the proposal after it, makeReplicateMessage raft.go:474-498), the second
+ * carrying one entry at Term when GR_CM_ENTRY2 is set; or two ReplicateResp
+ * accepts, the second with LogIndex + 1 (their acks, raft.go:971-974). Replicate
+ * transport batches a target's messages the same way (MessageBatch). */
+#define GR_CM_ENTRY2 0x20
+#define GR_CM_PAIR 0x40
 #define GR_CM_EXT 0x80
 typedef struct gr_cmsg {
   uint32_t peer;       /* as gr_message.peer */
@@ -358,17 +368,22 @@ typedef struct gr_clocal {
   uint64_t rand;
 } gr_clocal;
 
-/* gr_cresult: a gr_peer_result without the per-pass extras. GR_CR_EXT: the lane
- * has ReadyToRead records, forwarded proposals or a changed term/vote, and
- * ext_results[ext] is its full record. propose_first (when propose_result is
- * GR_PROP_APPENDED) is last_index - propose_entries + 1. */
+/* gr_cresult: a gr_peer_result without the per-pass extras, indexes relative
+ * to last_index: committed = last_index - commit_lag; save_from = last_index -
+ * save_count + 1, or 0 (nothing to save) when save_count is 0. GR_CR_EXT: the
+ * lane has ReadyToRead records, forwarded proposals, a changed term/vote or an
+ * escalation, or an index that does not fit (commit_lag >= 2^32, more than 255
+ * entries to save), and ext_results[aux] is its full record; otherwise aux is
+ * esc_item (0). propose_first (when propose_result is GR_PROP_APPENDED) is
+ * last_index - propose_entries + 1. */
 #define GR_CR_EXT 0x80
 typedef struct gr_cresult {
   uint32_t peer;
-  uint8_t escalation, propose_result, flags, pad;
-  uint32_t esc_item;
-  uint32_t ext;
-  uint64_t committed, last_index, save_from; /* as gr_peer_result */
+  uint8_t escalation, propose_result, flags;
+  uint8_t save_count;
+  uint32_t aux;
+  uint32_t commit_lag;
+  uint64_t last_index;
 } gr_cresult;
 
 typedef struct gr_cinbox {
@@ -414,7 +429,13 @@ int gr_release_coutbox(gr_engine* e, gr_coutbox* out);
 /* Host-side conversions (no engine): full records -> compact records plus ext
  * records (*n_ext of them, ext must have room for n), and back. */
 int gr_pack_messages(const gr_message* in, size_t n, gr_cmsg* out, gr_message* ext, size_t* n_ext);
+/* gr_unpack_messages writes gr_cmsg_count(in, n) records (a GR_CM_PAIR record
+ * expands to two). gr_pair_messages merges, in place, each run of two
+ * consecutive records that GR_CM_PAIR can carry (records that are not EXT);
+ * *n_out = the records left. */
 int gr_unpack_messages(const gr_cmsg* in, size_t n, const gr_message* ext, size_t n_ext, gr_message* out);
+size_t gr_cmsg_count(const gr_cmsg* in, size_t n);
+int gr_pair_messages(gr_cmsg* c, size_t n, size_t* n_out);
 int gr_pack_locals(const gr_local_input* in, size_t n, gr_clocal* out, gr_local_input* ext, size_t* n_ext);
 int gr_stats_get(gr_engine* e, gr_stats* out);
 int gr_stats_reset(gr_engine* e);
@@ -545,7 +566,7 @@ int gr_step_wire(gr_engine* e, const struct grw_message* d_msgs, size_t n_msgs, 
                  size_t n_ents, const gr_local_input* locals, size_t n_locals, gr_outbox* out,
                  gr_wire_unrouted* unrouted);
 /* gr_step_wire with the outbox and results as compact records (gr_coutbox, as
- * gr_step_compact returns them: 24-B gr_cmsg / 40-B gr_cresult, full records as
+ * gr_step_compact returns them: 24-B gr_cmsg / 24-B gr_cresult, full records as
  * ext only where they do not fit); release with gr_release_coutbox. */
 int gr_step_wire_compact(gr_engine* e, const struct grw_message* d_msgs, size_t n_msgs,
                          const struct grw_entry* d_ents, size_t n_ents, const gr_local_input* locals,

@@ -92,12 +92,18 @@ class GpuCompactBackend(GpuBackend):
 
     def step(self, msgs, loc):
         cm, xm = self.eng.pack_messages(msgs)
+        cm = self.eng.pair_messages(cm)  # the device takes GR_CM_PAIR records as two messages
         cl, xl = self.eng.pack_locals(loc)
         om, ox, cr, rx = self.eng.step_compact(cm, xm, cl, xl, halves=self.halves)
         out = self.eng.unpack_messages(om, ox)
         res = np.zeros(len(cr), abi.RESULT)
-        for f in ("peer", "escalation", "propose_result", "esc_item", "committed", "last_index", "save_from"):
+        for f in ("peer", "escalation", "propose_result", "last_index"):
             res[f] = cr[f]
+        # gpuraft.h gr_cresult: indexes relative to last_index, aux = esc_item (not EXT)
+        res["esc_item"] = cr["aux"]
+        res["committed"] = cr["last_index"] - cr["commit_lag"]
+        sc = cr["save_count"].astype(np.uint64)
+        res["save_from"] = np.where(sc > 0, cr["last_index"] - sc + np.uint64(1), 0)
         st = self.eng.sync(self.n)
         p = cr["peer"].astype(np.int64)
         res["term"], res["vote"] = st["term"][p], st["vote"][p]
@@ -108,7 +114,7 @@ class GpuCompactBackend(GpuBackend):
         res["propose_first"] = np.where(app, cr["last_index"] - nprop[p] + np.uint64(1), 0)
         x = (cr["flags"] & abi.CR_EXT) != 0
         if x.any():
-            res[x] = rx[cr["ext"][x].astype(np.int64)]
+            res[x] = rx[cr["aux"][x].astype(np.int64)]
         return out, res
 
 

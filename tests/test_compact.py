@@ -1,10 +1,11 @@
 """The compact boundary (gr_step_compact, gpuraft.h gr_cmsg/gr_clocal/gr_cresult):
 the C-ABI path a Go step worker calls, with the steady state's messages in 24 B
-instead of 80 and results in 40 B instead of 168.
+instead of 80, two per record where a mailbox's pair repeats itself (GR_CM_PAIR),
+and results in 24 B instead of 168.
 
-CPU: gr_pack_messages / gr_unpack_messages / gr_pack_locals are exact inverses
-on every message shape the engine and the oracle produce (a record that does not
-fit its compact form travels in full as an ext record).
+CPU: gr_pack_messages / gr_pair_messages / gr_unpack_messages / gr_pack_locals
+are exact inverses on every message shape the engine and the oracle produce (a
+record that does not fit its compact form travels in full as an ext record).
 GPU: the compact path against the oracle after every pass (the Lockstep of
 tests/simulate.py with GpuCompactBackend): steady state, leader churn, ticks +
 ReadIndex (heartbeats with contexts, ReadyToRead: ext records both ways), BASELINE
@@ -33,7 +34,8 @@ def _pack(lib, msgs):
 
 
 def _unpack(lib, c, ext):
-    out = np.zeros(len(c), abi.MESSAGE)
+    lib.gr_cmsg_count.restype = ctypes.c_size_t
+    out = np.zeros(int(lib.gr_cmsg_count(c.ctypes.data, len(c))), abi.MESSAGE)
     assert lib.gr_unpack_messages(c.ctypes.data, len(c), ext.ctypes.data if len(ext) else None, len(ext),
                                   out.ctypes.data) == 0
     return out
@@ -90,6 +92,66 @@ def test_pack_round_trip(built):
     s["n_entries"][1], s["n_runs"][1], s["run_term"][1, 0] = 1, 1, 7
     c, ext = _pack(lib, s)
     assert len(ext) == 0 and _unpack(lib, c, ext).tobytes() == s.tobytes()
+
+
+def _pair(lib, c):
+    c = c.copy()
+    n = ctypes.c_size_t()
+    assert lib.gr_pair_messages(c.ctypes.data, len(c), ctypes.byref(n)) == 0
+    return c[:n.value].copy()
+
+
+def test_pair_round_trip(built):
+    """GR_CM_PAIR: the steady state's mailbox pairs (a commit broadcast and the
+    proposal after it at one LogIndex; two accepts at LogIndex, LogIndex + 1) merge
+    into one record each and unpack to the same messages in order; anything else
+    (other types, rejects, unequal fields, ext records, other mailboxes) stays
+    single."""
+    lib = _lib()
+    rng = np.random.default_rng(4)
+    n = 3000
+    base = np.zeros(n, abi.MESSAGE)
+    base["peer"] = rng.integers(0, 50, n)
+    base["slot"] = rng.integers(0, 3, n)
+    base["term"] = rng.integers(1, 4, n)
+    base["log_index"] = rng.integers(2**32, 2**32 + 4, n, dtype=np.uint64)
+    kind = rng.integers(0, 4, n)
+    m = []
+    for k in range(n):
+        a = base[k].copy()
+        if kind[k] == 0:  # Replicate pair: empty commit broadcast + one-entry proposal
+            a["type"], a["log_term"], a["commit"] = abi.REPLICATE, a["term"], a["log_index"] - np.uint64(1)
+            b = a.copy()
+            b["n_entries"], b["n_runs"], b["run_term"][0] = 1, 1, a["term"]
+            if rng.random() < 0.2:
+                b["commit"] += np.uint64(1)  # unequal Commit: no pair
+            m += [a, b]
+        elif kind[k] == 1:  # accept pair
+            a["type"] = abi.REPLICATE_RESP
+            b = a.copy()
+            b["log_index"] += np.uint64(1 if rng.random() < 0.8 else 2)
+            m += [a, b]
+        elif kind[k] == 2:  # reject + accept: no pair
+            a["type"], a["reject"], a["hint"] = abi.REPLICATE_RESP, 1, a["log_index"]
+            b = a.copy()
+            b["reject"], b["hint"], b["log_index"] = 0, 0, a["log_index"] + np.uint64(1)
+            m += [a, b]
+        else:  # a heartbeat and a wide-term Replicate (ext): single
+            a["type"], a["commit"] = abi.HEARTBEAT, a["log_index"]
+            b = base[k].copy()
+            b["type"], b["term"] = abi.REPLICATE, 2**32 + 1
+            m += [a, b]
+    msgs = np.array(m, abi.MESSAGE)
+    c, ext = _pack(lib, msgs)
+    cp = _pair(lib, c)
+    pairs = (cp["flags"] & abi.CM_PAIR) != 0
+    assert 0 < pairs.sum() < len(cp) < len(c)
+    assert len(c) - len(cp) == pairs.sum()
+    assert _unpack(lib, cp, ext).tobytes() == msgs.tobytes()
+    # only Replicates and accepts pair; ENTRY2 only on a pair
+    assert set(np.unique(cp["type"][pairs])) <= {abi.REPLICATE, abi.REPLICATE_RESP}
+    assert not np.any((cp["flags"] & abi.CM_ENTRY2 != 0) & ~pairs)
+    assert not np.any(pairs & ((cp["flags"] & (abi.CM_REJECT | abi.CM_EXT)) != 0))
 
 
 def test_pack_locals_round_trip(built):

@@ -6,7 +6,8 @@ reloads) happens outside the timed region; the reported time is the sum of the
 two kernels' HIP-event durations per pass (gr_timing), i.e. the device pass. A
 device fill queued ahead of each pass hides the CPU launch latency from the events.
 
-  config 2: 10k groups x 3, one 1-entry proposal per leader per pass
+  config 2: 10k groups x 3, one 1-entry proposal per leader per pass (replica
+            blocks padded to whole waves with idle groups: 10,048 lanes each)
   config 3: 100k groups x 5, 90% quiesced (QuiescedTick), 10% active: a Tick per
             replica and a ReadIndex on the leader per pass (all acks delivered:
             the device path has no drop filter)
@@ -118,7 +119,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--only", default="2,3,5")
     ap.add_argument("--graph-reps", type=int, default=200, help="config 2: replays of a 2-pass HIP graph (0: off)")
-    ap.add_argument("--groups2", type=int, default=10_000, help="config 2's group count (A/B of the layout)")
+    ap.add_argument("--groups2", type=int, default=10_000, help="config 2's group count")
+    ap.add_argument("--align", type=int, default=64, help="config 2: replica blocks padded to this many lanes")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -127,10 +129,18 @@ def main():
     res = []
     want = set(args.only.split(","))
     if "2" in want:
+        # replica blocks padded to whole waves (Gl = G rounded up to 64 lanes): the
+        # Gl - G padding groups get no input (idle groups, as a host has), so every
+        # wave holds lanes of one replica, i.e. one role, and keeps its steady hint;
+        # unpadded, the waves straddling the three block boundaries mix leaders and
+        # followers, lose the closed forms and set the pass time (A/B: --align 1)
         G, R = args.groups2, 3
-        peers = P.make_groups(G, R, seed=2)
-        res.append(run(f"2: {G} x 3, uniform proposals", peers, G, R, args.passes, args.warmup,
-                       lambda k, eng, n: P.propose_locals(n, np.arange(G), pass_index=k), graph_reps=args.graph_reps))
+        Gl = -(-G // args.align) * args.align
+        peers = P.make_groups(Gl, R, seed=2)
+        r = run(f"2: {G} x 3, uniform proposals", peers, Gl, R, args.passes, args.warmup,
+                lambda k, eng, n: P.propose_locals(n, np.arange(G), pass_index=k), graph_reps=args.graph_reps)
+        r["groups"], r["lane_groups"] = G, Gl
+        res.append(r)
     if "3" in want:
         G, R = 100_000, 5
         peers, active = P.config3(G, R)
