@@ -497,9 +497,15 @@ struct Lane {
   // routes, mailbox count bytes and local inputs, read once per pass in the
   // first load round (preload): the message and local-input loops then start
   // without a dependent load round per slot
+  // GR_LANE_PRELOAD=0 (A/B builds): routes and counts computed or loaded where
+  // they are used instead (fewer live registers across the message loop)
+#ifndef GR_LANE_PRELOAD
+#define GR_LANE_PRELOAD 1
+#endif
   uint32_t gin_[S], gout_[S], pcb_[S];
   uint32_t plf_ = 0, pnt_ = 0, pnq_ = 0, pnp_ = 0;
   GR_HD void preload() {
+    if (!GR_LANE_PRELOAD) return;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       gin_[j] = route_of(kp, 0, (uint32_t)j, i);
@@ -514,8 +520,8 @@ struct Lane {
       pnp_ = kp.ln.u32(LR_PROPOSE)[i];
     }
   }
-  GR_HD uint32_t out_gpos(uint32_t j) const { return sel(gout_, j); }
-  GR_HD uint32_t in_gpos(uint32_t j) const { return sel(gin_, j); }
+  GR_HD uint32_t out_gpos(uint32_t j) const { return GR_LANE_PRELOAD ? sel(gout_, j) : route_of(kp, 1, j, i); }
+  GR_HD uint32_t in_gpos(uint32_t j) const { return GR_LANE_PRELOAD ? sel(gin_, j) : route_of(kp, 0, j, i); }
   // raft.send (raft.go:457-461): From is implied by the mailbox; Term is
   // r.term unless the type is a request (finalizeMessageTerm :444-455).
   GR_HD int emit(uint32_t j, const OutMsg& m) {
@@ -1187,6 +1193,75 @@ struct Lane {
 
   // ---------------------------------------------------------------- messages
   GR_HD void read_msg(const Mailbox& mb, uint32_t cb, uint32_t k, InMsg& m) const {
+#ifndef GR_READ_RECORD
+#define GR_READ_RECORD 0
+#endif
+#if GR_READ_RECORD
+    // A/B: a full-record message's cold fields in one round with its hot ones:
+    // the 64-byte record as four 16-byte loads, decoded by type in registers
+    // (layout: gr_layout.h Mailbox), instead of the tag first and the fields
+    // the type names after it
+    if (!(cb & MB_UNIFORM)) {
+      const uint4* r = reinterpret_cast<const uint4*>(mb.rec(k));
+      const uint4 w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3];
+      const uint64_t li = mb.u64(k, MF_LOG_INDEX);
+      const uint32_t cd = mb.t32(k, MT_CDELTA);
+      m.type = (uint8_t)(w0.x & 0xFFu);
+      m.flags = (uint8_t)((w0.x >> 8) & 0xFFu);
+      m.term = w0.y;
+      m.n = 0; m.run2 = 0;
+      m.log_index = 0; m.log_term = 0; m.commit = 0; m.hint = 0; m.hint_high = 0; m.rt0 = 0; m.rt1 = 0;
+      const uint64_t commit = (uint64_t)w2.x | ((uint64_t)w2.y << 32), hint = (uint64_t)w2.z | ((uint64_t)w2.w << 32),
+                     hint_high = (uint64_t)w3.x | ((uint64_t)w3.y << 32);
+      switch (m.type) {
+        case GR_REPLICATE:
+          m.log_index = li;
+          if (m.flags & MFL_COMPACT) {
+            m.n = (m.flags & MFL_N1) ? 1u : 0u;
+            m.log_term = m.term;
+            m.commit = commit_of(cd, li);
+            m.rt0 = m.n ? m.term : 0;
+            break;
+          }
+          m.n = w0.z;
+          m.log_term = w1.x;
+          m.commit = (m.flags & MFL_WIDE_COMMIT) ? commit : commit_of(cd, li);
+          if (m.n) {
+            m.rt0 = w1.y;
+            if (((m.flags >> MFL_RUNS_SHIFT) & 3u) == 2) {
+              m.run2 = w0.w;
+              m.rt1 = w1.z;
+            }
+          }
+          break;
+        case GR_REPLICATE_RESP:
+          m.log_index = li;
+          if (m.flags & MFL_REJECT) m.hint = hint;
+          break;
+        case GR_HEARTBEAT:
+          m.commit = commit;
+          m.hint = hint;
+          m.hint_high = hint_high;
+          break;
+        case GR_HEARTBEAT_RESP:
+          m.hint = hint;
+          m.hint_high = hint_high;
+          break;
+        default:
+          m.n = w0.z;
+          m.run2 = w0.w;
+          m.log_index = li;
+          m.log_term = w1.x;
+          m.commit = commit;
+          m.hint = hint;
+          m.hint_high = hint_high;
+          m.rt0 = w1.y;
+          m.rt1 = w1.z;
+          break;
+      }
+      return;
+    }
+#endif
     const uint32_t tg = mb.tag_at(k, cb);  // cb: the count byte (MB_UNIFORM: tag and term implied)
     m.type = (uint8_t)tg;
     m.flags = (uint8_t)(tg >> 8);
@@ -1491,7 +1566,7 @@ struct Lane {
       const uint32_t g = in_gpos(j);
       if (g == NOPOS) continue;
       const Mailbox mb = kp.in.at(g);
-      const uint32_t cb = sel(pcb_, j), c = mb_n(cb);
+      const uint32_t cb = GR_LANE_PRELOAD ? sel(pcb_, j) : (uint32_t)mb.cnt(), c = mb_n(cb);
 #pragma unroll 1
       for (uint32_t k = 0; k < c; ++k) {
         if (item == limit) { *at = item; return 0; }
@@ -1508,7 +1583,10 @@ struct Lane {
       }
     }
     if (kp.has_locals) {
-      const uint32_t lf = plf_, nt = pnt_, nq = pnq_, np = pnp_;
+      const uint32_t lf = GR_LANE_PRELOAD ? plf_ : kp.ln.u8(LR_LFLAGS)[i];
+      const uint32_t nt = GR_LANE_PRELOAD ? pnt_ : kp.ln.u32(LR_TICKS)[i];
+      const uint32_t nq = GR_LANE_PRELOAD ? pnq_ : kp.ln.u32(LR_QTICKS)[i];
+      const uint32_t np = GR_LANE_PRELOAD ? pnp_ : kp.ln.u32(LR_PROPOSE)[i];
       if (lf & LF_READ_INDEX) {
         if (item == limit) { *at = item; return 0; }
         need(G_CORE);
