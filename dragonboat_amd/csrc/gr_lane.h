@@ -498,7 +498,9 @@ struct Lane {
   // first load round (preload): the message and local-input loops then start
   // without a dependent load round per slot
   // GR_LANE_PRELOAD=0 (A/B builds): routes and counts computed or loaded where
-  // they are used instead (fewer live registers across the message loop)
+  // they are used instead (fewer live registers across the message loop: 72 B
+  // of scratch instead of 128, but config 5's general kernel measured 178 vs
+  // 173 us per pass, the setup round saved and more dependent rounds in the loop)
 #ifndef GR_LANE_PRELOAD
 #define GR_LANE_PRELOAD 1
 #endif
@@ -1194,13 +1196,14 @@ struct Lane {
   // ---------------------------------------------------------------- messages
   GR_HD void read_msg(const Mailbox& mb, uint32_t cb, uint32_t k, InMsg& m) const {
 #ifndef GR_READ_RECORD
-#define GR_READ_RECORD 0
+#define GR_READ_RECORD 1
 #endif
 #if GR_READ_RECORD
-    // A/B: a full-record message's cold fields in one round with its hot ones:
-    // the 64-byte record as four 16-byte loads, decoded by type in registers
-    // (layout: gr_layout.h Mailbox), instead of the tag first and the fields
-    // the type names after it
+    // A full-record message's cold fields in one round with its hot ones: the
+    // 64-byte record as four 16-byte loads, decoded by type in registers (layout:
+    // gr_layout.h Mailbox), instead of the tag first and the fields the type
+    // names after it (config 5 A/B: general kernel 167.6 vs 173.1 us per pass;
+    // GR_READ_RECORD=0 builds the two-round form)
     if (!(cb & MB_UNIFORM)) {
       const uint4* r = reinterpret_cast<const uint4*>(mb.rec(k));
       const uint4 w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3];
