@@ -15,14 +15,16 @@ import devsim
 pytestmark = pytest.mark.gpu
 
 
-def test_device_config2_full_size(gpu):
+@pytest.mark.parametrize("Gl", [10_000, 10_048])
+def test_device_config2_full_size(gpu, Gl):
     """BASELINE config 2: 10k x 3, one proposal per leader per pass (a small pass:
-    the fused gr_small_kernel)."""
+    the fused gr_small_kernel). Gl = 10,048: the layout tools/bench_configs.py times,
+    replica blocks padded to whole waves with 48 idle groups (no input)."""
     G, R = 10_000, 3
-    ls = devsim.DeviceLockstep(P.make_groups(G, R, seed=2), G, R)
+    ls = devsim.DeviceLockstep(P.make_groups(Gl, R, seed=2), Gl, R)
     try:
         for k in range(8):
-            ls.step(P.propose_locals(R * G, np.arange(G), pass_index=k))
+            ls.step(P.propose_locals(R * Gl, np.arange(G), pass_index=k))
         assert ls.stats["escalations"] == 0 and ls.stats["commits"] >= 5 * 3 * G
     finally:
         ls.close()
