@@ -89,6 +89,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--launch", choices=["stream", "graph"], default="stream",
+                    help="timed passes launched kernel by kernel, or replayed from the library's two-pass HIP "
+                         "graph (gr_graph_capture / gr_graph_replay; local placement, even --steps)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--groups", type=int, default=1_000_000, help="groups per GPU")
     ap.add_argument("--replicas", type=int, default=3)
@@ -483,6 +486,14 @@ def main():
 
     for k in range(args.warmup):
         pipe.step(k)
+    k0 = args.warmup
+    use_graph = args.launch == "graph" and pipe.graph_ready() and args.steps % 2 == 0
+    if use_graph:  # untimed: align to the captured pair (it starts in space 0), capture, one warm replay
+        if k0 % 2:
+            pipe.step(k0)
+            k0 += 1
+        pipe.graph_steps(k0, 2)
+        k0 += 2
     pipe.synchronize()
     if world > 1:
         dist.barrier()
@@ -491,8 +502,11 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        pipe.step(args.warmup + k)
+    if use_graph:
+        pipe.graph_steps(k0, args.steps)
+    else:
+        for k in range(args.steps):
+            pipe.step(k0 + k)
     pipe.synchronize()
     if world > 1:
         dist.barrier()
@@ -508,7 +522,7 @@ def main():
     # on the bank's stream), so the events add nothing to `value`.
     pipe.timing_begin()
     for k in range(args.steps):
-        pipe.step(args.warmup + args.steps + k)
+        pipe.step(k0 + args.steps + k)
     pipe.synchronize()
     tm = pipe.timing_end()
     xbytes = pipe.exchange_bytes_per_pass()
@@ -567,6 +581,7 @@ def main():
                        "parallelism": f"clusterID shards x{world}" + (", replicas on distinct GPUs, RCCL "
                                                                     "all_to_all per pass" if placement == "spread"
                                                                     else "")},
+            "launch": "graph (gr_graph_replay of a captured two-pass graph)" if use_graph else "stream (kernel launches)",
             "escalations": esc,
             "exchange_bytes_per_pass": xbytes,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -170,8 +170,8 @@ __device__ inline __attribute__((always_inline)) uint32_t general_bin(const Step
   return st * 8 + (higher ? 4u : 0u) + (lower ? 2u : 0u) + (full ? 1u : 0u);
 }
 
-// Hand lane i (peer p) to the general kernel: one append per class present in
-// the wave (bin_general), else by role and workgroup (lead: a leader lane).
+// Hand lane i (peer p) to the general kernel: appended to its class's list
+// (bin_general), else by role and workgroup (lead: a leader lane).
 template <int S>
 __device__ inline __attribute__((always_inline)) void general_append(const StepParams& kp, bool mine, bool lead, uint32_t i,
                                                                      uint32_t p, uint32_t bid, uint32_t* bail_list,
@@ -184,12 +184,23 @@ __device__ inline __attribute__((always_inline)) void general_append(const StepP
   } else {
     key = (lead ? kGeneralLists / 2 : 0u) + bid % (kGeneralLists / 2);
   }
-  while (bm) {  // wave-uniform
-    const uint32_t k = (uint32_t)__shfl((int)key, __ffsll((unsigned long long)bm) - 1);
-    const bool mm = mine && key == k;
-    bail_append(mm, k, bail_list, counters, list_cap, i);
-    bm &= ~__ballot(mm);
+  // each lane's class-mates (one ballot per class present: register work only),
+  // then one returning atomic per class issued by all classes' first lanes in
+  // the same instruction, so a wave with several classes waits for one round
+  // trip, not one per class
+  uint64_t same = 0;
+  for (uint64_t rest = bm; rest;) {  // wave-uniform
+    const uint32_t k = (uint32_t)__shfl((int)key, __ffsll((unsigned long long)rest) - 1);
+    const uint64_t m = __ballot(mine && key == k);
+    if (mine && key == k) same = m;
+    rest &= ~m;
   }
+  const uint32_t lane = threadIdx.x & 63;
+  const int first = mine ? __ffsll((unsigned long long)same) - 1 : (int)lane;
+  uint32_t base = 0;
+  if (mine && (uint32_t)first == lane) base = atomicAdd(counters + key * kCounterStride, (uint32_t)__popcll(same));
+  base = (uint32_t)__shfl((int)base, first);
+  if (mine) bail_list[(uint64_t)key * list_cap + base + (uint32_t)__popcll(same & ((1ull << lane) - 1))] = i;
 }
 
 #ifndef GR_FAST_MIN_WAVES

@@ -300,6 +300,25 @@ class Pipeline:
                 if not ex.pingpong:
                     self.work[b] = ex.exchange(eng, self.spaces[b], s.cuda_stream)
 
+    def graph_ready(self):
+        """Graph mode applies: every bank's spaces ping-pong (no exchange step)."""
+        return all(ex.pingpong for ex in self.ex)
+
+    def graph_steps(self, k0, K):
+        """Passes k0 .. k0 + K - 1 (k0 and K even) as replays of each bank's
+        two-pass HIP graph (gr_graph_capture over the ping-pong spaces, captured on
+        first use): the launch model of SURVEY.md §7(d), no CPU launch per kernel.
+        The bound locals are the same every pass, so a replay does a pass's work."""
+        assert k0 % 2 == 0 and K % 2 == 0 and self.graph_ready()
+        if not getattr(self, "graphs", None):
+            self.graphs = []
+            for ex, eng, sp in zip(self.ex, self.engines, self.spaces):
+                self.graphs.append(eng.graph_capture(sp[0].data_ptr(), sp[1].data_ptr(), ex.n_chunks, ex.positions,
+                                                     ex.n_peers, n_passes=2, depth=ex.depth))
+        for _ in range(K // 2):
+            for b, (eng, g) in enumerate(zip(self.engines, self.graphs)):
+                eng.graph_replay(g, self.streams[b].cuda_stream)
+
     def exchange_bytes_per_pass(self):
         """Bytes this rank sends to other ranks per pass (hot regions + side
         buffers of the chunks for other ranks; 0 for local placement)."""
@@ -342,6 +361,9 @@ class Pipeline:
         return tot
 
     def close(self):
+        for eng, g in zip(self.engines, getattr(self, "graphs", None) or []):
+            eng.graph_destroy(g)
+        self.graphs = []
         for eng in self.engines:
             eng.close()
         self.engines = []
