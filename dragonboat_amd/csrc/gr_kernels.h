@@ -711,6 +711,16 @@ constexpr uint32_t kTickBlocks = 1024;
 // the chip at their occupancy; with no listed wave each wave reads its flags
 // (one 64-byte load per 64 waves) and leaves.
 constexpr uint32_t kRoleBlocks = 1024;
+// GR_ROLE_BLOCKS overrides it (A/B runs: an empty launch of the role instances
+// costs about its waves' dispatch, ~4 us at 1024 workgroups)
+inline uint32_t role_blocks() {
+  static const uint32_t v = [] {
+    const char* e = getenv("GR_ROLE_BLOCKS");
+    const long x = e ? strtol(e, nullptr, 10) : 0;
+    return x > 0 ? (uint32_t)x : kRoleBlocks;
+  }();
+  return v;
+}
 // GR_ROLES_MERGED=1: both role instances in one launch (gr_roles_kernel; A/B runs)
 inline bool roles_merged() {
   static const bool v = [] {
@@ -732,7 +742,7 @@ hipError_t launch_fast(const StepParams& kp0, uint32_t blocks, uint32_t* bail_li
       hipLaunchKernelGGL((gr_steady_kernel<S, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
       const hipError_t e0 = hipGetLastError();
       if (e0 != hipSuccess) return e0;
-      const uint32_t rb = blocks < kRoleBlocks ? blocks : kRoleBlocks;
+      const uint32_t rb = blocks < role_blocks() ? blocks : role_blocks();
       if (roles_merged()) {
         hipLaunchKernelGGL((gr_roles_kernel<S, RM>), dim3(2 * rb), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
         return hipGetLastError();
