@@ -586,7 +586,7 @@ def main():
             "exchange_bytes_per_pass": xbytes,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": f"lean kernels of one pass (gr_steady_kernel<{S}> + gr_fast_kernel<{S}, role>)",
+                         "kernel": f"lean kernels of one pass (gr_steady_kernel<{S}> + gr_roles_kernel<{S}>, the role instances in one launch)",
                          "kernel_ms": kavg,
                          "algorithmic_bytes_per_launch": alg,
                          "algorithmic_unit": (f"group-round at this engine's encoding, {ENCODED_ROUND_BYTES[R]} B "

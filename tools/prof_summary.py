@@ -28,10 +28,12 @@ def counters(d, kernel_sub):
 
 
 # The lean kernels of one headline pass (gr_kernels.h, a split pass over
-# loopback routes, RM = 3): the steady kernel, then the role instances <S, 2>
-# (followers) and <S, 1> (leaders) over its wave lists. A device pass's
-# lean-kernel bytes are the sum over the kernels it ran.
-ROLE_INSTANCES = ("gr_steady_kernel<3, 3>", "gr_fast_kernel<3, 2, 3, true>", "gr_fast_kernel<3, 1, 3, true>")
+# loopback routes, RM = 3): the steady kernel, then the role instances over its
+# wave lists, in one launch (gr_roles_kernel, round 4) or as <S, 2> (followers)
+# and <S, 1> (leaders) with GR_ROLES_MERGED=0. A device pass's lean-kernel bytes
+# are the sum over the kernels it ran.
+ROLE_INSTANCES_MERGED = ("gr_steady_kernel<3, 3>", "gr_roles_kernel<3, 3>")
+ROLE_INSTANCES_SPLIT = ("gr_steady_kernel<3, 3>", "gr_fast_kernel<3, 2, 3, true>", "gr_fast_kernel<3, 1, 3, true>")
 
 
 def main(o):
@@ -67,6 +69,8 @@ def main(o):
             sq = counters(os.path.join(o, sub), kname)
             k.setdefault("sq", {}).update({c: sum(v[3:] or v) / len(v[3:] or v) for c, v in sq.items() if v})
         s["kernels"][kname] = k
+    merged = bool(counters(os.path.join(o, "fetch"), "gr_roles_kernel<3, 3>").get("FETCH_SIZE"))
+    ROLE_INSTANCES = ROLE_INSTANCES_MERGED if merged else ROLE_INSTANCES_SPLIT
     for kname in ROLE_INSTANCES:  # per instance, for the per-pass sum below
         f = counters(os.path.join(o, "fetch"), kname).get("FETCH_SIZE", [])
         w = counters(os.path.join(o, "write"), kname).get("WRITE_SIZE", [])
@@ -90,7 +94,7 @@ def main(o):
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         from dragonboat_amd.build import source_digest
         with open(os.path.join(o, "pmc_latest.json"), "w") as fh:
-            json.dump({"kernel": "gr_steady_kernel<3, 3> + gr_fast_kernel<3, {2,1}, 3, true> (the lean kernels of one pass)", "groups": groups, "replicas": 3,
+            json.dump({"kernel": " + ".join(ROLE_INSTANCES) + " (the lean kernels of one pass)", "groups": groups, "replicas": 3,
                        "source_digest": source_digest(),
                        "hbm_bytes_per_launch": fk["hbm_bytes_per_launch"],
                        "read_bytes": fk["read_bytes"], "write_bytes": fk["write_bytes"],
