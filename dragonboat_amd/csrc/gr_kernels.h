@@ -209,9 +209,10 @@ __device__ inline __attribute__((always_inline)) void general_append(const StepP
 #ifndef GR_LISTED_MIN_WAVES
 #define GR_LISTED_MIN_WAVES 1  // the role instances over listed waves (A/B builds: 4 and 5 spill)
 #endif
-// Role instances. A large pass (StepParams::split) runs R = FL_FOLLOWER then R =
-// FL_LEADER, each with the other role's code and registers compiled out (66 and
-// 92 VGPRs at S = 3: 7 and 5 waves per SIMD): a wave whose hint (as the pass
+// Role instances. A large pass (StepParams::split) runs R = FL_FOLLOWER and R =
+// FL_LEADER (side by side in one gr_roles_kernel launch by default, in sequence
+// with GR_ROLES_MERGED=0), each with the other role's code and registers compiled
+// out: a wave whose hint (as the pass
 // started) names a role goes to that instance, and an unhinted wave to both, each
 // stepping the lanes of its role and leaving the others untouched (FastLane
 // `take`). A small pass runs the single instance R = FL_ANY, which picks the
