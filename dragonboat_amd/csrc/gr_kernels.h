@@ -93,6 +93,12 @@ constexpr uint32_t WF_LISTED = 0x80;     // wave flag: the role instances step t
 // zero and the retry lists empty the role instances return at once. Cleared for
 // the next pass with the counters.
 constexpr uint32_t kListedWord = 1;
+// Word 2: the general kernel's next 64-lane chunk past the grid's first (each
+// wave's first chunk is its own index; a wave that finishes takes the next one
+// with one returning atomic, so a pass with more lanes than the grid's waves
+// holds puts the extra chunks on the waves that finish first). Cleared with the
+// next pass's counters.
+constexpr uint32_t kGeneralNext = 2;
 __host__ __device__ inline uint64_t wave_flag_words(uint32_t cap) { return ((uint64_t)cap / 64 + 64) / 4 * 2; }
 // Lanes one tick list can receive: the lanes of every kTickLists-th block, from
 // the steady kernel and the listed role waves (keyed by lane), plus as many
@@ -558,7 +564,7 @@ __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(Step
 #endif
 template <int S>
 __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(StepParams kp, const uint32_t* bail_list,
-                                                         const uint32_t* counters, uint32_t* next_counters,
+                                                         uint32_t* counters, uint32_t* next_counters,
                                                          uint32_t list_cap) {
   uint32_t start[kGeneralLists + 1];
   start[0] = 0;
@@ -567,12 +573,21 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
   const uint32_t n = start[kGeneralLists];
   if (blockIdx.x == 0 && threadIdx.x < kCounters) next_counters[threadIdx.x * kCounterStride] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters) next_counters[kListedWord] = 0;
-  if (blockIdx.x * kBlock >= n) return;  // uniform per block: nothing to do, no stats row touched
+  if (blockIdx.x == 0 && threadIdx.x == kCounters + 1) next_counters[kGeneralNext] = 0;
+  // 64-lane chunks of the concatenated lists: each wave's first chunk is its
+  // index in the grid, later ones come from the kGeneralNext counter (waves, not
+  // the grid, stride: a wave that finishes early takes the next chunk). The lists
+  // run leader classes first, so the chunks handed out late are followers' (the
+  // lighter classes: GR_WAVE_CLOCK).
+  const uint32_t lane = threadIdx.x & 63, W = gridDim.x * (kBlock / 64);
+  uint32_t chunk = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);  // wave-uniform
+  if (chunk * 64 >= n) return;  // nothing for this wave, no stats row touched
   const uint64_t t0 = kp.wclock ? wall_clock64() : 0;
   LaneStats acc;
   uint64_t tph[3] = {0, 0, 0};  // GR_WAVE_CLOCK: the first round's phase marks
-  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-    const uint32_t x = base + threadIdx.x;
+  uint32_t l0 = ~0u;            // ... and the list (handler class) of the lane's first round
+  while (chunk * 64 < n) {  // wave-uniform
+    const uint32_t x = chunk * 64 + lane;
     uint32_t i = 0;
     if (x < n) {
       uint32_t l = 0;
@@ -582,6 +597,7 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
 #pragma unroll
       for (uint32_t k = 0; k < kGeneralLists; ++k) off = (k == l) ? x - start[k] : off;
       i = bail_list[(uint64_t)l * list_cap + off];
+      l0 = l0 == ~0u ? l : l0;
     }
     if (x < n) {
       const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
@@ -604,6 +620,10 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
       acc.entries += ls.entries;
       acc.bailed += 1;
     }
+    if ((uint64_t)W * 64 >= n) break;  // the first chunks covered every lane: no atomic
+    uint32_t c = 0;
+    if (lane == 0) c = W + atomicAdd(counters + kGeneralNext, 1u);
+    chunk = (uint32_t)__shfl((int)c, 0);
   }
   if (kp.wclock) {  // profiling: this wave's span and what it stepped
     const uint64_t t1 = wall_clock64();
@@ -616,9 +636,12 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
       r[1] = t1;
       r[2] = nl;
       r[3] = nm;
-      r[4] = ne;
+      r[4] = ne;  // the list of the wave's first lane goes in the high word (below)
       r[5] = nli;
     }
+    const uint64_t wl = __ballot(l0 != ~0u);
+    const uint32_t cls = wl ? (uint32_t)__shfl((int)l0, __ffsll((unsigned long long)wl) - 1) : 0u;
+    if ((threadIdx.x & 63) == 0) kp.wclock[(uint64_t)w * kWaveClockWords + 4] = (uint64_t)ne | ((uint64_t)cls << 32);
     // the phase marks of the wave's first round (any active lane's: the wave runs them together)
     const uint64_t any = __ballot(tph[0] != 0);
     if (any) {
@@ -664,6 +687,7 @@ __global__ __launch_bounds__(kBlock, 1) void gr_small_kernel(StepParams kp, uint
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
   if (blockIdx.x == 0 && threadIdx.x < kCounters) next_counters[threadIdx.x * kCounterStride] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters) next_counters[kListedWord] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == kCounters + 1) next_counters[kGeneralNext] = 0;
   const uint32_t hw = kp.hints ? sload_u32(kp.hints + (uint64_t)blockIdx.x * (kBlock / 64)) : 0u;
   const uint32_t hint = (hw >> (8 * (wave & 3))) & 0xFFu;
   const int wk = wave_kernel(hint, S);
@@ -809,8 +833,8 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   if (kp.wclock &&
       (err = hipMemsetAsync(kp.wclock, 0, (size_t)gblocks * (kBlock / 64) * kWaveClockWords * 8, s)) != hipSuccess)
     return err;
-  hipLaunchKernelGGL(gr_step_kernel<S>, dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list,
-                     (const uint32_t*)cur, nxt, list_cap);
+  hipLaunchKernelGGL(gr_step_kernel<S>, dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list, cur, nxt,
+                     list_cap);
   if ((err = hipGetLastError()) != hipSuccess) return err;
   if (t && (err = hipEventRecord(t->ev[2], s)) != hipSuccess) return err;
   return hipSuccess;

@@ -26,7 +26,9 @@ def main(path):
     start = (t0 - base) * TICK_NS / 1e3
     dur = (t1 - t0) * TICK_NS / 1e3
     end = (t1 - base) * TICK_NS / 1e3
-    lanes, msgs, esc, lmsg = (r[:, k].astype(np.int64) for k in (2, 3, 4, 5))
+    lanes, msgs, lmsg = (r[:, k].astype(np.int64) for k in (2, 3, 5))
+    esc = (r[:, 4] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    cls = (r[:, 4] >> np.uint64(32)).astype(np.int64)  # the general list of the wave's first lane
     print(f"waves {len(r)}  lanes {lanes.sum()}  msgs {msgs.sum()}  escalated {esc.sum()}")
     print(f"kernel span {end.max():.1f} us; wave start p0/p50/p100 {start.min():.1f}/{np.median(start):.1f}/"
           f"{start.max():.1f} us")
@@ -51,6 +53,15 @@ def main(path):
                         ("after store (single-round waves)", rest[one])):
             if len(v):
                 print(f"phase {name:34s} p50 {np.median(v):7.1f}  p90 {np.percentile(v, 90):7.1f} us")
+    # by handler class (gr_kernels.h general_bin: list = class x 2 + parity; class =
+    # non-leader x 8 + higher-term x 4 + lower-term x 2 + full-record mailbox)
+    print("by class of the wave's first lane: class waves p50_us p90_us msgs/lane")
+    for c in sorted(set((cls // 2).tolist())):
+        m = (cls // 2) == c
+        names = ("leader" if c < 8 else "other") + (" higher" if c & 4 else "") + (" lower" if c & 2 else "") + \
+            (" full" if c & 1 else "")
+        print(f"  {c:2d} {names:28s} {m.sum():5d} {np.median(dur[m]):7.1f} {np.percentile(dur[m], 90):7.1f} "
+              f"{msgs[m].sum() / max(lanes[m].sum(), 1):5.2f}")
     hist, edges = np.histogram(dur, bins=12)
     for h, a, b in zip(hist, edges[:-1], edges[1:]):
         print(f"  {a:7.1f}-{b:7.1f} us {h:5d} " + "#" * int(60 * h / max(hist.max(), 1)))
