@@ -1,0 +1,18 @@
+# Non-leader general lanes load remote rows lazily: config 5 A/B against the
+# previous build (ab/libgpuraft_prev.so), interleaved, then the full -m gpu suite +
+# smoke and the bench line on this build.
+set -u
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/ab
+for i in 1 2; do
+  for v in prev new; do
+    if [ $v = prev ]; then export GPURAFT_LIB=$GRAFT_REPO_ROOT/dragonboat_amd/_build/ab/libgpuraft_prev.so; else unset GPURAFT_LIB; fi
+    timeout -k 10 300 python -u tools/bench_configs.py --passes 10 --only 5 > gpurun_out/ab/r_$v$i.json 2> gpurun_out/ab/r_$v$i.err || { tail -5 gpurun_out/ab/r_$v$i.err; exit 1; }
+    python -c "
+import json
+d=json.loads(open('gpurun_out/ab/r_$v$i.json').read().strip().splitlines()[-1]); print('$v$i', '%.1f us' % (d['device_ms_per_pass']*1e3), 'fast %.1f gen %.1f' % (d['fast_ms']*1e3, d['general_ms']*1e3))
+"
+  done
+done
+unset GPURAFT_LIB
+PROFILE=0 bash tools/gpu_round.sh
