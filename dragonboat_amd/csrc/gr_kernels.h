@@ -589,7 +589,6 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
   while (chunk * 64 < n) {  // wave-uniform
     const uint32_t x = chunk * 64 + lane;
     uint32_t i = 0;
-    bool lead = true;
     if (x < n) {
       uint32_t l = 0;
 #pragma unroll
@@ -599,13 +598,12 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
       for (uint32_t k = 0; k < kGeneralLists; ++k) off = (k == l) ? x - start[k] : off;
       i = bail_list[(uint64_t)l * list_cap + off];
       l0 = l0 == ~0u ? l : l0;
-      lead = !kp.bin_general || l / 2 < 8;  // the class lists: leader classes 0..7 (general_bin)
     }
     if (x < n) {
       const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
       LaneStats ls;
       Lane<S> L(kp, i, p);
-      L.step(&ls, lead);
+      L.step(&ls);
       GR_CHECK_STATE(kp.st, p);
       if (!tph[0]) {
         tph[0] = L.tclk[0];

@@ -1637,9 +1637,7 @@ struct Lane {
 
   // Kernel body for one lane: run, and on escalation re-run the prefix on the
   // pristine state so the escalating item is left entirely to the host.
-  // remotes: load the remote rows with the first round (false: a lane handed over
-  // as a non-leader, whose handlers rarely read them; need() loads them on first use)
-  GR_HD bool step(LaneStats* ls, bool remotes = true) {
+  GR_HD bool step(LaneStats* ls) {
     GR_COVER(GENERAL_LANE);
     uint32_t at = 0, limit = 0xFFFFFFFFu;
     int esc = 0;
@@ -1649,7 +1647,7 @@ struct Lane {
       begin();
       // the groups nearly every handed-over lane reads, in one round of loads
       // instead of one dependent round per group as the handlers reach them
-      need(G_CORE | G_WIN | G_ETICK | G_LID | (remotes ? (uint32_t)G_REM : 0u));
+      need(G_CORE | G_WIN | G_REM | G_ETICK | G_LID);
       if (attempt == 0) tclk[0] = lane_clock(kp);
       const int e = run(limit, &at);
       if (attempt == 0) tclk[1] = lane_clock(kp);
