@@ -1544,6 +1544,10 @@ struct gr_graph {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   uint32_t n_passes = 0;
+  // the engine's counter-set and hint-set parities the captured pass 0 assumes
+  // (launches & 1, hint_flip & 1): a replay at any other parity would read a
+  // counter set nobody zeroed and the wrong hint set, so it is refused
+  uint32_t launch_par = 0, hint_par = 0;
 };
 
 int gr_graph_capture(gr_engine* e, void* space_a, void* space_b, uint32_t n_chunks, uint32_t positions,
@@ -1561,6 +1565,11 @@ int gr_graph_capture(gr_engine* e, void* space_a, void* space_b, uint32_t n_chun
   gr_graph* g = new gr_graph();
   g->e = e;
   g->n_passes = n_passes;
+  g->launch_par = (uint32_t)(e->launches & 1);
+  g->hint_par = (uint32_t)(e->hint_flip & 1);
+  // recording runs no pass: the engine's counters are restored afterwards on
+  // every path (a failed capture must not leave the parities advanced)
+  const uint64_t saved_launches = e->launches, saved_flip = e->hint_flip, saved_passes = e->passes;
   int r = GR_OK;
   if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) r = GR_EDEVICE;
   // pass k reads space k % 2 and writes the other; the launch and hint parities
@@ -1574,6 +1583,9 @@ int gr_graph_capture(gr_engine* e, void* space_a, void* space_b, uint32_t n_chun
   if (r == GR_OK && hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0) != hipSuccess) r = GR_EDEVICE;
   g->graph = graph;
   (void)hipStreamDestroy(cs);
+  e->launches = saved_launches;
+  e->hint_flip = saved_flip;
+  e->passes = saved_passes;
   if (r != GR_OK) {
     gr_graph_destroy(g);
     return r;
@@ -1586,8 +1598,14 @@ int gr_graph_replay(gr_graph* g, void* stream) {
   if (!g || !g->exec) return GR_EINVAL;
   std::lock_guard<std::mutex> guard(g->e->mu);
   GR_REFUSE_PENDING(g->e);
+  gr_engine* e = g->e;
+  // passes run between replays must come in even numbers (gpuraft.h)
+  if ((uint32_t)(e->launches & 1) != g->launch_par || (uint32_t)(e->hint_flip & 1) != g->hint_par)
+    return GR_ESTATE;
   HIPCHK(hipGraphLaunch(g->exec, (hipStream_t)stream));
-  g->e->passes += g->n_passes;
+  e->launches += g->n_passes;
+  e->hint_flip += g->n_passes;
+  e->passes += g->n_passes;
   return GR_OK;
 }
 

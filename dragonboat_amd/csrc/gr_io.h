@@ -98,8 +98,11 @@ __global__ void key_scatter(const uint32_t* keys, const uint32_t* slot, uint32_t
   }
 }
 // Arrival order inside mailbox `key`: its record indexes ascending (insertion
-// sort; a mailbox with more records than fit in registers uses a heap sort in
-// place, an input the engine escalates CAPACITY for anyway).
+// sort for the few records a mailbox holds). Only the first GR_C + 1 records in
+// arrival order matter beyond that (encode_sorted writes GR_C of them and marks
+// the mailbox overflowed; the receiver escalates CAPACITY at message GR_C), so an
+// overfull mailbox (malformed or adversarial input) gets a partial selection of
+// its GR_C + 1 smallest indexes: O(c * (GR_C + 1)) on its thread, not a full sort.
 __global__ void key_order(const uint32_t* cnt, const uint32_t* base, uint32_t nkeys, uint32_t* sidx) {
   for (uint32_t key = io_tid(); key < nkeys; key += io_stride()) {
     const uint32_t c = cnt[key];
@@ -117,24 +120,12 @@ __global__ void key_order(const uint32_t* cnt, const uint32_t* base, uint32_t nk
       }
       continue;
     }
-    // heap sort (max-heap, then repeated extraction)
-    auto sift = [&](uint32_t root, uint32_t end) {
-      while (2 * root + 1 < end) {
-        uint32_t ch = 2 * root + 1;
-        if (ch + 1 < end && a[ch] < a[ch + 1]) ++ch;
-        if (a[root] >= a[ch]) return;
-        const uint32_t t = a[root];
-        a[root] = a[ch];
-        a[ch] = t;
-        root = ch;
-      }
-    };
-    for (uint32_t r = c / 2; r-- > 0;) sift(r, c);
-    for (uint32_t end = c - 1; end > 0; --end) {
-      const uint32_t t = a[0];
-      a[0] = a[end];
-      a[end] = t;
-      sift(0, end);
+    for (uint32_t t = 0; t <= (uint32_t)GR_C; ++t) {
+      uint32_t m = t;
+      for (uint32_t u = t + 1; u < c; ++u) m = a[u] < a[m] ? u : m;
+      const uint32_t x = a[t];
+      a[t] = a[m];
+      a[m] = x;
     }
   }
 }
@@ -717,8 +708,10 @@ __global__ void compact_rows(StateBase st, const uint32_t* slots, const uint64_t
     for (int k = 0; k < GR_K; ++k)
       if ((uint32_t)k + 1 == nn) newest = ns[k];
     const bool ge = nn && newest >= i;
-    // the run bits are cleared (the covering run may now start above committed)
-    st.u64(SR_HDR)[p] = h_make(h_state(h), h_self(h), nn, ge, h_flags(h), h_ric(h), h_rb(h)) & ~H_RUN_MASK;
+    // the run bits are cleared (the covering run may now start above committed);
+    // with S > 6 those header bits are slot 7's rb field and stay
+    const uint64_t rmask = has_run_bits((int)st.S) ? H_RUN_MASK : 0ull;
+    st.u64(SR_HDR)[p] = h_make(h_state(h), h_self(h), nn, ge, h_flags(h), h_ric(h), h_rb(h)) & ~rmask;
   }
 }
 

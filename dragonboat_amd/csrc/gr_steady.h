@@ -277,7 +277,10 @@ struct SteadyFollower : SteadyBase<RM> {
     // ---- preconditions
     const uint32_t flags = h_flags(hdr);
     const uint32_t c = mb_n(cbL);
-    bool ok = h_state(hdr) == GR_FOLLOWER && !(hdr & H_SYNC_MASK) && (hdr & H_RUN_MASK) == H_RUN_MASK &&
+    // the sync bits exist for S <= 3 only: above that, bits 40-59 are remote
+    // slots' rb fields (gr_layout.h), which a follower's voters always set
+    bool ok = h_state(hdr) == GR_FOLLOWER && !(has_sync_bits(S) && (hdr & H_SYNC_MASK)) &&
+              (hdr & H_RUN_MASK) == H_RUN_MASK &&
               h_nruns(hdr) >= 1 && h_gelo(hdr) && (flags & F_ETZ) && ((flags & F_LSLOT) >> F_LSLOT_SHIFT) == hL + 1 &&
               lw == 0 && other == 0 && !wide_term(term, 0, 0, 0);
     ok = ok && (c == 0 || ((cbL & MB_UNIFORM) && !(cbL & MB_RESP) && c <= 2 && (uint64_t)fmt == term));

@@ -523,8 +523,12 @@ int gr_step_device(gr_engine* e, const void* in_space, void* out_space, uint32_t
  * (execengine.go:453-465's per-group stepNode loop) pays one launch per
  * n_passes passes. Replays continue from the state the previous pass left (n_passes is
  * even, so every replay starts in space_a); gr_step_device calls may be mixed
- * in. Capture refuses while per-pass timing is on (GR_ESTATE); the spaces,
- * routes and locals must stay as captured until gr_graph_destroy. */
+ * in, in even numbers between replays (each pass flips the engine's counter and
+ * hint sets and the live space): a replay at the other parity returns GR_ESTATE
+ * and runs nothing. Capturing runs no pass and leaves the engine's pass count
+ * and parities as they were. Capture refuses while per-pass timing is on
+ * (GR_ESTATE); the spaces, routes and locals must stay as captured until
+ * gr_graph_destroy. */
 typedef struct gr_graph gr_graph;
 int gr_graph_capture(gr_engine* e, void* space_a, void* space_b, uint32_t n_chunks, uint32_t positions,
                      uint32_t depth, uint32_t n_peers, uint32_t n_passes, gr_graph** out);

@@ -123,14 +123,15 @@ def test_device_steady_leader_staggered_acks(gpu, monkeypatch):
 @pytest.mark.parametrize("G,split", [(10_000, False), (4096, True)])
 def test_graph_replay_matches_oracle(gpu, monkeypatch, G, split):
     """Graph mode (gr_graph_capture / gr_graph_replay): two passes captured once,
-    replayed three times through the C-ABI, then one more pass by
-    gr_step_device: after every replay the state and the space the next pass
-    reads equal the oracle's after the same number of passes. G = 10k is
-    BASELINE config 2 (the fused small-pass kernel); the split schedule is forced
-    on 4096 groups (steady kernel, role instances, general kernel in the graph)."""
+    replayed three times through the C-ABI, then one pass by gr_step_device (the
+    engine's parity is now odd: a replay is refused with GR_ESTATE and runs
+    nothing), a second one, and one more replay: after every replay the state
+    and the space the next pass reads equal the oracle's after the same number
+    of passes. G = 10k is BASELINE config 2 (the fused small-pass
+    kernel); the split schedule is forced on 4096 groups (steady kernel, role
+    instances, general kernel in the graph)."""
     import torch
-    from dragonboat_amd.engine import decode_space
-    from oracle.pyoracle import OraclePopulation
+    from dragonboat_amd.engine import decode_space, GpuRaftError
     import parity
     if split:
         monkeypatch.setenv("GR_SPLIT_MIN_LANES", "1")
@@ -144,27 +145,41 @@ def test_graph_replay_matches_oracle(gpu, monkeypatch, G, split):
         g = ls.eng.graph_capture(a.data_ptr(), b.data_ptr(), 1, ls.positions, ls.n, n_passes=2, depth=ls.depth)
         pop = ls.pop
         msgs = np.zeros(0, abi.MESSAGE)
+        stream = torch.cuda.current_stream().cuda_stream
+
+        def replay_and_check(rep):
+            nonlocal msgs
+            ls.eng.graph_replay(g, stream)
+            torch.cuda.synchronize()
+            for _ in range(2):
+                o = pop.step(msgs, loc)
+                msgs = ls._route(o["msgs"])
+            bad = parity.compare_states(ls.eng.sync(ls.n), pop.export(), R)
+            assert not bad, (rep, bad[:3])
+            got = decode_space(a.cpu().numpy(), 1, ls.positions, ls.depth)
+            pos = got["peer"].astype(np.int64)
+            got["peer"] = ls.inv[0][pos].astype(np.uint32)
+            got["slot"] = ls.inv[1][pos].astype(np.uint8)
+            bad = parity.compare_msgs(got, msgs)
+            assert not bad, (rep, bad[:3])
+
         try:
             for rep in range(3):
-                ls.eng.graph_replay(g, torch.cuda.current_stream().cuda_stream)
-                torch.cuda.synchronize()
-                for _ in range(2):
-                    o = pop.step(msgs, loc)
-                    msgs = ls._route(o["msgs"])
-                bad = parity.compare_states(ls.eng.sync(ls.n), pop.export(), R)
-                assert not bad, (rep, bad[:3])
-                got = decode_space(a.cpu().numpy(), 1, ls.positions, ls.depth)
-                pos = got["peer"].astype(np.int64)
-                got["peer"] = ls.inv[0][pos].astype(np.uint32)
-                got["slot"] = ls.inv[1][pos].astype(np.uint8)
-                bad = parity.compare_msgs(got, msgs)
-                assert not bad, (rep, bad[:3])
+                replay_and_check(rep)
+            # a plain pass after the replays continues from their state (space a)
+            ls.msgs = msgs
+            ls.k = 0
+            ls.step(loc)
+            before = ls.eng.sync(ls.n)
+            with pytest.raises(GpuRaftError):  # odd parity: refused, nothing ran
+                ls.eng.graph_replay(g, stream)
+            torch.cuda.synchronize()
+            assert not parity.compare_states(ls.eng.sync(ls.n), before, R)
+            ls.step(loc)  # even again: the live space is a
+            msgs = ls.msgs
+            replay_and_check(3)
         finally:
             ls.eng.graph_destroy(g)
-        # a plain pass after the replays continues from their state (space a)
-        ls.msgs = msgs
-        ls.k = 0
-        ls.step(loc)
         assert ls.stats["escalations"] == 0
     finally:
         ls.close()
