@@ -85,6 +85,7 @@ struct gr_engine {
   uint64_t hint_flip = 0;
   uint64_t launches = 0;         // never reset: selects the live counter set
   uint64_t timing_bailed0 = 0;   // ST_BAILED when timing began
+  uint64_t timing_churn0 = 0;      // ST_CHURN when timing began
   bool timing = false;
   std::vector<PassTiming> timings;  // one per pass while timing
   bool routes_bound = false;
@@ -98,6 +99,8 @@ struct gr_engine {
   // each wave's span; gr_destroy writes the last pass's records to <path>
   uint64_t* wclock = nullptr;
   uint8_t bin_general = 1;  // StepParams::bin_general (GR_BIN_GENERAL=0 at gr_create: off, A/B runs)
+  uint32_t* tail_hint = nullptr;  // StepParams::tail_hint: pinned, host-visible (GR_TAIL_HINT=0: off)
+  uint8_t tail_mode = 0;          // StepParams::tail_mode (GR_TAIL_MODE at gr_create: tests, A/B runs)
   std::string wclock_path;
 
   // gr_step buffers (gr_io.h), grown on demand and reused
@@ -215,6 +218,8 @@ StepParams base_params(gr_engine* e) {
   kp.small_blocks = e->small_blocks;
   kp.wclock = e->wclock;
   kp.bin_general = e->bin_general;
+  kp.tail_hint = e->tail_hint;
+  kp.tail_mode = e->tail_mode;
   return kp;
 }
 
@@ -393,6 +398,7 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
   }
   if (const char* sb = getenv("GR_SMALL_BLOCKS")) e->small_blocks = (uint32_t)strtoul(sb, nullptr, 10);
   if (const char* bg = getenv("GR_BIN_GENERAL")) e->bin_general = bg[0] == '1';
+  if (const char* tm = getenv("GR_TAIL_MODE")) e->tail_mode = (uint8_t)(strtoul(tm, nullptr, 10) & 3u);
   if (const char* wc = getenv("GR_WAVE_CLOCK")) {
     if (hipMalloc((void**)&e->wclock, (size_t)kGeneralWaveSlots * kWaveClockWords * 8) == hipSuccess &&
         hipMemset(e->wclock, 0, (size_t)kGeneralWaveSlots * kWaveClockWords * 8) == hipSuccess)
@@ -422,6 +428,13 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
     gr_destroy(e);
     return GR_EDEVICE;
   }
+  const char* th = getenv("GR_TAIL_HINT");
+  if (!(th && th[0] == '0')) {  // a failed allocation only leaves the grids full
+    if (hipHostMalloc((void**)&e->tail_hint, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+      e->tail_hint = nullptr;
+    else
+      *(volatile uint32_t*)e->tail_hint = kTailAll;
+  }
   *out = e;
   return GR_OK;
 }
@@ -436,6 +449,7 @@ void gr_destroy(gr_engine* e) {
   if (e->counters) (void)hipFree(e->counters);
   if (e->route_base) (void)hipFree(e->route_base);
   if (e->hints) (void)hipFree(e->hints);
+  if (e->tail_hint) (void)hipHostFree(e->tail_hint);
   if (e->wclock) {
     std::vector<uint64_t> h((size_t)kGeneralWaveSlots * kWaveClockWords);
     if (!e->wclock_path.empty() && hipStreamSynchronize(e->stream) == hipSuccess &&
@@ -1400,7 +1414,9 @@ int gr_timing_begin(gr_engine* e) {
   HIPCHK(hipDeviceSynchronize());
   free_timings(e);
   e->timings.reserve(1 << 16);  // records are referenced by pointer until the pass is enqueued
-  const int r = stat_total(e, ST_BAILED, &e->timing_bailed0);
+  int r = stat_total(e, ST_BAILED, &e->timing_bailed0);
+  if (r) return r;
+  r = stat_total(e, ST_CHURN, &e->timing_churn0);
   if (r) return r;
   e->timing = true;
   return GR_OK;
@@ -1421,7 +1437,11 @@ int gr_timing_end(gr_engine* e, gr_timing* out) {
   uint64_t bailed = 0;
   const int r = stat_total(e, ST_BAILED, &bailed);
   if (r) return r;
-  out->bailed_lanes = bailed - e->timing_bailed0;  // lanes the general kernel stepped while timing
+  out->bailed_lanes = bailed - e->timing_bailed0;  // lanes that left the lean kernels while timing
+  uint64_t churn = 0;
+  const int r2 = stat_total(e, ST_CHURN, &churn);
+  if (r2) return r2;
+  out->churn_lanes = churn - e->timing_churn0;  // ... of which the churn lane finished
   free_timings(e);
   e->timing = false;
   return GR_OK;

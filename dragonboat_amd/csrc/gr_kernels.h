@@ -16,6 +16,7 @@
 #include "gr_fast.h"
 #include "gr_steady.h"
 #include "gr_lane.h"
+#include "gr_churn.h"
 #include "gr_tick.h"
 
 namespace gr {
@@ -35,18 +36,18 @@ __device__ inline __attribute__((always_inline)) uint32_t wave_sum(uint32_t v) {
 // barrier, so a wave never waits for the rest of its workgroup to finish.
 __device__ inline __attribute__((always_inline)) void block_stats(const StepParams& kp, const LaneStats& ls,
                                                                   uint32_t bid = blockIdx.x) {
-  constexpr int N = 9;
+  constexpr int N = 10;
   // one named field at a time: a register array indexed in a loop was put in scratch
   const uint32_t f0 = wave_sum(ls.leader_commit), f1 = wave_sum(ls.follower_commit),
                  f2 = wave_sum(ls.escalated), f3 = wave_sum(ls.msgs_in), f4 = wave_sum(ls.msgs_out),
                  f5 = wave_sum(ls.leader_in), f6 = wave_sum(ls.leader_out), f7 = wave_sum(ls.entries),
-                 f8 = wave_sum(ls.bailed);
+                 f8 = wave_sum(ls.bailed), f9 = wave_sum(ls.churn);
   const uint32_t k = threadIdx.x & 63;
   if (k < (uint32_t)N) {
     constexpr uint32_t field[N] = {ST_LEADER_COMMITS, ST_FOLLOWER_COMMITS, ST_ESCALATIONS, ST_MSGS_IN, ST_MSGS_OUT,
-                                   ST_LEADER_MSGS_IN, ST_LEADER_MSGS_OUT, ST_REPLICATE_ENTRIES, ST_BAILED};
+                                   ST_LEADER_MSGS_IN, ST_LEADER_MSGS_OUT, ST_REPLICATE_ENTRIES, ST_BAILED, ST_CHURN};
     const uint32_t v = k == 0 ? f0 : k == 1 ? f1 : k == 2 ? f2 : k == 3 ? f3 : k == 4 ? f4 : k == 5 ? f5
-                     : k == 6 ? f6 : k == 7 ? f7 : f8;
+                     : k == 6 ? f6 : k == 7 ? f7 : k == 8 ? f8 : f9;
     uint32_t f = 0;
 #pragma unroll
     for (uint32_t x = 0; x < (uint32_t)N; ++x) f = k == x ? field[x] : f;
@@ -84,8 +85,13 @@ __device__ inline __attribute__((always_inline)) void block_stats(const StepPara
 // saturates near 90 appends per us (MI355X_MICROARCH.md, "dequeue"), so 8 list
 // counters made those appends most of the steady kernel's time.
 constexpr uint32_t kTickLists = 64;
+// The churn kernel's leftovers (round 5): lanes of general list l the churn lane
+// (gr_churn.h) hands back go to churn list l / 2 (their handler class), after
+// the tick lists.
+constexpr uint32_t kChurnLists = 16;
 constexpr uint32_t kBailLists = 40, kGeneralLists = 32, kRetryList0 = 32,
-                   kTickCounter0 = kBailLists, kCounters = kBailLists + kTickLists,
+                   kTickCounter0 = kBailLists, kChurnCounter0 = kBailLists + kTickLists,
+                   kCounters = kBailLists + kTickLists + kChurnLists,
                    kCounterStride = 64;  // counters 256 B apart
 constexpr uint32_t WF_LISTED = 0x80;     // wave flag: the role instances step this wave's masked lanes
 // Word 1 of counter 0's 256-B slot: nonzero when a split pass's steady kernel
@@ -99,6 +105,8 @@ constexpr uint32_t kListedWord = 1;
 // holds puts the extra chunks on the waves that finish first). Cleared with the
 // next pass's counters.
 constexpr uint32_t kGeneralNext = 2;
+// Word 3: the churn kernel's next 64-lane chunk (as kGeneralNext).
+constexpr uint32_t kChurnNext = 3;
 __host__ __device__ inline uint64_t wave_flag_words(uint32_t cap) { return ((uint64_t)cap / 64 + 64) / 4 * 2; }
 // Lanes one tick list can receive: the lanes of every kTickLists-th block, from
 // the steady kernel and the listed role waves (keyed by lane), plus as many
@@ -109,9 +117,11 @@ __host__ __device__ inline uint64_t tick_cap(uint32_t cap) {
 __host__ __device__ inline uint64_t tick_off(uint32_t cap) {
   return (uint64_t)kBailLists * cap + wave_flag_words(cap) + 2 * ((uint64_t)cap / 64 + 1);
 }
+__host__ __device__ inline uint64_t churn_off(uint32_t cap) { return tick_off(cap) + kTickLists * tick_cap(cap); }
 // u32 words of the list storage: kBailLists lane lists of cap, the wave flags,
-// the wave masks (u64), the kTickLists tick lists of tick_cap
-__host__ __device__ inline uint64_t bail_words(uint32_t cap) { return tick_off(cap) + kTickLists * tick_cap(cap); }
+// the wave masks (u64), the kTickLists tick lists of tick_cap, the kChurnLists
+// churn leftover lists of cap
+__host__ __device__ inline uint64_t bail_words(uint32_t cap) { return churn_off(cap) + (uint64_t)kChurnLists * cap; }
 __host__ __device__ inline uint8_t* wave_flags(uint32_t* bail_list, uint32_t cap) {
   return (uint8_t*)(bail_list + (uint64_t)kBailLists * cap);
 }
@@ -556,105 +566,296 @@ __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(Step
   if (kp.stats) block_stats(kp, acc);
 }
 
+// The lists a tail kernel walks: nl <= NL lists (list l at base + l * stride
+// words, its count at counters[(c0 + l) * kCounterStride]) as one concatenated
+// range, in 64-lane chunks. Wave-uniform. One range object serves every list set
+// a kernel walks in turn (re-initialised), so one prefix array stays live.
+template <int NL>
+struct ListRange {
+  uint32_t start[NL + 1];
+  const uint32_t* base;
+  uint64_t stride;
+  __device__ inline void init(const uint32_t* counters, uint32_t c0, const uint32_t* b, uint64_t st,
+                              uint32_t nl = NL) {
+    base = b;
+    stride = st;
+    start[0] = 0;
+#pragma unroll
+    for (uint32_t l = 0; l < (uint32_t)NL; ++l)  // wave-uniform: scalar registers, not 33 VGPRs
+      start[l + 1] = (uint32_t)__builtin_amdgcn_readfirstlane(
+          start[l] + (l < nl ? counters[(c0 + l) * kCounterStride] : 0u));
+  }
+  __device__ inline uint32_t total() const { return start[NL]; }
+  // entry x (< total): the lane, and its list in *lo
+  __device__ inline uint32_t at(uint32_t x, uint32_t* lo) const {
+    uint32_t l = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < (uint32_t)NL; ++k) l = x >= start[k] ? k : l;
+    uint32_t off = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)NL; ++k) off = (k == l) ? x - start[k] : off;
+    *lo = l;
+    return base[(uint64_t)l * stride + off];
+  }
+};
+
+// Walk `r` in 64-lane chunks: each wave's first chunk is its index in the grid,
+// later ones come from the counter at counters[next_word] (a wave that finishes
+// early takes the next chunk). f(entry lane, its list, valid) runs for every lane
+// of every chunk, valid = x < total (the wave stays converged for its ballots).
+template <int NL, class F>
+__device__ inline void walk_chunks(const ListRange<NL>& r, uint32_t* counters, uint32_t next_word, F f) {
+  const uint32_t n = r.total();
+  const uint32_t lane = threadIdx.x & 63, W = gridDim.x * (kBlock / 64);
+  uint32_t chunk = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);  // wave-uniform
+  while (chunk * 64 < n) {  // wave-uniform
+    const uint32_t x = chunk * 64 + lane;
+    uint32_t l = 0, i = 0;
+    if (x < n) i = r.at(x, &l);
+    f(i, l, x < n);
+    if ((uint64_t)W * 64 >= n) break;  // the first chunks covered every lane: no atomic
+    uint32_t c = 0;
+    if (lane == 0) c = W + atomicAdd(counters + next_word, 1u);
+    chunk = (uint32_t)__shfl((int)c, 0);
+  }
+}
+
+__device__ inline __attribute__((always_inline)) void stats_add(LaneStats& acc, const LaneStats& ls) {
+  acc.leader_commit += ls.leader_commit;
+  acc.follower_commit += ls.follower_commit;
+  acc.escalated += ls.escalated;
+  acc.msgs_in += ls.msgs_in;
+  acc.msgs_out += ls.msgs_out;
+  acc.leader_in += ls.leader_in;
+  acc.leader_out += ls.leader_out;
+  acc.entries += ls.entries;
+}
+
+// One wave's appends to the churn leftover list of each lane's class `key`
+// (< kChurnLists): one returning atomic per class present, as general_append.
+__device__ inline __attribute__((always_inline)) void churn_append(bool mine, uint32_t key, uint32_t i, uint32_t* bail_list,
+                                                                 uint32_t* counters, uint32_t list_cap) {
+  const uint64_t bm = __ballot(mine);
+  if (!bm) return;
+  uint64_t same = 0;
+  for (uint64_t rest = bm; rest;) {  // wave-uniform
+    const uint32_t k = (uint32_t)__shfl((int)key, __ffsll((unsigned long long)rest) - 1);
+    const uint64_t m = __ballot(mine && key == k);
+    if (mine && key == k) same = m;
+    rest &= ~m;
+  }
+  const uint32_t lane = threadIdx.x & 63;
+  const int first = mine ? __ffsll((unsigned long long)same) - 1 : (int)lane;
+  uint32_t base = 0;
+  if (mine && (uint32_t)first == lane)
+    base = atomicAdd(counters + (kChurnCounter0 + key) * kCounterStride, (uint32_t)__popcll(same));
+  base = (uint32_t)__shfl((int)base, first);
+  if (mine)
+    bail_list[churn_off(list_cap) + (uint64_t)key * list_cap + base + (uint32_t)__popcll(same & ((1ull << lane) - 1))] = i;
+}
+
+// Pass 2a': the churn lane (gr_churn.h: the general lane's follower path, term
+// adoption and step-down included) over the general lists, in a kernel of its
+// own so its register file is its own (216 VGPRs, two waves per SIMD; the full
+// lane holds 256 VGPRs + 256 AGPRs and spills: one wave per SIMD). A lane it
+// finishes is done; one it hands back (nothing stored) goes to churn list l / 2.
+// Launched when the tail hint says the general kernel had work lately
+// (TailPlan): the general kernel then walks the churn lists instead.
+#ifndef GR_CHURN_MIN_WAVES
+#define GR_CHURN_MIN_WAVES 1
+#endif
+template <int S>
+__global__ __launch_bounds__(kBlock, GR_CHURN_MIN_WAVES) void gr_churn_kernel(StepParams kp, uint32_t* bail_list,
+                                                                           uint32_t* counters, uint32_t list_cap) {
+  ListRange<kGeneralLists> r;
+  r.init(counters, 0, bail_list, list_cap);
+  if (blockIdx.x * kBlock >= r.total()) return;  // no stats row touched
+  LaneStats acc;
+  walk_chunks(r, counters, kChurnNext, [&](uint32_t i, uint32_t l, bool valid) {
+    bool back = false;
+    if (valid) {
+      const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+      LaneStats ls;
+      if (churn_step<S>(kp, i, p, &ls)) {
+        GR_CHECK_STATE(kp.st, p);
+        stats_add(acc, ls);
+        acc.bailed += 1;
+        acc.churn += 1;
+      } else {
+        back = true;
+      }
+    }
+    churn_append(back, l >> 1, i, bail_list, counters, list_cap);
+  });
+  if (kp.stats) block_stats(kp, acc);
+}
+
+// Tail kernel modes (TailPlan): the general kernel walks the churn leftover lists
+// instead of the general lists (the churn kernel ran), and/or steps the waves the
+// steady kernel listed and the lanes it left (the role instances did not run).
+constexpr uint32_t GM_CHURN_LISTS = 1, GM_LISTED = 2;
+
 // Pass 2b: the general lane (every handler, escalation with prefix re-run)
-// over the bailed lanes only, grid-stride over the concatenated lists; also
-// clears the counters the next pass's fast kernel will use.
+// over the handed-over lanes, grid-stride over the concatenated lists; also
+// clears the counters the next pass's kernels will use, and reports the pass
+// to the host (StepParams::tail_hint).
 #ifndef GR_GENERAL_MIN_WAVES
 #define GR_GENERAL_MIN_WAVES 1  // A/B builds: waves per SIMD for the general kernel
 #endif
-template <int S>
+// LISTED: the instance for mode GM_LISTED (a pass whose role instances did not
+// run); its listed-wave source keeps more state live across the general lane
+// (460 vs 156 B of scratch per lane), so the other passes run the instance
+// without it.
+template <int S, bool LISTED>
 __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(StepParams kp, const uint32_t* bail_list,
                                                          uint32_t* counters, uint32_t* next_counters,
-                                                         uint32_t list_cap) {
-  uint32_t start[kGeneralLists + 1];
-  start[0] = 0;
+                                                         uint32_t list_cap, uint32_t mode) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t listed = (uint32_t)__builtin_amdgcn_readfirstlane(counters[kListedWord]);
+  uint32_t nretry = 0;  // lanes the steady kernel left
 #pragma unroll
-  for (uint32_t l = 0; l < kGeneralLists; ++l) start[l + 1] = start[l] + counters[l * kCounterStride];
-  const uint32_t n = start[kGeneralLists];
+  for (uint32_t l = 0; l < 8; ++l) nretry += counters[(kRetryList0 + l) * kCounterStride];
+  uint32_t na = 0;  // the general lists' total: what the churn kernel would take next time
+#pragma unroll
+  for (uint32_t l = 0; l < kGeneralLists; ++l) na += counters[l * kCounterStride];
+  if (kp.tail_hint && blockIdx.x == 0 && threadIdx.x == 0)  // the next passes' tail plan (kTailAll)
+    *(volatile uint32_t*)kp.tail_hint = ((listed || nretry) ? 1u : 0u) | ((na < (1u << 30) ? na : (1u << 30)) << 1);
   if (blockIdx.x == 0 && threadIdx.x < kCounters) next_counters[threadIdx.x * kCounterStride] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters) next_counters[kListedWord] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters + 1) next_counters[kGeneralNext] = 0;
-  // 64-lane chunks of the concatenated lists: each wave's first chunk is its
-  // index in the grid, later ones come from the kGeneralNext counter (waves, not
-  // the grid, stride: a wave that finishes early takes the next chunk). The lists
-  // run leader classes first, so the chunks handed out late are followers' (the
-  // lighter classes: GR_WAVE_CLOCK).
-  const uint32_t lane = threadIdx.x & 63, W = gridDim.x * (kBlock / 64);
-  uint32_t chunk = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);  // wave-uniform
-  if (chunk * 64 >= n) return;  // nothing for this wave, no stats row touched
-  const uint64_t t0 = kp.wclock ? wall_clock64() : 0;
+  if (blockIdx.x == 0 && threadIdx.x == kCounters + 2) next_counters[kChurnNext] = 0;
   LaneStats acc;
   uint64_t tph[3] = {0, 0, 0};  // GR_WAVE_CLOCK: the first round's phase marks
   uint32_t l0 = ~0u;            // ... and the list (handler class) of the lane's first round
-  while (chunk * 64 < n) {  // wave-uniform
-    const uint32_t x = chunk * 64 + lane;
-    uint32_t i = 0;
-    if (x < n) {
-      uint32_t l = 0;
-#pragma unroll
-      for (uint32_t k = 1; k < kGeneralLists; ++k) l = x >= start[k] ? k : l;
-      uint32_t off = 0;
-#pragma unroll
-      for (uint32_t k = 0; k < kGeneralLists; ++k) off = (k == l) ? x - start[k] : off;
-      i = bail_list[(uint64_t)l * list_cap + off];
-      l0 = l0 == ~0u ? l : l0;
+  bool any = false;
+  const uint64_t t0 = kp.wclock ? wall_clock64() : 0;
+  // One loop, one call site of the general lane (each inlined copy of Lane::step
+  // costs code and scratch): every iteration takes 64 lanes of this wave from the
+  // current source. Sources, in order: the waves the steady kernel listed and the
+  // lanes it left (GM_LISTED: the role instances did not run), then the general
+  // or churn lists in 64-lane chunks (walk_chunks' scheme: the wave's grid index
+  // first, later chunks from the counter).
+  const uint32_t W = gridDim.x * (kBlock / 64);
+  const uint32_t g = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+  const uint8_t* wf = wave_flags(const_cast<uint32_t*>(bail_list), list_cap);
+  const uint64_t* wm = wave_masks(const_cast<uint32_t*>(bail_list), list_cap);
+  const uint32_t nw = (kp.n_lanes + 63) / 64;
+  // the lists: the retry lists while source 1 runs, then the general or churn lists
+  ListRange<kGeneralLists> rl;
+  const bool use_churn = mode & GM_CHURN_LISTS;
+  auto lists_init = [&] {
+    if (use_churn) rl.init(counters, kChurnCounter0, bail_list + churn_off(list_cap), list_cap, kChurnLists);
+    else rl.init(counters, 0, bail_list, list_cap);
+  };
+  // source 0: listed waves (r: the group of 64 grid-strided waves, todo: its
+  // listed ones left); 1: retry lanes (x0: this wave's next 64); 2: the lists
+  uint32_t src = (LISTED && (mode & GM_LISTED)) ? (listed ? 0u : 1u) : 2u;
+  if (src == 2) lists_init();
+  else rl.init(counters, kRetryList0, bail_list + (uint64_t)kRetryList0 * list_cap, list_cap, 8);
+  uint32_t r = 0, x0 = g * 64;
+  uint64_t todo = 0;
+  bool todo_loaded = false;
+  uint32_t chunk = g;
+  for (;;) {  // wave-uniform
+    bool valid = false;
+    uint32_t i = 0, l = 0;
+    if (LISTED && src == 0) {
+      if (!todo_loaded) {
+        if (g + (uint64_t)W * r >= nw) {
+          src = 1;
+          continue;
+        }
+        const uint64_t idx = g + (uint64_t)W * (r + lane);
+        const uint32_t f = idx < nw ? (uint32_t)wf[idx] : 0u;
+        todo = __ballot(f & WF_LISTED);
+        todo_loaded = true;
+      }
+      if (!todo) {
+        r += 64;
+        todo_loaded = false;
+        continue;
+      }
+      const uint32_t b = (uint32_t)__ffsll((unsigned long long)todo) - 1;
+      todo &= todo - 1;
+      const uint32_t wave = g + W * (r + b);
+      valid = (wm[wave] >> lane) & 1ull;
+      i = wave * 64 + lane;
+      if (lane == 0) kp.hints_out[wave] = 0;  // the role instances would have written one
+      if (valid) GR_COVER(TAIL_LISTED);
+    } else if (LISTED && src == 1) {
+      if (x0 >= rl.total()) {
+        src = 2;
+        lists_init();
+        continue;
+      }
+      const uint32_t x = x0 + lane;
+      if (x < rl.total()) {
+        i = rl.at(x, &l);
+        valid = true;
+      }
+      x0 += W * 64;
+    } else {
+      const uint32_t n = rl.total();
+      if (chunk * 64 >= n) break;
+      const uint32_t x = chunk * 64 + lane;
+      if (x < n) {
+        i = rl.at(x, &l);
+        valid = true;
+        l0 = l0 == ~0u ? l : l0;
+      }
+      if ((uint64_t)W * 64 >= n) {
+        chunk = n / 64 + 1;  // the first chunks covered every lane: no atomic
+      } else {
+        uint32_t c = 0;
+        if (lane == 0) c = W + atomicAdd(counters + kGeneralNext, 1u);
+        chunk = (uint32_t)__shfl((int)c, 0);
+      }
     }
-    if (x < n) {
+    if (valid) {
+      any = true;
       const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
       LaneStats ls;
       Lane<S> L(kp, i, p);
       L.step(&ls);
       GR_CHECK_STATE(kp.st, p);
+      stats_add(acc, ls);
+      acc.bailed += 1;
       if (!tph[0]) {
         tph[0] = L.tclk[0];
         tph[1] = L.tclk[1];
         tph[2] = L.tclk[2];
       }
-      acc.leader_commit += ls.leader_commit;
-      acc.follower_commit += ls.follower_commit;
-      acc.escalated += ls.escalated;
-      acc.msgs_in += ls.msgs_in;
-      acc.msgs_out += ls.msgs_out;
-      acc.leader_in += ls.leader_in;
-      acc.leader_out += ls.leader_out;
-      acc.entries += ls.entries;
-      acc.bailed += 1;
     }
-    if ((uint64_t)W * 64 >= n) break;  // the first chunks covered every lane: no atomic
-    uint32_t c = 0;
-    if (lane == 0) c = W + atomicAdd(counters + kGeneralNext, 1u);
-    chunk = (uint32_t)__shfl((int)c, 0);
   }
-  if (kp.wclock) {  // profiling: this wave's span and what it stepped
+  if (kp.wclock && __ballot(any)) {  // profiling: this wave's span and what it stepped
     const uint64_t t1 = wall_clock64();
     const uint32_t nl = wave_sum(acc.bailed), nm = wave_sum(acc.msgs_in), ne = wave_sum(acc.escalated),
                    nli = wave_sum(acc.leader_in);
     const uint32_t w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     if ((threadIdx.x & 63) == 0) {
-      uint64_t* r = kp.wclock + (uint64_t)w * kWaveClockWords;
-      r[0] = t0;
-      r[1] = t1;
-      r[2] = nl;
-      r[3] = nm;
-      r[4] = ne;  // the list of the wave's first lane goes in the high word (below)
-      r[5] = nli;
+      uint64_t* rr = kp.wclock + (uint64_t)w * kWaveClockWords;
+      rr[0] = t0;
+      rr[1] = t1;
+      rr[2] = nl;
+      rr[3] = nm;
+      rr[5] = nli;
     }
     const uint64_t wl = __ballot(l0 != ~0u);
     const uint32_t cls = wl ? (uint32_t)__shfl((int)l0, __ffsll((unsigned long long)wl) - 1) : 0u;
     if ((threadIdx.x & 63) == 0) kp.wclock[(uint64_t)w * kWaveClockWords + 4] = (uint64_t)ne | ((uint64_t)cls << 32);
     // the phase marks of the wave's first round (any active lane's: the wave runs them together)
-    const uint64_t any = __ballot(tph[0] != 0);
-    if (any) {
-      const int src = __ffsll((unsigned long long)any) - 1;
-      const uint64_t a = __shfl(tph[0], src), b = __shfl(tph[1], src), c = __shfl(tph[2], src);
+    const uint64_t anyp = __ballot(tph[0] != 0);
+    if (anyp) {
+      const int sl = __ffsll((unsigned long long)anyp) - 1;
+      const uint64_t a = __shfl(tph[0], sl), b = __shfl(tph[1], sl), c = __shfl(tph[2], sl);
       if ((threadIdx.x & 63) == 0) {
-        uint64_t* r = kp.wclock + (uint64_t)w * kWaveClockWords;
-        r[6] = a;
-        r[7] = ((b - a) << 32) | (c - b);
+        uint64_t* rr = kp.wclock + (uint64_t)w * kWaveClockWords;
+        rr[6] = a;
+        rr[7] = ((b - a) << 32) | (c - b);
       }
     }
   }
-  if (kp.stats) block_stats(kp, acc);
+  if (kp.stats && __ballot(acc.bailed != 0)) block_stats(kp, acc);
 }
 
 // The general kernel's grid: one 256-lane workgroup per CU fills the chip at its
@@ -688,6 +889,7 @@ __global__ __launch_bounds__(kBlock, 1) void gr_small_kernel(StepParams kp, uint
   if (blockIdx.x == 0 && threadIdx.x < kCounters) next_counters[threadIdx.x * kCounterStride] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters) next_counters[kListedWord] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters + 1) next_counters[kGeneralNext] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == kCounters + 2) next_counters[kChurnNext] = 0;
   const uint32_t hw = kp.hints ? sload_u32(kp.hints + (uint64_t)blockIdx.x * (kBlock / 64)) : 0u;
   const uint32_t hint = (hw >> (8 * (wave & 3))) & 0xFFu;
   const int wk = wave_kernel(hint, S);
@@ -729,6 +931,48 @@ struct PassTiming {
 };
 
 
+// The tail plan: which optional launches a pass makes after its lean kernels.
+// Every tail launch but the general kernel's is optional for correctness: the
+// general lane handles any lane (it steps listed waves itself when the role
+// instances do not run, and every hand-over when the churn kernel does not). So
+// the host decides from the last pass the device has reported (StepParams::
+// tail_hint, written by the general kernel into host-visible memory and read
+// here without synchronising: one or more passes back). In the steady state
+// nothing is listed and nothing handed over: the pass is the steady kernel and
+// one empty general launch. A launch with nothing to do costs its workgroups'
+// dispatch (round-5 A/B, 1M x 3: steady kernel alone 0.0622 ms per pass, with
+// the round-4 tail of role instances + general kernel 0.0671).
+constexpr uint32_t kTailAll = 0xFFFFFFFFu;  // no report yet: every launch
+// the churn kernel when the last reported pass handed at least this many lanes to
+// the general lists
+constexpr uint32_t kChurnMinLanes = 1;
+inline uint32_t tail_word(const StepParams& kp) {
+  return kp.tail_hint ? __atomic_load_n(kp.tail_hint, __ATOMIC_RELAXED) : kTailAll;
+}
+struct TailPlan {
+  bool roles, churn;
+};
+inline TailPlan tail_plan(const StepParams& kp) {
+  const uint32_t th = tail_word(kp);
+  switch (kp.tail_mode) {
+    case 1: return {true, true};
+    case 2: return {false, false};
+    case 3: return {true, false};
+    default: return {(th & 1u) != 0, (th >> 1) >= kChurnMinLanes};
+  }
+}
+// The churn kernel's grid: resident capacity at two waves per SIMD (GR_CHURN_BLOCKS
+// overrides it, A/B runs).
+constexpr uint32_t kChurnBlocks = 512;
+inline uint32_t churn_blocks() {
+  static const uint32_t v = [] {
+    const char* e = getenv("GR_CHURN_BLOCKS");
+    const long x = e ? strtol(e, nullptr, 10) : 0;
+    return x > 0 ? (uint32_t)x : kChurnBlocks;
+  }();
+  return v;
+}
+
 // The tick kernel's grid: its lanes are at most the active share of a pass.
 constexpr uint32_t kTickBlocks = 1024;
 
@@ -759,18 +1003,47 @@ inline bool roles_merged() {
   return v;
 }
 
+// Measurement knobs (A/B runs only; never set in tests or the bench):
+// GR_STEADY_LDS=<bytes> gives each steady-kernel workgroup that much dynamic LDS,
+// which caps its workgroups per CU (occupancy) without changing its code;
+// GR_SKIP_TAIL=<n> launches the steady kernel alone from the engine's n-th
+// launch on (no role instances, tick or general kernel, counters never cleared):
+// correct only while nothing is listed or handed over, i.e. the floor of a
+// steady-state pass after warm-up.
+inline uint32_t env_u32(const char* name) {
+  const char* e = getenv(name);
+  const long x = e ? strtol(e, nullptr, 10) : 0;
+  return x > 0 ? (uint32_t)x : 0u;
+}
+inline uint32_t steady_lds() {
+  static const uint32_t v = env_u32("GR_STEADY_LDS");
+  return v;
+}
+inline uint32_t skip_tail_from() {
+  static const uint32_t v = env_u32("GR_SKIP_TAIL");
+  return v;
+}
+
+// *listed_left: the steady kernel ran and the role instances did not (the general
+// kernel steps the listed waves, GM_LISTED).
 template <int S, int RM>
 hipError_t launch_fast(const StepParams& kp0, uint32_t blocks, uint32_t* bail_list, uint32_t* cur, uint32_t list_cap,
-                       hipStream_t s) {
+                       hipStream_t s, bool skip_tail, bool roles, bool* listed_left) {
   StepParams kp = kp0;
+  *listed_left = false;
   if (kp.hints && kp.split) {  // a large pass: the role instances
     // the steady kernel steps lane i = peer i with compile-time routes
     if (RM != RM_ANY && !kp.has_lane_peer) {
       // the steady lanes, then the role instances over the waves it listed and
       // the lanes it left
-      hipLaunchKernelGGL((gr_steady_kernel<S, RM>), dim3(blocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
+      hipLaunchKernelGGL((gr_steady_kernel<S, RM>), dim3(blocks), dim3(kBlock), steady_lds(), s, kp, bail_list, cur,
+                         list_cap);
       const hipError_t e0 = hipGetLastError();
-      if (e0 != hipSuccess) return e0;
+      if (e0 != hipSuccess || skip_tail) return e0;
+      if (!roles) {
+        *listed_left = true;
+        return hipSuccess;
+      }
       const uint32_t rb = blocks < role_blocks() ? blocks : role_blocks();
       if (roles_merged()) {
         hipLaunchKernelGGL((gr_roles_kernel<S, RM>), dim3(2 * rb), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
@@ -818,14 +1091,26 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   // the lean instances built for the bound route mode (no route branches); a
   // loopback instance also assumes one-chunk spaces
   const bool loop1 = kp.route_mode == RT_LOOPBACK && kp.in.n_chunks == 1 && kp.out.n_chunks == 1;
-  if (loop1) err = launch_fast<S, RT_LOOPBACK>(kp, blocks, bail_list, cur, list_cap, s);
-  else if (kp.route_mode == RT_AFFINE) err = launch_fast<S, RT_AFFINE>(kp, blocks, bail_list, cur, list_cap, s);
-  else err = launch_fast<S, RM_ANY>(kp, blocks, bail_list, cur, list_cap, s);
+  const bool skip = skip_tail_from() && parity >= skip_tail_from();
+  const TailPlan plan = tail_plan(kp);
+  bool listed_left = false;
+  if (loop1)
+    err = launch_fast<S, RT_LOOPBACK>(kp, blocks, bail_list, cur, list_cap, s, skip, plan.roles, &listed_left);
+  else if (kp.route_mode == RT_AFFINE)
+    err = launch_fast<S, RT_AFFINE>(kp, blocks, bail_list, cur, list_cap, s, skip, plan.roles, &listed_left);
+  else
+    err = launch_fast<S, RM_ANY>(kp, blocks, bail_list, cur, list_cap, s, skip, plan.roles, &listed_left);
   if (err != hipSuccess) return err;
   if (t && (err = hipEventRecord(t->ev[1], s)) != hipSuccess) return err;
+  if (skip) return t ? hipEventRecord(t->ev[2], s) : hipSuccess;
   if (tick_lanes) {  // some lane may carry ticks or a ReadIndex (LW_OTHER)
     const uint32_t tblocks = blocks < kTickBlocks ? blocks : kTickBlocks;
     hipLaunchKernelGGL(gr_tick_kernel<S>, dim3(tblocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
+    if ((err = hipGetLastError()) != hipSuccess) return err;
+  }
+  if (plan.churn) {  // the churn lane first; the general kernel then walks its leftovers
+    const uint32_t cblocks = blocks < churn_blocks() ? blocks : churn_blocks();
+    hipLaunchKernelGGL(gr_churn_kernel<S>, dim3(cblocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
     if ((err = hipGetLastError()) != hipSuccess) return err;
   }
   uint32_t gblocks = blocks < general_blocks() ? blocks : general_blocks();
@@ -833,8 +1118,13 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   if (kp.wclock &&
       (err = hipMemsetAsync(kp.wclock, 0, (size_t)gblocks * (kBlock / 64) * kWaveClockWords * 8, s)) != hipSuccess)
     return err;
-  hipLaunchKernelGGL(gr_step_kernel<S>, dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list, cur, nxt,
-                     list_cap);
+  const uint32_t mode = (plan.churn ? GM_CHURN_LISTS : 0u) | (listed_left ? GM_LISTED : 0u);
+  if (listed_left)
+    hipLaunchKernelGGL((gr_step_kernel<S, true>), dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list,
+                       cur, nxt, list_cap, mode);
+  else
+    hipLaunchKernelGGL((gr_step_kernel<S, false>), dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list,
+                       cur, nxt, list_cap, mode);
   if ((err = hipGetLastError()) != hipSuccess) return err;
   if (t && (err = hipEventRecord(t->ev[2], s)) != hipSuccess) return err;
   return hipSuccess;

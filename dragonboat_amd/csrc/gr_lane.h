@@ -269,14 +269,16 @@ struct Lane {
       for (int j = 0; j < S; ++j)
         if ((snapz >> j) & 1u) s64(R::SNAP + j) = 0;
     }
-    if (dirty & D_RI) {
+    if (dirty & D_RI) {  // the live entries only: nothing reads past the count (gr_tick.h, parity)
 #pragma unroll
       for (int q = 0; q < GR_Q; ++q) {
-        s64(R::RI_INDEX + q) = rii[q];
-        s64(R::RI_LO + q) = rilo[q];
-        s64(R::RI_HI + q) = rihi[q];
-        s8(R::B_RIFROM + q) = (uint8_t)(rifrom >> (8 * q));
-        s8(R::B_RIACK + q) = (uint8_t)(riack >> (8 * q));
+        if ((uint32_t)q < ric) {
+          s64(R::RI_INDEX + q) = rii[q];
+          s64(R::RI_LO + q) = rilo[q];
+          s64(R::RI_HI + q) = rihi[q];
+          s8(R::B_RIFROM + q) = (uint8_t)(rifrom >> (8 * q));
+          s8(R::B_RIACK + q) = (uint8_t)(riack >> (8 * q));
+        }
       }
     }
     // one header word for the small fields; the run bits follow term, committed

@@ -494,7 +494,7 @@ struct SpaceView {
 enum StatField : uint32_t {
   ST_PASSES = 0, ST_LEADER_COMMITS = 1, ST_FOLLOWER_COMMITS = 2, ST_ESCALATIONS = 3,
   ST_MSGS_IN = 4, ST_MSGS_OUT = 5, ST_LEADER_MSGS_IN = 6, ST_LEADER_MSGS_OUT = 7,
-  ST_REPLICATE_ENTRIES = 8, ST_BAILED = 9, NSTAT = 16
+  ST_REPLICATE_ENTRIES = 8, ST_BAILED = 9, ST_CHURN = 10, NSTAT = 16
 };
 // Per-lane counters of one pass (reduced per workgroup into the stats rows).
 // "leader" = the lane ended the pass as leader; entries = sum of n over the
@@ -502,7 +502,8 @@ enum StatField : uint32_t {
 struct LaneStats {
   uint32_t leader_commit = 0, follower_commit = 0, escalated = 0;
   uint32_t msgs_in = 0, msgs_out = 0, leader_in = 0, leader_out = 0, entries = 0;
-  uint32_t bailed = 0;  // stepped by the general kernel
+  uint32_t bailed = 0;  // left the lean kernels (stepped by the tick, churn or general lane)
+  uint32_t churn = 0;   // ... and finished by the churn lane (gr_churn.h)
 };
 
 // Route modes: where lane i reads (dir 0) / writes (dir 1) the mailbox of
@@ -565,6 +566,16 @@ struct StepParams {
   // lanes handed to the general kernel go to lists keyed by handler class
   // (gr_kernels.h general_bin) instead of by role and workgroup
   uint8_t bin_general;
+  // the tail hint (gr_kernels.h kTailAll): one word of host-visible pinned
+  // memory the general kernel writes after each split pass (did the role
+  // instances have work, how many lanes the general kernel stepped), which the
+  // host reads, unsynchronised, to size the next launches' grids; nullptr: off
+  uint32_t* tail_hint;
+  // which tail launches a pass makes (gr_kernels.h TailPlan): 0 = from the
+  // tail hint; 1 = role instances and the churn kernel always; 2 = neither (the
+  // general kernel steps the listed waves and every hand-over); 3 = role
+  // instances always, no churn kernel (round 4's schedule). GR_TAIL_MODE at gr_create.
+  uint8_t tail_mode;
 };
 constexpr uint32_t kWaveClockWords = 8;
 // The wave's clock for GR_WAVE_CLOCK phase marks (0 when off, and in host builds).

@@ -14,6 +14,7 @@
 #include "gr_steady.h"
 #include "gr_host.h"
 #include "gr_lane.h"
+#include "gr_churn.h"
 #include "gr_tick.h"
 
 #ifdef GR_BAIL_TRACE
@@ -39,7 +40,8 @@ using namespace gr::host;
 
 namespace {
 
-static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0, g_tick_lanes = 0, g_steady_lanes = 0, g_steady_leaders = 0;
+static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0, g_tick_lanes = 0, g_steady_lanes = 0, g_steady_leaders = 0,
+                g_churn_lanes = 0;
 static uint32_t g_hint_salt = 0;  // varies the drawn wave hints from call to call
 static bool g_true_hints = false;  // hl_true_hints: every wave gets the device's hint (diagnostics)
 
@@ -47,7 +49,7 @@ template <int S>
 void run_lanes(const StepParams& kp) {
   // the kernel's two passes: the steady-state subset first, the general lane
   // for the lanes it bails on (tests the bail leaves no trace)
-  std::vector<uint32_t> bailed;
+  std::vector<uint32_t> bailed, listed;
   for (uint32_t i = 0; i < kp.n_lanes; ++i) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     LaneStats ls;
@@ -120,6 +122,11 @@ void run_lanes(const StepParams& kp) {
       // lanes in closed form, ticks and ReadIndex straight to the tick lane
       done = q0 == QS_DONE;
       g_steady_lanes += done;
+    } else if (split && (((i >> 6) + (g_hint_salt >> 4)) & 7u) == 3u) {
+      // a listed wave of a pass whose role instances did not run (gr_kernels.h
+      // TailPlan, GM_LISTED): the general kernel steps it with the general lane
+      listed.push_back(i);
+      continue;
     } else if (fk == FL_LEADER) {
       done = fast_step<S, FL_LEADER>(kp, i, p, &ls, nullptr, hint);
     } else if (fk == FL_FOLLOWER) {
@@ -138,6 +145,14 @@ void run_lanes(const StepParams& kp) {
     if (!done) bailed.push_back(i);
     else GR_CHECK_STATE(kp.st, p);
   }
+  for (uint32_t i : listed) {
+    const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+    LaneStats ls;
+    GR_COVER(TAIL_LISTED);
+    Lane<S> L(kp, i, p);
+    L.step(&ls);
+    GR_CHECK_STATE(kp.st, p);
+  }
   for (uint32_t i : bailed) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     LaneStats ls;
@@ -147,13 +162,25 @@ void run_lanes(const StepParams& kp) {
       g_tick_lanes++;
       continue;
     }
+    // the churn lane (gr_kernels.h gr_churn_kernel) first on three passes in
+    // four, as the device does when the tail hint says the general lists had
+    // work; a lane it hands back stored nothing and the general lane steps it
+    if ((g_hint_salt >> 5) & 3u) {
+      ls = LaneStats{};
+      if (churn_step<S>(kp, i, p, &ls)) {
+        GR_CHECK_STATE(kp.st, p);
+        g_churn_lanes++;
+        continue;
+      }
+    }
+    ls = LaneStats{};
     Lane<S> L(kp, i, p);
     L.step(&ls);
     GR_CHECK_STATE(kp.st, p);
   }
   g_hint_salt += 0x9E3779B9u;
-  g_fast_lanes += kp.n_lanes - bailed.size();
-  g_bailed_lanes += bailed.size();
+  g_fast_lanes += kp.n_lanes - bailed.size() - listed.size();
+  g_bailed_lanes += bailed.size() + listed.size();
 }
 
 uint32_t inst(uint32_t want) { return want <= 1 ? 1 : want <= 3 ? 3 : want <= 5 ? 5 : want <= GR_SMAX ? GR_SMAX : 0; }
@@ -287,6 +314,9 @@ extern "C" void hl_counters(uint64_t* fast, uint64_t* bailed) {
 
 // lanes the heartbeat/ReadIndex/tick lane finished (of the bailed ones)
 extern "C" uint64_t hl_tick_lanes() { return g_tick_lanes; }
+
+// lanes the churn lane finished (of the bailed ones)
+extern "C" uint64_t hl_churn_lanes() { return g_churn_lanes; }
 
 // lanes the split pass's steady kernel emulation finished (gr_steady.h)
 extern "C" uint64_t hl_steady_lanes() { return g_steady_lanes; }

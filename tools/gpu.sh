@@ -1,0 +1,86 @@
+#!/bin/bash
+# tools/gpu.sh — one GPU session as a list of steps, each under its own time
+# limit. A crash, abort or timeout (any status other than 0/1) ends the session;
+# test failures (status 1) are reported and the session goes on.
+#
+#   gpurun -- bash tools/gpu.sh STEP [STEP ...]
+#
+# STEP = KIND[@TAG][:VAR=V,VAR=V...]   (the VARs are set for that step only)
+#   warm              import torch and touch the device (first import is slow)
+#   tests             python -m pytest tests -m gpu ($TESTS selects files/-k)
+#   bench             bench.py $BENCH_ARGS        -> gpurun_out/bench_TAG.log
+#   configs           tools/bench_configs.py $CFG_ARGS -> gpurun_out/cfg_TAG.json
+#   trace             rocprofv3 --kernel-trace --stats of bench.py -> gpurun_out/trace_TAG/
+#   cfgtrace          the same over tools/bench_configs.py $CFG_ARGS
+#   profile           tools/profile.sh (trace + calibrated PMC passes), TAG=...
+#   smoke             __graft_entry__.smoke()
+# Defaults: BENCH_ARGS="--steps 20 --warmup 5 --cpu-baseline off --host-path off".
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+R=$PWD
+: "${BENCH_ARGS:=--steps 20 --warmup 5 --cpu-baseline off --host-path off}"
+: "${CFG_ARGS:=--passes 10}"
+: "${TESTS:=tests}"
+
+fatal() {  # $1 status, $2 step
+  case "$1" in
+    0) return 0 ;;
+    1) echo "[$2] status 1 (failures), continuing" ; return 0 ;;
+    *) echo "[$2] fatal status $1; stopping"; exit "$1" ;;
+  esac
+}
+
+run_step() {
+  local spec="$1" kind tag envs
+  kind="${spec%%[@:]*}"
+  tag="x"
+  [[ "$spec" == *@* ]] && { tag="${spec#*@}"; tag="${tag%%:*}"; }
+  envs=""
+  [[ "$spec" == *:* ]] && envs="${spec#*:}"
+  local -a ev=()
+  if [ -n "$envs" ]; then IFS=',' read -r -a ev <<< "$envs"; fi
+  echo "== $kind tag=$tag env=${envs:-none}"
+  local rc=0
+  case "$kind" in
+    warm)
+      env "${ev[@]}" timeout -k 10 300 python -c "import torch; print(torch.cuda.get_device_name(0))" \
+        > $OUT/warm.log 2>&1; rc=$?; tail -1 $OUT/warm.log ;;
+    tests)
+      env "${ev[@]}" timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v --timeout 240 \
+        --timeout-method thread --durations 15 > $OUT/tests_$tag.log 2>&1; rc=$?; tail -3 $OUT/tests_$tag.log ;;
+    bench)
+      env "${ev[@]}" timeout -k 10 400 python -u bench.py $BENCH_ARGS > $OUT/bench_$tag.log 2>&1; rc=$?
+      python - "$OUT/bench_$tag.log" <<'EOF'
+import json, sys
+for l in open(sys.argv[1]):
+    if l.startswith("{"):
+        d = json.loads(l); r = d.get("roofline", {})
+        print("ms_per_step %.4f  kernel_ms %.4f  general_ms %.4f  value %.3g" %
+              (d["ms_per_step"], r.get("kernel_ms", 0), r.get("general_kernel_ms", 0), d["value"]))
+EOF
+      ;;
+    configs)
+      env "${ev[@]}" timeout -k 10 600 python -u tools/bench_configs.py $CFG_ARGS > $OUT/cfg_$tag.json \
+        2> $OUT/cfg_$tag.err; rc=$?; tail -2 $OUT/cfg_$tag.err ;;
+    trace)
+      ( cd /tmp && export TMPDIR=/tmp && env "${ev[@]}" timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+          -d $R/$OUT/trace_$tag -o t -- python3 $R/bench.py $BENCH_ARGS > $R/$OUT/trace_$tag.log 2>&1 ); rc=$? ;;
+    cfgtrace)
+      ( cd /tmp && export TMPDIR=/tmp && env "${ev[@]}" timeout -k 10 600 rocprofv3 --kernel-trace --stats \
+          -d $R/$OUT/cfgtrace_$tag -o t -- python3 $R/tools/bench_configs.py $CFG_ARGS \
+          > $R/$OUT/cfgtrace_$tag.log 2>&1 ); rc=$? ;;
+    profile)
+      env "${ev[@]}" TAG=$tag timeout -k 10 900 bash tools/profile.sh > $OUT/profile_$tag.log 2>&1; rc=$?
+      tail -3 $OUT/profile_$tag.log ;;
+    smoke)
+      env "${ev[@]}" timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
+        > $OUT/smoke.log 2>&1; rc=$?; tail -1 $OUT/smoke.log ;;
+    *) echo "unknown step $kind"; exit 2 ;;
+  esac
+  fatal $rc "$kind@$tag"
+}
+
+for s in "$@"; do run_step "$s"; done
+echo "session done"
