@@ -107,6 +107,11 @@ constexpr uint32_t kListedWord = 1;
 constexpr uint32_t kGeneralNext = 2;
 // Word 3: the churn kernel's next 64-lane chunk (as kGeneralNext).
 constexpr uint32_t kChurnNext = 3;
+// Tail kernel modes (TailPlan): the general kernel walks the churn leftover lists
+// instead of the general lists (the churn kernel ran); GM_RETRY: the retry lists
+// (32..39) hold lanes no role instance stepped (the steady kernel's no_roles
+// mode), so the churn and general kernels walk lists 0..39, not 0..31.
+constexpr uint32_t GM_CHURN_LISTS = 1, GM_RETRY = 2;
 __host__ __device__ inline uint64_t wave_flag_words(uint32_t cap) { return ((uint64_t)cap / 64 + 64) / 4 * 2; }
 // Lanes one tick list can receive: the lanes of every kTickLists-th block, from
 // the steady kernel and the listed role waves (keyed by lane), plus as many
@@ -458,8 +463,22 @@ __global__ __launch_bounds__(kBlock, GR_LISTED_MIN_WAVES) void gr_roles_kernel(S
 // preconditions fail stores nothing and is queued for FastLane (lists 24..31).
 template <int S, int RM>
 __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(StepParams kp, uint32_t* bail_list,
-                                                                               uint32_t* counters, uint32_t list_cap) {
+                                                                               uint32_t* counters, uint32_t list_cap,
+                                                                               const uint32_t* prev_counters) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (kp.tail_hint && i == 0) {
+    // the tail hint (TailPlan) from the previous pass's final counts (the other
+    // counter set: this pass's general kernel zeroes it after this kernel), so
+    // the write to host memory is issued at the start of the pass, not at the
+    // end of its last kernel, where the kernel's completion would wait for it
+    uint32_t nretry = 0, na = 0;
+#pragma unroll
+    for (uint32_t l = 0; l < 8; ++l) nretry += prev_counters[(kRetryList0 + l) * kCounterStride];
+#pragma unroll
+    for (uint32_t l = 0; l < kGeneralLists; ++l) na += prev_counters[l * kCounterStride];
+    const uint32_t roles = prev_counters[kListedWord] || nretry;
+    *(volatile uint32_t*)kp.tail_hint = (roles ? 1u : 0u) | ((na < (1u << 30) ? na : (1u << 30)) << 1);
+  }
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(i >> 6);
   const uint32_t hw = sload_u32(kp.hints + (uint64_t)blockIdx.x * (kBlock / 64));
   const uint32_t hint = (hw >> (8 * (wave & 3))) & 0xFFu;
@@ -472,6 +491,16 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
     const bool active = i < kp.n_lanes;
     const int q = active ? quiet_step<S, RM>(kp, i, i) : QS_DONE;
     tick_append(q == QS_TICK, i, bail_list, counters, list_cap, i);
+    if (kp.no_roles) {
+      // no role instances follow (TailPlan): the rest go straight to the retry
+      // lists, which the churn and general kernels then walk with their own lists
+      bail_append(q == QS_OTHER, kRetryList0 + blockIdx.x % 8, bail_list, counters, list_cap, i);
+      if ((threadIdx.x & 63) == 0) {
+        wave_flags(bail_list, list_cap)[wave] = 0;
+        kp.hints_out[wave] = 0;
+      }
+      return;
+    }
     const uint64_t rem = __ballot(q == QS_OTHER);
     if ((threadIdx.x & 63) == 0) {
       wave_flags(bail_list, list_cap)[wave] = (uint8_t)(rem ? (WF_LISTED | hint) : 0u);
@@ -666,9 +695,10 @@ __device__ inline __attribute__((always_inline)) void churn_append(bool mine, ui
 #endif
 template <int S>
 __global__ __launch_bounds__(kBlock, GR_CHURN_MIN_WAVES) void gr_churn_kernel(StepParams kp, uint32_t* bail_list,
-                                                                           uint32_t* counters, uint32_t list_cap) {
-  ListRange<kGeneralLists> r;
-  r.init(counters, 0, bail_list, list_cap);
+                                                                           uint32_t* counters, uint32_t list_cap,
+                                                                           uint32_t mode) {
+  ListRange<kBailLists> r;
+  r.init(counters, 0, bail_list, list_cap, (mode & GM_RETRY) ? kBailLists : kGeneralLists);
   if (blockIdx.x * kBlock >= r.total()) return;  // no stats row touched
   LaneStats acc;
   walk_chunks(r, counters, kChurnNext, [&](uint32_t i, uint32_t l, bool valid) {
@@ -685,41 +715,25 @@ __global__ __launch_bounds__(kBlock, GR_CHURN_MIN_WAVES) void gr_churn_kernel(St
         back = true;
       }
     }
-    churn_append(back, l >> 1, i, bail_list, counters, list_cap);
+    // a retry lane (no role instance ran) joins the last class
+    churn_append(back, l < kGeneralLists ? l >> 1 : kChurnLists - 1, i, bail_list, counters, list_cap);
   });
   if (kp.stats) block_stats(kp, acc);
 }
 
-// Tail kernel modes (TailPlan): the general kernel walks the churn leftover lists
-// instead of the general lists (the churn kernel ran), and/or steps the waves the
-// steady kernel listed and the lanes it left (the role instances did not run).
-constexpr uint32_t GM_CHURN_LISTS = 1, GM_LISTED = 2;
-
 // Pass 2b: the general lane (every handler, escalation with prefix re-run)
-// over the handed-over lanes, grid-stride over the concatenated lists; also
-// clears the counters the next pass's kernels will use, and reports the pass
-// to the host (StepParams::tail_hint).
+// over the handed-over lanes, in 64-lane chunks of the concatenated lists; also
+// clears the counters the next pass's kernels will use.
 #ifndef GR_GENERAL_MIN_WAVES
 #define GR_GENERAL_MIN_WAVES 1  // A/B builds: waves per SIMD for the general kernel
 #endif
-// LISTED: the instance for mode GM_LISTED (a pass whose role instances did not
-// run); its listed-wave source keeps more state live across the general lane
-// (460 vs 156 B of scratch per lane), so the other passes run the instance
-// without it.
-template <int S, bool LISTED>
+template <int S>
 __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(StepParams kp, const uint32_t* bail_list,
                                                          uint32_t* counters, uint32_t* next_counters,
                                                          uint32_t list_cap, uint32_t mode) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t listed = (uint32_t)__builtin_amdgcn_readfirstlane(counters[kListedWord]);
-  uint32_t nretry = 0;  // lanes the steady kernel left
-#pragma unroll
-  for (uint32_t l = 0; l < 8; ++l) nretry += counters[(kRetryList0 + l) * kCounterStride];
-  uint32_t na = 0;  // the general lists' total: what the churn kernel would take next time
-#pragma unroll
-  for (uint32_t l = 0; l < kGeneralLists; ++l) na += counters[l * kCounterStride];
-  if (kp.tail_hint && blockIdx.x == 0 && threadIdx.x == 0)  // the next passes' tail plan (kTailAll)
-    *(volatile uint32_t*)kp.tail_hint = ((listed || nretry) ? 1u : 0u) | ((na < (1u << 30) ? na : (1u << 30)) << 1);
+  ListRange<kBailLists> rl;
+  if (mode & GM_CHURN_LISTS) rl.init(counters, kChurnCounter0, bail_list + churn_off(list_cap), list_cap, kChurnLists);
+  else rl.init(counters, 0, bail_list, list_cap, (mode & GM_RETRY) ? kBailLists : kGeneralLists);
   if (blockIdx.x == 0 && threadIdx.x < kCounters) next_counters[threadIdx.x * kCounterStride] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters) next_counters[kListedWord] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters + 1) next_counters[kGeneralNext] = 0;
@@ -729,104 +743,25 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
   uint32_t l0 = ~0u;            // ... and the list (handler class) of the lane's first round
   bool any = false;
   const uint64_t t0 = kp.wclock ? wall_clock64() : 0;
-  // One loop, one call site of the general lane (each inlined copy of Lane::step
-  // costs code and scratch): every iteration takes 64 lanes of this wave from the
-  // current source. Sources, in order: the waves the steady kernel listed and the
-  // lanes it left (GM_LISTED: the role instances did not run), then the general
-  // or churn lists in 64-lane chunks (walk_chunks' scheme: the wave's grid index
-  // first, later chunks from the counter).
-  const uint32_t W = gridDim.x * (kBlock / 64);
-  const uint32_t g = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
-  const uint8_t* wf = wave_flags(const_cast<uint32_t*>(bail_list), list_cap);
-  const uint64_t* wm = wave_masks(const_cast<uint32_t*>(bail_list), list_cap);
-  const uint32_t nw = (kp.n_lanes + 63) / 64;
-  // the lists: the retry lists while source 1 runs, then the general or churn lists
-  ListRange<kGeneralLists> rl;
-  const bool use_churn = mode & GM_CHURN_LISTS;
-  auto lists_init = [&] {
-    if (use_churn) rl.init(counters, kChurnCounter0, bail_list + churn_off(list_cap), list_cap, kChurnLists);
-    else rl.init(counters, 0, bail_list, list_cap);
-  };
-  // source 0: listed waves (r: the group of 64 grid-strided waves, todo: its
-  // listed ones left); 1: retry lanes (x0: this wave's next 64); 2: the lists
-  uint32_t src = (LISTED && (mode & GM_LISTED)) ? (listed ? 0u : 1u) : 2u;
-  if (src == 2) lists_init();
-  else rl.init(counters, kRetryList0, bail_list + (uint64_t)kRetryList0 * list_cap, list_cap, 8);
-  uint32_t r = 0, x0 = g * 64;
-  uint64_t todo = 0;
-  bool todo_loaded = false;
-  uint32_t chunk = g;
-  for (;;) {  // wave-uniform
-    bool valid = false;
-    uint32_t i = 0, l = 0;
-    if (LISTED && src == 0) {
-      if (!todo_loaded) {
-        if (g + (uint64_t)W * r >= nw) {
-          src = 1;
-          continue;
-        }
-        const uint64_t idx = g + (uint64_t)W * (r + lane);
-        const uint32_t f = idx < nw ? (uint32_t)wf[idx] : 0u;
-        todo = __ballot(f & WF_LISTED);
-        todo_loaded = true;
-      }
-      if (!todo) {
-        r += 64;
-        todo_loaded = false;
-        continue;
-      }
-      const uint32_t b = (uint32_t)__ffsll((unsigned long long)todo) - 1;
-      todo &= todo - 1;
-      const uint32_t wave = g + W * (r + b);
-      valid = (wm[wave] >> lane) & 1ull;
-      i = wave * 64 + lane;
-      if (lane == 0) kp.hints_out[wave] = 0;  // the role instances would have written one
-      if (valid) GR_COVER(TAIL_LISTED);
-    } else if (LISTED && src == 1) {
-      if (x0 >= rl.total()) {
-        src = 2;
-        lists_init();
-        continue;
-      }
-      const uint32_t x = x0 + lane;
-      if (x < rl.total()) {
-        i = rl.at(x, &l);
-        valid = true;
-      }
-      x0 += W * 64;
-    } else {
-      const uint32_t n = rl.total();
-      if (chunk * 64 >= n) break;
-      const uint32_t x = chunk * 64 + lane;
-      if (x < n) {
-        i = rl.at(x, &l);
-        valid = true;
-        l0 = l0 == ~0u ? l : l0;
-      }
-      if ((uint64_t)W * 64 >= n) {
-        chunk = n / 64 + 1;  // the first chunks covered every lane: no atomic
-      } else {
-        uint32_t c = 0;
-        if (lane == 0) c = W + atomicAdd(counters + kGeneralNext, 1u);
-        chunk = (uint32_t)__shfl((int)c, 0);
-      }
+  // The lists run leader classes first, so the chunks handed out late are
+  // followers' (the lighter classes: GR_WAVE_CLOCK).
+  walk_chunks(rl, counters, kGeneralNext, [&](uint32_t i, uint32_t l, bool valid) {
+    if (!valid) return;
+    any = true;
+    l0 = l0 == ~0u ? l : l0;
+    const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
+    LaneStats ls;
+    Lane<S> L(kp, i, p);
+    L.step(&ls);
+    GR_CHECK_STATE(kp.st, p);
+    stats_add(acc, ls);
+    acc.bailed += 1;
+    if (!tph[0]) {
+      tph[0] = L.tclk[0];
+      tph[1] = L.tclk[1];
+      tph[2] = L.tclk[2];
     }
-    if (valid) {
-      any = true;
-      const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-      LaneStats ls;
-      Lane<S> L(kp, i, p);
-      L.step(&ls);
-      GR_CHECK_STATE(kp.st, p);
-      stats_add(acc, ls);
-      acc.bailed += 1;
-      if (!tph[0]) {
-        tph[0] = L.tclk[0];
-        tph[1] = L.tclk[1];
-        tph[2] = L.tclk[2];
-      }
-    }
-  }
+  });
   if (kp.wclock && __ballot(any)) {  // profiling: this wave's span and what it stepped
     const uint64_t t1 = wall_clock64();
     const uint32_t nl = wave_sum(acc.bailed), nm = wave_sum(acc.msgs_in), ne = wave_sum(acc.escalated),
@@ -933,19 +868,22 @@ struct PassTiming {
 
 // The tail plan: which optional launches a pass makes after its lean kernels.
 // Every tail launch but the general kernel's is optional for correctness: the
-// general lane handles any lane (it steps listed waves itself when the role
-// instances do not run, and every hand-over when the churn kernel does not). So
-// the host decides from the last pass the device has reported (StepParams::
-// tail_hint, written by the general kernel into host-visible memory and read
-// here without synchronising: one or more passes back). In the steady state
-// nothing is listed and nothing handed over: the pass is the steady kernel and
-// one empty general launch. A launch with nothing to do costs its workgroups'
-// dispatch (round-5 A/B, 1M x 3: steady kernel alone 0.0622 ms per pass, with
-// the round-4 tail of role instances + general kernel 0.0671).
+// general lane handles any lane (the lanes no role instance steps reach it
+// through the retry lists, GM_RETRY; every hand-over when the churn kernel does
+// not run). So the host decides from the last pass the device has reported
+// (StepParams::tail_hint, written by the steady kernel of each split pass from
+// the previous pass's counts into host-visible memory, read here without
+// synchronising: one or more passes back). In the steady state nothing is
+// listed: the pass is the steady kernel and one empty general launch. A launch
+// with nothing to do costs its workgroups' dispatch (round-5 A/B, 1M x 3: steady
+// kernel alone 0.0622 ms per pass, with the round-4 tail of role instances +
+// general kernel 0.0671).
+// The churn kernel (gr_churn.h) runs only when forced (GR_TAIL_MODE=1): as a
+// launch of its own it measured slower on config 5 (296 vs 246 us per pass, one
+// A/B call, round 5): it took 25.7k of the 53.5k hand-overs, but the general
+// kernel's span is its slowest wave's chain of dependent scattered loads, which
+// half the lanes did not shorten.
 constexpr uint32_t kTailAll = 0xFFFFFFFFu;  // no report yet: every launch
-// the churn kernel when the last reported pass handed at least this many lanes to
-// the general lists
-constexpr uint32_t kChurnMinLanes = 1;
 inline uint32_t tail_word(const StepParams& kp) {
   return kp.tail_hint ? __atomic_load_n(kp.tail_hint, __ATOMIC_RELAXED) : kTailAll;
 }
@@ -958,7 +896,7 @@ inline TailPlan tail_plan(const StepParams& kp) {
     case 1: return {true, true};
     case 2: return {false, false};
     case 3: return {true, false};
-    default: return {(th & 1u) != 0, (th >> 1) >= kChurnMinLanes};
+    default: return {(th & 1u) != 0, false};
   }
 }
 // The churn kernel's grid: resident capacity at two waves per SIMD (GR_CHURN_BLOCKS
@@ -1024,24 +962,25 @@ inline uint32_t skip_tail_from() {
   return v;
 }
 
-// *listed_left: the steady kernel ran and the role instances did not (the general
-// kernel steps the listed waves, GM_LISTED).
+// *retry_left: the steady kernel ran without role instances after it (no_roles:
+// the lanes it did not finish are in the retry lists, GM_RETRY).
 template <int S, int RM>
-hipError_t launch_fast(const StepParams& kp0, uint32_t blocks, uint32_t* bail_list, uint32_t* cur, uint32_t list_cap,
-                       hipStream_t s, bool skip_tail, bool roles, bool* listed_left) {
+hipError_t launch_fast(const StepParams& kp0, uint32_t blocks, uint32_t* bail_list, uint32_t* cur, uint32_t* prev,
+                       uint32_t list_cap, hipStream_t s, bool skip_tail, bool roles, bool* retry_left) {
   StepParams kp = kp0;
-  *listed_left = false;
+  *retry_left = false;
   if (kp.hints && kp.split) {  // a large pass: the role instances
     // the steady kernel steps lane i = peer i with compile-time routes
     if (RM != RM_ANY && !kp.has_lane_peer) {
       // the steady lanes, then the role instances over the waves it listed and
       // the lanes it left
+      kp.no_roles = roles ? 0 : 1;
       hipLaunchKernelGGL((gr_steady_kernel<S, RM>), dim3(blocks), dim3(kBlock), steady_lds(), s, kp, bail_list, cur,
-                         list_cap);
+                         list_cap, (const uint32_t*)prev);
       const hipError_t e0 = hipGetLastError();
       if (e0 != hipSuccess || skip_tail) return e0;
       if (!roles) {
-        *listed_left = true;
+        *retry_left = true;
         return hipSuccess;
       }
       const uint32_t rb = blocks < role_blocks() ? blocks : role_blocks();
@@ -1093,13 +1032,16 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   const bool loop1 = kp.route_mode == RT_LOOPBACK && kp.in.n_chunks == 1 && kp.out.n_chunks == 1;
   const bool skip = skip_tail_from() && parity >= skip_tail_from();
   const TailPlan plan = tail_plan(kp);
-  bool listed_left = false;
+  bool retry_left = false;
+  StepParams kq = kp;
+  if (parity < 2) kq.tail_hint = nullptr;  // the first passes' counts describe no steady state yet
   if (loop1)
-    err = launch_fast<S, RT_LOOPBACK>(kp, blocks, bail_list, cur, list_cap, s, skip, plan.roles, &listed_left);
+    err = launch_fast<S, RT_LOOPBACK>(kq, blocks, bail_list, cur, nxt, list_cap, s, skip, plan.roles, &retry_left);
   else if (kp.route_mode == RT_AFFINE)
-    err = launch_fast<S, RT_AFFINE>(kp, blocks, bail_list, cur, list_cap, s, skip, plan.roles, &listed_left);
+    err = launch_fast<S, RT_AFFINE>(kq, blocks, bail_list, cur, nxt, list_cap, s, skip, plan.roles, &retry_left);
   else
-    err = launch_fast<S, RM_ANY>(kp, blocks, bail_list, cur, list_cap, s, skip, plan.roles, &listed_left);
+    err = launch_fast<S, RM_ANY>(kq, blocks, bail_list, cur, nxt, list_cap, s, skip, plan.roles, &retry_left);
+  const uint32_t mode = (plan.churn ? GM_CHURN_LISTS : 0u) | (retry_left ? GM_RETRY : 0u);
   if (err != hipSuccess) return err;
   if (t && (err = hipEventRecord(t->ev[1], s)) != hipSuccess) return err;
   if (skip) return t ? hipEventRecord(t->ev[2], s) : hipSuccess;
@@ -1110,7 +1052,7 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   }
   if (plan.churn) {  // the churn lane first; the general kernel then walks its leftovers
     const uint32_t cblocks = blocks < churn_blocks() ? blocks : churn_blocks();
-    hipLaunchKernelGGL(gr_churn_kernel<S>, dim3(cblocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
+    hipLaunchKernelGGL(gr_churn_kernel<S>, dim3(cblocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap, mode);
     if ((err = hipGetLastError()) != hipSuccess) return err;
   }
   uint32_t gblocks = blocks < general_blocks() ? blocks : general_blocks();
@@ -1118,13 +1060,8 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   if (kp.wclock &&
       (err = hipMemsetAsync(kp.wclock, 0, (size_t)gblocks * (kBlock / 64) * kWaveClockWords * 8, s)) != hipSuccess)
     return err;
-  const uint32_t mode = (plan.churn ? GM_CHURN_LISTS : 0u) | (listed_left ? GM_LISTED : 0u);
-  if (listed_left)
-    hipLaunchKernelGGL((gr_step_kernel<S, true>), dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list,
-                       cur, nxt, list_cap, mode);
-  else
-    hipLaunchKernelGGL((gr_step_kernel<S, false>), dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list,
-                       cur, nxt, list_cap, mode);
+  hipLaunchKernelGGL(gr_step_kernel<S>, dim3(gblocks), dim3(kBlock), 0, s, kp, (const uint32_t*)bail_list, cur, nxt,
+                     list_cap, mode);
   if ((err = hipGetLastError()) != hipSuccess) return err;
   if (t && (err = hipEventRecord(t->ev[2], s)) != hipSuccess) return err;
   return hipSuccess;

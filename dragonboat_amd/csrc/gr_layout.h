@@ -576,6 +576,9 @@ struct StepParams {
   // general kernel steps the listed waves and every hand-over); 3 = role
   // instances always, no churn kernel (round 4's schedule). GR_TAIL_MODE at gr_create.
   uint8_t tail_mode;
+  // set by the launcher for the steady kernel of a pass whose role instances do
+  // not run: its non-steady lanes go to the retry lists (gr_kernels.h GM_RETRY)
+  uint8_t no_roles;
 };
 constexpr uint32_t kWaveClockWords = 8;
 // The wave's clock for GR_WAVE_CLOCK phase marks (0 when off, and in host builds).

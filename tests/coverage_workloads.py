@@ -199,9 +199,10 @@ def device_battery(lib_path):
     import os
     import devsim
     out = {}
-    saved = {k: os.environ.get(k) for k in ("GR_SPLIT_MIN_LANES", "GR_SMALL_BLOCKS")}
-    os.environ["GR_SPLIT_MIN_LANES"] = "1"  # both read at gr_create
+    saved = {k: os.environ.get(k) for k in ("GR_SPLIT_MIN_LANES", "GR_SMALL_BLOCKS", "GR_TAIL_MODE")}
+    os.environ["GR_SPLIT_MIN_LANES"] = "1"  # all three read at gr_create
     os.environ["GR_SMALL_BLOCKS"] = "0"     # not the fused small-pass kernel
+    os.environ["GR_TAIL_MODE"] = "1"        # the role instances and the churn kernel (gr_churn.h) every pass
     try:
         G, R = 1024, 3
         topo = P.Topology(G, R)

@@ -123,8 +123,8 @@ void run_lanes(const StepParams& kp) {
       done = q0 == QS_DONE;
       g_steady_lanes += done;
     } else if (split && (((i >> 6) + (g_hint_salt >> 4)) & 7u) == 3u) {
-      // a listed wave of a pass whose role instances did not run (gr_kernels.h
-      // TailPlan, GM_LISTED): the general kernel steps it with the general lane
+      // a lane of a pass whose role instances did not run (gr_kernels.h TailPlan,
+      // GM_RETRY): the steady kernel lists it for the general kernel
       listed.push_back(i);
       continue;
     } else if (fk == FL_LEADER) {
@@ -148,7 +148,6 @@ void run_lanes(const StepParams& kp) {
   for (uint32_t i : listed) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     LaneStats ls;
-    GR_COVER(TAIL_LISTED);
     Lane<S> L(kp, i, p);
     L.step(&ls);
     GR_CHECK_STATE(kp.st, p);
