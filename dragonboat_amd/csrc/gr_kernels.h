@@ -559,11 +559,14 @@ __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(Step
   }
   __syncthreads();
   const uint32_t n = tstart[kTickLists];
-  if (blockIdx.x * kBlock >= n) return;
+  // one-wave workgroups by default (tick_wg): a config-3 pass hands ~50k lanes to
+  // this kernel, 196 workgroups of 256 lanes would leave 60 of the 256 CUs idle
+  const uint32_t bw = blockDim.x;
+  if (blockIdx.x * bw >= n) return;
   const uint32_t* tl = bail_list + tick_off(list_cap);
   const uint64_t tc = tick_cap(list_cap);
   LaneStats acc;
-  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+  for (uint32_t base = blockIdx.x * bw; base < n; base += gridDim.x * bw) {
     const uint32_t x = base + threadIdx.x;
     bool hand = false;
     uint32_t i = 0;
@@ -592,7 +595,8 @@ __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(Step
     general_append<S>(kp, hand, false, i, hand && kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i, blockIdx.x,
                       bail_list, counters, list_cap);
   }
-  if (kp.stats) block_stats(kp, acc);
+  // stats rows belong to 256-lane workgroups: smaller workgroups share them
+  if (kp.stats) block_stats(kp, acc, blockIdx.x * bw / kBlock);
 }
 
 // The lists a tail kernel walks: nl <= NL lists (list l at base + l * stride
@@ -882,7 +886,9 @@ struct PassTiming {
 // launch of its own it measured slower on config 5 (296 vs 246 us per pass, one
 // A/B call, round 5): it took 25.7k of the 53.5k hand-overs, but the general
 // kernel's span is its slowest wave's chain of dependent scattered loads, which
-// half the lanes did not shorten.
+// half the lanes did not shorten. Inlined into the role instances instead (the
+// lanes FastLane hands over, in the same wave) it raised their kernel to 255
+// VGPRs, one wave per SIMD: config 5 400 us per pass (role instances 109 -> 281).
 constexpr uint32_t kTailAll = 0xFFFFFFFFu;  // no report yet: every launch
 inline uint32_t tail_word(const StepParams& kp) {
   return kp.tail_hint ? __atomic_load_n(kp.tail_hint, __ATOMIC_RELAXED) : kTailAll;
@@ -911,8 +917,17 @@ inline uint32_t churn_blocks() {
   return v;
 }
 
-// The tick kernel's grid: its lanes are at most the active share of a pass.
+// The tick kernel's grid: its lanes are at most the active share of a pass
+// (kTickBlocks x 256 lanes in flight, in workgroups of tick_wg() lanes).
 constexpr uint32_t kTickBlocks = 1024;
+inline uint32_t tick_wg() {  // GR_TICK_WG=256 (A/B runs): round 4's 256-lane workgroups
+  static const uint32_t v = [] {
+    const char* e = getenv("GR_TICK_WG");
+    const long x = e ? strtol(e, nullptr, 10) : 0;
+    return (x == 64 || x == 128 || x == 256) ? (uint32_t)x : 64u;
+  }();
+  return v;
+}
 
 // The role instances' grid when they scan the wave flags: enough waves to fill
 // the chip at their occupancy; with no listed wave each wave reads its flags
@@ -1046,8 +1061,9 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   if (t && (err = hipEventRecord(t->ev[1], s)) != hipSuccess) return err;
   if (skip) return t ? hipEventRecord(t->ev[2], s) : hipSuccess;
   if (tick_lanes) {  // some lane may carry ticks or a ReadIndex (LW_OTHER)
-    const uint32_t tblocks = blocks < kTickBlocks ? blocks : kTickBlocks;
-    hipLaunchKernelGGL(gr_tick_kernel<S>, dim3(tblocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap);
+    const uint32_t tw = tick_wg(), tmax = kTickBlocks * (kBlock / tw);
+    const uint32_t tblocks = blocks * (kBlock / tw) < tmax ? blocks * (kBlock / tw) : tmax;
+    hipLaunchKernelGGL(gr_tick_kernel<S>, dim3(tblocks), dim3(tw), 0, s, kp, bail_list, cur, list_cap);
     if ((err = hipGetLastError()) != hipSuccess) return err;
   }
   if (plan.churn) {  // the churn lane first; the general kernel then walks its leftovers

@@ -95,6 +95,10 @@ class GpuCompactBackend(GpuBackend):
         cm = self.eng.pair_messages(cm)  # the device takes GR_CM_PAIR records as two messages
         cl, xl = self.eng.pack_locals(loc)
         om, ox, cr, rx = self.eng.step_compact(cm, xm, cl, xl, halves=self.halves)
+        return self.expand(om, ox, cr, rx, loc)
+
+    def expand(self, om, ox, cr, rx, loc):
+        """Compact outputs -> full outbox and result records (the Lockstep's form)."""
         out = self.eng.unpack_messages(om, ox)
         res = np.zeros(len(cr), abi.RESULT)
         for f in ("peer", "escalation", "propose_result", "last_index"):
@@ -151,6 +155,21 @@ class GpuWireBackend(GpuBackend):
     def close(self):
         self.feed.close()
         super().close()
+
+
+class GpuWireCompactBackend(GpuWireBackend):
+    """The wire path with the compact outbox (gr_step_wire_compact): frames in,
+    24-B gr_cmsg / gr_cresult records (ext records where they do not fit) out,
+    expanded as GpuCompactBackend expands gr_step_compact's."""
+    result_fields = GpuCompactBackend.result_fields
+    expand = GpuCompactBackend.expand
+
+    def step(self, msgs, loc):
+        dm, nm, de, ne, keep = self.feed.decode(msgs)
+        got, idx, why = self.eng.step_wire(dm, nm, de, ne, loc, compact=True)
+        assert len(idx) == 0, [abi.WIRE_REASONS[w] for w in why[:4]]
+        om, ox, cr, rx = got
+        return self.expand(om, ox, cr, rx, loc)
 
 
 def res_esc_free(res, n):

@@ -35,6 +35,23 @@ def test_wire_path_ticks_read_index(gpu):
     assert st["ready"] > 0
 
 
+def test_wire_compact_at_scale_churn_heartbeats(gpu):
+    """gr_step_wire_compact (frames in, compact records out) at BASELINE config 5's
+    size, 100k x 3, against the oracle after every pass: leader changes with
+    p = 0.1 from the second pass (step-downs, term adoptions, rejects, truncations,
+    multi-entry catch-ups), and a Tick on every replica every third pass (leader
+    heartbeats and their acks: full records through the codec and back)."""
+    G, R = 100_000, 3
+    topo = P.Topology(G, R)
+    rng = np.random.default_rng(55)
+
+    def locals_fn(k, s):
+        return P.propose_locals(R * G, P.current_leaders(s, topo), pass_index=k, ticks=1 if k % 3 == 2 else 0)
+    st = SIM.simulate(SIM.GpuWireCompactBackend, P.make_groups(G, R, seed=55), topo, 6, locals_fn,
+                      inject_fn=lambda k, cur: P.inject_leader_change(cur, topo, 0.1, rng) if k >= 1 else None)
+    assert st["commits"] > 0 and st["msgs"] > 3 * G
+
+
 def test_wire_unrouted_reasons(gpu):
     """Messages the device cannot step stay with the host, each with its reason;
     the others step exactly as gr_step steps the same records."""
