@@ -481,7 +481,8 @@ def main():
     G = args.groups
     # N > 1: BASELINE config 4 (replicas on distinct GPUs, RCCL all-to-all per pass)
     placement = args.placement or ("spread" if world > 1 else "local")
-    pipe = Pipeline(G, R, S, world, rank, placement, banks=args.banks)
+    codec = os.environ.get("GR_BENCH_CODEC", "cx")  # the spread exchange's form (exchange.py)
+    pipe = Pipeline(G, R, S, world, rank, placement, banks=args.banks, codec=codec)
     pipe.setup(Engine, dev, ordinal)
 
     for k in range(args.warmup):
@@ -526,6 +527,7 @@ def main():
     pipe.synchronize()
     tm = pipe.timing_end()
     xbytes = pipe.exchange_bytes_per_pass()
+    xbytes_heavy = pipe.exchange_bytes_per_pass(heavy=True)
     banks = len(pipe.ex)
     pipe.close()
     commits = st["leader_commits"]
@@ -584,6 +586,8 @@ def main():
             "launch": "graph (gr_graph_replay of a captured two-pass graph)" if use_graph else "stream (kernel launches)",
             "escalations": esc,
             "exchange_bytes_per_pass": xbytes,
+            "exchange_bytes_heavy_pass": xbytes_heavy,
+            "exchange_codec": codec if placement == "spread" and world > 1 else None,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"lean kernels of one pass (gr_steady_kernel<{S}> + gr_roles_kernel<{S}>, the role instances in one launch)",

@@ -163,7 +163,8 @@ EXPORTS = [
     "gr_load_peers", "gr_sync_peers_to_host", "gr_notify_applied", "gr_compact_log", "gr_commit_update", "gr_space_bytes", "gr_space_chunk_bytes",
     "gr_space_hot_chunk_bytes", "gr_space_hot_tile_bytes", "gr_space_tile_positions", "gr_space_cold_used",
     "gr_space_side_bytes", "gr_space_side_pack", "gr_space_side_unpack", "gr_space_side_pack_host",
-    "gr_space_side_unpack_host", "gr_bind_routes",
+    "gr_space_side_unpack_host", "gr_space_cx_bytes", "gr_space_cx_pack", "gr_space_cx_unpack",
+    "gr_space_cx_pack_host", "gr_space_cx_unpack_host", "gr_bind_routes",
     "gr_set_locals", "gr_step_device", "gr_step_compact", "gr_step_compact_begin", "gr_step_compact_end", "gr_cinbox_reserve", "gr_release_coutbox",
     "gr_pack_messages", "gr_unpack_messages", "gr_cmsg_count", "gr_pair_messages", "gr_pack_locals",
     "gr_collect_results", "gr_space_decode", "gr_space_encode", "gr_timing_begin", "gr_timing_end",

@@ -713,6 +713,123 @@ int gr_space_side_unpack_host(void* space_host, uint32_t n_chunks, uint32_t posi
   return GR_OK;
 }
 
+uint64_t gr_space_cx_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth, const uint32_t* capacities,
+                           uint32_t side_capacity) {
+  if (depth == 0 || depth > GR_C || !capacities || n_chunks > io::kCxMaxChunks) return 0;
+  return io::cx_caps(space_pad_positions(positions), depth, n_chunks, capacities, side_capacity).off[n_chunks];
+}
+
+#define GR_CX_ARGS_OK(space, cx, depth, n_chunks, capacities)                                                  \
+  ((space) && (cx) && (capacities) && (depth) > 0 && (depth) <= GR_C && (n_chunks) > 0 &&                     \
+   (n_chunks) <= io::kCxMaxChunks)
+
+int gr_space_cx_pack(void* space, uint32_t n_chunks, uint32_t positions, uint32_t depth, void* cx,
+                     const uint32_t* capacities, uint32_t side_capacity, void* stream) {
+  if (!GR_CX_ARGS_OK(space, cx, depth, n_chunks, capacities)) return GR_EINVAL;
+  const hipStream_t s = (hipStream_t)stream;
+  const SpaceView v = make_view(space, n_chunks, positions, depth);
+  const io::CxCaps C = io::cx_caps(v.pc, depth, n_chunks, capacities, side_capacity);
+  for (uint32_t c = 0; c < n_chunks; ++c) HIPCHK(hipMemsetAsync((uint8_t*)cx + C.off[c], 0, io::kCxHdr, s));
+  hipLaunchKernelGGL(io::cx_pack, dim3(io_grid((size_t)n_chunks * v.pc)), dim3(io::kIoBlock), 0, s, v, (uint8_t*)cx,
+                     C);
+  HIPCHK(hipGetLastError());
+  return GR_OK;
+}
+
+int gr_space_cx_unpack(void* space, uint32_t n_chunks, uint32_t positions, uint32_t depth, const void* cx,
+                       const uint32_t* capacities, uint32_t side_capacity, void* stream) {
+  if (!GR_CX_ARGS_OK(space, cx, depth, n_chunks, capacities)) return GR_EINVAL;
+  const hipStream_t s = (hipStream_t)stream;
+  const SpaceView v = make_view(space, n_chunks, positions, depth);
+  const io::CxCaps C = io::cx_caps(v.pc, depth, n_chunks, capacities, side_capacity);
+  hipLaunchKernelGGL(io::cx_unpack_waves, dim3(io_grid((size_t)n_chunks * v.pc)), dim3(io::kIoBlock), 0, s, v,
+                     (const uint8_t*)cx, C);
+  HIPCHK(hipGetLastError());
+  if (side_capacity) {
+    hipLaunchKernelGGL(io::cx_unpack_side, dim3(io_grid((size_t)n_chunks * side_capacity)), dim3(io::kIoBlock), 0, s,
+                       v, (const uint8_t*)cx, C);
+    HIPCHK(hipGetLastError());
+  }
+  return GR_OK;
+}
+
+// The same codec over host memory (tests): records and side entries in position
+// order (the device packer's order may differ; what unpacks does not).
+int gr_space_cx_pack_host(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth, void* cx_host,
+                          const uint32_t* capacities, uint32_t side_capacity) {
+  if (!GR_CX_ARGS_OK(space_host, cx_host, depth, n_chunks, capacities)) return GR_EINVAL;
+  const SpaceView v = make_view(space_host, n_chunks, positions, depth);
+  const io::CxCaps C = io::cx_caps(v.pc, depth, n_chunks, capacities, side_capacity);
+  for (uint32_t c = 0; c < n_chunks; ++c) {
+    const uint32_t capacity = C.cap[c];
+    const io::CxLayout L = io::cx_layout(v.pc, depth, capacity, side_capacity);
+    uint8_t* buf = (uint8_t*)cx_host + C.off[c];
+    memset(buf, 0, io::kCxHdr);
+    uint32_t* nrec = (uint32_t*)buf;
+    uint32_t* nside = nrec + 1;
+    for (uint32_t wl = 0; wl < L.nwv; ++wl) {
+      uint32_t hi = 0;
+      bool have = false;
+      for (uint32_t lane = 0; lane < 64 && !have; ++lane) {
+        const Mailbox mb = v.at(c * v.pc + wl * 64 + lane);
+        uint32_t w3;
+        if (io::cx_record_kind(mb, mb.cnt(), &w3)) {
+          hi = (uint32_t)(mb.u64(0, MF_LOG_INDEX) >> 32);
+          have = true;
+        }
+      }
+      uint64_t mask = 0, lost = 0;
+      const uint32_t base = *nrec;
+      for (uint32_t lane = 0; lane < 64; ++lane) {
+        const uint32_t pos = wl * 64 + lane;
+        const Mailbox mb = v.at(c * v.pc + pos);
+        const uint32_t cb = mb.cnt();
+        uint32_t w3 = 0;
+        const bool rec = io::cx_record_kind(mb, cb, &w3) && (uint32_t)(mb.u64(0, MF_LOG_INDEX) >> 32) == hi;
+        if (rec && *nrec < capacity) {
+          io::cx_put_record(mb, w3, buf, L, (*nrec)++);
+          mask |= 1ull << lane;
+          continue;
+        }
+        if (rec) ++*nrec;  // counted, as the device's atomic counts it
+        if (!mb_n(cb)) continue;
+        if (*nside < side_capacity) io::cx_put_side(mb, cb, pos, buf, L, depth, *nside);
+        else lost |= 1ull << lane;
+        ++*nside;
+      }
+      uint8_t* h = buf + L.waves + (uint64_t)wl * io::kCxWave;
+      ((uint64_t*)h)[0] = mask;
+      ((uint64_t*)h)[1] = lost;
+      ((uint32_t*)h)[4] = base;
+      ((uint32_t*)h)[5] = hi;
+    }
+  }
+  return GR_OK;
+}
+
+int gr_space_cx_unpack_host(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
+                            const void* cx_host, const uint32_t* capacities, uint32_t side_capacity) {
+  if (!GR_CX_ARGS_OK(space_host, cx_host, depth, n_chunks, capacities)) return GR_EINVAL;
+  const SpaceView v = make_view(space_host, n_chunks, positions, depth);
+  const io::CxCaps C = io::cx_caps(v.pc, depth, n_chunks, capacities, side_capacity);
+  for (uint32_t c = 0; c < n_chunks; ++c) {
+    const io::CxLayout L = io::cx_layout(v.pc, depth, C.cap[c], side_capacity);
+    const uint8_t* buf = (const uint8_t*)cx_host + C.off[c];
+    for (uint32_t wl = 0; wl < L.nwv; ++wl) {
+      const uint8_t* h = buf + L.waves + (uint64_t)wl * io::kCxWave;
+      for (uint32_t lane = 0; lane < 64; ++lane)
+        io::cx_get_lane(v.at(c * v.pc + wl * 64 + lane), buf, L, ((const uint64_t*)h)[0], ((const uint64_t*)h)[1],
+                        ((const uint32_t*)h)[4], ((const uint32_t*)h)[5], lane);
+    }
+    const uint32_t ns = ((const uint32_t*)buf)[1];
+    for (uint32_t x = 0; x < ns && x < side_capacity; ++x) {
+      const uint8_t* e = buf + L.side + (uint64_t)x * io::cx_side_entry_bytes(depth);
+      io::cx_get_side(v.at(c * v.pc + ((const uint32_t*)e)[0]), e, depth);
+    }
+  }
+  return GR_OK;
+}
+
 int gr_space_encode(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
                     const gr_message* msgs, size_t n, const uint32_t* pos_of_msg) {
   if (!space_host || (n && (!msgs || !pos_of_msg)) || depth == 0 || depth > GR_C) return GR_EINVAL;

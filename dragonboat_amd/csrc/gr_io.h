@@ -584,6 +584,221 @@ __global__ void side_unpack(SpaceView v, const uint8_t* side, uint32_t cap) {
   }
 }
 
+// ---------------------------------------------------------------- compact exchange
+// The spread placement's all-to-all (exchange.py) in a compact
+// form: per chunk a fixed-size buffer (fixed, so the all-to-all split sizes are
+// known without the host reading anything back) that carries only the mailboxes
+// with messages. A uniform mailbox whose messages repeat message 0's hot fields
+// (one message, or a shared pair: gr_layout.h MB_SHARED -- the steady state's
+// commit broadcast + proposal, and their two accepts) travels as a 12-byte
+// record: its term word, the low 32 bits of its LogIndex (the high bits are the
+// wave's, in the wave header), and its count byte with a 24-bit Commit offset
+// (Replicates; |Commit - LogIndex| < 2^23). A mailbox outside that takes the full
+// path. Every other mailbox with messages travels
+// as a full side entry (hot fields of every message and their cold records). An
+// empty mailbox costs one bit. Layout of a chunk's buffer (cx_layout):
+//   header 64 B: u32 records, u32 side entries (the packers' counters)
+//   per 64 positions (a wave): u64 record mask, u64 lost mask, u32 first record,
+//     u32 LogIndex high bits
+//   records, structure of arrays over `cap`: u32 term word, u32 LogIndex low
+//     bits, u32 count byte | Commit offset << 8
+//   side entries (`scap`): u32 position, u32 count byte, u32 term word, u32 pad,
+//     per message (u32 Commit offset, u32 pad, u64 LogIndex), then per message
+//     the kColdUsed bytes of its cold record
+// A mailbox that fits neither (records past `cap`, side entries past `scap`)
+// reaches the receiver as lost (count 1 | MB_COLD_LOST, not uniform): its reader
+// escalates CAPACITY at its first message, as with gr_space_side_pack.
+// In the steady state of BASELINE config 4 at N = 8 a rank sends 4 chunks of
+// 2 x 1M positions, half of them empty with the benchmark's leaders (replica 0:
+// the follower-to-follower slots) and a third with leaders spread evenly:
+// 4 x (cap x 12 B + 31k wave headers x 24 B + side entries) = 58 MB per pass at
+// cap = 0.55 x positions, 70 MB at 0.7, against 328 MB for the hot regions
+// (41 B per position). exchange.py sizes cap.
+constexpr uint32_t kCxHdr = 64, kCxWave = 24;
+__host__ __device__ inline uint32_t cx_side_entry_bytes(uint32_t depth) { return 16 + depth * (16 + kColdUsed); }
+struct CxLayout {
+  uint64_t waves, cb, term, lo, cd, side, bytes;
+  uint32_t nwv, cap, scap;
+};
+__host__ __device__ inline CxLayout cx_layout(uint32_t pc, uint32_t depth, uint32_t cap, uint32_t scap) {
+  CxLayout L;
+  L.nwv = pc / 64;
+  L.cap = cap;
+  L.scap = scap;
+  L.waves = kCxHdr;
+  L.term = round256(kCxHdr + (uint64_t)L.nwv * kCxWave);
+  L.lo = L.term + round256(4ull * cap);
+  L.cb = L.lo + round256(4ull * cap);  // count byte | Commit offset << 8
+  L.cd = L.cb;
+  L.side = L.cb + round256(4ull * cap);
+  L.bytes = L.side + round256((uint64_t)scap * cx_side_entry_bytes(depth));
+  return L;
+}
+// Mailbox mb (count byte cb) travels as a record: its hot fields are message 0's,
+// and a Replicate's Commit offset fits 24 bits (*w: the record's third word).
+__host__ __device__ inline bool cx_record_kind(const Mailbox& mb, uint32_t cb, uint32_t* w) {
+  const uint32_t n = mb_n(cb);
+  if (!(n && (cb & MB_UNIFORM) && (n == 1 || mb_shared(cb)))) return false;
+  if (cb & MB_RESP) {  // an accept has no Commit
+    *w = cb;
+    return true;
+  }
+  const uint32_t d = mb.t32(0, MT_CDELTA) - 0x80000000u + 0x800000u;  // Commit - LogIndex + 2^23
+  *w = cb | (d << 8);
+  return (d >> 24) == 0;
+}
+__host__ __device__ inline void cx_put_record(const Mailbox& mb, uint32_t w, uint8_t* buf, const CxLayout& L,
+                                              uint32_t r) {
+  reinterpret_cast<uint32_t*>(buf + L.term)[r] = mb.mterm();
+  reinterpret_cast<uint32_t*>(buf + L.lo)[r] = (uint32_t)mb.u64(0, MF_LOG_INDEX);
+  reinterpret_cast<uint32_t*>(buf + L.cb)[r] = w;
+}
+__host__ __device__ inline void cx_put_side(const Mailbox& mb, uint32_t cb, uint32_t pos, uint8_t* buf,
+                                            const CxLayout& L, uint32_t depth, uint32_t x) {
+  uint8_t* e = buf + L.side + (uint64_t)x * cx_side_entry_bytes(depth);
+  const uint32_t n = mb_n(cb) < depth ? mb_n(cb) : depth;
+  uint32_t* w = reinterpret_cast<uint32_t*>(e);
+  w[0] = pos;
+  w[1] = cb;
+  w[2] = mb.mterm();
+  w[3] = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    uint32_t* h = reinterpret_cast<uint32_t*>(e + 16 + 16 * k);
+    h[0] = mb.t32(k, MT_CDELTA);
+    h[1] = 0;
+    *reinterpret_cast<uint64_t*>(h + 2) = mb.u64(k, MF_LOG_INDEX);
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(mb.rec(k));
+    uint64_t* dst = reinterpret_cast<uint64_t*>(e + 16 + 16 * depth + kColdUsed * k);
+    for (uint32_t q = 0; q < kColdUsed / 8; ++q) dst[q] = src[q];
+  }
+}
+__host__ __device__ inline void cx_get_side(const Mailbox& mb, const uint8_t* e, uint32_t depth) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(e);
+  const uint32_t cb = w[1], n = mb_n(cb) < depth ? mb_n(cb) : depth;
+  mb.cnt() = (uint8_t)cb;
+  mb.mterm() = w[2];
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t* h = reinterpret_cast<const uint32_t*>(e + 16 + 16 * k);
+    mb.t32(k, MT_CDELTA) = h[0];
+    mb.u64(k, MF_LOG_INDEX) = *reinterpret_cast<const uint64_t*>(h + 2);
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(e + 16 + 16 * depth + kColdUsed * k);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(mb.rec(k));
+    for (uint32_t q = 0; q < kColdUsed / 8; ++q) dst[q] = src[q];
+  }
+}
+// The wave header's effect on one position (lane): count byte and hot fields.
+__host__ __device__ inline void cx_get_lane(const Mailbox& mb, const uint8_t* buf, const CxLayout& L, uint64_t mask,
+                                            uint64_t lost, uint32_t base, uint32_t hi, uint32_t lane) {
+  if ((mask >> lane) & 1ull) {
+    const uint32_t r = base + (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1));
+    const uint32_t w = reinterpret_cast<const uint32_t*>(buf + L.cb)[r];
+    mb.cnt() = (uint8_t)w;
+    mb.mterm() = reinterpret_cast<const uint32_t*>(buf + L.term)[r];
+    if (!(w & MB_RESP)) mb.t32(0, MT_CDELTA) = (w >> 8) - 0x800000u + 0x80000000u;
+    mb.u64(0, MF_LOG_INDEX) = ((uint64_t)hi << 32) | reinterpret_cast<const uint32_t*>(buf + L.lo)[r];
+  } else {
+    mb.cnt() = ((lost >> lane) & 1ull) ? (uint8_t)(1u | MB_COLD_LOST) : (uint8_t)0;
+  }
+}
+
+// Per-chunk record capacities (a chunk's fill depends on which replica pairs it
+// carries: exchange.py) and the chunks' buffer offsets; kernel argument by value.
+constexpr uint32_t kCxMaxChunks = 8;
+struct CxCaps {
+  uint32_t n, scap;
+  uint32_t cap[kCxMaxChunks];
+  uint64_t off[kCxMaxChunks + 1];
+};
+__host__ __device__ inline CxCaps cx_caps(uint32_t pc, uint32_t depth, uint32_t n, const uint32_t* caps,
+                                          uint32_t scap) {
+  CxCaps C{};
+  C.n = n;
+  C.scap = scap;
+  C.off[0] = 0;
+  for (uint32_t c = 0; c < n && c < kCxMaxChunks; ++c) {
+    C.cap[c] = caps[c];
+    C.off[c + 1] = C.off[c] + cx_layout(pc, depth, caps[c], scap).bytes;
+  }
+  return C;
+}
+
+// Pack: one wave per 64 positions of the out space (their buffer headers zeroed
+// before). Record slots and side entries are taken with one returning atomic
+// per wave each; a wave's records are consecutive, in lane order.
+__global__ void cx_pack(SpaceView v, uint8_t* cx, CxCaps C) {
+  const uint32_t nwv = v.pc / 64;
+  const uint64_t nw = (uint64_t)v.n_chunks * nwv;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t w = (uint64_t)blockIdx.x * (kIoBlock / 64) + (threadIdx.x >> 6); w < nw;
+       w += (uint64_t)gridDim.x * (kIoBlock / 64)) {
+    const uint32_t c = (uint32_t)(w / nwv), wl = (uint32_t)(w % nwv), pos = wl * 64 + lane;
+    const uint32_t cap = C.cap[c], scap = C.scap;
+    const CxLayout L = cx_layout(v.pc, v.depth, cap, scap);
+    uint8_t* buf = cx + C.off[c];
+    const Mailbox mb = v.at(c * v.pc + pos);
+    const uint32_t cb = mb.cnt();
+    uint32_t w3 = 0;
+    bool rec = cx_record_kind(mb, cb, &w3);
+    const uint64_t li = rec ? mb.u64(0, MF_LOG_INDEX) : 0ull;
+    const uint64_t any = __ballot(rec);
+    const uint32_t hi =
+        any ? (uint32_t)(__shfl((unsigned long long)li, __ffsll((unsigned long long)any) - 1) >> 32) : 0u;
+    rec = rec && (uint32_t)(li >> 32) == hi;
+    const uint64_t mask = __ballot(rec);
+    uint32_t base = 0;
+    if (lane == 0 && mask) base = atomicAdd(reinterpret_cast<uint32_t*>(buf), (uint32_t)__popcll(mask));
+    base = (uint32_t)__shfl((int)base, 0);
+    const uint32_t r = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1));
+    const bool fits = rec && r < cap;  // the lanes past cap are the wave's last ones
+    if (fits) cx_put_record(mb, w3, buf, L, r);
+    const bool side = mb_n(cb) && !fits;
+    const uint64_t smask = __ballot(side);
+    uint32_t sbase = 0;
+    if (lane == 0 && smask) sbase = atomicAdd(reinterpret_cast<uint32_t*>(buf) + 1, (uint32_t)__popcll(smask));
+    sbase = (uint32_t)__shfl((int)sbase, 0);
+    const uint32_t x = sbase + (uint32_t)__popcll(smask & ((1ull << lane) - 1));
+    const bool sfits = side && x < scap;
+    if (sfits) cx_put_side(mb, cb, pos, buf, L, v.depth, x);
+    const uint64_t fmask = __ballot(fits), lost = __ballot(side && !sfits);
+    if (lane == 0) {
+      uint8_t* h = buf + L.waves + (uint64_t)wl * kCxWave;
+      reinterpret_cast<uint64_t*>(h)[0] = fmask;
+      reinterpret_cast<uint64_t*>(h)[1] = lost;
+      reinterpret_cast<uint32_t*>(h)[4] = base;
+      reinterpret_cast<uint32_t*>(h)[5] = hi;
+    }
+  }
+}
+// Unpack, part 1: every position's count byte and its record's hot fields.
+__global__ void cx_unpack_waves(SpaceView v, const uint8_t* cx, CxCaps C) {
+  const uint32_t nwv = v.pc / 64;
+  const uint64_t nw = (uint64_t)v.n_chunks * nwv;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t w = (uint64_t)blockIdx.x * (kIoBlock / 64) + (threadIdx.x >> 6); w < nw;
+       w += (uint64_t)gridDim.x * (kIoBlock / 64)) {
+    const uint32_t c = (uint32_t)(w / nwv), wl = (uint32_t)(w % nwv);
+    const CxLayout L = cx_layout(v.pc, v.depth, C.cap[c], C.scap);
+    const uint8_t* buf = cx + C.off[c];
+    const uint8_t* h = buf + L.waves + (uint64_t)wl * kCxWave;
+    const uint64_t mask = reinterpret_cast<const uint64_t*>(h)[0], lost = reinterpret_cast<const uint64_t*>(h)[1];
+    const uint32_t base = reinterpret_cast<const uint32_t*>(h)[4], hi = reinterpret_cast<const uint32_t*>(h)[5];
+    cx_get_lane(v.at(c * v.pc + wl * 64 + lane), buf, L, mask, lost, base, hi, lane);
+  }
+}
+// Unpack, part 2 (after part 1): the side entries.
+__global__ void cx_unpack_side(SpaceView v, const uint8_t* cx, CxCaps C) {
+  const uint32_t scap = C.scap;
+  const uint64_t n = (uint64_t)v.n_chunks * scap;
+  for (uint64_t t = io_tid(); t < n; t += io_stride()) {
+    const uint32_t c = (uint32_t)(t / scap), x = (uint32_t)(t % scap);
+    const CxLayout L = cx_layout(v.pc, v.depth, C.cap[c], scap);
+    const uint8_t* buf = cx + C.off[c];
+    if (x >= reinterpret_cast<const uint32_t*>(buf)[1]) continue;
+    const uint8_t* e = buf + L.side + (uint64_t)x * cx_side_entry_bytes(v.depth);
+    cx_get_side(v.at(c * v.pc + reinterpret_cast<const uint32_t*>(e)[0]), e, v.depth);
+  }
+}
+
 // Zero the mailbox counts of chunk 0's first `positions` positions (the
 // host-path inbox before encoding): one byte row untiled, the first 64 bytes of
 // each tile with GR_TILE.

@@ -85,6 +85,14 @@ def load_library(path=LIB_PATH):
                                     c.c_void_p]
     for f in ("gr_space_side_pack_host", "gr_space_side_unpack_host"):
         getattr(lib, f).argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_uint32]
+    lib.gr_space_cx_bytes.restype = c.c_uint64
+    lib.gr_space_cx_bytes.argtypes = [c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_uint32]
+    for f in ("gr_space_cx_pack", "gr_space_cx_unpack"):
+        getattr(lib, f).argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_void_p,
+                                    c.c_uint32, c.c_void_p]
+    for f in ("gr_space_cx_pack_host", "gr_space_cx_unpack_host"):
+        getattr(lib, f).argtypes = [c.c_void_p, c.c_uint32, c.c_uint32, c.c_uint32, c.c_void_p, c.c_void_p,
+                                    c.c_uint32]
     lib.gr_bind_routes.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32]
     lib.gr_bind_nodes.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint32]
     lib.gr_step_wire.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t, c.c_void_p, c.c_size_t, c.c_void_p,
@@ -391,6 +399,24 @@ class Engine:
         _check(self.lib.gr_space_side_unpack(space_ptr, n_chunks, positions, depth, side_ptr, capacity, stream),
                "gr_space_side_unpack")
 
+    def cx_bytes(self, n_chunks, positions, depth, capacities, side_capacity):
+        """Bytes of the compact-exchange buffers of n_chunks chunks (gr_space_cx_bytes);
+        capacities: the record capacity of each chunk."""
+        caps = cx_caps_array(capacities, n_chunks)
+        return int(self.lib.gr_space_cx_bytes(n_chunks, positions, depth, caps.ctypes.data, side_capacity))
+
+    def cx_pack(self, space_ptr, n_chunks, positions, depth, cx_ptr, capacities, side_capacity, stream=0):
+        """Pack the device out space's mailboxes into the compact buffers, on `stream` (no wait)."""
+        caps = cx_caps_array(capacities, n_chunks)
+        _check(self.lib.gr_space_cx_pack(space_ptr, n_chunks, positions, depth, cx_ptr, caps.ctypes.data,
+                                         side_capacity, stream), "gr_space_cx_pack")
+
+    def cx_unpack(self, space_ptr, n_chunks, positions, depth, cx_ptr, capacities, side_capacity, stream=0):
+        """Write received compact buffers into the device in space, on `stream`."""
+        caps = cx_caps_array(capacities, n_chunks)
+        _check(self.lib.gr_space_cx_unpack(space_ptr, n_chunks, positions, depth, cx_ptr, caps.ctypes.data,
+                                           side_capacity, stream), "gr_space_cx_unpack")
+
     def bind_routes(self, in_pos, out_pos):
         """in_pos/out_pos: uint32 arrays [slots][n_peers] (mailbox positions, 0xFFFFFFFF = none)."""
         in_pos = np.ascontiguousarray(in_pos, np.uint32)
@@ -427,6 +453,16 @@ class Engine:
         out = np.zeros(n, abi.RESULT)
         _check(self.lib.gr_collect_results(self._h, first, out.ctypes.data, n), "gr_collect_results")
         return out
+
+
+def cx_caps_array(capacities, n_chunks):
+    """Per-chunk record capacities as the uint32 array the C-ABI takes (an int
+    means the same capacity for every chunk)."""
+    if np.isscalar(capacities):
+        capacities = [capacities] * n_chunks
+    caps = np.ascontiguousarray(capacities, np.uint32)
+    assert len(caps) == n_chunks
+    return caps
 
 
 def decode_space(buf, n_chunks, positions, depth=MAILBOX_DEPTH, lost_ok=False):

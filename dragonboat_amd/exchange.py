@@ -16,13 +16,26 @@ their outgoing messages straight into mailbox "spaces" in HBM:
   reaches) moves every mailbox across xGMI once per pass. At R = 3 that is
   4 of N chunks for N ≥ 5, and the spaces hold depth-3 mailboxes (the steady
   state's two Replicates per follower per pass plus a heartbeat on a tick; a
-  fourth message escalates CAPACITY). The hot region (counts + compact
-  Replicates + non-reject acks, 41 B per depth-3 mailbox) crosses every pass;
-  the cold fields cross only for the mailboxes that need them, compacted on the
-  device into a fixed-capacity side buffer per chunk (gr_space_side_pack /
-  _unpack), so the all-to-all sizes are fixed and the host never waits on the
-  device inside the pass loop. A mailbox whose cold fields do not fit escalates
-  CAPACITY at its reader (detected one pass later, never silently lost).
+  fourth message escalates CAPACITY). What crosses (``codec``):
+  - ``cx`` (round 5, the default): the compact exchange (gr_space_cx_pack /
+    _unpack): per chunk one fixed-size buffer holding only the mailboxes with
+    messages, a 12-byte record for the steady state's uniform mailboxes and a
+    full entry for the rest, one bit for an empty one (63 MB per GPU per pass
+    designed at N = 8 and 1M groups per GPU, against 0.33 GB for ``dense``;
+    31.5 MB against 186 MB measured in the N = 2 rehearsal);
+  - ``dense`` (round 4): the hot region (counts + compact Replicates +
+    non-reject acks, 41 B per depth-3 mailbox) every pass, the cold fields of
+    the mailboxes that need them compacted into a fixed-capacity side buffer per
+    chunk (gr_space_side_pack / _unpack).
+  Either way the all-to-all sizes are fixed and the host never waits on the
+  device inside the pass loop. A mailbox that does not fit escalates CAPACITY
+  at its reader (detected one pass later, never silently lost). The compact
+  buffers are sized for the steady state (records for the mailboxes that hold
+  messages, full entries for 1/256 of the positions); a pass the caller knows to
+  be heavy -- a tick pass and the pass after it (every leader's heartbeats,
+  then every follower's ack, are full entries) or a burst of leader changes
+  larger than the side capacity -- exchanges ``dense`` instead (``heavy=True``,
+  the same on every rank: ``codec="cx"`` keeps both forms' buffers).
 
 Peers on a rank are laid out replica-major: peer r*G + g is replica r of the
 group (home = (rank - r) % N, index g), so a wave's accesses stay contiguous.
@@ -45,6 +58,31 @@ def count_bytes(hot, n_chunks, hot_chunk, hot_tile, positions):
 
 TILE_W = 256  # gr_layout.h kTileW (GR_TILE_SHIFT = 8); Exchange checks it against the library
 SIDE_DIV, SIDE_MIN = 32, 1024  # side-buffer capacity per chunk: positions / SIDE_DIV, at least SIDE_MIN
+# compact exchange capacities per chunk: records for the share of a chunk's
+# positions that hold messages in the steady state plus CX_MARGIN, full entries
+# for 1/CX_SIDE_DIV of them (at least CX_SIDE_MIN). A chunk carries the replica
+# pairs (r -> j) of one rank offset; with the benchmark's leaders (replica 0 of
+# every group) only the pairs with the leader on one end hold messages (a
+# leader's Replicates, its followers' acks): half of an N = 8 chunk's positions,
+# two thirds at N = 3, all of the offset-2 chunk at N = 4.
+CX_MARGIN, CX_SIDE_DIV, CX_SIDE_MIN = 0.05, 256, 256
+
+
+def cx_fill(R, N, offset, leader=0):
+    """Steady-state share of a chunk's positions (rank offset `offset`) that hold
+    messages when replica `leader` of every group leads."""
+    pairs = offset_pairs(R, N)
+    per = max(len(v) for v in pairs.values())
+    return sum(1 for r, j in pairs[offset] if leader in (r, j)) / per
+
+
+def cx_capacities(positions, fill, frac=None):
+    """(record capacity, full-entry capacity) of one compact-exchange chunk whose
+    steady-state fill is `fill` (frac: a fixed share instead of fill + margin)."""
+    pc = pad_positions(positions)
+    share = frac if frac is not None else fill + CX_MARGIN
+    cap = min(pc, (int(pc * share) + 63) // 64 * 64)
+    return cap, max(CX_SIDE_MIN, pc // CX_SIDE_DIV)
 
 
 def pad_positions(positions):
@@ -126,9 +164,13 @@ def spread_peers(G, R, N, rank, seed=2, **kw):
 class Exchange:
     """Spaces + routes for one rank; `step` launches one pass and exchanges."""
 
-    def __init__(self, G, R, S, world, rank, placement, seed=2, exchange=None):
+    def __init__(self, G, R, S, world, rank, placement, seed=2, exchange=None, codec="cx", cx_frac=None):
         """exchange=True keeps the one-rank spread exchange (copy + side buffers)
-        that a one-rank run otherwise skips (tests of the N > 1 code on one GPU)."""
+        that a one-rank run otherwise skips (tests of the N > 1 code on one GPU).
+        codec: "cx" (compact exchange) or "dense" (hot region + side buffers)."""
+        assert codec in ("cx", "dense")
+        self.codec, self.cx_frac = codec, cx_frac
+        self.last_cx = codec == "cx"  # the form of the last exchange (unpack reads it)
         self.G, self.R, self.S = G, R, S
         self.world, self.rank, self.placement = world, rank, placement
         self.n_peers = R * G
@@ -166,28 +208,59 @@ class Exchange:
         assert nbytes == self.n_chunks * cb and 0 < hb < cb
         self.hot_region = self.n_chunks * hb  # hot chunks first, then the cold chunks
         self.hot_tile = eng.hot_tile_bytes(self.depth)  # positions tiled by 64, counts first in a tile
-        if not self.pingpong:  # all_to_all split sizes, bytes per peer rank
-            self.hot_splits = ([hb if d in self.dests else 0 for d in range(self.world)],
-                               [hb if a in self.srcs else 0 for a in range(self.world)])
-            # side buffers: the cold fields of up to 1/32 of a chunk's mailboxes
-            # (at least 1024), a fixed size every pass
-            self.side_cap = max(SIDE_MIN, pad_positions(self.positions) // SIDE_DIV)
-            sb = eng.side_bytes(1, self.depth, self.side_cap)
-            self.side_splits = ([sb if d in self.dests else 0 for d in range(self.world)],
-                                [sb if a in self.srcs else 0 for a in range(self.world)])
-            self.side = [torch.zeros(self.n_chunks * sb, dtype=torch.uint8, device=device) for _ in range(2)]
+        if not self.pingpong:  # both forms' buffers: a heavy pass exchanges dense
+            self._alloc_dense(eng, device, hb)
+        if not self.pingpong and self.codec == "cx":
+            # one fixed-size compact buffer per chunk, sent and received; a chunk's
+            # record capacity follows its rank offset (cx_fill), the same on the
+            # sender (destination d: offset d - rank) and the receiver (source a:
+            # offset rank - a)
+            N = self.world
+            cap_of = lambda o: cx_capacities(self.positions, cx_fill(self.R, N, o), self.cx_frac)
+            self.cx_send_caps = [cap_of((d - self.rank) % N)[0] for d in self.dests]
+            self.cx_recv_caps = [cap_of((self.rank - a) % N)[0] for a in self.srcs]
+            self.cx_scap = cap_of(0)[1]
+            sb = [eng.cx_bytes(1, self.positions, self.depth, [c], self.cx_scap) for c in self.cx_send_caps]
+            rb = [eng.cx_bytes(1, self.positions, self.depth, [c], self.cx_scap) for c in self.cx_recv_caps]
+            self.cx_splits = ([sb[self.dests.index(d)] if d in self.dests else 0 for d in range(self.world)],
+                              [rb[self.srcs.index(a)] if a in self.srcs else 0 for a in range(self.world)])
+            self.cx = [torch.zeros(sum(sb), dtype=torch.uint8, device=device),
+                       torch.zeros(sum(rb), dtype=torch.uint8, device=device)]
         a = torch.zeros(nbytes, dtype=torch.uint8, device=device)
         b = torch.zeros(nbytes, dtype=torch.uint8, device=device)
         return [a, b]
 
-    def exchange(self, eng, spaces, h):
-        """Spread placement, after a pass on stream handle h: compact the out
-        space's cold fields, move the hot region and the side buffers (fixed
-        sizes), unpack the side buffers into the in space. Returns the pending
-        collective work (empty with one rank or a host backend). The copies and
-        collectives run on torch's current stream, which the caller makes the
-        stream of h (Exchange.step, Pipeline.step)."""
+    def _alloc_dense(self, eng, device, hb):
+        import torch
+        # all_to_all split sizes, bytes per peer rank
+        self.hot_splits = ([hb if d in self.dests else 0 for d in range(self.world)],
+                           [hb if a in self.srcs else 0 for a in range(self.world)])
+        # side buffers: the cold fields of up to 1/32 of a chunk's mailboxes
+        # (at least 1024), a fixed size every pass
+        self.side_cap = max(SIDE_MIN, pad_positions(self.positions) // SIDE_DIV)
+        sb = eng.side_bytes(1, self.depth, self.side_cap)
+        self.side_splits = ([sb if d in self.dests else 0 for d in range(self.world)],
+                            [sb if a in self.srcs else 0 for a in range(self.world)])
+        self.side = [torch.zeros(self.n_chunks * sb, dtype=torch.uint8, device=device) for _ in range(2)]
+
+    def exchange(self, eng, spaces, h, heavy=False):
+        """Spread placement, after a pass on stream handle h: pack the out space
+        (compact buffers, or for a heavy pass / the dense codec: its cold fields
+        into the side buffers) and move it (fixed sizes). Returns the pending
+        collective work (empty with one rank or a host backend); unpack() then
+        writes what arrived into the in space. The copies and collectives run on
+        torch's current stream, which the caller makes the stream of h
+        (Exchange.step, Pipeline.step)."""
         inp, out = spaces
+        self.last_cx = self.codec == "cx" and not heavy
+        if self.last_cx:
+            send, recv = self.cx
+            eng.cx_pack(out.data_ptr(), self.n_chunks, self.positions, self.depth, send.data_ptr(),
+                        self.cx_send_caps, self.cx_scap, h)
+            if self.world == 1:
+                recv.copy_(send)
+                return []
+            return [_all_to_all(recv, send, self.cx_splits[1], self.cx_splits[0])]
         side_out, side_in = self.side
         eng.side_pack(out.data_ptr(), self.n_chunks, self.positions, self.depth, side_out.data_ptr(),
                       self.side_cap, h)
@@ -202,13 +275,18 @@ class Exchange:
         return work
 
     def unpack(self, eng, spaces, h):
-        """Write the received side-buffer entries into the in space (after the
-        exchange's work has completed on stream h)."""
+        """Write what the exchange received into the in space (after its work has
+        completed on stream h)."""
+        if self.last_cx:
+            eng.cx_unpack(spaces[0].data_ptr(), self.n_chunks, self.positions, self.depth, self.cx[1].data_ptr(),
+                          self.cx_recv_caps, self.cx_scap, h)
+            return
         eng.side_unpack(spaces[0].data_ptr(), self.n_chunks, self.positions, self.depth, self.side[1].data_ptr(),
                         self.side_cap, h)
 
-    def step(self, eng, spaces, k, stream, events=None):
-        """One pass: kernel (optionally bracketed by `events`), then the exchange."""
+    def step(self, eng, spaces, k, stream, events=None, heavy=False):
+        """One pass: kernel (optionally bracketed by `events`), then the exchange
+        (heavy: the dense form, for a pass with ticks or leader changes)."""
         h = stream.cuda_stream
         if self.pingpong:
             src, dst = spaces[k % 2], spaces[(k + 1) % 2]
@@ -225,7 +303,7 @@ class Exchange:
             # exchange() copies (one rank) and issues RCCL on torch's current
             # stream: make that the pass's stream, so they follow the pack
             with torch.cuda.stream(stream):
-                for w in self.exchange(eng, spaces, h):
+                for w in self.exchange(eng, spaces, h, heavy=heavy):
                     w.wait()
             self.unpack(eng, spaces, h)
 
@@ -250,7 +328,8 @@ class Pipeline:
     is one bank whose two spaces ping-pong (no exchange).
     """
 
-    def __init__(self, G, R, S, world, rank, placement="spread", banks=None, seed=2, exchange=None):
+    def __init__(self, G, R, S, world, rank, placement="spread", banks=None, seed=2, exchange=None, codec="cx",
+                 cx_frac=None):
         if banks is None:  # banks overlap one another's exchange: only with one to overlap
             banks = 2 if placement == "spread" and world > 1 and G >= 128 else 1
         # bank sizes a multiple of 64 but the last: a wave's lanes then share a
@@ -258,7 +337,8 @@ class Pipeline:
         base = (G // banks) // 64 * 64 if G // banks >= 64 else G // banks
         sizes = [base] * (banks - 1) + [G - base * (banks - 1)]
         self.R, self.S, self.world, self.rank, self.placement = R, S, world, rank, placement
-        self.ex = [Exchange(Gb, R, S, world, rank, placement, seed=seed + 7919 * b, exchange=exchange)
+        self.ex = [Exchange(Gb, R, S, world, rank, placement, seed=seed + 7919 * b, exchange=exchange, codec=codec,
+                            cx_frac=cx_frac)
                    for b, Gb in enumerate(sizes)]
         self.groups = G
         self.engines, self.spaces, self.streams = [], [], []
@@ -282,7 +362,9 @@ class Pipeline:
             self.spaces.append(ex.allocate(eng, device))
             self.streams.append(torch.cuda.Stream(device=device))
 
-    def step(self, k):
+    def step(self, k, heavy=False):
+        """Pass k of every bank (heavy: the pass's exchange in the dense form,
+        Exchange.exchange)."""
         import torch
         for b, (ex, eng) in enumerate(zip(self.ex, self.engines)):
             s = self.streams[b]
@@ -298,7 +380,7 @@ class Pipeline:
                 eng.step_device(src.data_ptr(), dst.data_ptr(), ex.n_chunks, ex.positions, ex.n_chunks,
                                 ex.positions, ex.n_peers, s.cuda_stream, depth=ex.depth)
                 if not ex.pingpong:
-                    self.work[b] = ex.exchange(eng, self.spaces[b], s.cuda_stream)
+                    self.work[b] = ex.exchange(eng, self.spaces[b], s.cuda_stream, heavy=heavy)
 
     def graph_ready(self):
         """Graph mode applies: every bank's spaces ping-pong (no exchange step)."""
@@ -319,12 +401,17 @@ class Pipeline:
             for b, (eng, g) in enumerate(zip(self.engines, self.graphs)):
                 eng.graph_replay(g, self.streams[b].cuda_stream)
 
-    def exchange_bytes_per_pass(self):
-        """Bytes this rank sends to other ranks per pass (hot regions + side
-        buffers of the chunks for other ranks; 0 for local placement)."""
+    def exchange_bytes_per_pass(self, heavy=False):
+        """Bytes this rank sends to other ranks per pass (its buffers for the
+        chunks of other ranks: compact, or hot regions + side buffers for the
+        dense form and heavy passes; 0 for local placement)."""
         tot = 0
         for ex in self.ex:
-            if not ex.pingpong:
+            if ex.pingpong:
+                continue
+            if ex.codec == "cx" and not heavy:
+                tot += sum(n for d, n in zip(range(self.world), ex.cx_splits[0]) if d != self.rank)
+            else:
                 tot += sum(n for d, n in zip(range(self.world), ex.hot_splits[0]) if d != self.rank)
                 tot += sum(n for d, n in zip(range(self.world), ex.side_splits[0]) if d != self.rank)
         return tot

@@ -510,6 +510,32 @@ int gr_space_side_pack_host(void* space_host, uint32_t n_chunks, uint32_t positi
                             void* side_host, uint32_t capacity);
 int gr_space_side_unpack_host(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
                               const void* side_host, uint32_t capacity);
+/* Compact exchange (round 5): the form in which a space crosses GPUs instead of
+ * its whole hot region plus side buffers. Per chunk one fixed-size buffer
+ * (gr_space_cx_bytes) carries only the mailboxes with messages: a 13-byte record
+ * for a uniform mailbox whose messages repeat message 0's hot fields (one
+ * message, or the steady state's shared pairs), a full entry (hot fields and cold
+ * records) for any other, one bit for an empty one. capacities[c] records for
+ * chunk c (at most 8 chunks) and `side_capacity` full entries per chunk; the
+ * receiver passes the sender's capacities for its chunks. A mailbox that fits neither arrives as
+ * lost (count 1 with bit 4, not uniform) and its reader escalates
+ * GR_ESC_CAPACITY. gr_space_cx_pack reads a (device) out space into the buffers,
+ * gr_space_cx_unpack writes received buffers into an in space (every count byte
+ * of its chunks), both on `stream` without waiting; the _host forms run the same
+ * codec over host memory (tests). The buffers of n_chunks chunks are one range
+ * per chunk, in chunk order (an all-to-all's split sizes). The reference's model:
+ * per-target batching of only the messages that exist
+ * (internal/transport/transport.go:399-476). */
+uint64_t gr_space_cx_bytes(uint32_t n_chunks, uint32_t positions, uint32_t depth, const uint32_t* capacities,
+                           uint32_t side_capacity);
+int gr_space_cx_pack(void* space, uint32_t n_chunks, uint32_t positions, uint32_t depth, void* cx,
+                     const uint32_t* capacities, uint32_t side_capacity, void* stream);
+int gr_space_cx_unpack(void* space, uint32_t n_chunks, uint32_t positions, uint32_t depth, const void* cx,
+                       const uint32_t* capacities, uint32_t side_capacity, void* stream);
+int gr_space_cx_pack_host(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth, void* cx_host,
+                          const uint32_t* capacities, uint32_t side_capacity);
+int gr_space_cx_unpack_host(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth,
+                            const void* cx_host, const uint32_t* capacities, uint32_t side_capacity);
 int gr_bind_routes(gr_engine* e, const uint32_t* in_pos, const uint32_t* out_pos, uint32_t n_peers);
 int gr_set_locals(gr_engine* e, const gr_local_input* locals, size_t n);
 /* Launch one pass on `stream` (a hipStream_t, may be NULL) without syncing.

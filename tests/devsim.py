@@ -20,17 +20,20 @@ def inverse_routes(in_pos):
     return inv
 
 
-def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None, inject_p=0.0, mix=False):
+def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None, inject_p=0.0, mix=False,
+               codec="cx"):
     """tick_every > 0: one Tick for every peer on passes k % tick_every == tick_every - 1
     (leader heartbeats and their acks: messages with cold fields).
     inject_p > 0: BASELINE config 5's leader changes (populations.inject_leader_change)
     before every pass after the first, on both sides, proposals on the current leaders.
     mix: peers in a group-major order (peer g*R + r), so every wave holds leaders
-    and followers; the routes are then plain tables (local placement only)."""
+    and followers; the routes are then plain tables (local placement only).
+    codec: the spread exchange's form ("cx" compact buffers, "dense" hot region +
+    side buffers); stats["side_entries"] counts the full entries per pass."""
     import torch
     S = R
     # spread on one rank: keep the exchange (copy + side buffers) under test
-    ex = Exchange(G, R, S, 1, 0, placement, seed=seed, exchange=placement == "spread")
+    ex = Exchange(G, R, S, 1, 0, placement, seed=seed, exchange=placement == "spread", codec=codec)
     n = ex.n_peers
     # perm[x] = engine peer of replica-major peer x (identity unless mix)
     perm = np.arange(n)
@@ -81,12 +84,21 @@ def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None
         elif tick_every:
             loc = locals_of(k, ex.leader_slots)
             eng.set_locals(loc)
-        ex.step(eng, spaces, k, stream)
+        # a tick pass and the pass after it are heavy (every leader's heartbeats,
+        # then every follower's ack, each a full entry): the dense form crosses
+        heavy = bool(tick_every) and k > 0 and k % tick_every in (tick_every - 1, 0)
+        ex.step(eng, spaces, k, stream, heavy=heavy)
         torch.cuda.synchronize()
-        if placement == "spread" and stats is not None:  # cold-field entries the side buffers carried
-            sb = len(ex.side[1]) // ex.n_chunks
-            hdr = ex.side[1].cpu().numpy().reshape(ex.n_chunks, sb)[:, :4].copy().view(np.uint32)[:, 0]
-            stats.setdefault("side_entries", []).append(int(hdr.sum()))
+        if placement == "spread" and stats is not None:  # what the exchange carried
+            if ex.last_cx:  # records, full entries (one chunk: headers at offset 0)
+                hdr = ex.cx[1][:8].cpu().numpy().view(np.uint32)
+                stats.setdefault("records", []).append(int(hdr[0]))
+                stats.setdefault("side_entries", []).append(int(hdr[1]))
+            else:
+                sb = len(ex.side[1]) // ex.n_chunks
+                hdr = ex.side[1].cpu().numpy().reshape(ex.n_chunks, sb)[:, :4].copy().view(np.uint32)[:, 0]
+                stats.setdefault("records", []).append(0)
+                stats.setdefault("side_entries", []).append(int(hdr.sum()))
         o = pop.step(msgs, loc)
         res = eng.collect_results(n)
         assert not np.any(res["escalation"]), "unexpected escalation on the device path"
@@ -96,12 +108,21 @@ def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None
         # the space the next pass reads
         nxt = spaces[(k + 1) % 2] if placement == "local" else spaces[0]
         raw = nxt.cpu().numpy()
-        got = decode_space(raw, ex.n_chunks, ex.positions, ex.depth)
+        got = decode_space(raw, ex.n_chunks, ex.positions, ex.depth, lost_ok=True)
+        # oracle messages -> (receiver, sender slot) records in arrival order
+        want = route(o["msgs"], ex, G, R, perm)
+        lost = got["reject"] == 0xFF
+        if np.any(lost):  # the exchange dropped cold fields: name the pass and what they held
+            lp = set(int(x) for x in got["peer"][lost])
+            kinds = {}
+            for m in want:
+                if (int(m["peer"]), int(m["slot"])) in {inv[x] for x in lp}:
+                    kinds[int(m["type"])] = kinds.get(int(m["type"]), 0) + 1
+            raise AssertionError(f"pass {k} (heavy={heavy}): {len(lp)} mailboxes lost in the exchange, "
+                                 f"message types {kinds}, stats {stats}")
         for m in got:
             p, j = inv[int(m["peer"])]
             m["peer"], m["slot"] = p, j
-        # oracle messages -> (receiver, sender slot) records in arrival order
-        want = route(o["msgs"], ex, G, R, perm)
         bad = parity.compare_msgs(got, want)
         assert not bad, f"pass {k}: mailboxes {bad[:3]}"
         bad = parity.compare_results(res, o["results"])

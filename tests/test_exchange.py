@@ -210,6 +210,21 @@ class _SideCodec:
     def side_unpack(self, ptr, n_chunks, positions, depth, side_ptr, cap, stream=0):
         assert self.lib.gr_space_side_unpack_host(ptr, n_chunks, positions, depth, side_ptr, cap) == 0
 
+    def cx_bytes(self, n_chunks, positions, depth, caps, scap):
+        from dragonboat_amd.engine import cx_caps_array
+        c = cx_caps_array(caps, n_chunks)
+        return int(self.lib.gr_space_cx_bytes(n_chunks, positions, depth, c.ctypes.data, scap))
+
+    def cx_pack(self, ptr, n_chunks, positions, depth, cx_ptr, caps, scap, stream=0):
+        from dragonboat_amd.engine import cx_caps_array
+        c = cx_caps_array(caps, n_chunks)
+        assert self.lib.gr_space_cx_pack_host(ptr, n_chunks, positions, depth, cx_ptr, c.ctypes.data, scap) == 0
+
+    def cx_unpack(self, ptr, n_chunks, positions, depth, cx_ptr, caps, scap, stream=0):
+        from dragonboat_amd.engine import cx_caps_array
+        c = cx_caps_array(caps, n_chunks)
+        assert self.lib.gr_space_cx_unpack_host(ptr, n_chunks, positions, depth, cx_ptr, c.ctypes.data, scap) == 0
+
 
 class _MockEngine(_SideCodec):
     """A no-op pass: lets Exchange.step's collectives run over gloo on CPU tensors."""
@@ -261,7 +276,7 @@ def _encode_chunks(lib, ex, rank, out):
     return want
 
 
-def _step_worker(rank, world, port, side_min, q):
+def _step_worker(rank, world, port, side_min, codec, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from dragonboat_amd.engine import decode_space
@@ -269,8 +284,9 @@ def _step_worker(rank, world, port, side_min, q):
     class _S:
         cuda_stream = 0
     X.SIDE_MIN, X.SIDE_DIV = side_min, 1 << 30
+    X.CX_SIDE_MIN, X.CX_SIDE_DIV = side_min, 1 << 30
     G, R = 40, 3
-    ex = X.Exchange(G, R, R, world, rank, "spread")
+    ex = X.Exchange(G, R, R, world, rank, "spread", codec=codec)
     eng = _MockEngine()
     spaces = ex.allocate(eng, torch.device("cpu"))
     mine = _encode_chunks(eng.lib, ex, rank, spaces[1])
@@ -302,13 +318,15 @@ def _step_worker(rank, world, port, side_min, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,side_min", [(2, 1024), (3, 1024), (5, 1024), (3, 2)])
-def test_gloo_spread_step_side_buffers(built, world, side_min):
-    """Exchange.step over gloo: every chunk's hot region reaches the rank it was
-    written for, and the cold fields of its non-uniform mailboxes (heartbeats)
-    arrive through the fixed-size side buffers. With a side capacity of 2 the
-    heartbeats beyond it are not lost silently: their count bytes carry
-    MB_COLD_LOST (a reading lane escalates CAPACITY)."""
+@pytest.mark.parametrize("world,side_min,codec", [(2, 1024, "dense"), (3, 1024, "dense"), (5, 1024, "dense"),
+                                                  (3, 2, "dense"), (2, 1024, "cx"), (5, 1024, "cx"), (3, 2, "cx")])
+def test_gloo_spread_step_side_buffers(built, world, side_min, codec):
+    """Exchange.step over gloo: every mailbox reaches the rank it was written for.
+    dense: the hot region whole, the cold fields of the non-uniform mailboxes
+    (heartbeats) through the fixed-size side buffers; cx: the compact buffers
+    (records for the uniform Replicates, full entries for the heartbeats). With a
+    full-entry capacity of 2 the heartbeats beyond it are not lost silently:
+    their count bytes carry MB_COLD_LOST (a reading lane escalates CAPACITY)."""
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -316,7 +334,7 @@ def test_gloo_spread_step_side_buffers(built, world, side_min):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_step_worker, args=(r, world, port, side_min, q)) for r in range(world)]
+    procs = [ctx.Process(target=_step_worker, args=(r, world, port, side_min, codec, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
@@ -384,14 +402,14 @@ class _HostlaneEngine(_SideCodec):
         return bool(np.any(((cnt & 7) != 0) & ((cnt & 8) == 0)))
 
 
-def _raft_worker(rank, world, port, G, passes, q):
+def _raft_worker(rank, world, port, G, passes, codec, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
     class _S:
         cuda_stream = 0
     R = 3
-    ex = X.Exchange(G, R, R, world, rank, "spread", seed=11)
+    ex = X.Exchange(G, R, R, world, rank, "spread", seed=11, codec=codec)
     eng = _HostlaneEngine(ex)
     spaces = ex.allocate(eng, torch.device("cpu"))
     states = []
@@ -402,8 +420,8 @@ def _raft_worker(rank, world, port, G, passes, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_spread_raft_matches_oracle(built, world):
+@pytest.mark.parametrize("world,codec", [(2, "dense"), (3, "dense"), (2, "cx"), (3, "cx")])
+def test_gloo_spread_raft_matches_oracle(built, world, codec):
     """Config 4 rehearsed on CPU: every rank steps its replicas with the kernels'
     lane code (host build), the Replicate/ReplicateResp mailboxes cross ranks
     through Exchange.step's all_to_all_single (gloo), and after every pass each
@@ -420,7 +438,7 @@ def test_gloo_spread_raft_matches_oracle(built, world):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_raft_worker, args=(r, world, port, G, passes, q)) for r in range(world)]
+    procs = [ctx.Process(target=_raft_worker, args=(r, world, port, G, passes, codec, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -450,3 +468,74 @@ def test_gloo_spread_raft_matches_oracle(built, world):
                 bad = parity.compare_states(dev[sl], orc[h][k][sl], R)
                 assert not bad, (rank, k, r, bad[:2])
     assert all(int(res[r][-1]["committed"][:G].min()) > int(res[r][0]["committed"][:G].min()) for r in res)
+
+
+def test_cx_codec_round_trip(built):
+    """The compact exchange's host codec (gr_space_cx_pack_host / _unpack_host,
+    the device kernels' logic): a space of uniform compact Replicates and accepts
+    (records), heartbeats and multi-entry Replicates (full entries) and empty
+    mailboxes unpacks to the same messages; with small capacities the overflow
+    is marked lost, never silently dropped; the designed steady-state volume at
+    N = 8 and 1M groups per GPU stays under 70 MB per pass."""
+    from dragonboat_amd import abi
+    from dragonboat_amd.engine import load_library, decode_space
+    lib = load_library()
+    n_chunks, positions, depth = 2, 700, 3
+    rng = np.random.default_rng(3)
+    msgs, pos = [], []
+    pc = X.pad_positions(positions)
+    for c in range(n_chunks):
+        for q in range(positions):
+            kind = rng.integers(0, 5)
+            if kind == 4:
+                continue
+            for k in range(1 if kind != 1 else 3):
+                m = np.zeros(1, abi.MESSAGE)[0]
+                m["term"] = 9
+                if kind in (0, 1):
+                    m["type"] = abi.REPLICATE
+                    m["log_index"] = 2**32 + q + 10 * k if q % 50 else 2**34 + q
+                    m["log_term"] = 9
+                    m["commit"] = m["log_index"] - 1 if q % 13 else m["log_index"] + 2**30
+                elif kind == 2:
+                    m["type"] = abi.HEARTBEAT
+                    m["commit"] = q
+                    m["hint"] = q + 1
+                else:
+                    m["type"] = abi.REPLICATE_RESP
+                    m["log_index"] = 2**32 + q
+                msgs.append(m)
+                pos.append(c * pc + q)
+    msgs = np.array(msgs, abi.MESSAGE)
+    pos = np.array(pos, np.uint32)
+    nb = int(lib.gr_space_bytes(n_chunks, positions, depth))
+    src = np.zeros(nb, np.uint8)
+    assert lib.gr_space_encode(src.ctypes.data, n_chunks, positions, depth, msgs.ctypes.data, len(msgs),
+                               pos.ctypes.data) == 0
+    want = decode_space(src.copy(), n_chunks, positions, depth)
+    key = lambda a: np.sort(a, order=["peer", "slot", "type", "log_index", "commit", "hint"])
+    from dragonboat_amd.engine import cx_caps_array
+    for cap, scap, expect_lost in [(pc, pc, False), ([64, 128], 16, True)]:
+        caps = cx_caps_array(cap, n_chunks)
+        cb = int(lib.gr_space_cx_bytes(n_chunks, positions, depth, caps.ctypes.data, scap))
+        cx = np.zeros(cb, np.uint8)
+        dst = np.full(nb, 0xA5, np.uint8)  # every count byte is rewritten
+        assert lib.gr_space_cx_pack_host(src.ctypes.data, n_chunks, positions, depth, cx.ctypes.data,
+                                         caps.ctypes.data, scap) == 0
+        assert lib.gr_space_cx_unpack_host(dst.ctypes.data, n_chunks, positions, depth, cx.ctypes.data,
+                                           caps.ctypes.data, scap) == 0
+        got = decode_space(dst, n_chunks, positions, depth, lost_ok=True)
+        lost = got["reject"] == 0xFF
+        assert bool(lost.any()) == expect_lost
+        ok = np.isin(want["peer"], got["peer"][~lost])
+        assert np.array_equal(key(got[~lost]), key(want[ok]))
+        assert np.array_equal(np.unique(got["peer"]), np.unique(want["peer"]))  # lost ones still arrive, marked
+    # the design volume (exchange.py cx_capacities): N = 8, G = 1M per GPU, R = 3
+    _, _, positions8 = X.spread_routes(64, 3, 3, 8, 0)
+    pos = positions8 // 64 * 1_000_000
+    dests, _ = X.spread_peer_ranks(3, 8, 0)
+    tot = 0
+    for d in dests:
+        cap, scap = X.cx_capacities(pos, X.cx_fill(3, 8, d % 8))
+        tot += int(lib.gr_space_cx_bytes(1, pos, 3, cx_caps_array([cap], 1).ctypes.data, scap))
+    assert tot < 70e6, tot

@@ -84,17 +84,105 @@ def test_split_pass_churn(gpu, mix, monkeypatch):
     assert st["injected"] > 0
 
 
-def test_spread_cold_fields_by_side_buffer(gpu):
-    """Spread exchange: the hot region every pass, the cold fields of the
-    mailboxes that need them (heartbeats and their acks, ticks every third pass)
-    through the device-packed side buffers, with no host read-back; parity every
-    pass."""
+@pytest.mark.parametrize("codec", ["dense", "cx"])
+def test_spread_cold_fields_by_side_buffer(gpu, codec):
+    """Spread exchange, no host read-back, parity every pass. dense: the hot region
+    every pass, the cold fields of the mailboxes that need them (heartbeats and
+    their acks, ticks every third pass) through the device-packed side buffers.
+    cx (the compact exchange): 12-byte records for the steady mailboxes on the
+    passes without ticks, the dense form on the tick passes and the passes of
+    their acks (heavy)."""
     import devsim
     st = {}
-    final = devsim.run_device(500, 3, 9, placement="spread", tick_every=3, stats=st)
+    final = devsim.run_device(500, 3, 9, placement="spread", tick_every=3, stats=st, codec=codec)
     assert np.all(final["committed"][:500] > 2**32)
     used = [n > 0 for n in st["side_entries"]]
     assert any(used) and not all(used), st
+    if codec == "cx":  # records on the passes that are neither the first nor heavy
+        assert all(st["records"][k] > 0 for k in (1, 4, 7)), st
+
+
+def test_cx_pack_unpack(gpu):
+    """gr_space_cx_pack/_unpack on the device equal the host codec: every mailbox
+    of a space (uniform compact Replicates and accepts as records, heartbeats and
+    multi-entry Replicates as full entries, a LogIndex whose high bits differ from
+    its wave's as a full entry) lands in the target space; with small capacities
+    the records overflow into full entries and those past the full capacity
+    arrive as lost (MB_COLD_LOST)."""
+    import torch
+    from dragonboat_amd import abi
+    from dragonboat_amd.engine import Engine, decode_space, cx_caps_array
+    eng = Engine(64, 3)
+    lib = eng.lib
+    n_chunks, positions, depth = 3, 1000, 3
+    rng = np.random.default_rng(9)
+    msgs, pos = [], []
+    for c in range(n_chunks):
+        for q in range(positions):
+            if rng.random() < 0.3:
+                continue
+            kind = rng.integers(0, 4)
+            base = (c << 20) + q
+            for k in range(1 if kind != 1 else 2):
+                m = np.zeros(1, abi.MESSAGE)[0]
+                m["term"] = 7
+                if kind in (0, 1):  # compact Replicate(s) at one LogIndex (a shared pair for kind 1)
+                    m["type"] = abi.REPLICATE
+                    m["log_index"] = (2**32 if q % 97 else 2**33) + base
+                    m["log_term"] = 7
+                    m["commit"] = m["log_index"] - 3 + k
+                    m["n_entries"] = k
+                    m["n_runs"] = k
+                    m["run_term"][0] = 7 if k else 0
+                elif kind == 2:
+                    m["type"] = abi.HEARTBEAT
+                    m["commit"] = base
+                    m["hint"] = base + 5
+                else:
+                    m["type"] = abi.REPLICATE_RESP
+                    m["log_index"] = 2**32 + base
+                msgs.append(m)
+                pos.append(c * X_pad(positions) + q)
+    msgs = np.array(msgs, abi.MESSAGE)
+    pos = np.array(pos, np.uint32)
+    nb = eng.space_bytes(n_chunks, positions, depth)
+    src = np.zeros(nb, np.uint8)
+    assert lib.gr_space_encode(src.ctypes.data, n_chunks, positions, depth, msgs.ctypes.data, len(msgs),
+                               pos.ctypes.data) == 0
+    want = decode_space(src.copy(), n_chunks, positions, depth, lost_ok=True)
+    for cap, scap in [(positions, positions), (200, 100)]:
+        cb = eng.cx_bytes(n_chunks, positions, depth, cap, scap)
+        h_cx = np.zeros(cb, np.uint8)
+        h_dst = np.full(nb, 0x5A, np.uint8)
+        caps = cx_caps_array(cap, n_chunks)
+        assert lib.gr_space_cx_pack_host(src.ctypes.data, n_chunks, positions, depth, h_cx.ctypes.data,
+                                         caps.ctypes.data, scap) == 0
+        assert lib.gr_space_cx_unpack_host(h_dst.ctypes.data, n_chunks, positions, depth, h_cx.ctypes.data,
+                                           caps.ctypes.data, scap) == 0
+        d_src = torch.from_numpy(src).cuda()
+        d_cx = torch.zeros(cb, dtype=torch.uint8, device="cuda")
+        d_dst = torch.full((nb,), 0x5A, dtype=torch.uint8, device="cuda")
+        eng.cx_pack(d_src.data_ptr(), n_chunks, positions, depth, d_cx.data_ptr(), cap, scap)
+        eng.cx_unpack(d_dst.data_ptr(), n_chunks, positions, depth, d_cx.data_ptr(), cap, scap)
+        torch.cuda.synchronize()
+        got_h = decode_space(h_dst, n_chunks, positions, depth, lost_ok=True)
+        got_d = decode_space(d_dst.cpu().numpy(), n_chunks, positions, depth, lost_ok=True)
+        key = lambda a: np.sort(a, order=["peer", "type", "log_index", "commit", "hint"])
+        assert np.array_equal(key(got_h), key(got_d))
+        lost = got_d["reject"] == 0xFF
+        if cap >= positions:
+            assert not lost.any()
+            assert np.array_equal(key(got_d), key(want))
+        else:
+            assert lost.any()
+            ok = np.isin(want["peer"], got_d["peer"][~lost])
+            assert np.array_equal(key(got_d[~lost]), key(want[ok]))
+    eng.close()
+
+
+def X_pad(positions):
+    from dragonboat_amd.exchange import pad_positions
+    return pad_positions(positions)
 
 
 def test_side_buffer_pack_unpack(gpu):
@@ -503,8 +591,9 @@ def test_compact_log_moves_first_index(built, gpu):
     eng.close()
 
 
-@pytest.mark.parametrize("banks,exchange", [(1, False), (1, True), (2, True)])
-def test_pipeline_spread_banks(gpu, banks, exchange):
+@pytest.mark.parametrize("banks,exchange,codec", [(1, False, "cx"), (1, True, "cx"), (2, True, "cx"),
+                                                  (2, True, "dense")])
+def test_pipeline_spread_banks(gpu, banks, exchange, codec):
     """The banked spread pipeline (dragonboat_amd.exchange.Pipeline: one engine
     and HIP stream per bank) at N = 1 equals an oracle run of every bank's groups
     after every pass: with the one-rank ping-pong (exchange=False, what bench.py
@@ -517,7 +606,7 @@ def test_pipeline_spread_banks(gpu, banks, exchange):
     from oracle.pyoracle import OraclePopulation
     import parity
     G, R, K = 900, 3, 5
-    pipe = Pipeline(G, R, R, 1, 0, "spread", banks=banks, exchange=exchange)
+    pipe = Pipeline(G, R, R, 1, 0, "spread", banks=banks, exchange=exchange, codec=codec)
     pipe.setup(Engine, torch.device("cuda", 0), 0)
     pops = [OraclePopulation(ex.peers, R) for ex in pipe.ex]
     msgs = [np.zeros(0, abi.MESSAGE) for _ in pipe.ex]

@@ -1,11 +1,17 @@
 """bench.py's N > 1 code path on one GPU: two ranks (processes) over gloo, each
 running exchange.Pipeline (spread placement: replica r of a group homed on
 rank h lives on rank (h + r) % 2, the mailboxes of other ranks cross through
-all_to_all_single every pass, cold fields through the side buffers) on cuda:0.
-After every pass every rank's replicas equal a single-process oracle run of
-the same groups (one population per bank and home rank, messages routed
-inside each group). RCCL refuses two ranks on one device, so the collective
-runs over gloo (host copies); everything else is the RCCL path's code."""
+all_to_all_single every pass, in the compact exchange's buffers or as the hot
+region plus side buffers) on cuda:0. After every pass every rank's replicas
+equal a single-process oracle run of the same groups (one population per bank
+and home rank, messages routed inside each group), which each rank runs beside
+its engines. RCCL refuses two ranks on one device, so the collective runs over
+gloo (host copies); everything else is the RCCL path's code.
+
+churn: BASELINE config 5's leader changes (p = 0.1 of the settled groups on
+passes 1 and 4, applied to the oracle and to whichever rank holds each changed
+replica) and a Tick on every replica every third pass, so step-downs, rejects,
+multi-entry catch-ups, heartbeats and their acks -- full records -- cross ranks."""
 import os
 import socket
 
@@ -15,85 +21,110 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, G, banks, passes, q):
+def _worker(rank, world, port, G, banks, passes, codec, churn, q):
     import torch
     import torch.distributed as dist
+    from dragonboat_amd import abi, populations as P
     from dragonboat_amd.engine import Engine
-    from dragonboat_amd.exchange import Pipeline
+    from dragonboat_amd.exchange import Pipeline, group_seed
+    from oracle.pyoracle import OraclePopulation
+    import parity
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    R = 3
     try:
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        pipe = Pipeline(G, 3, 3, world, rank, "spread", banks=banks, seed=11)
+        pipe = Pipeline(G, R, R, world, rank, "spread", banks=banks, seed=11, codec=codec)
         pipe.setup(Engine, torch.device("cuda", 0), 0)
-        states = []
+        # the oracle: every bank's groups of every home, as one population each
+        pops, msgs, topos = {}, {}, {}
+        for b, ex in enumerate(pipe.ex):
+            topos[b] = P.Topology(ex.G, R)
+            for h in range(world):
+                seed = int(np.random.SeedSequence(group_seed(11 + 7919 * b, h)).generate_state(1)[0])
+                pops[(b, h)] = OraclePopulation(P.make_groups(ex.G, R, seed=seed), R)
+                msgs[(b, h)] = np.zeros(0, abi.MESSAGE)
+        rng = np.random.default_rng(100 + 0)  # the same draws on every rank
+        bad, esc = None, 0
         for k in range(passes):
-            pipe.step(k)
+            tk = 1 if churn and k % 3 == 2 else 0
+            home_loc = {}
+            for b, ex in enumerate(pipe.ex):
+                Gb = ex.G
+                for h in range(world):
+                    pop = pops[(b, h)]
+                    if churn and k in (1, 4):
+                        cur = pop.export()
+                        ch = P.inject_leader_change(cur, topos[b], 0.1, rng)
+                        if len(ch):
+                            pop.reload(ch, cur[ch])
+                            mine = [(int(s) % Gb, int(s) // Gb) for s in ch if (h + int(s) // Gb) % world == rank]
+                            if mine:
+                                local = np.array([r * Gb + g for g, r in mine], np.uint32)
+                                pipe.engines[b].load_peers(local, cur[[r * Gb + g for g, r in mine]])
+                    st = pop.export()
+                    leaders = np.nonzero(st["state"] == abi.LEADER)[0] if churn else np.arange(Gb)
+                    home_loc[(b, h)] = P.propose_locals(R * Gb, leaders, pass_index=k if churn else 0, ticks=tk)
+                # this rank's replica r of home (rank - r) % world takes that home's local input
+                loc = np.zeros(R * Gb, abi.LOCAL)
+                for r in range(R):
+                    h = (rank - r) % world
+                    sl = slice(r * Gb, (r + 1) * Gb)
+                    loc[sl] = home_loc[(b, h)][sl]
+                loc["peer"] = np.arange(R * Gb, dtype=np.uint32)
+                pipe.engines[b].set_locals(loc)
+            # a tick pass and the pass of its acks are heavy: the dense form crosses
+            # (exchange.py); the leader changes' traffic crosses as compact records
+            # and full entries
+            pipe.step(k, heavy=churn and k > 0 and k % 3 in (2, 0))
             pipe.synchronize()
-            states.append([eng.sync(ex.n_peers) for ex, eng in zip(pipe.ex, pipe.engines)])
+            for b, ex in enumerate(pipe.ex):
+                Gb = ex.G
+                dev = pipe.engines[b].sync(ex.n_peers)
+                res = pipe.engines[b].collect_results(ex.n_peers)
+                esc += int(np.count_nonzero(res["escalation"]))
+                for h in range(world):
+                    o = pops[(b, h)].step(msgs[(b, h)], home_loc[(b, h)])
+                    msgs[(b, h)] = topos[b].route_messages(o["msgs"])
+                for r in range(R):
+                    h = (rank - r) % world
+                    sl = slice(r * Gb, (r + 1) * Gb)
+                    d = parity.compare_states(dev[sl], pops[(b, h)].export()[sl], R)
+                    if d and bad is None:
+                        bad = (k, b, r, d[:2])
         st = pipe.stats()
         pipe.close()
         dist.destroy_process_group()
-        q.put((rank, states, st["escalations"], None))
+        q.put((rank, bad, esc, st["leader_commits"], None))
     except Exception as e:  # reported to the test, never a hang
-        q.put((rank, None, 0, repr(e)))
+        import traceback
+        q.put((rank, None, 0, 0, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("banks", [1, 2])
-def test_pipeline_world2_gloo_matches_oracle(gpu, banks):
+@pytest.mark.parametrize("banks,codec,churn", [(1, "cx", False), (2, "cx", False), (2, "dense", False),
+                                               (1, "cx", True), (2, "dense", True)])
+def test_pipeline_world2_gloo_matches_oracle(gpu, banks, codec, churn):
     import torch.multiprocessing as mp
-    from dragonboat_amd import abi, populations as P
-    from dragonboat_amd.exchange import Exchange, group_seed
-    from oracle.pyoracle import OraclePopulation
-    import parity
-    world, G, passes, R = 2, 1000, 6, 3
+    world, G, passes = 2, 1000, 7 if churn else 6
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, G, banks, passes, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, G, banks, passes, codec, churn, q))
+             for r in range(world)]
     for p in procs:
         p.start()
-    res = {}
     try:
         for _ in procs:
-            rank, states, esc, err = q.get(timeout=240)
+            rank, bad, esc, commits, err = q.get(timeout=240)
             assert err is None, (rank, err)
-            assert esc == 0
-            res[rank] = states
+            assert esc == 0, (rank, esc)
+            assert bad is None, (rank, bad)
+            assert commits > 0
     finally:
         for p in procs:
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
-    # bank layout as Pipeline builds it (sizes and seeds per bank)
-    from dragonboat_amd.exchange import Pipeline
-    layout = Pipeline(G, R, R, world, 0, "spread", banks=banks, seed=11)
-    topo = {}
-    for b, ex in enumerate(layout.ex):
-        seed = 11 + 7919 * b
-        Gb = ex.G
-        tp = P.Topology(Gb, R)
-        for h in range(world):
-            peers = P.make_groups(Gb, R, seed=int(np.random.SeedSequence(group_seed(seed, h)).generate_state(1)[0]))
-            pop = OraclePopulation(peers, R)
-            msgs = np.zeros(0, abi.MESSAGE)
-            seq = []
-            for k in range(passes):
-                o = pop.step(msgs, P.propose_locals(R * Gb, np.arange(Gb), pass_index=0))
-                seq.append(pop.export())
-                msgs = tp.route_messages(o["msgs"])
-            topo[(b, h)] = seq
-    for rank in range(world):
-        for k in range(passes):
-            for b, ex in enumerate(layout.ex):
-                dev = res[rank][k][b]
-                Gb = ex.G
-                for r in range(R):
-                    h = (rank - r) % world
-                    sl = slice(r * Gb, (r + 1) * Gb)
-                    bad = parity.compare_states(dev[sl], topo[(b, h)][k][sl], R)
-                    assert not bad, (rank, k, b, r, bad[:2])
-    assert all(int(res[r][-1][0]["committed"][:10].min()) > int(res[r][0][0]["committed"][:10].min()) for r in res)

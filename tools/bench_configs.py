@@ -29,12 +29,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(name, peers, G, R, passes, warmup, prepare, graph_reps=0):
+def run(name, peers, G, R, passes, warmup, prepare, graph_reps=0, stream_reps=0):
     """prepare(k, eng, n_peers) -> local inputs of pass k (may also reload groups).
     graph_reps > 0: afterwards, two passes captured with the library's graph mode
     (gr_graph_capture) and replayed graph_reps times (gr_graph_replay): the per-pass
     time with no CPU launch in it. The local inputs then stay
-    those of the last pass (config 2's proposals are the same every pass)."""
+    those of the last pass (config 2's proposals are the same every pass).
+    stream_reps > 0: the same passes through gr_step_device, stream_reps of them
+    enqueued back to back behind a device sleep (no caller-side graph, no event
+    between passes): HIP events around the batch give the per-pass device time,
+    perf_counter around the enqueue loop the host's cost per call."""
     import torch
     from dragonboat_amd.engine import Engine
     from dragonboat_amd.exchange import Exchange
@@ -94,6 +98,29 @@ def run(name, peers, G, R, passes, warmup, prepare, graph_reps=0):
         graph = {"api": "gr_graph_capture/gr_graph_replay", "passes": 2 * graph_reps, "ms_per_pass": gms,
                  "leader_commits_per_pass": commits / (2 * graph_reps),
                  "leader_commits_per_s": commits / (2 * graph_reps * gms * 1e-3)}
+    stream = None
+    if stream_reps:
+        k0 = warmup + passes + (2 if graph_reps else 0) + ((warmup + passes) & 1 if graph_reps else 0)
+        cs = torch.cuda.current_stream()
+        for k in range(k0, k0 + 4):  # warm
+            ex.step(eng, spaces, k, cs)
+        torch.cuda.synchronize()
+        c0 = eng.stats()["leader_commits"]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(int(2.4e9 * 25e-6 * stream_reps))  # outlasts the host's enqueue loop
+        e0.record()
+        th = time.perf_counter()
+        for k in range(k0 + 4, k0 + 4 + stream_reps):
+            ex.step(eng, spaces, k, cs)
+        th = time.perf_counter() - th
+        e1.record()
+        torch.cuda.synchronize()
+        sms = e0.elapsed_time(e1) / stream_reps
+        commits = eng.stats()["leader_commits"] - c0
+        stream = {"api": "gr_step_device, passes enqueued back to back", "passes": stream_reps, "ms_per_pass": sms,
+                  "host_enqueue_us_per_pass": th / stream_reps * 1e6,
+                  "leader_commits_per_pass": commits / stream_reps,
+                  "leader_commits_per_s": commits / (stream_reps * sms * 1e-3)}
     from dragonboat_amd import abi
     import numpy as np
     res = eng.collect_results(ex.n_peers)  # the last pass's per-lane results
@@ -111,6 +138,8 @@ def run(name, peers, G, R, passes, warmup, prepare, graph_reps=0):
            "last_pass_escalations": reasons}
     if graph:
         out["graph"] = graph
+    if stream:
+        out["stream"] = stream
     eng.close()
     return out
 
@@ -121,6 +150,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--only", default="2,3,5")
     ap.add_argument("--graph-reps", type=int, default=200, help="config 2: replays of a 2-pass HIP graph (0: off)")
+    ap.add_argument("--stream-reps", type=int, default=400,
+                    help="config 2: gr_step_device passes enqueued back to back (0: off)")
     ap.add_argument("--groups2", type=int, default=10_000, help="config 2's group count")
     ap.add_argument("--align", type=int, default=64, help="config 2: replica blocks padded to this many lanes")
     args = ap.parse_args()
@@ -140,7 +171,8 @@ def main():
         Gl = -(-G // args.align) * args.align
         peers = P.make_groups(Gl, R, seed=2)
         r = run(f"2: {G} x 3, uniform proposals", peers, Gl, R, args.passes, args.warmup,
-                lambda k, eng, n: P.propose_locals(n, np.arange(G), pass_index=k), graph_reps=args.graph_reps)
+                lambda k, eng, n: P.propose_locals(n, np.arange(G), pass_index=k), graph_reps=args.graph_reps,
+                stream_reps=args.stream_reps)
         r["groups"], r["lane_groups"] = G, Gl
         res.append(r)
     if "3" in want:

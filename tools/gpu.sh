@@ -5,7 +5,8 @@
 #
 #   gpurun -- bash tools/gpu.sh STEP [STEP ...]
 #
-# STEP = KIND[@TAG][:VAR=V,VAR=V...]   (the VARs are set for that step only)
+# STEP = KIND[@TAG][:VAR=V,VAR=V...]   (the VARs are set for that step only; a
+#        '+' in a value stands for a space: BENCH_ARGS=--groups+2000000)
 #   warm              import torch and touch the device (first import is slow)
 #   tests             python -m pytest tests -m gpu ($TESTS selects files/-k)
 #   bench             bench.py $BENCH_ARGS        -> gpurun_out/bench_TAG.log
@@ -13,6 +14,8 @@
 #   trace             rocprofv3 --kernel-trace --stats of bench.py -> gpurun_out/trace_TAG/
 #   cfgtrace          the same over tools/bench_configs.py $CFG_ARGS
 #   profile           tools/profile.sh (trace + calibrated PMC passes), TAG=...
+#   cfgprofile        tools/profile_configs.sh (configs 2, 3, 5 traced; PMC of 3, 5), TAG=...
+#   rehearse          bench.py at N = 2 on one GPU over gloo (torch.distributed.run) -> rehearse_TAG.log
 #   smoke             __graft_entry__.smoke()
 # Defaults: BENCH_ARGS="--steps 20 --warmup 5 --cpu-baseline off --host-path off".
 set -u
@@ -41,7 +44,14 @@ run_step() {
   [[ "$spec" == *:* ]] && envs="${spec#*:}"
   local -a ev=()
   if [ -n "$envs" ]; then IFS=',' read -r -a ev <<< "$envs"; fi
+  local i
+  for i in "${!ev[@]}"; do ev[$i]="${ev[$i]//+/ }"; done
   echo "== $kind tag=$tag env=${envs:-none}"
+  # the step's variables also reach this script's own expansions ($BENCH_ARGS ...)
+  local BENCH_ARGS="$BENCH_ARGS" CFG_ARGS="$CFG_ARGS" TESTS="$TESTS"
+  for i in "${!ev[@]}"; do
+    case "${ev[$i]}" in BENCH_ARGS=*|CFG_ARGS=*|TESTS=*) eval "${ev[$i]%%=*}=\"\${ev[$i]#*=}\"" ;; esac
+  done
   local rc=0
   case "$kind" in
     warm)
@@ -74,6 +84,14 @@ EOF
     profile)
       env "${ev[@]}" TAG=$tag timeout -k 10 900 bash tools/profile.sh > $OUT/profile_$tag.log 2>&1; rc=$?
       tail -3 $OUT/profile_$tag.log ;;
+    cfgprofile)
+      env "${ev[@]}" TAG=$tag timeout -k 10 900 bash tools/profile_configs.sh > $OUT/cfgprofile_$tag.log 2>&1; rc=$?
+      tail -3 $OUT/cfgprofile_$tag.log ;;
+    rehearse)  # bench.py's N > 1 script at N = 2 on one GPU, collectives over gloo
+      env "${ev[@]}" GR_BENCH_BACKEND=gloo GR_BENCH_ONE_DEVICE=1 timeout -k 10 600 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 \
+        $BENCH_ARGS > $OUT/rehearse_$tag.log 2>&1; rc=$?
+      grep '^{' $OUT/rehearse_$tag.log | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('N=2 ms_per_step %.4f exchange_bytes_per_pass %s heavy %s value %.3g' % (d['ms_per_step'], d.get('exchange_bytes_per_pass'), d.get('exchange_bytes_heavy_pass'), d['value']))" ;;
     smoke)
       env "${ev[@]}" timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
         > $OUT/smoke.log 2>&1; rc=$?; tail -1 $OUT/smoke.log ;;
