@@ -53,6 +53,16 @@ def source_digest():
     return h.hexdigest()[:16]
 
 
+def _locked(out):
+    """An exclusive lock on `out`'s build (test workers build on first use, side
+    by side: one builds, the others wait and then find it fresh)."""
+    import fcntl
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    lk = open(out + ".lock", "w")
+    fcntl.flock(lk, fcntl.LOCK_EX)
+    return lk
+
+
 def _stale(out, deps):
     if not os.path.exists(out):
         return True
@@ -71,7 +81,7 @@ def _run(cmd):
 # lean lane made a 1M x 3 pass 6x slower (0.82 vs 0.13 ms) and moved 3 GB of
 # scratch traffic per launch. The compiler's resource remarks are checked at
 # build time, so such a build fails instead of shipping.
-NO_SCRATCH_KERNELS = ("gr_fast_kernel", "gr_roles_kernel")
+NO_SCRATCH_KERNELS = ("gr_fast_kernel", "gr_roles_kernel", "gr_steady_kernel")
 RESOURCE_REMARKS = "-Rpass-analysis=kernel-resource-usage"
 
 
@@ -91,9 +101,15 @@ def _hip_lib(out, srcs, deps, extra=(), force=False, scratch_check=True):
     """Compile every source to an object in parallel (hipcc, gfx950), then link `out`.
     scratch_check: refuse lean-kernel instances that use scratch (product builds;
     the coverage build's hit counters cost registers, and it is never timed)."""
-    os.makedirs(os.path.dirname(out), exist_ok=True)
     if not (force or _stale(out, deps)):
         return out
+    with _locked(out):
+        if not (force or _stale(out, deps)):  # built while this worker waited
+            return out
+        return _hip_lib_locked(out, srcs, extra, scratch_check)
+
+
+def _hip_lib_locked(out, srcs, extra, scratch_check):
     odir = out + ".o.d"
     os.makedirs(odir, exist_ok=True)
     # the lean lane's message loop (gr_fast.h: slots x messages, each able to
@@ -143,7 +159,12 @@ def build_oracle(force=False):
 def build_hostlane(force=False):
     os.makedirs(os.path.dirname(HOSTLANE_LIB), exist_ok=True)
     src = os.path.join(ROOT, "tests", "native", "hostlane.hip")
-    if force or _stale(HOSTLANE_LIB, ENGINE_DEPS + [src]):
+    deps = ENGINE_DEPS + [src]
+    if not (force or _stale(HOSTLANE_LIB, deps)):
+        return HOSTLANE_LIB
+    with _locked(HOSTLANE_LIB):
+        if not (force or _stale(HOSTLANE_LIB, deps)):
+            return HOSTLANE_LIB
         _run([HIPCC, "--cuda-host-only", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-DGR_COVERAGE",
               "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "dragonboat_amd", "csrc"),
               src, "-o", HOSTLANE_LIB])

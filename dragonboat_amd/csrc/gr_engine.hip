@@ -73,6 +73,7 @@ struct gr_engine {
   uint64_t* stats = nullptr;
   uint32_t stats_rows = 0;
   uint32_t* bail = nullptr;      // kBailLists lists of cap lanes each, then the wave lists (bail_words)
+  uint64_t* tick_stage = nullptr;  // a TickStage record per tick-list entry (gr_layout.h)
   uint32_t* counters = nullptr;  // [2 (pass parity)][kCounters][kCounterStride]
   // gr_step_device passes of at least this many lanes run the role instances
   // (StepParams::split); GR_SPLIT_MIN_LANES at gr_create overrides it (tests)
@@ -220,6 +221,7 @@ StepParams base_params(gr_engine* e) {
   kp.bin_general = e->bin_general;
   kp.tail_hint = e->tail_hint;
   kp.tail_mode = e->tail_mode;
+  kp.tick_stage = e->tick_stage;
   return kp;
 }
 
@@ -408,6 +410,7 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
   if (hipMalloc(&ds, sb) != hipSuccess || hipMalloc(&dl, lb) != hipSuccess ||
       hipMalloc((void**)&e->stats, (size_t)e->stats_rows * NSTAT * 8) != hipSuccess ||
       hipMalloc((void**)&e->bail, bail_words(e->cap) * 4) != hipSuccess ||
+      hipMalloc((void**)&e->tick_stage, (size_t)kTickLists * tick_cap(e->cap) * kTickStageWords * 8) != hipSuccess ||
       hipMalloc((void**)&e->counters, 2 * kCounters * kCounterStride * 4) != hipSuccess ||
       hipMalloc((void**)&e->route_base, 2 * GR_SMAX * GR_SMAX * 4) != hipSuccess ||
       hipMalloc((void**)&e->hints, 2 * hint_stride(e->cap)) != hipSuccess) {
@@ -446,6 +449,7 @@ void gr_destroy(gr_engine* e) {
   if (e->ln.base) (void)hipFree(e->ln.base);
   if (e->stats) (void)hipFree(e->stats);
   if (e->bail) (void)hipFree(e->bail);
+  if (e->tick_stage) (void)hipFree(e->tick_stage);
   if (e->counters) (void)hipFree(e->counters);
   if (e->route_base) (void)hipFree(e->route_base);
   if (e->hints) (void)hipFree(e->hints);

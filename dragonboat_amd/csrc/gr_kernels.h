@@ -150,19 +150,25 @@ __device__ inline __attribute__((always_inline)) void bail_append(bool mine, uin
 
 // One wave's appends to the tick list of lanes with key `key` (a lane or retry
 // entry index; key >> 8, its 256-lane block, is the same for the wave's lanes).
-__device__ inline __attribute__((always_inline)) void tick_append(bool mine, uint32_t key, uint32_t* bail_list,
-                                                                  uint32_t* counters, uint32_t list_cap, uint32_t i) {
+// Returns the lane's entry (list * tick_cap + index: its TickStage record).
+// unstaged: the TickStage records (StepParams::tick_stage) of an appender that
+// stages nothing, whose entries' tag words are overwritten so that no record of
+// an earlier pass (or graph replay) passes for this one's.
+__device__ inline __attribute__((always_inline)) uint64_t tick_append(bool mine, uint32_t key, uint32_t* bail_list,
+                                                                      uint32_t* counters, uint32_t list_cap,
+                                                                      uint32_t i, uint64_t* unstaged = nullptr) {
   const uint64_t bm = __ballot(mine);
-  if (!bm) return;
+  if (!bm) return 0;
   const uint32_t l = ((uint32_t)__builtin_amdgcn_readfirstlane(key) >> 8) % kTickLists;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t first = (uint32_t)__ffsll((unsigned long long)bm) - 1;
   uint32_t base = 0;
   if (lane == first) base = atomicAdd(counters + (kTickCounter0 + l) * kCounterStride, (uint32_t)__popcll(bm));
   base = __shfl(base, (int)first);
-  if (mine)
-    bail_list[tick_off(list_cap) + (uint64_t)l * tick_cap(list_cap) + base +
-              (uint32_t)__popcll(bm & ((1ull << lane) - 1))] = i;
+  const uint64_t e = (uint64_t)l * tick_cap(list_cap) + base + (uint32_t)__popcll(bm & ((1ull << lane) - 1));
+  if (mine) bail_list[tick_off(list_cap) + e] = i;
+  if (mine && unstaged) unstaged[e * kTickStageWords + 2] = ~0ull;
+  return e;
 }
 
 // The general kernel's lane classes (StepParams::bin_general): role, whether a
@@ -290,7 +296,7 @@ __device__ inline __attribute__((always_inline)) void wave_finish(const StepPara
   const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
   const uint32_t p = bail && !tickish && kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
   general_append<S>(kp, bail && !tickish, lead, i, p, bid, bail_list, counters, list_cap);
-  tick_append(tickish, wave * 64, bail_list, counters, list_cap, i);  // the wave's lanes share a block
+  tick_append(tickish, wave * 64, bail_list, counters, list_cap, i, kp.tick_stage);  // the wave's lanes share a block
   if (kp.stats) block_stats(kp, ls, bid);
 }
 
@@ -405,7 +411,7 @@ __device__ inline __attribute__((always_inline)) void roles_listed(const StepPar
     const bool lead = role == GR_LEADER;
     const bool tickish = bail && kp.has_locals && (kp.ln.u32(LR_LWORD)[li] & LW_OTHER);
     general_append<S>(kp, bail && !tickish, lead, li, li, bid, bail_list, counters, list_cap);
-    tick_append(tickish, base, bail_list, counters, list_cap, li);  // keyed by the entry's block
+    tick_append(tickish, base, bail_list, counters, list_cap, li, kp.tick_stage);  // keyed by the entry's block
   }
   if (kp.stats && n > bid * kBlock) block_stats(kp, acc, bid);
 }
@@ -489,8 +495,14 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
     // form), lanes with ticks or a ReadIndex go straight to the tick lists, and
     // the rest are listed for the role instances (wave flag + lane mask)
     const bool active = i < kp.n_lanes;
-    const int q = active ? quiet_step<S, RM>(kp, i, i) : QS_DONE;
-    tick_append(q == QS_TICK, i, bail_list, counters, list_cap, i);
+    uint64_t stage[kTickStageWords] = {};
+    const int q = active ? quiet_step<S, RM>(kp, i, i, stage, kp.tick_stage != nullptr) : QS_DONE;
+    const uint64_t te = tick_append(q == QS_TICK, i, bail_list, counters, list_cap, i);
+    if (q == QS_TICK && kp.tick_stage) {  // the tick lane's record (gr_layout.h TickStage)
+      uint64_t* r = kp.tick_stage + te * kTickStageWords;
+#pragma unroll
+      for (uint32_t w = 0; w < kTickStageWords; ++w) r[w] = stage[w];
+    }
     if (kp.no_roles) {
       // no role instances follow (TailPlan): the rest go straight to the retry
       // lists, which the churn and general kernels then walk with their own lists
@@ -541,7 +553,7 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
 #ifndef GR_TICK_MIN_WAVES
 #define GR_TICK_MIN_WAVES 1
 #endif
-template <int S>
+template <int S, int RM>
 __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(StepParams kp, uint32_t* bail_list,
                                                                              uint32_t* counters, uint32_t list_cap) {
   // the lists' exclusive prefix (one wave scans the kTickLists counters)
@@ -574,10 +586,14 @@ __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(Step
       uint32_t l = 0;  // the last list whose start is at or below x (binary search)
 #pragma unroll
       for (uint32_t step = kTickLists / 2; step > 0; step >>= 1) l = tstart[l + step] <= x ? l + step : l;
-      i = tl[(uint64_t)l * tc + (x - tstart[l])];
+      const uint64_t e = (uint64_t)l * tc + (x - tstart[l]);
+      i = tl[e];
       const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
       LaneStats ls;
-      if (tick_step<S>(kp, i, p, &ls)) {
+      // the entry's staged record (the steady kernel's entries; any other's
+      // carries an older pass tag, and the lane loads its fields itself)
+      const uint64_t* stg = kp.tick_stage ? kp.tick_stage + e * kTickStageWords : nullptr;
+      if (tick_step<S, RM>(kp, i, p, &ls, stg)) {
         GR_CHECK_STATE(kp.st, p);
         acc.leader_commit += ls.leader_commit;
         acc.follower_commit += ls.follower_commit;
@@ -1027,9 +1043,11 @@ hipError_t launch_fast(const StepParams& kp0, uint32_t blocks, uint32_t* bail_li
 }
 
 template <int S>
-hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters, uint32_t list_cap,
+hipError_t launch(const StepParams& kp_in, uint32_t* bail_list, uint32_t* counters, uint32_t list_cap,
                          uint32_t parity, hipStream_t s, const PassTiming* t, bool tick_lanes) {
-  if (kp.n_lanes == 0) return hipSuccess;
+  if (kp_in.n_lanes == 0) return hipSuccess;
+  StepParams kp = kp_in;
+  kp.pass_tag = parity;  // the launch number (TickStage records of this pass)
   const uint32_t blocks = (kp.n_lanes + kBlock - 1) / kBlock;
   uint32_t* cur = counters + (parity & 1) * kCounters * kCounterStride;
   uint32_t* nxt = counters + ((parity + 1) & 1) * kCounters * kCounterStride;
@@ -1063,7 +1081,14 @@ hipError_t launch(const StepParams& kp, uint32_t* bail_list, uint32_t* counters,
   if (tick_lanes) {  // some lane may carry ticks or a ReadIndex (LW_OTHER)
     const uint32_t tw = tick_wg(), tmax = kTickBlocks * (kBlock / tw);
     const uint32_t tblocks = blocks * (kBlock / tw) < tmax ? blocks * (kBlock / tw) : tmax;
-    hipLaunchKernelGGL(gr_tick_kernel<S>, dim3(tblocks), dim3(tw), 0, s, kp, bail_list, cur, list_cap);
+    // the route mode as the lean instances have it (compile-time routes: every
+    // address of the lane's first round known before its first load)
+    if (loop1)
+      hipLaunchKernelGGL((gr_tick_kernel<S, RT_LOOPBACK>), dim3(tblocks), dim3(tw), 0, s, kp, bail_list, cur, list_cap);
+    else if (kp.route_mode == RT_AFFINE)
+      hipLaunchKernelGGL((gr_tick_kernel<S, RT_AFFINE>), dim3(tblocks), dim3(tw), 0, s, kp, bail_list, cur, list_cap);
+    else
+      hipLaunchKernelGGL((gr_tick_kernel<S, RM_ANY>), dim3(tblocks), dim3(tw), 0, s, kp, bail_list, cur, list_cap);
     if ((err = hipGetLastError()) != hipSuccess) return err;
   }
   if (plan.churn) {  // the churn lane first; the general kernel then walks its leftovers

@@ -579,7 +579,18 @@ struct StepParams {
   // set by the launcher for the steady kernel of a pass whose role instances do
   // not run: its non-steady lanes go to the retry lists (gr_kernels.h GM_RETRY)
   uint8_t no_roles;
+  // the tick lane's staged inputs (TickStage): one record per tick-list entry,
+  // written by the steady kernel (nullptr: the tick lane loads everything itself)
+  uint64_t* tick_stage;
+  uint32_t pass_tag;  // the launch number: a record of this pass carries it
 };
+// A tick-list entry's staged inputs (round 5): the fields the steady kernel
+// loads for every lane of a wave that is not steady (coalesced: the wave's
+// quiesced lanes load the same lines), so the tick lane reads one 32-byte record
+// instead of a header, electionTick, locals word and S count bytes scattered
+// over as many lines. Words: header, electionTick, locals word | pass tag << 32,
+// the S in-mailbox count bytes.
+constexpr uint32_t kTickStageWords = 4;
 constexpr uint32_t kWaveClockWords = 8;
 // The wave's clock for GR_WAVE_CLOCK phase marks (0 when off, and in host builds).
 __host__ __device__ inline uint64_t lane_clock(const StepParams& kp) {

@@ -350,21 +350,40 @@ constexpr int QS_DONE = 0, QS_TICK = 1, QS_OTHER = 2;
 // in-mailbox, no proposal, no tick or ReadIndex. Quiesced populations carry no
 // role hint (a wave of quiet groups has no input to speculate on), so their
 // lanes would otherwise all go through the role instances.
+// stage (a lane with ticks or a ReadIndex, QS_TICK): its TickStage words (the
+// header, electionTick, locals word and count bytes, loaded here with the
+// wave's quiesced lanes), and its out counts zeroed here (coalesced with theirs;
+// the tick lane then writes only the mailboxes it fills).
 template <int S, int RM>
-GF_HD int quiet_step(const StepParams& kp, uint32_t i, uint32_t p) {  // lane i, peer p
+GF_HD int quiet_step(const StepParams& kp, uint32_t i, uint32_t p, uint64_t* stage, bool do_stage) {  // lane i, peer p
   constexpr bool kOneChunk = RM == RT_LOOPBACK;
   if (!kp.has_locals) return QS_OTHER;
   const uint32_t lw = ntld(kp.ln.u32(LR_LWORD)[i]);
-  if (lw & LW_OTHER) return QS_TICK;
+  const bool tick = (lw & LW_OTHER) != 0;
+  if (tick && !do_stage) return QS_TICK;
   const uint32_t np = lw & 0xFFFFu, nq = (lw >> LW_QT_SHIFT) & LW_QT_MAX;
-  if (!nq || np) return QS_OTHER;
+  if (!tick && (!nq || np)) return QS_OTHER;
   uint32_t gin[S], gout[S];
   routes_of<S, RM>(kp, i, gin, gout);
   const uint64_t hdr = ntld(kp.st.u64(SR_HDR)[p]), et = ntld(kp.st.u64(SR_ETICK)[p]);
   uint32_t any = 0;
+  uint64_t cw = 0;
 #pragma unroll
-  for (int j = 0; j < S; ++j)
-    any |= gin[j] != NOPOS ? mb_n((uint32_t)ntld(kp.in.template at<kOneChunk>(gin[j]).cnt())) : 0u;
+  for (int j = 0; j < S; ++j) {
+    const uint32_t b = gin[j] != NOPOS ? (uint32_t)ntld(kp.in.template at<kOneChunk>(gin[j]).cnt()) : 0u;
+    any |= mb_n(b);
+    cw |= (uint64_t)(b & 0xFFu) << (8 * j);
+  }
+  if (tick) {
+    stage[0] = hdr;
+    stage[1] = et;
+    stage[2] = lw | ((uint64_t)kp.pass_tag << 32);
+    stage[3] = cw;
+#pragma unroll
+    for (int j = 0; j < S; ++j)
+      if (gout[j] != NOPOS) ntst(kp.out.template at<kOneChunk>(gout[j]).cnt(), (uint8_t)0);
+    return QS_TICK;
+  }
   if (any) return QS_OTHER;
   ntst(kp.st.u64(SR_ETICK)[p], (uint64_t)(et + nq));
   if (h_flags(hdr) & F_ETZ) ntst(kp.st.u64(SR_HDR)[p], hdr & ~((uint64_t)F_ETZ << H_FLAGS_SHIFT));

@@ -36,7 +36,18 @@ GT_HD uint32_t gt_popc8(uint32_t x) {
   return (x + (x >> 4)) & 0x0Fu;
 }
 
-template <int S>
+// The value as an opaque definition (device code): an empty asm that reads and
+// writes it, so code that uses the value only under a condition cannot make its
+// load conditional. Identity in host builds.
+template <class T>
+GT_HD T gt_keep(T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(v));
+#endif
+  return v;
+}
+
+template <int S, int RM = RM_ANY>
 struct TickLane {
   using Rw = Rows<S>;
   static constexpr int MK = 2;  // messages per mailbox handled here
@@ -47,7 +58,7 @@ struct TickLane {
   uint64_t hdr = 0;
   uint32_t state = 0, self = 0, flags = 0, nruns = 0;
   bool gelo = false;
-  uint64_t term = 0, committed = 0, committed0 = 0, hi = 0, rsn = 0, rtn = 0;
+  uint64_t term = 0, committed = 0, committed0 = 0, hi = 0, rsn = 0, rtn = 0, rclo = 0, rchi = 0;
   uint64_t etick = 0, etick0 = 0;
   // leader
   uint64_t match[S];
@@ -62,7 +73,10 @@ struct TickLane {
   uint32_t gout[S], outc[S];
   uint32_t nmi = 0, nmo = 0;
 
-  GT_HD TickLane(const StepParams& k, uint32_t lane, uint32_t peer) : kp(k), i(lane), p(peer) {}
+  const uint64_t* stage;  // the entry's TickStage record, or nullptr
+  bool staged = false;    // ... written this pass: the out counts are zero already
+  GT_HD TickLane(const StepParams& k, uint32_t lane, uint32_t peer, const uint64_t* stg = nullptr)
+      : kp(k), i(lane), p(peer), stage(stg) {}
   GT_HD uint64_t& s64(uint32_t row) const { return kp.st.u64(row)[p]; }
   GT_HD uint8_t& s8(uint32_t row) const { return kp.st.u8(row)[p]; }
 
@@ -201,23 +215,66 @@ struct TickLane {
     broadcast_heartbeat(clo, chi);  // also for a duplicate (raft.go:1200-1201)
   }
 
+  // Loads whose need is known only per lane are issued unconditionally, with
+  // the address of a line the lane reads anyway (its header) or of one shared
+  // line (position 0) when the value is not needed: a branch around a load made
+  // the compiler wait for it before the next slot's, so the lane's two rounds of
+  // loads became one round trip per slot and message (round 5: 80 vmcnt waits
+  // in the S = 5 kernel).
+  GT_HD uint64_t ld64(uint32_t row, bool need) const {
+    const uint64_t v = kp.st.u64(need ? row : (uint32_t)SR_HDR)[p];
+    return need ? v : 0ull;
+  }
+  GT_HD uint32_t ld8(uint32_t row, bool need) const {
+    const uint32_t v = kp.st.u8(row)[need ? p : 0u];
+    return need ? v : 0u;
+  }
+
   GT_HD bool step(LaneStats* ls) {
-    // ---- round 1
-    hdr = s64(SR_HDR);
+    // ---- round 1: every address is known before any load (routes from the
+    // lane index; compile-time route mode)
+    uint32_t gin[S];
+    routes_of<S, RM>(kp, i, gin, gout);
+    uint64_t sw[kTickStageWords] = {};
+    if (stage) {
+#pragma unroll
+      for (uint32_t w = 0; w < kTickStageWords; ++w) sw[w] = stage[w];
+    }
+    term = s64(SR_TERM);
+    committed = s64(SR_COMMITTED);
+    hi = s64(SR_LAST_INDEX);
+    staged = stage && (uint32_t)(sw[2] >> 32) == kp.pass_tag;
+    uint32_t lw = 0, cnt[S], cbs[S];
+    if (staged) {  // the steady kernel's loads of this pass (gr_steady.h quiet_step)
+      hdr = sw[0];
+      etick = sw[1];
+      lw = (uint32_t)sw[2];
+#pragma unroll
+      for (int j = 0; j < S; ++j) cbs[j] = (uint32_t)(sw[3] >> (8 * j)) & 0xFFu;
+    } else {
+      hdr = s64(SR_HDR);
+      etick = s64(SR_ETICK);
+      lw = kp.has_locals ? kp.ln.u32(LR_LWORD)[i] : 0u;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const uint32_t c = kp.in.at(gin[j] != NOPOS ? gin[j] : 0u).cnt();
+        cbs[j] = gin[j] != NOPOS ? c : 0u;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      outc[j] = 0;
+      cnt[j] = mb_n(cbs[j]);
+    }
     state = h_state(hdr);
     self = h_self(hdr);
     flags = h_flags(hdr);
     nruns = h_nruns(hdr);
     gelo = h_gelo(hdr);
-    term = s64(SR_TERM);
-    committed = s64(SR_COMMITTED);
-    hi = s64(SR_LAST_INDEX);
     uint32_t lf = 0, nt = 0, nq = 0, np = 0;
-    uint64_t rclo = 0, rchi = 0;
     if (kp.has_locals) {
       // the packed word holds the whole input when it is ticks and a ReadIndex
       // only (LW_TICKONLY): one row instead of four (gr_layout.h)
-      const uint32_t lw = kp.ln.u32(LR_LWORD)[i];
       if (lw & LW_TICKONLY) {
         nt = (lw >> LW_TICK_SHIFT) & LW_TICK_MAX;
         lf = (lw & LW_RI) ? LF_READ_INDEX : 0u;
@@ -227,19 +284,6 @@ struct TickLane {
         nq = kp.ln.u32(LR_QTICKS)[i];
         np = kp.ln.u32(LR_PROPOSE)[i];
       }
-      if (lf & LF_READ_INDEX) {
-        rclo = kp.ln.u64(LR_RI_LO)[i];
-        rchi = kp.ln.u64(LR_RI_HI)[i];
-      }
-    }
-    uint32_t gin[S], cnt[S], cbs[S];
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-      gin[j] = route_of(kp, 0, j, i);
-      gout[j] = route_of(kp, 1, j, i);
-      outc[j] = 0;
-      cbs[j] = gin[j] != NOPOS ? (uint32_t)kp.in.at(gin[j]).cnt() : 0u;
-      cnt[j] = mb_n(cbs[j]);
     }
     const bool leader = state == GR_LEADER;
     GT_BAIL(!leader && state != GR_FOLLOWER);
@@ -247,12 +291,18 @@ struct TickLane {
     for (int j = 0; j < S; ++j)  // cold fields lost in the exchange (gr_io.h side_pack): general lane
       GT_BAIL(cnt[j] && !(cbs[j] & MB_UNIFORM) && (cbs[j] & MB_COLD_LOST));
     GT_BAIL((lf & LF_PROPOSE_CC) || nq || np);
-    // ---- round 2
-    etick = s64(SR_ETICK);
+    // ---- round 2: one batch of loads, each at a real address when needed
+    const bool ri = (lf & LF_READ_INDEX) != 0;
+    {
+      const uint64_t a = kp.ln.u64(LR_RI_LO)[ri ? i : 0u], b = kp.ln.u64(LR_RI_HI)[ri ? i : 0u];
+      rclo = ri ? a : 0ull;
+      rchi = ri ? b : 0ull;
+    }
     uint64_t retimeout = 0;
-    if (nruns && leader && (lf & LF_READ_INDEX)) {  // the newest run (the last row): read_index's term test
-      rsn = s64(SR_RUN_START + GR_K - 1);
-      rtn = s64(SR_RUN_TERM + GR_K - 1);
+    {  // the newest run (the last row): read_index's term test
+      const bool nr = nruns && leader && ri;
+      rsn = ld64(SR_RUN_START + GR_K - 1, nr);
+      rtn = ld64(SR_RUN_TERM + GR_K - 1, nr);
     }
     uint32_t mh[S][MK];
     uint64_t mterm[S][MK], mcom[S][MK], mlo[S][MK], mhi[S][MK];
@@ -260,47 +310,67 @@ struct TickLane {
     for (int j = 0; j < S; ++j) {
 #pragma unroll
       for (int k = 0; k < MK; ++k) {
-        mh[j][k] = 0; mterm[j][k] = 0; mcom[j][k] = 0; mlo[j][k] = 0; mhi[j][k] = 0;
-        if ((uint32_t)k < cnt[j]) {
-          const Mailbox mb = kp.in.at(gin[j]);
-          mh[j][k] = mb.tag_at(k, cbs[j]) & 0xFFu;  // MB_UNIFORM: implied by the count byte
-          mterm[j][k] = mb.term_at(k, cbs[j]);
-          if (!leader) mcom[j][k] = mb.u64(k, MF_COMMIT);
-          mlo[j][k] = mb.u64(k, MF_HINT);
-          mhi[j][k] = mb.u64(k, MF_HINT_HIGH);
-        }
+        // message k's cold record (tag, term, Commit, Hint, HintHigh: one
+        // 64-byte line); a uniform mailbox (Replicates, acks) fails the type
+        // test below whatever the record holds
+        const bool has = (uint32_t)k < cnt[j];
+        const Mailbox mb = kp.in.at(has ? gin[j] : 0u);
+        const uint32_t kk = has ? (uint32_t)k : 0u;
+        mh[j][k] = mb.tag(kk);
+        mterm[j][k] = mb.t32(kk, MT_TERM);
+        mcom[j][k] = mb.u64(kk, MF_COMMIT);
+        mlo[j][k] = mb.u64(kk, MF_HINT);
+        mhi[j][k] = mb.u64(kk, MF_HINT_HIGH);
       }
     }
-    if (leader) {
-      htick = s64(SR_HTICK);
-      etimeout = s64(SR_ETIMEOUT);
-      htimeout = s64(SR_HTIMEOUT);
-      ric = h_ric(hdr);
+    htick = ld64(SR_HTICK, leader);
+    etimeout = ld64(SR_ETIMEOUT, leader);
+    htimeout = ld64(SR_HTIMEOUT, leader);
+    retimeout = ld64(SR_RETIMEOUT, !leader);
+    ric = leader ? h_ric(hdr) : 0u;
+    {
       const uint64_t rb = h_rb(hdr);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         // H_MS: the self slot's MATCH row is stale, its match is lastIndex;
         // H_MP: another slot's is lastIndex - 2
-        match[j] = (has_sync_bits(S) && h_ms(hdr) && (uint32_t)j == self)                ? hi
-                   : (has_sync_bits(S) && h_mp(hdr, (uint32_t)j) && (uint32_t)j != self) ? hi - 2
-                                                                                         : s64(Rw::MATCH + j);
-        rst[j] = rb_state(rb, j);
-        ract[j] = rb_active(rb, j);
-        rkind[j] = rb_kind(rb, j);
+        const bool ms = has_sync_bits(S) && h_ms(hdr) && (uint32_t)j == self;
+        const bool mp = has_sync_bits(S) && h_mp(hdr, (uint32_t)j) && (uint32_t)j != self;
+        const uint64_t m = ld64(Rw::MATCH + j, leader && !ms && !mp);
+        match[j] = ms ? hi : mp ? hi - 2 : m;
+        rst[j] = leader ? rb_state(rb, j) : 0u;
+        ract[j] = leader ? rb_active(rb, j) : 0u;
+        rkind[j] = leader ? rb_kind(rb, j) : 0u;
       }
-      // the FIFO's live entries only (entries at or past the count are never
-      // read: parity and the host compare the first read_index_count)
+    }
+    // the FIFO's live entries only (entries at or past the count are never
+    // read: parity and the host compare the first read_index_count)
 #pragma unroll
-      for (int q = 0; q < GR_Q; ++q) {
-        const bool live = (uint32_t)q < ric;
-        rii[q] = live ? s64(Rw::RI_INDEX + q) : 0;
-        rilo[q] = live ? s64(Rw::RI_LO + q) : 0;
-        rihi[q] = live ? s64(Rw::RI_HI + q) : 0;
-        rifrom |= live ? (uint32_t)s8(Rw::B_RIFROM + q) << (8 * q) : 0u;
-        riack |= live ? (uint32_t)s8(Rw::B_RIACK + q) << (8 * q) : 0u;
+    for (int q = 0; q < GR_Q; ++q) {
+      const bool live = (uint32_t)q < ric;
+      rii[q] = ld64(Rw::RI_INDEX + q, live);
+      rilo[q] = ld64(Rw::RI_LO + q, live);
+      rihi[q] = ld64(Rw::RI_HI + q, live);
+      rifrom |= ld8(Rw::B_RIFROM + q, live) << (8 * q);
+      riack |= ld8(Rw::B_RIACK + q, live) << (8 * q);
+    }
+    // every round-2 load is issued before the first value is used: the values
+    // pass through an empty asm (gt_keep), so the optimiser cannot sink the
+    // loads under a per-message branch (it did: one wait per message)
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+#pragma unroll
+      for (int k = 0; k < MK; ++k) {
+        const bool has = (uint32_t)k < cnt[j];
+        const uint32_t tg = gt_keep(mh[j][k]);
+        const uint64_t tm = gt_keep(mterm[j][k]), cm = gt_keep(mcom[j][k]);
+        const uint64_t lo = gt_keep(mlo[j][k]), hh = gt_keep(mhi[j][k]);
+        mh[j][k] = has ? ((cbs[j] & MB_UNIFORM) ? Mailbox::uniform_tag(cbs[j], k) : tg) & 0xFFu : 0u;
+        mterm[j][k] = has ? tm : 0ull;
+        mcom[j][k] = has && !leader ? cm : 0ull;
+        mlo[j][k] = has ? lo : 0ull;
+        mhi[j][k] = has ? hh : 0ull;
       }
-    } else {
-      retimeout = s64(SR_RETIMEOUT);
     }
     committed0 = committed;
     etick0 = etick;
@@ -429,7 +499,7 @@ struct TickLane {
     if (nh != hdr) s64(SR_HDR) = nh;
 #pragma unroll
     for (int j = 0; j < S; ++j)
-      if (gout[j] != NOPOS) kp.out.at(gout[j]).cnt() = (uint8_t)outc[j];
+      if (gout[j] != NOPOS && (outc[j] || !staged)) kp.out.at(gout[j]).cnt() = (uint8_t)outc[j];
     uint8_t rf = 0;
     if (rtrc) {
       rf |= RF_READY;
@@ -457,9 +527,9 @@ struct TickLane {
   }
 };
 
-template <int S>
-GT_HD bool tick_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls) {
-  TickLane<S> L(kp, i, p);
+template <int S, int RM = RM_ANY>
+GT_HD bool tick_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, const uint64_t* stage = nullptr) {
+  TickLane<S, RM> L(kp, i, p, stage);
   return L.step(ls);
 }
 

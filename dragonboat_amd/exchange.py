@@ -76,13 +76,17 @@ def cx_fill(R, N, offset, leader=0):
     return sum(1 for r, j in pairs[offset] if leader in (r, j)) / per
 
 
-def cx_capacities(positions, fill, frac=None):
+def cx_capacities(positions, fill, frac=None, side=None):
     """(record capacity, full-entry capacity) of one compact-exchange chunk whose
-    steady-state fill is `fill` (frac: a fixed share instead of fill + margin)."""
+    steady-state fill is `fill` (frac: a fixed share instead of fill + margin;
+    side: the full-entry share of the positions instead of 1/CX_SIDE_DIV, for
+    callers whose passes are seldom steady, e.g. ticks on every pass; Exchange's
+    cx_side also sizes the dense form's side buffers)."""
     pc = pad_positions(positions)
     share = frac if frac is not None else fill + CX_MARGIN
     cap = min(pc, (int(pc * share) + 63) // 64 * 64)
-    return cap, max(CX_SIDE_MIN, pc // CX_SIDE_DIV)
+    scap = max(CX_SIDE_MIN, pc // CX_SIDE_DIV) if side is None else max(64, min(pc, int(pc * side)))
+    return cap, scap
 
 
 def pad_positions(positions):
@@ -164,12 +168,13 @@ def spread_peers(G, R, N, rank, seed=2, **kw):
 class Exchange:
     """Spaces + routes for one rank; `step` launches one pass and exchanges."""
 
-    def __init__(self, G, R, S, world, rank, placement, seed=2, exchange=None, codec="cx", cx_frac=None):
+    def __init__(self, G, R, S, world, rank, placement, seed=2, exchange=None, codec="cx", cx_frac=None,
+                 cx_side=None):
         """exchange=True keeps the one-rank spread exchange (copy + side buffers)
         that a one-rank run otherwise skips (tests of the N > 1 code on one GPU).
         codec: "cx" (compact exchange) or "dense" (hot region + side buffers)."""
         assert codec in ("cx", "dense")
-        self.codec, self.cx_frac = codec, cx_frac
+        self.codec, self.cx_frac, self.cx_side = codec, cx_frac, cx_side
         self.last_cx = codec == "cx"  # the form of the last exchange (unpack reads it)
         self.G, self.R, self.S = G, R, S
         self.world, self.rank, self.placement = world, rank, placement
@@ -216,7 +221,7 @@ class Exchange:
             # sender (destination d: offset d - rank) and the receiver (source a:
             # offset rank - a)
             N = self.world
-            cap_of = lambda o: cx_capacities(self.positions, cx_fill(self.R, N, o), self.cx_frac)
+            cap_of = lambda o: cx_capacities(self.positions, cx_fill(self.R, N, o), self.cx_frac, self.cx_side)
             self.cx_send_caps = [cap_of((d - self.rank) % N)[0] for d in self.dests]
             self.cx_recv_caps = [cap_of((self.rank - a) % N)[0] for a in self.srcs]
             self.cx_scap = cap_of(0)[1]
@@ -237,7 +242,9 @@ class Exchange:
                            [hb if a in self.srcs else 0 for a in range(self.world)])
         # side buffers: the cold fields of up to 1/32 of a chunk's mailboxes
         # (at least 1024), a fixed size every pass
-        self.side_cap = max(SIDE_MIN, pad_positions(self.positions) // SIDE_DIV)
+        pc = pad_positions(self.positions)  # cx_side sizes the dense form's side buffers too
+        self.side_cap = max(SIDE_MIN, pc // SIDE_DIV) if self.cx_side is None else \
+            max(SIDE_MIN, min(pc, int(pc * self.cx_side)))
         sb = eng.side_bytes(1, self.depth, self.side_cap)
         self.side_splits = ([sb if d in self.dests else 0 for d in range(self.world)],
                             [sb if a in self.srcs else 0 for a in range(self.world)])
@@ -329,7 +336,7 @@ class Pipeline:
     """
 
     def __init__(self, G, R, S, world, rank, placement="spread", banks=None, seed=2, exchange=None, codec="cx",
-                 cx_frac=None):
+                 cx_frac=None, cx_side=None):
         if banks is None:  # banks overlap one another's exchange: only with one to overlap
             banks = 2 if placement == "spread" and world > 1 and G >= 128 else 1
         # bank sizes a multiple of 64 but the last: a wave's lanes then share a
@@ -338,7 +345,7 @@ class Pipeline:
         sizes = [base] * (banks - 1) + [G - base * (banks - 1)]
         self.R, self.S, self.world, self.rank, self.placement = R, S, world, rank, placement
         self.ex = [Exchange(Gb, R, S, world, rank, placement, seed=seed + 7919 * b, exchange=exchange, codec=codec,
-                            cx_frac=cx_frac)
+                            cx_frac=cx_frac, cx_side=cx_side)
                    for b, Gb in enumerate(sizes)]
         self.groups = G
         self.engines, self.spaces, self.streams = [], [], []

@@ -512,7 +512,7 @@ int gr_space_side_unpack_host(void* space_host, uint32_t n_chunks, uint32_t posi
                               const void* side_host, uint32_t capacity);
 /* Compact exchange (round 5): the form in which a space crosses GPUs instead of
  * its whole hot region plus side buffers. Per chunk one fixed-size buffer
- * (gr_space_cx_bytes) carries only the mailboxes with messages: a 13-byte record
+ * (gr_space_cx_bytes) carries only the mailboxes with messages: a 12-byte record
  * for a uniform mailbox whose messages repeat message 0's hot fields (one
  * message, or the steady state's shared pairs), a full entry (hot fields and cold
  * records) for any other, one bit for an empty one. capacities[c] records for

@@ -21,7 +21,7 @@ def inverse_routes(in_pos):
 
 
 def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None, inject_p=0.0, mix=False,
-               codec="cx"):
+               codec="cx", cx_side=None, heavy_every=0):
     """tick_every > 0: one Tick for every peer on passes k % tick_every == tick_every - 1
     (leader heartbeats and their acks: messages with cold fields).
     inject_p > 0: BASELINE config 5's leader changes (populations.inject_leader_change)
@@ -33,7 +33,8 @@ def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None
     import torch
     S = R
     # spread on one rank: keep the exchange (copy + side buffers) under test
-    ex = Exchange(G, R, S, 1, 0, placement, seed=seed, exchange=placement == "spread", codec=codec)
+    ex = Exchange(G, R, S, 1, 0, placement, seed=seed, exchange=placement == "spread", codec=codec,
+                  cx_side=cx_side)
     n = ex.n_peers
     # perm[x] = engine peer of replica-major peer x (identity unless mix)
     perm = np.arange(n)
@@ -84,9 +85,9 @@ def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None
         elif tick_every:
             loc = locals_of(k, ex.leader_slots)
             eng.set_locals(loc)
-        # a tick pass and the pass after it are heavy (every leader's heartbeats,
-        # then every follower's ack, each a full entry): the dense form crosses
-        heavy = bool(tick_every) and k > 0 and k % tick_every in (tick_every - 1, 0)
+        # heavy_every > 0: passes k % heavy_every == heavy_every - 1 exchange the
+        # dense form (Exchange.exchange), the others the compact one
+        heavy = bool(heavy_every) and k % heavy_every == heavy_every - 1
         ex.step(eng, spaces, k, stream, heavy=heavy)
         torch.cuda.synchronize()
         if placement == "spread" and stats is not None:  # what the exchange carried

@@ -50,6 +50,9 @@ void run_lanes(const StepParams& kp) {
   // the kernel's two passes: the steady-state subset first, the general lane
   // for the lanes it bails on (tests the bail leaves no trace)
   std::vector<uint32_t> bailed, listed;
+  // the tick lanes' staged records (gr_layout.h TickStage), by lane
+  std::vector<uint64_t> stage((size_t)kp.n_lanes * kTickStageWords, 0);
+  std::vector<uint8_t> staged(kp.n_lanes, 0);
   for (uint32_t i = 0; i < kp.n_lanes; ++i) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     LaneStats ls;
@@ -117,10 +120,11 @@ void run_lanes(const StepParams& kp) {
           if (skip) abort();
         }
       }
-    } else if (split && (q0 = quiet_step<S, RM_ANY>(kp, i, p)) != QS_OTHER) {
+    } else if (split && (q0 = quiet_step<S, RM_ANY>(kp, i, p, &stage[(size_t)i * kTickStageWords], true)) != QS_OTHER) {
       // a split pass's steady kernel on a wave that is not steady: quiesced
       // lanes in closed form, ticks and ReadIndex straight to the tick lane
       done = q0 == QS_DONE;
+      staged[i] = q0 == QS_TICK;
       g_steady_lanes += done;
     } else if (split && (((i >> 6) + (g_hint_salt >> 4)) & 7u) == 3u) {
       // a lane of a pass whose role instances did not run (gr_kernels.h TailPlan,
@@ -156,7 +160,10 @@ void run_lanes(const StepParams& kp) {
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     LaneStats ls;
     const bool tickish = kp.has_locals && (kp.ln.u32(LR_LWORD)[i] & LW_OTHER);
-    if (tickish && tick_step<S>(kp, i, p, &ls)) {
+    // a lane the steady kernel's quiet_step sent here reads its staged record
+    // (gr_layout.h TickStage), as the device's tick kernel does
+    const uint64_t* stg = staged[i] ? &stage[(size_t)i * kTickStageWords] : nullptr;
+    if (tickish && tick_step<S>(kp, i, p, &ls, stg)) {
       GR_CHECK_STATE(kp.st, p);
       g_tick_lanes++;
       continue;

@@ -89,17 +89,23 @@ def test_spread_cold_fields_by_side_buffer(gpu, codec):
     """Spread exchange, no host read-back, parity every pass. dense: the hot region
     every pass, the cold fields of the mailboxes that need them (heartbeats and
     their acks, ticks every third pass) through the device-packed side buffers.
-    cx (the compact exchange): 12-byte records for the steady mailboxes on the
-    passes without ticks, the dense form on the tick passes and the passes of
-    their acks (heavy)."""
+    cx (the compact exchange), sized with a full entry for every position
+    (cx_side = 1: ticks every third pass at this scale leave few steady passes):
+    12-byte records for the steady mailboxes, full entries for the heartbeats,
+    acks and the catch-ups after them; every fourth pass exchanges the dense form
+    instead (a heavy pass), so the forms alternate between passes."""
     import devsim
     st = {}
-    final = devsim.run_device(500, 3, 9, placement="spread", tick_every=3, stats=st, codec=codec)
+    cx = codec == "cx"
+    final = devsim.run_device(500, 3, 9, placement="spread", tick_every=3, stats=st, codec=codec,
+                              cx_side=1.0 if cx else None, heavy_every=4 if cx else 0)
     assert np.all(final["committed"][:500] > 2**32)
     used = [n > 0 for n in st["side_entries"]]
     assert any(used) and not all(used), st
-    if codec == "cx":  # records on the passes that are neither the first nor heavy
-        assert all(st["records"][k] > 0 for k in (1, 4, 7)), st
+    if cx:
+        assert st["records"][0] > 0 and st["records"][1] > 0, st  # steady passes: records only
+        assert any(st["side_entries"][k] > 0 for k in (2, 4, 5, 6, 8)), st  # full entries, compact form
+        assert any(st["side_entries"][k] > 0 for k in (3, 7)), st  # cold fields, dense form
 
 
 def test_cx_pack_unpack(gpu):
@@ -168,15 +174,21 @@ def test_cx_pack_unpack(gpu):
         got_h = decode_space(h_dst, n_chunks, positions, depth, lost_ok=True)
         got_d = decode_space(d_dst.cpu().numpy(), n_chunks, positions, depth, lost_ok=True)
         key = lambda a: np.sort(a, order=["peer", "type", "log_index", "commit", "hint"])
-        assert np.array_equal(key(got_h), key(got_d))
         lost = got_d["reject"] == 0xFF
         if cap >= positions:
+            assert np.array_equal(key(got_h), key(got_d))
             assert not lost.any()
             assert np.array_equal(key(got_d), key(want))
         else:
+            # which mailboxes fit depends on the packer's order (the device's
+            # waves take record slots in atomic order, the host in position
+            # order), how many do not: every mailbox arrives whole or as lost
+            lost_h = got_h["reject"] == 0xFF
             assert lost.any()
+            assert len(np.unique(got_d["peer"][~lost])) == len(np.unique(got_h["peer"][~lost_h]))
             ok = np.isin(want["peer"], got_d["peer"][~lost])
             assert np.array_equal(key(got_d[~lost]), key(want[ok]))
+            assert set(np.unique(want["peer"])) == set(np.unique(got_d["peer"]))
     eng.close()
 
 

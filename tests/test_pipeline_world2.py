@@ -11,7 +11,9 @@ gloo (host copies); everything else is the RCCL path's code.
 churn: BASELINE config 5's leader changes (p = 0.1 of the settled groups on
 passes 1 and 4, applied to the oracle and to whichever rank holds each changed
 replica) and a Tick on every replica every third pass, so step-downs, rejects,
-multi-entry catch-ups, heartbeats and their acks -- full records -- cross ranks."""
+multi-entry catch-ups, heartbeats and their acks -- full records -- cross ranks.
+With the compact exchange the tick passes are heavy (dense form) and the others
+compact, so both forms cross and alternate."""
 import os
 import socket
 
@@ -34,7 +36,10 @@ def _worker(rank, world, port, G, banks, passes, codec, churn, q):
     try:
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        pipe = Pipeline(G, R, R, world, rank, "spread", banks=banks, seed=11, codec=codec)
+        # with churn and ticks few passes are steady: room for a full entry (compact
+        # form) or a side entry (dense form) at every position
+        pipe = Pipeline(G, R, R, world, rank, "spread", banks=banks, seed=11, codec=codec,
+                        cx_side=1.0 if churn else None)
         pipe.setup(Engine, torch.device("cuda", 0), 0)
         # the oracle: every bank's groups of every home, as one population each
         pops, msgs, topos = {}, {}, {}
@@ -73,16 +78,18 @@ def _worker(rank, world, port, G, banks, passes, codec, churn, q):
                     loc[sl] = home_loc[(b, h)][sl]
                 loc["peer"] = np.arange(R * Gb, dtype=np.uint32)
                 pipe.engines[b].set_locals(loc)
-            # a tick pass and the pass of its acks are heavy: the dense form crosses
-            # (exchange.py); the leader changes' traffic crosses as compact records
-            # and full entries
-            pipe.step(k, heavy=churn and k > 0 and k % 3 in (2, 0))
+            # the tick passes are heavy (the dense form crosses, exchange.py); the
+            # others, leader changes included, cross as compact records and full entries
+            pipe.step(k, heavy=bool(tk))
             pipe.synchronize()
             for b, ex in enumerate(pipe.ex):
                 Gb = ex.G
                 dev = pipe.engines[b].sync(ex.n_peers)
                 res = pipe.engines[b].collect_results(ex.n_peers)
-                esc += int(np.count_nonzero(res["escalation"]))
+                # the exchange never loses a mailbox (a lost one escalates CAPACITY);
+                # the churn's own escalations (elections, run windows) are the
+                # oracle's too and its states are compared below
+                esc += int(np.count_nonzero(res["escalation"] == abi.ESC_NAMES.index("capacity")))
                 for h in range(world):
                     o = pops[(b, h)].step(msgs[(b, h)], home_loc[(b, h)])
                     msgs[(b, h)] = topos[b].route_messages(o["msgs"])

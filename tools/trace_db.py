@@ -11,10 +11,12 @@ import sqlite3
 
 
 def load(path):
+    if not os.path.exists(path):
+        raise SystemExit(f"{path}: no such trace")
     dbs = glob.glob(os.path.join(path, "**", "*.db"), recursive=True) if os.path.isdir(path) else [path]
     rows = []
     for db in dbs:
-        c = sqlite3.connect(db)
+        c = sqlite3.connect(f"file:{db}?mode=ro", uri=True)  # never creates a file
         rows += c.execute("select name, start, end, duration, queue_id, grid_x, workgroup_x, vgpr_count, "
                           "accum_vgpr_count, scratch_size from kernels order by start").fetchall()
     return rows
