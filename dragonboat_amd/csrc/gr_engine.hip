@@ -402,8 +402,9 @@ int gr_create(const gr_config* cfg, gr_engine** out) {
   if (const char* bg = getenv("GR_BIN_GENERAL")) e->bin_general = bg[0] == '1';
   if (const char* tm = getenv("GR_TAIL_MODE")) e->tail_mode = (uint8_t)(strtoul(tm, nullptr, 10) & 3u);
   if (const char* wc = getenv("GR_WAVE_CLOCK")) {
-    if (hipMalloc((void**)&e->wclock, (size_t)kGeneralWaveSlots * kWaveClockWords * 8) == hipSuccess &&
-        hipMemset(e->wclock, 0, (size_t)kGeneralWaveSlots * kWaveClockWords * 8) == hipSuccess)
+    // two regions: the general kernel's waves, then the tick kernel's (gr_kernels.h)
+    if (hipMalloc((void**)&e->wclock, 2 * (size_t)kGeneralWaveSlots * kWaveClockWords * 8) == hipSuccess &&
+        hipMemset(e->wclock, 0, 2 * (size_t)kGeneralWaveSlots * kWaveClockWords * 8) == hipSuccess)
       e->wclock_path = wc;
   }
   void *ds = nullptr, *dl = nullptr;
@@ -455,7 +456,7 @@ void gr_destroy(gr_engine* e) {
   if (e->hints) (void)hipFree(e->hints);
   if (e->tail_hint) (void)hipHostFree(e->tail_hint);
   if (e->wclock) {
-    std::vector<uint64_t> h((size_t)kGeneralWaveSlots * kWaveClockWords);
+    std::vector<uint64_t> h(2 * (size_t)kGeneralWaveSlots * kWaveClockWords);
     if (!e->wclock_path.empty() && hipStreamSynchronize(e->stream) == hipSuccess &&
         hipMemcpy(h.data(), e->wclock, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
       if (FILE* f = fopen(e->wclock_path.c_str(), "wb")) {

@@ -85,6 +85,9 @@ __device__ inline __attribute__((always_inline)) void block_stats(const StepPara
 // saturates near 90 appends per us (MI355X_MICROARCH.md, "dequeue"), so 8 list
 // counters made those appends most of the steady kernel's time.
 constexpr uint32_t kTickLists = 64;
+// GR_WAVE_CLOCK records per region (the general grid's waves at most; the tick
+// kernel's one-wave workgroups in the second region)
+constexpr uint32_t kGeneralWaveSlots = 4096;
 // The churn kernel's leftovers (round 5): lanes of general list l the churn lane
 // (gr_churn.h) hands back go to churn list l / 2 (their handler class), after
 // the tick lists.
@@ -116,8 +119,10 @@ __host__ __device__ inline uint64_t wave_flag_words(uint32_t cap) { return ((uin
 // Lanes one tick list can receive: the lanes of every kTickLists-th block, from
 // the steady kernel and the listed role waves (keyed by lane), plus as many
 // retry entries (keyed by entry index): twice one key's bound.
+// The steady kernel keys by role as well (leaders to lists 32..63, the rest to
+// 0..31, each half by block % 32), so the bound counts every 32nd block.
 __host__ __device__ inline uint64_t tick_cap(uint32_t cap) {
-  return 2 * (((uint64_t)(cap + 255) / 256 + kTickLists - 1) / kTickLists * 256);
+  return 2 * (((uint64_t)(cap + 255) / 256 + kTickLists / 2 - 1) / (kTickLists / 2) * 256);
 }
 __host__ __device__ inline uint64_t tick_off(uint32_t cap) {
   return (uint64_t)kBailLists * cap + wave_flag_words(cap) + 2 * ((uint64_t)cap / 64 + 1);
@@ -154,12 +159,17 @@ __device__ inline __attribute__((always_inline)) void bail_append(bool mine, uin
 // unstaged: the TickStage records (StepParams::tick_stage) of an appender that
 // stages nothing, whose entries' tag words are overwritten so that no record of
 // an earlier pass (or graph replay) passes for this one's.
+// half >= 0: the list is block % 32 in that half (the steady kernel's role
+// split: leaders in half 1), so the tick kernel's waves take lanes of one role
+// and run one role's path (a mixed wave ran both, one after the other).
 __device__ inline __attribute__((always_inline)) uint64_t tick_append(bool mine, uint32_t key, uint32_t* bail_list,
                                                                       uint32_t* counters, uint32_t list_cap,
-                                                                      uint32_t i, uint64_t* unstaged = nullptr) {
+                                                                      uint32_t i, uint64_t* unstaged = nullptr,
+                                                                      int half = -1) {
   const uint64_t bm = __ballot(mine);
   if (!bm) return 0;
-  const uint32_t l = ((uint32_t)__builtin_amdgcn_readfirstlane(key) >> 8) % kTickLists;
+  const uint32_t blk = (uint32_t)__builtin_amdgcn_readfirstlane(key) >> 8;
+  const uint32_t l = half < 0 ? blk % kTickLists : blk % (kTickLists / 2) + (uint32_t)half * (kTickLists / 2);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t first = (uint32_t)__ffsll((unsigned long long)bm) - 1;
   uint32_t base = 0;
@@ -497,7 +507,11 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
     const bool active = i < kp.n_lanes;
     uint64_t stage[kTickStageWords] = {};
     const int q = active ? quiet_step<S, RM>(kp, i, i, stage, kp.tick_stage != nullptr) : QS_DONE;
-    const uint64_t te = tick_append(q == QS_TICK, i, bail_list, counters, list_cap, i);
+    // by role (the staged header): leaders to the tick lists' upper half
+    const bool tq = q == QS_TICK, lead = tq && h_state(stage[0]) == GR_LEADER;
+    const uint64_t te0 = tick_append(tq && !lead, i, bail_list, counters, list_cap, i, nullptr, 0);
+    const uint64_t te1 = tick_append(lead, i, bail_list, counters, list_cap, i, nullptr, 1);
+    const uint64_t te = lead ? te1 : te0;
     if (q == QS_TICK && kp.tick_stage) {  // the tick lane's record (gr_layout.h TickStage)
       uint64_t* r = kp.tick_stage + te * kTickStageWords;
 #pragma unroll
@@ -578,6 +592,9 @@ __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(Step
   const uint32_t* tl = bail_list + tick_off(list_cap);
   const uint64_t tc = tick_cap(list_cap);
   LaneStats acc;
+  const uint64_t t0 = kp.wclock ? wall_clock64() : 0;
+  uint64_t tph[3] = {0, 0, 0};  // GR_WAVE_CLOCK: the wave's first entries' phase marks
+  bool lead0 = false;
   for (uint32_t base = blockIdx.x * bw; base < n; base += gridDim.x * bw) {
     const uint32_t x = base + threadIdx.x;
     bool hand = false;
@@ -593,7 +610,15 @@ __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(Step
       // the entry's staged record (the steady kernel's entries; any other's
       // carries an older pass tag, and the lane loads its fields itself)
       const uint64_t* stg = kp.tick_stage ? kp.tick_stage + e * kTickStageWords : nullptr;
-      if (tick_step<S, RM>(kp, i, p, &ls, stg)) {
+      uint64_t clk[3] = {0, 0, 0};
+      const bool fin = tick_step<S, RM>(kp, i, p, &ls, stg, kp.wclock ? clk : nullptr);
+      if (kp.wclock && !tph[0]) {
+        tph[0] = clk[0];
+        tph[1] = clk[1];
+        tph[2] = clk[2];
+        lead0 = l >= kTickLists / 2;
+      }
+      if (fin) {
         GR_CHECK_STATE(kp.st, p);
         acc.leader_commit += ls.leader_commit;
         acc.follower_commit += ls.follower_commit;
@@ -610,6 +635,24 @@ __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(Step
     }
     general_append<S>(kp, hand, false, i, hand && kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i, blockIdx.x,
                       bail_list, counters, list_cap);
+  }
+  if (kp.wclock && bw == 64) {  // profiling: the wave's span and its first entries' phases (second region)
+    const uint64_t anyp = __ballot(tph[0] != 0);
+    if (anyp) {
+      const int sl = __ffsll((unsigned long long)anyp) - 1;
+      const uint64_t a = __shfl(tph[0], sl), b = __shfl(tph[1], sl), c = __shfl(tph[2], sl);
+      const uint32_t nl = wave_sum(acc.bailed), nld = wave_sum(lead0 ? 1u : 0u);
+      if (threadIdx.x == 0 && blockIdx.x < kGeneralWaveSlots) {
+        uint64_t* rr = kp.wclock + ((uint64_t)kGeneralWaveSlots + blockIdx.x) * kWaveClockWords;
+        rr[0] = t0;
+        rr[1] = wall_clock64();
+        rr[2] = nl;
+        rr[3] = nld;
+        rr[4] = a;
+        rr[5] = b;
+        rr[6] = c;
+      }
+    }
   }
   // stats rows belong to 256-lane workgroups: smaller workgroups share them
   if (kp.stats) block_stats(kp, acc, blockIdx.x * bw / kBlock);
@@ -818,7 +861,6 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
 // block has rows for. Kept small because with no bailed lanes the launch is pure
 // overhead. GR_GENERAL_BLOCKS overrides it (A/B runs).
 constexpr uint32_t kGeneralBlocks = 256;
-constexpr uint32_t kGeneralWaveSlots = 4096;  // GR_WAVE_CLOCK records: the general grid's waves at most
 inline uint32_t general_blocks() {
   static const uint32_t v = [] {
     const char* e = getenv("GR_GENERAL_BLOCKS");

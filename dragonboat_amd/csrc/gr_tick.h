@@ -73,6 +73,7 @@ struct TickLane {
   uint32_t gout[S], outc[S];
   uint32_t nmi = 0, nmo = 0;
 
+  uint64_t tclk[3] = {0, 0, 0};  // GR_WAVE_CLOCK marks: round 1 in, round 2 in, stores issued
   const uint64_t* stage;  // the entry's TickStage record, or nullptr
   bool staged = false;    // ... written this pass: the out counts are zero already
   GT_HD TickLane(const StepParams& k, uint32_t lane, uint32_t peer, const uint64_t* stg = nullptr)
@@ -271,6 +272,7 @@ struct TickLane {
     flags = h_flags(hdr);
     nruns = h_nruns(hdr);
     gelo = h_gelo(hdr);
+    tclk[0] = lane_clock(kp);
     uint32_t lf = 0, nt = 0, nq = 0, np = 0;
     if (kp.has_locals) {
       // the packed word holds the whole input when it is ticks and a ReadIndex
@@ -372,6 +374,7 @@ struct TickLane {
         mhi[j][k] = has ? hh : 0ull;
       }
     }
+    tclk[1] = lane_clock(kp);
     committed0 = committed;
     etick0 = etick;
     htick0 = htick;
@@ -514,6 +517,7 @@ struct TickLane {
       }
     }
     kp.ln.u8(LR_RFLAGS)[i] = rf;
+    tclk[2] = lane_clock(kp);
     const bool adv = committed > committed0;
     ls->leader_commit = adv && leader;
     ls->follower_commit = adv && !leader;
@@ -528,9 +532,16 @@ struct TickLane {
 };
 
 template <int S, int RM = RM_ANY>
-GT_HD bool tick_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, const uint64_t* stage = nullptr) {
+GT_HD bool tick_step(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, const uint64_t* stage = nullptr,
+                     uint64_t* clk = nullptr) {
   TickLane<S, RM> L(kp, i, p, stage);
-  return L.step(ls);
+  const bool ok = L.step(ls);
+  if (clk) {
+    clk[0] = L.tclk[0];
+    clk[1] = L.tclk[1];
+    clk[2] = L.tclk[2];
+  }
+  return ok;
 }
 
 }  // namespace gr

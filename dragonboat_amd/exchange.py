@@ -169,10 +169,12 @@ class Exchange:
     """Spaces + routes for one rank; `step` launches one pass and exchanges."""
 
     def __init__(self, G, R, S, world, rank, placement, seed=2, exchange=None, codec="cx", cx_frac=None,
-                 cx_side=None):
+                 cx_side=None, depth=None):
         """exchange=True keeps the one-rank spread exchange (copy + side buffers)
         that a one-rank run otherwise skips (tests of the N > 1 code on one GPU).
-        codec: "cx" (compact exchange) or "dense" (hot region + side buffers)."""
+        codec: "cx" (compact exchange) or "dense" (hot region + side buffers).
+        depth: messages per mailbox of a spread space (default 3; a fuller one
+        escalates CAPACITY at its writer)."""
         assert codec in ("cx", "dense")
         self.codec, self.cx_frac, self.cx_side = codec, cx_frac, cx_side
         self.last_cx = codec == "cx"  # the form of the last exchange (unpack reads it)
@@ -193,7 +195,7 @@ class Exchange:
             self.dests, self.srcs = spread_peer_ranks(R, world, rank)
             self.n_chunks = len(self.dests)
             assert len(self.srcs) == self.n_chunks
-            self.depth = 3  # two Replicates (or acks) + a heartbeat (or its ack) per pass
+            self.depth = depth or 3  # two Replicates (or acks) + a heartbeat (or its ack) per pass
         else:
             raise ValueError(placement)
         # one rank: every mailbox is the rank's own, at the same position on both
@@ -336,7 +338,7 @@ class Pipeline:
     """
 
     def __init__(self, G, R, S, world, rank, placement="spread", banks=None, seed=2, exchange=None, codec="cx",
-                 cx_frac=None, cx_side=None):
+                 cx_frac=None, cx_side=None, depth=None):
         if banks is None:  # banks overlap one another's exchange: only with one to overlap
             banks = 2 if placement == "spread" and world > 1 and G >= 128 else 1
         # bank sizes a multiple of 64 but the last: a wave's lanes then share a
@@ -345,7 +347,7 @@ class Pipeline:
         sizes = [base] * (banks - 1) + [G - base * (banks - 1)]
         self.R, self.S, self.world, self.rank, self.placement = R, S, world, rank, placement
         self.ex = [Exchange(Gb, R, S, world, rank, placement, seed=seed + 7919 * b, exchange=exchange, codec=codec,
-                            cx_frac=cx_frac, cx_side=cx_side)
+                            cx_frac=cx_frac, cx_side=cx_side, depth=depth)
                    for b, Gb in enumerate(sizes)]
         self.groups = G
         self.engines, self.spaces, self.streams = [], [], []

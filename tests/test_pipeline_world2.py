@@ -37,9 +37,11 @@ def _worker(rank, world, port, G, banks, passes, codec, churn, q):
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         # with churn and ticks few passes are steady: room for a full entry (compact
-        # form) or a side entry (dense form) at every position
+        # form) or a side entry (dense form) at every position, and full-depth
+        # mailboxes (a new leader's catch-ups, proposal and heartbeats to one
+        # follower in one pass overflow depth 3: CAPACITY, the host's to resolve)
         pipe = Pipeline(G, R, R, world, rank, "spread", banks=banks, seed=11, codec=codec,
-                        cx_side=1.0 if churn else None)
+                        cx_side=1.0 if churn else None, depth=abi.GR_C if churn else None)
         pipe.setup(Engine, torch.device("cuda", 0), 0)
         # the oracle: every bank's groups of every home, as one population each
         pops, msgs, topos = {}, {}, {}
@@ -50,7 +52,7 @@ def _worker(rank, world, port, G, banks, passes, codec, churn, q):
                 pops[(b, h)] = OraclePopulation(P.make_groups(ex.G, R, seed=seed), R)
                 msgs[(b, h)] = np.zeros(0, abi.MESSAGE)
         rng = np.random.default_rng(100 + 0)  # the same draws on every rank
-        bad, esc = None, 0
+        bad, esc, first_esc = None, 0, None
         for k in range(passes):
             tk = 1 if churn and k % 3 == 2 else 0
             home_loc = {}
@@ -86,23 +88,32 @@ def _worker(rank, world, port, G, banks, passes, codec, churn, q):
                 Gb = ex.G
                 dev = pipe.engines[b].sync(ex.n_peers)
                 res = pipe.engines[b].collect_results(ex.n_peers)
-                # the exchange never loses a mailbox (a lost one escalates CAPACITY);
-                # the churn's own escalations (elections, run windows) are the
-                # oracle's too and its states are compared below
-                esc += int(np.count_nonzero(res["escalation"] == abi.ESC_NAMES.index("capacity")))
+                outs = {}
                 for h in range(world):
-                    o = pops[(b, h)].step(msgs[(b, h)], home_loc[(b, h)])
-                    msgs[(b, h)] = topos[b].route_messages(o["msgs"])
+                    # the oracle's mailboxes hold what the exchange's do (a fourth
+                    # message escalates CAPACITY on both sides)
+                    outs[h] = pops[(b, h)].step(msgs[(b, h)], home_loc[(b, h)], in_depth=ex.depth,
+                                                out_depth=ex.depth)
+                    msgs[(b, h)] = topos[b].route_messages(outs[h]["msgs"])
                 for r in range(R):
                     h = (rank - r) % world
                     sl = slice(r * Gb, (r + 1) * Gb)
                     d = parity.compare_states(dev[sl], pops[(b, h)].export()[sl], R)
                     if d and bad is None:
                         bad = (k, b, r, d[:2])
+                    # every escalation is the oracle's too (the churn's own: elections,
+                    # full mailboxes); a mailbox the exchange lost would escalate
+                    # CAPACITY at its reader where the oracle does not
+                    de, oe = res["escalation"][sl], outs[h]["results"]["escalation"][sl]
+                    mm = np.nonzero(de != oe)[0]
+                    if len(mm) and esc == 0:
+                        first_esc = (k, b, r, int(mm[0]), abi.ESC_NAMES[int(de[mm[0]])],
+                                     abi.ESC_NAMES[int(oe[mm[0]])])
+                    esc += len(mm)
         st = pipe.stats()
         pipe.close()
         dist.destroy_process_group()
-        q.put((rank, bad, esc, st["leader_commits"], None))
+        q.put((rank, bad, (esc, first_esc), st["leader_commits"], None))
     except Exception as e:  # reported to the test, never a hang
         import traceback
         q.put((rank, None, 0, 0, traceback.format_exc()))
@@ -127,8 +138,9 @@ def test_pipeline_world2_gloo_matches_oracle(gpu, banks, codec, churn):
         for _ in procs:
             rank, bad, esc, commits, err = q.get(timeout=240)
             assert err is None, (rank, err)
-            assert esc == 0, (rank, esc)
-            assert bad is None, (rank, bad)
+            # esc: (count, first: pass, bank, replica, lane, device's, oracle's)
+            assert bad is None, (rank, bad, esc)
+            assert esc[0] == 0, (rank, esc)
             assert commits > 0
     finally:
         for p in procs:

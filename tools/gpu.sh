@@ -16,6 +16,7 @@
 #   profile           tools/profile.sh (trace + calibrated PMC passes), TAG=...
 #   cfgprofile        tools/profile_configs.sh (configs 2, 3, 5 traced; PMC of 3, 5), TAG=...
 #   rehearse          bench.py at N = 2 on one GPU over gloo (torch.distributed.run) -> rehearse_TAG.log
+#   tickclock         config 3 with GR_WAVE_CLOCK: the tick kernel's wave phases
 #   smoke             __graft_entry__.smoke()
 # Defaults: BENCH_ARGS="--steps 20 --warmup 5 --cpu-baseline off --host-path off".
 set -u
@@ -92,6 +93,10 @@ EOF
         --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 \
         $BENCH_ARGS > $OUT/rehearse_$tag.log 2>&1; rc=$?
       grep '^{' $OUT/rehearse_$tag.log | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('N=2 ms_per_step %.4f exchange_bytes_per_pass %s heavy %s value %.3g' % (d['ms_per_step'], d.get('exchange_bytes_per_pass'), d.get('exchange_bytes_heavy_pass'), d['value']))" ;;
+    tickclock)  # config 3's tick-kernel wave phases (GR_WAVE_CLOCK, tools/tick_clock.py)
+      env "${ev[@]}" GR_WAVE_CLOCK=$OUT/wclk_$tag.bin timeout -k 10 300 python -u tools/bench_configs.py --only 3 \
+        --passes 6 > $OUT/tickclock_$tag.json 2> $OUT/tickclock_$tag.err; rc=$?
+      [ $rc -eq 0 ] && python tools/tick_clock.py $OUT/wclk_$tag.bin | tee $OUT/tickclock_$tag.txt ;;
     smoke)
       env "${ev[@]}" timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
         > $OUT/smoke.log 2>&1; rc=$?; tail -1 $OUT/smoke.log ;;
