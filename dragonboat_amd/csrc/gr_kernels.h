@@ -802,6 +802,9 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
   if (blockIdx.x == 0 && threadIdx.x == kCounters + 1) next_counters[kGeneralNext] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters + 2) next_counters[kChurnNext] = 0;
   LaneStats acc;
+  // the general lane's message prefetch (gr_lane.h Lane::prefetch): one region
+  // per wave (S <= 3: 30 KB; 120 KB for the workgroup's four waves)
+  __shared__ __attribute__((aligned(16))) uint8_t pf_lds[(kBlock / 64) * (Lane<S>::kPfWave ? Lane<S>::kPfWave : 16)];
   uint64_t tph[3] = {0, 0, 0};  // GR_WAVE_CLOCK: the first round's phase marks
   uint32_t l0 = ~0u;            // ... and the list (handler class) of the lane's first round
   bool any = false;
@@ -815,6 +818,7 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
     const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
     LaneStats ls;
     Lane<S> L(kp, i, p);
+    L.pf_ = Lane<S>::kPfWave ? pf_lds + (threadIdx.x >> 6) * Lane<S>::kPfWave : nullptr;  // the wave's region
     L.step(&ls);
     GR_CHECK_STATE(kp.st, p);
     stats_add(acc, ls);

@@ -125,6 +125,18 @@ struct Lane {
   uint32_t msgs_in = 0, msgs_out = 0, entries_in = 0;
 
 
+  // The general kernel's message prefetch (round 5, device builds, S <= 3): the
+  // first kPfK messages of every in-mailbox, loaded before the message loop by
+  // LDS-DMA (global_load_lds) into this wave's region of the kernel's LDS, so the
+  // loop reads them there instead of making one dependent round of global loads
+  // per message (GR_WAVE_CLOCK, round 4: the loop was 85-110 us of a config-5
+  // wave's 60-200). Per message: the 64-byte cold record as 4 x 16 B, then
+  // LogIndex low, high, Commit offset and the term word as 4 x 4 B; each piece
+  // is one wave-instruction (64 lanes, lane-linear). pf_ = nullptr: no prefetch.
+  static constexpr uint32_t kPfK = 2, kPfRec = 4 * 64 * 16, kPfBytes = kPfRec + 4 * 64 * 4;
+  static constexpr uint32_t kPfWave = S <= 3 ? (uint32_t)S * kPfK * kPfBytes : 0u;
+  uint8_t* pf_ = nullptr;
+
   GR_HD Lane(const StepParams& k, uint32_t lane, uint32_t peer) : kp(k), p(peer), i(lane) {}
 
   GR_HD uint64_t& s64(uint32_t row) const { return kp.st.u64(row)[p]; }
@@ -523,6 +535,36 @@ struct Lane {
       pnq_ = kp.ln.u32(LR_QTICKS)[i];
       pnp_ = kp.ln.u32(LR_PROPOSE)[i];
     }
+  }
+  // Issue the message prefetch (pf_): every piece of every (slot, message) pair
+  // below kPfK, at its address when the mailbox holds that message (the cold
+  // record only for a mailbox without MB_UNIFORM), else at position 0's (one
+  // shared line). Needs preload()'s routes and count bytes.
+  GR_HD void prefetch() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (!GR_LANE_PRELOAD || kPfWave == 0 || !pf_) return;
+    const Mailbox d0 = kp.in.at(0);
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+#pragma unroll
+      for (uint32_t k = 0; k < kPfK; ++k) {
+        const uint32_t cb = pcb_[j];
+        const bool v = gin_[j] != NOPOS && k < mb_n(cb) && k < kp.in.depth;
+        const Mailbox mb = v ? kp.in.at(gin_[j]) : d0;
+        const uint32_t kk = v ? k : 0u;
+        const bool full = v && !(cb & MB_UNIFORM);
+        const uint4* rec = reinterpret_cast<const uint4*>(full ? mb.rec(kk) : d0.rec(0));
+        uint8_t* base = pf_ + ((uint32_t)j * kPfK + k) * kPfBytes;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) __builtin_amdgcn_global_load_lds((const void*)(rec + q), (void*)(base + q * 1024), 16, 0, 0);
+        const uint32_t* li = reinterpret_cast<const uint32_t*>(&mb.u64(kk, MF_LOG_INDEX));
+        __builtin_amdgcn_global_load_lds((const void*)li, (void*)(base + kPfRec), 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(li + 1), (void*)(base + kPfRec + 256), 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)&mb.t32(kk, MT_CDELTA), (void*)(base + kPfRec + 512), 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)&mb.mterm(), (void*)(base + kPfRec + 768), 4, 0, 0);
+      }
+    }
+#endif
   }
   GR_HD uint32_t out_gpos(uint32_t j) const { return GR_LANE_PRELOAD ? sel(gout_, j) : route_of(kp, 1, j, i); }
   GR_HD uint32_t in_gpos(uint32_t j) const { return GR_LANE_PRELOAD ? sel(gin_, j) : route_of(kp, 0, j, i); }
@@ -1196,21 +1238,75 @@ struct Lane {
   }
 
   // ---------------------------------------------------------------- messages
-  GR_HD void read_msg(const Mailbox& mb, uint32_t cb, uint32_t k, InMsg& m) const {
-#ifndef GR_READ_RECORD
-#define GR_READ_RECORD 1
+  // Message k of slot j's in-mailbox mb (count byte cb): its raw words from the
+  // prefetch when it holds them (pf_, k < kPfK), else from the mailbox, then one
+  // decoding. A uniform mailbox's tag and term are implied by the count byte and
+  // its term word (a shared pair's second message: message 0's hot fields); a
+  // full record is read in one round with its hot fields: the 64-byte record as
+  // four 16-byte words, decoded by type in registers (gr_layout.h Mailbox; round
+  // 4 A/B against the tag first and the named fields after it: general kernel
+  // 167.6 vs 173.1 us per pass on config 5).
+  GR_HD void read_msg(const Mailbox& mb, uint32_t cb, uint32_t k, InMsg& m, uint32_t j = 0) const {
+    const bool uni = (cb & MB_UNIFORM) != 0;
+    const bool shared = k && mb_shared(cb);
+    const uint32_t kh = uni && shared ? 0u : k;  // the message whose hot fields it carries
+    uint64_t li;
+    uint32_t cd, mt = 0;
+    uint4 w0 = {0, 0, 0, 0}, w1 = w0, w2 = w0, w3 = w0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (kPfWave && pf_ && k < kPfK) {
+      const uint32_t lane = threadIdx.x & 63u;
+      const uint8_t* ph = pf_ + (j * kPfK + kh) * kPfBytes + kPfRec + lane * 4;
+      li = (uint64_t)*reinterpret_cast<const uint32_t*>(ph) | ((uint64_t)*reinterpret_cast<const uint32_t*>(ph + 256) << 32);
+      cd = *reinterpret_cast<const uint32_t*>(ph + 512);
+      mt = *reinterpret_cast<const uint32_t*>(ph + 768);
+      if (!uni) {
+        const uint8_t* pr = pf_ + (j * kPfK + k) * kPfBytes + lane * 16;
+        w0 = *reinterpret_cast<const uint4*>(pr);
+        w1 = *reinterpret_cast<const uint4*>(pr + 1024);
+        w2 = *reinterpret_cast<const uint4*>(pr + 2048);
+        w3 = *reinterpret_cast<const uint4*>(pr + 3072);
+      }
+    } else
 #endif
-#if GR_READ_RECORD
-    // A full-record message's cold fields in one round with its hot ones: the
-    // 64-byte record as four 16-byte loads, decoded by type in registers (layout:
-    // gr_layout.h Mailbox), instead of the tag first and the fields the type
-    // names after it (config 5 A/B: general kernel 167.6 vs 173.1 us per pass;
-    // GR_READ_RECORD=0 builds the two-round form)
-    if (!(cb & MB_UNIFORM)) {
-      const uint4* r = reinterpret_cast<const uint4*>(mb.rec(k));
-      const uint4 w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3];
-      const uint64_t li = mb.u64(k, MF_LOG_INDEX);
-      const uint32_t cd = mb.t32(k, MT_CDELTA);
+    {
+      li = mb.u64(kh, MF_LOG_INDEX);
+      cd = mb.t32(kh, MT_CDELTA);
+      if (uni) {
+        mt = mb.mterm();
+      } else {
+        const uint4* r = reinterpret_cast<const uint4*>(mb.rec(k));
+        w0 = r[0];
+        w1 = r[1];
+        w2 = r[2];
+        w3 = r[3];
+      }
+    }
+    if (!uni) {
+      decode_record(w0, w1, w2, w3, li, cd, m);
+      return;
+    }
+    const uint32_t tg = Mailbox::uniform_tag(cb, k);
+    m.type = (uint8_t)tg;
+    m.flags = (uint8_t)(tg >> 8);
+    m.term = mt;
+    m.n = 0; m.run2 = 0;
+    m.log_index = 0; m.log_term = 0; m.commit = 0; m.hint = 0; m.hint_high = 0; m.rt0 = 0; m.rt1 = 0;
+    if (m.type == GR_REPLICATE) {  // uniform Replicates are compact: LogTerm = Term, <= 1 entry at Term
+      m.log_index = li;
+      m.n = (m.flags & MFL_N1) ? 1u : 0u;
+      m.log_term = m.term;
+      m.commit = commit_of(cd, li);
+      m.rt0 = m.n ? m.term : 0;
+    } else {  // an accept (MB_RESP): a shared pair's second is at message 0's LogIndex + 1
+      m.log_index = li + (shared ? (uint64_t)k : 0ull);
+    }
+  }
+  // A full-record message from its cold record's words and its hot LogIndex and
+  // Commit offset (gr_layout.h Mailbox).
+  GR_HD static void decode_record(const uint4& w0, const uint4& w1, const uint4& w2, const uint4& w3, uint64_t li,
+                                  uint32_t cd, InMsg& m) {
+    {
       m.type = (uint8_t)(w0.x & 0xFFu);
       m.flags = (uint8_t)((w0.x >> 8) & 0xFFu);
       m.term = w0.y;
@@ -1264,61 +1360,6 @@ struct Lane {
           m.rt1 = w1.z;
           break;
       }
-      return;
-    }
-#endif
-    const uint32_t tg = mb.tag_at(k, cb);  // cb: the count byte (MB_UNIFORM: tag and term implied)
-    m.type = (uint8_t)tg;
-    m.flags = (uint8_t)(tg >> 8);
-    m.term = (uint64_t)mb.term_at(k, cb);
-    m.n = 0; m.run2 = 0;
-    m.log_index = 0; m.log_term = 0; m.commit = 0; m.hint = 0; m.hint_high = 0; m.rt0 = 0; m.rt1 = 0;
-    switch (m.type) {
-      case GR_REPLICATE:
-        m.log_index = mb.log_index_at(k, cb);  // a shared mailbox: message 0's
-        if (m.flags & MFL_COMPACT) {  // LogTerm = Term, <= 1 entry at Term, narrow Commit
-          m.n = (m.flags & MFL_N1) ? 1u : 0u;
-          m.log_term = m.term;
-          m.commit = commit_of(mb.cdelta_at(k, cb), m.log_index);
-          m.rt0 = m.n ? m.term : 0;
-          break;
-        }
-        m.n = mb.n(k);
-        m.log_term = (uint64_t)mb.t32(k, MT_LOG_TERM);
-        m.commit = (m.flags & MFL_WIDE_COMMIT) ? mb.u64(k, MF_COMMIT)
-                                               : commit_of(mb.t32(k, MT_CDELTA), m.log_index);
-        if (m.n) {
-          m.rt0 = (uint64_t)mb.t32(k, MT_RT0);
-          if (((m.flags >> MFL_RUNS_SHIFT) & 3u) == 2) {
-            m.run2 = mb.run2(k);
-            m.rt1 = (uint64_t)mb.t32(k, MT_RT1);
-          }
-        }
-        break;
-      case GR_REPLICATE_RESP:
-        m.log_index = mb.log_index_at(k, cb);  // a shared mailbox: message 0's + k
-        if (m.flags & MFL_REJECT) m.hint = mb.u64(k, MF_HINT);
-        break;
-      case GR_HEARTBEAT:
-        m.commit = mb.u64(k, MF_COMMIT);
-        m.hint = mb.u64(k, MF_HINT);
-        m.hint_high = mb.u64(k, MF_HINT_HIGH);
-        break;
-      case GR_HEARTBEAT_RESP:
-        m.hint = mb.u64(k, MF_HINT);
-        m.hint_high = mb.u64(k, MF_HINT_HIGH);
-        break;
-      default:
-        m.n = mb.n(k);
-        m.run2 = mb.run2(k);
-        m.log_index = mb.u64(k, MF_LOG_INDEX);
-        m.log_term = (uint64_t)mb.t32(k, MT_LOG_TERM);
-        m.commit = mb.u64(k, MF_COMMIT);
-        m.hint = mb.u64(k, MF_HINT);
-        m.hint_high = mb.u64(k, MF_HINT_HIGH);
-        m.rt0 = (uint64_t)mb.t32(k, MT_RT0);
-        m.rt1 = (uint64_t)mb.t32(k, MT_RT1);
-        break;
     }
   }
   GR_HD OutMsg as_out(const InMsg& m) const {
@@ -1579,7 +1620,7 @@ struct Lane {
         // its cold fields did not fit the exchange's side buffer (gr_io.h side_pack)
         if (!(cb & MB_UNIFORM) && (cb & MB_COLD_LOST)) { *at = item; return GR_ESC_CAPACITY; }
         InMsg m;
-        read_msg(mb, cb, k, m);
+        read_msg(mb, cb, k, m, j);
         if (m.type == MT_WIDE) { *at = item; return GR_ESC_WIDE_TERM; }  // terms >= 2^32: host path
         const int e = handle(m, j);
         if (e) { *at = item; return e; }
@@ -1644,6 +1685,7 @@ struct Lane {
     uint32_t at = 0, limit = 0xFFFFFFFFu;
     int esc = 0;
     preload();
+    prefetch();
 #pragma unroll 1
     for (int attempt = 0; attempt < 2; ++attempt) {  // one call site keeps run() inlined
       begin();

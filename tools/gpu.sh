@@ -17,6 +17,7 @@
 #   cfgprofile        tools/profile_configs.sh (configs 2, 3, 5 traced; PMC of 3, 5), TAG=...
 #   rehearse          bench.py at N = 2 on one GPU over gloo (torch.distributed.run) -> rehearse_TAG.log
 #   tickclock         config 3 with GR_WAVE_CLOCK: the tick kernel's wave phases
+#   genclock          config 5 with GR_WAVE_CLOCK: the general kernel's wave phases
 #   smoke             __graft_entry__.smoke()
 # Defaults: BENCH_ARGS="--steps 20 --warmup 5 --cpu-baseline off --host-path off".
 set -u
@@ -97,6 +98,10 @@ EOF
       env "${ev[@]}" GR_WAVE_CLOCK=$OUT/wclk_$tag.bin timeout -k 10 300 python -u tools/bench_configs.py --only 3 \
         --passes 6 > $OUT/tickclock_$tag.json 2> $OUT/tickclock_$tag.err; rc=$?
       [ $rc -eq 0 ] && python tools/tick_clock.py $OUT/wclk_$tag.bin | tee $OUT/tickclock_$tag.txt ;;
+    genclock)  # config 5's general-kernel wave phases (GR_WAVE_CLOCK, tools/wave_clock.py)
+      env "${ev[@]}" GR_WAVE_CLOCK=$OUT/wc5_$tag.bin timeout -k 10 300 python -u tools/bench_configs.py --only 5 \
+        --passes 6 > $OUT/genclock_$tag.json 2> $OUT/genclock_$tag.err; rc=$?
+      [ $rc -eq 0 ] && python tools/wave_clock.py $OUT/wc5_$tag.bin | tee $OUT/genclock_$tag.txt ;;
     smoke)
       env "${ev[@]}" timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
         > $OUT/smoke.log 2>&1; rc=$?; tail -1 $OUT/smoke.log ;;

@@ -16,6 +16,7 @@ TICK_NS = 10.0  # wall_clock64 at 100 MHz
 
 def main(path):
     r = np.fromfile(path, dtype=np.uint64).reshape(-1, WORDS)
+    r = r[:4096]  # the general kernel's region (the tick kernel's follows: tools/tick_clock.py)
     r = r[r[:, 1] > 0]
     if len(r) == 0:
         print("no waves recorded")
