@@ -476,23 +476,53 @@ struct FastLane {
     // ---- round 2 (only where the hint did not match): leader remotes and messages
     if (kLeaderPath && leader) {
       rbw = h_rb(hdr) & ((1ull << (5 * S)) - 1);
-      // remote rows: stale ones (sync bits) from lastIndex, the rest loaded unless the hint did
+      // remote rows: stale ones (sync bits) from lastIndex, the rest loaded unless
+      // the hint did. Every load of this round is issued before any value is used,
+      // each at its row or, when not needed, at the header's line (loaded already),
+      // and the values pass through keep_value: a branch around each load made one
+      // round trip per slot (gr_layout.h keep_value).
       const uint64_t sb = kSync ? hdr : 0;
+      uint64_t mv[S], nv[S];
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        if (h_ms(sb) && (uint32_t)j == self) match[j] = hi;
-        else if (h_mp(sb, (uint32_t)j) && (uint32_t)j != self) match[j] = hi - 2;
-        else if (!((have_m >> j) & 1u)) match[j] = ntld(s64(Rw::MATCH + j));
+        const bool ms = h_ms(sb) && (uint32_t)j == self, mp = h_mp(sb, (uint32_t)j) && (uint32_t)j != self;
+        const bool lm = !ms && !mp && !((have_m >> j) & 1u), ln = !h_nx(sb, (uint32_t)j) && !((have_n >> j) & 1u);
+        mv[j] = ntld(s64(lm ? (uint32_t)(Rw::MATCH + j) : (uint32_t)SR_HDR));
+        nv[j] = ntld(s64(ln ? (uint32_t)(Rw::NEXT + j) : (uint32_t)SR_HDR));
+      }
+      uint32_t lmr[S];
+      uint64_t lir[S][MK];
+      if (!hl) {  // wave-uniform
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          lmr[j] = ntld(min_at(cnt[j] ? gin[j] : 0u).mterm());
+#pragma unroll
+          for (int k = 0; k < MK; ++k) {
+            const bool ck = (uint32_t)k < cnt[j];
+            lir[j][k] = ntld(min_at(ck ? gin[j] : 0u).u64(ck ? (uint32_t)k : 0u, MF_LOG_INDEX));
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const bool ms = h_ms(sb) && (uint32_t)j == self, mp = h_mp(sb, (uint32_t)j) && (uint32_t)j != self;
+        const uint64_t m = keep_value(mv[j]), n = keep_value(nv[j]);
+        if (ms) match[j] = hi;
+        else if (mp) match[j] = hi - 2;
+        else if (!((have_m >> j) & 1u)) match[j] = m;
         if (h_nx(sb, (uint32_t)j)) next[j] = hi + 1;
-        else if (!((have_n >> j) & 1u)) next[j] = ntld(s64(Rw::NEXT + j));
+        else if (!((have_n >> j) & 1u)) next[j] = n;
       }
       if (!hl) {
 #pragma unroll
         for (int j = 0; j < S; ++j) {
-          lmt[j] = cnt[j] ? ntld(min_at(gin[j]).mterm()) : 0u;
+          const uint32_t t = keep_value(lmr[j]);
+          lmt[j] = cnt[j] ? t : 0u;
 #pragma unroll
-          for (int k = 0; k < MK; ++k)
-            lidx[j][k] = (uint32_t)k < cnt[j] ? ntld(min_at(gin[j]).u64(k, MF_LOG_INDEX)) : 0;
+          for (int k = 0; k < MK; ++k) {
+            const uint64_t v = keep_value(lir[j][k]);
+            lidx[j][k] = (uint32_t)k < cnt[j] ? v : 0;
+          }
         }
       }
     }
@@ -508,11 +538,20 @@ struct FastLane {
       // the term word of every uniform mailbox with messages (the hinted one's is
       // loaded already): one at a lower term is dropped whole (raft.go:1014-1044),
       // unless it holds Replicates and checkQuorum asks for a NoOP reply
-      uint32_t ft[S];
+      // (one batch: address-selected loads, then keep_value, as the leader's round 2)
+      uint32_t ft[S], ftr[S];
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         const bool have = hf && (uint32_t)j == hL && ghL != NOPOS;
-        ft[j] = have ? fmt : (cnt[j] && !((nonu >> j) & 1u)) ? ntld(min_at(gin[j]).mterm()) : 0u;
+        const bool need = !have && cnt[j] && !((nonu >> j) & 1u);
+        ftr[j] = ntld(min_at(need ? gin[j] : 0u).mterm());
+      }
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const bool have = hf && (uint32_t)j == hL && ghL != NOPOS;
+        const bool need = !have && cnt[j] && !((nonu >> j) & 1u);
+        const uint32_t t = keep_value(ftr[j]);
+        ft[j] = have ? fmt : need ? t : 0u;
       }
 #pragma unroll
       for (int j = 0; j < S; ++j) {
@@ -532,13 +571,22 @@ struct FastLane {
       const uint32_t cc = c < (uint32_t)MK ? c : (uint32_t)MK;
       const bool spec = hf && L == hL;  // the hinted mailbox is the one that sent
       if (c) fmt = ft[L];
+      uint64_t fir[MK];
+      uint32_t fcr[MK];
+#pragma unroll
+      for (int k = 0; k < MK; ++k) {  // one batch (keep_value)
+        const bool ld = (uint32_t)k < cc && !spec;
+        const Mailbox mb = min_at(ld ? gl : 0u);
+        fir[k] = ntld(mb.u64(ld ? (uint32_t)k : 0u, MF_LOG_INDEX));
+        fcr[k] = ntld(mb.t32(ld ? (uint32_t)k : 0u, MT_CDELTA));
+      }
 #pragma unroll
       for (int k = 0; k < MK; ++k) {
-        if ((uint32_t)k < cc && !spec) {
-          const Mailbox mb = min_at(gl);
-          fidx[k] = ntld(mb.u64(k, MF_LOG_INDEX));
-          fcd[k] = ntld(mb.t32(k, MT_CDELTA));
-        }
+        const bool ld = (uint32_t)k < cc && !spec;
+        const uint64_t a = keep_value(fir[k]);
+        const uint32_t b = keep_value(fcr[k]);
+        fidx[k] = ld ? a : fidx[k];
+        fcd[k] = ld ? b : fcd[k];
       }
       if (mb_shared(cbL)) {  // a shared Replicate pair (MB_SHARED): message 0's fields
         fidx[1] = fidx[0];

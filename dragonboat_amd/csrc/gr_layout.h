@@ -397,6 +397,19 @@ __host__ __device__ inline T ntld(const T& r) {
 #ifndef GR_NT_ST
 #define GR_NT_ST 0
 #endif
+// The value as an opaque definition (device code): an empty asm that reads and
+// writes it, so code that uses a loaded value only under a condition cannot make
+// the load conditional (a branch around a load made the compiler wait for it
+// before the next one: one round trip per slot and message). Issue a batch of
+// loads, then pass each value through this. Identity in host builds.
+template <class T>
+__host__ __device__ inline T keep_value(T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(v));
+#endif
+  return v;
+}
+
 template <class T>
 __host__ __device__ inline void ntst(T& r, T v) {
 #if GR_NT_ST && defined(__HIP_DEVICE_COMPILE__)

@@ -36,17 +36,6 @@ GT_HD uint32_t gt_popc8(uint32_t x) {
   return (x + (x >> 4)) & 0x0Fu;
 }
 
-// The value as an opaque definition (device code): an empty asm that reads and
-// writes it, so code that uses the value only under a condition cannot make its
-// load conditional. Identity in host builds.
-template <class T>
-GT_HD T gt_keep(T v) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm volatile("" : "+v"(v));
-#endif
-  return v;
-}
-
 template <int S, int RM = RM_ANY>
 struct TickLane {
   using Rw = Rows<S>;
@@ -357,16 +346,16 @@ struct TickLane {
       riack |= ld8(Rw::B_RIACK + q, live) << (8 * q);
     }
     // every round-2 load is issued before the first value is used: the values
-    // pass through an empty asm (gt_keep), so the optimiser cannot sink the
+    // pass through an empty asm (keep_value, gr_layout.h), so the optimiser cannot sink the
     // loads under a per-message branch (it did: one wait per message)
 #pragma unroll
     for (int j = 0; j < S; ++j) {
 #pragma unroll
       for (int k = 0; k < MK; ++k) {
         const bool has = (uint32_t)k < cnt[j];
-        const uint32_t tg = gt_keep(mh[j][k]);
-        const uint64_t tm = gt_keep(mterm[j][k]), cm = gt_keep(mcom[j][k]);
-        const uint64_t lo = gt_keep(mlo[j][k]), hh = gt_keep(mhi[j][k]);
+        const uint32_t tg = keep_value(mh[j][k]);
+        const uint64_t tm = keep_value(mterm[j][k]), cm = keep_value(mcom[j][k]);
+        const uint64_t lo = keep_value(mlo[j][k]), hh = keep_value(mhi[j][k]);
         mh[j][k] = has ? ((cbs[j] & MB_UNIFORM) ? Mailbox::uniform_tag(cbs[j], k) : tg) & 0xFFu : 0u;
         mterm[j][k] = has ? tm : 0ull;
         mcom[j][k] = has && !leader ? cm : 0ull;
