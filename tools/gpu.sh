@@ -18,6 +18,7 @@
 #   rehearse          bench.py at N = 2 on one GPU over gloo (torch.distributed.run) -> rehearse_TAG.log
 #   tickclock         config 3 with GR_WAVE_CLOCK: the tick kernel's wave phases
 #   genclock          config 5 with GR_WAVE_CLOCK: the general kernel's wave phases
+#   wirepath          tools/bench_wire_path.py at 1M x 3, full and compact outboxes
 #   smoke             __graft_entry__.smoke()
 # Defaults: BENCH_ARGS="--steps 20 --warmup 5 --cpu-baseline off --host-path off".
 set -u
@@ -102,6 +103,10 @@ EOF
       env "${ev[@]}" GR_WAVE_CLOCK=$OUT/wc5_$tag.bin timeout -k 10 300 python -u tools/bench_configs.py --only 5 \
         --passes 6 > $OUT/genclock_$tag.json 2> $OUT/genclock_$tag.err; rc=$?
       [ $rc -eq 0 ] && python tools/wave_clock.py $OUT/wc5_$tag.bin | tee $OUT/genclock_$tag.txt ;;
+    wirepath)  # the 1M x 3 wire path (frames in, tools/bench_wire_path.py), full and compact outboxes
+      env "${ev[@]}" timeout -k 10 400 python -u tools/bench_wire_path.py > $OUT/wirepath_$tag.json 2> $OUT/wirepath_$tag.err \
+        && env "${ev[@]}" timeout -k 10 400 python -u tools/bench_wire_path.py --compact > $OUT/wirepath_${tag}_compact.json \
+        2>> $OUT/wirepath_$tag.err; rc=$?; tail -c 600 $OUT/wirepath_${tag}_compact.json ;;
     smoke)
       env "${ev[@]}" timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" \
         > $OUT/smoke.log 2>&1; rc=$?; tail -1 $OUT/smoke.log ;;
