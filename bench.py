@@ -564,6 +564,15 @@ def main():
                 traffic = None
         copy_gbs = copy_peak_gbs()
         traffic_gbs = traffic / (kavg * 1e-3) / 1e9 if traffic else None
+        try:  # provenance: the loaded library's build record against this tree's sources
+            from dragonboat_amd.build import build_record, source_digest
+            brec = build_record(os.environ.get("GPURAFT_LIB") or None) or {}
+            build_info = {"lib": brec.get("lib"), "built_from": brec.get("source_digest"),
+                          "tree": source_digest(), "built_at": brec.get("built_at"),
+                          "compiler": brec.get("compiler")}
+            build_info["matches_tree"] = build_info["built_from"] == build_info["tree"]
+        except Exception:  # the record is informational; never fail the bench over it
+            build_info = None
         line = {
             "metric": "commit-index updates/sec (1M groups x 3 replicas) + achieved HBM GB/s",
             "value": value,
@@ -588,6 +597,7 @@ def main():
             "exchange_bytes_per_pass": xbytes,
             "exchange_bytes_heavy_pass": xbytes_heavy,
             "exchange_codec": codec if placement == "spread" and world > 1 else None,
+            "build": build_info,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"lean kernels of one pass (gr_steady_kernel<{S}> + gr_roles_kernel<{S}>, the role instances in one launch)",

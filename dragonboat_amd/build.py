@@ -128,7 +128,35 @@ def _hip_lib_locked(out, srcs, extra, scratch_check):
             if scratch_check:
                 check_no_scratch(r, s)
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out])
+    write_build_record(out, extra)
     return out
+
+
+def write_build_record(out, extra=()):
+    """<lib>.build.json beside a built library: the engine source digest it was
+    built from, when, and by which compiler (bench.py reports it with the digest
+    of the tree it runs in, so a stale prebuilt library shows)."""
+    import json
+    import time
+    try:
+        ver = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout.splitlines()
+        ver = next((v for v in ver if "HIP version" in v or "clang version" in v), ver[0] if ver else "")
+    except OSError:
+        ver = ""
+    rec = {"lib": os.path.basename(out), "source_digest": source_digest(), "built_at": time.strftime("%Y-%m-%dT%H:%M:%S"),
+           "compiler": ver.strip(), "arch": ARCH, "flags": list(extra)}
+    with open(out + ".build.json", "w") as fh:
+        json.dump(rec, fh)
+
+
+def build_record(lib=None):
+    """The build record of a library (default: the engine), or None."""
+    import json
+    try:
+        with open((lib or ENGINE_LIB) + ".build.json") as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return None
 
 
 def build_engine(force=False):
