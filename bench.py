@@ -466,7 +466,15 @@ def main():
     torch.cuda.set_device(ordinal)  # before the process group: RCCL binds the current device
     dev = torch.device("cuda", ordinal)
     cdev = dev if backend == "nccl" else torch.device("cpu")  # where the control collectives run
-    if world > 1:
+    # GR_BENCH_COLLECTIVE=1 (measurement, not the driver's): with one rank and
+    # --placement spread, a one-rank RCCL group moves the exchange buffers with
+    # the async all_to_all_single an N > 1 run issues (Exchange(collective=True)),
+    # so the N = 8 exchange path's device cost is timed on one GPU
+    collective = os.environ.get("GR_BENCH_COLLECTIVE") == "1"
+    if world > 1 or collective:
+        if world == 1:
+            for k_, v_ in (("RANK", "0"), ("WORLD_SIZE", "1"), ("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531")):
+                os.environ.setdefault(k_, v_)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -482,7 +490,7 @@ def main():
     # N > 1: BASELINE config 4 (replicas on distinct GPUs, RCCL all-to-all per pass)
     placement = args.placement or ("spread" if world > 1 else "local")
     codec = os.environ.get("GR_BENCH_CODEC", "cx")  # the spread exchange's form (exchange.py)
-    pipe = Pipeline(G, R, S, world, rank, placement, banks=args.banks, codec=codec)
+    pipe = Pipeline(G, R, S, world, rank, placement, banks=args.banks, codec=codec, collective=collective or None)
     pipe.setup(Engine, dev, ordinal)
 
     for k in range(args.warmup):
@@ -596,7 +604,10 @@ def main():
             "escalations": esc,
             "exchange_bytes_per_pass": xbytes,
             "exchange_bytes_heavy_pass": xbytes_heavy,
-            "exchange_codec": codec if placement == "spread" and world > 1 else None,
+            "exchange_codec": codec if placement == "spread" and (world > 1 or collective) else None,
+            "exchange_collective": "RCCL all_to_all_single, async on the bank's stream" + (
+                " (one-rank rehearsal: GR_BENCH_COLLECTIVE=1)" if world == 1 else "")
+            if placement == "spread" and (world > 1 or collective) else None,
             "build": build_info,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -634,7 +645,7 @@ def main():
             except Exception as e:  # baseline is reported, not required
                 line["cpu_baseline"] = {"value": None, "error": str(e)}
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if world > 1 or collective:
         dist.destroy_process_group()
 
 

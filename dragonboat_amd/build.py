@@ -42,12 +42,13 @@ def _code_only(text):
     return "\n".join(ln.rstrip() for ln in text.splitlines() if ln.strip())
 
 
-def source_digest():
+def source_digest(deps=None):
     """Digest of the engine's code (comments and blank lines stripped): ties a
-    PMC measurement (profiles/) to the build it measured; comment edits keep it."""
+    PMC measurement (profiles/) to the build it measured; comment edits keep it.
+    deps: another target's sources (its build record's digest)."""
     import hashlib
     h = hashlib.sha1()
-    for f in sorted(ENGINE_DEPS):
+    for f in sorted(deps or ENGINE_DEPS):
         with open(f, encoding="utf-8") as fh:
             h.update(_code_only(fh.read()).encode())
     return h.hexdigest()[:16]
@@ -63,9 +64,19 @@ def _locked(out):
     return lk
 
 
-def _stale(out, deps):
+def _stale(out, deps, extra=None):
+    """A target needs building when it is missing or its build record's digest
+    (and flags, when given) differ from its sources' now. Digests, not mtimes: a
+    prebuilt library pushed with a tree whose sources differ (the GPU box gets
+    fresh mtimes for both) is rebuilt; a comment-only edit is not. A target
+    without a record falls back to mtimes (the CPU-only test builds)."""
     if not os.path.exists(out):
         return True
+    rec = build_record(out)
+    if rec is not None and "source_digest" in rec:
+        if extra is not None and list(rec.get("flags", [])) != list(extra):
+            return True
+        return rec["source_digest"] != source_digest(deps)
     t = os.path.getmtime(out)
     return any(os.path.getmtime(d) > t for d in deps)
 
@@ -101,15 +112,16 @@ def _hip_lib(out, srcs, deps, extra=(), force=False, scratch_check=True):
     """Compile every source to an object in parallel (hipcc, gfx950), then link `out`.
     scratch_check: refuse lean-kernel instances that use scratch (product builds;
     the coverage build's hit counters cost registers, and it is never timed)."""
-    if not (force or _stale(out, deps)):
+    if not (force or _stale(out, deps, extra)):
         return out
     with _locked(out):
-        if not (force or _stale(out, deps)):  # built while this worker waited
+        if not (force or _stale(out, deps, extra)):  # built while this worker waited
             return out
-        return _hip_lib_locked(out, srcs, extra, scratch_check)
+        return _hip_lib_locked(out, srcs, deps, extra, scratch_check)
 
 
-def _hip_lib_locked(out, srcs, extra, scratch_check):
+def _hip_lib_locked(out, srcs, deps, extra, scratch_check):
+    digest = source_digest(deps)  # before compiling: the record names what was compiled
     odir = out + ".o.d"
     os.makedirs(odir, exist_ok=True)
     # the lean lane's message loop (gr_fast.h: slots x messages, each able to
@@ -128,14 +140,16 @@ def _hip_lib_locked(out, srcs, extra, scratch_check):
             if scratch_check:
                 check_no_scratch(r, s)
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out])
-    write_build_record(out, extra)
+    write_build_record(out, extra, digest, deps)
     return out
 
 
-def write_build_record(out, extra=()):
-    """<lib>.build.json beside a built library: the engine source digest it was
-    built from, when, and by which compiler (bench.py reports it with the digest
-    of the tree it runs in, so a stale prebuilt library shows)."""
+def write_build_record(out, extra=(), digest=None, deps=None):
+    """<lib>.build.json beside a built library: the source digest it was built
+    from (taken before compiling), when, and by which compiler (bench.py reports
+    it with the digest of the tree it runs in, so a stale prebuilt library
+    shows). A source edited during the build leaves no record, so the next
+    build() compiles again instead of claiming the newer tree."""
     import json
     import time
     try:
@@ -143,7 +157,14 @@ def write_build_record(out, extra=()):
         ver = next((v for v in ver if "HIP version" in v or "clang version" in v), ver[0] if ver else "")
     except OSError:
         ver = ""
-    rec = {"lib": os.path.basename(out), "source_digest": source_digest(), "built_at": time.strftime("%Y-%m-%dT%H:%M:%S"),
+    digest = digest or source_digest(deps)
+    if source_digest(deps) != digest:
+        try:
+            os.unlink(out + ".build.json")
+        except OSError:
+            pass
+        return
+    rec = {"lib": os.path.basename(out), "source_digest": digest, "built_at": time.strftime("%Y-%m-%dT%H:%M:%S"),
            "compiler": ver.strip(), "arch": ARCH, "flags": list(extra)}
     with open(out + ".build.json", "w") as fh:
         json.dump(rec, fh)
@@ -247,9 +268,14 @@ def _build_sanitized(force):
 def build_wire(force=False):
     """libgrwire.so: the wire codec (include/gpuraft_wire.h)."""
     os.makedirs(os.path.dirname(WIRE_LIB), exist_ok=True)
-    if force or _stale(WIRE_LIB, WIRE_DEPS):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, WIRE_SRC, "-o", WIRE_LIB])
+    if not (force or _stale(WIRE_LIB, WIRE_DEPS, ())):
+        return WIRE_LIB
+    with _locked(WIRE_LIB):
+        if force or _stale(WIRE_LIB, WIRE_DEPS, ()):
+            digest = source_digest(WIRE_DEPS)
+            _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+                  "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, WIRE_SRC, "-o", WIRE_LIB])
+            write_build_record(WIRE_LIB, (), digest, WIRE_DEPS)
     return WIRE_LIB
 
 

@@ -735,8 +735,9 @@ int gr_space_cx_pack(void* space, uint32_t n_chunks, uint32_t positions, uint32_
   const SpaceView v = make_view(space, n_chunks, positions, depth);
   const io::CxCaps C = io::cx_caps(v.pc, depth, n_chunks, capacities, side_capacity);
   for (uint32_t c = 0; c < n_chunks; ++c) HIPCHK(hipMemsetAsync((uint8_t*)cx + C.off[c], 0, io::kCxHdr, s));
-  hipLaunchKernelGGL(io::cx_pack, dim3(io_grid((size_t)n_chunks * v.pc)), dim3(io::kIoBlock), 0, s, v, (uint8_t*)cx,
-                     C);
+  const uint32_t nwv = v.pc / 64;
+  hipLaunchKernelGGL(io::cx_pack, dim3((nwv + io::kCxPackGroups - 1) / io::kCxPackGroups, n_chunks),
+                     dim3(io::kIoBlock), 0, s, v, (uint8_t*)cx, C);
   HIPCHK(hipGetLastError());
   return GR_OK;
 }
@@ -777,9 +778,12 @@ int gr_space_cx_pack_host(void* space_host, uint32_t n_chunks, uint32_t position
       bool have = false;
       for (uint32_t lane = 0; lane < 64 && !have; ++lane) {
         const Mailbox mb = v.at(c * v.pc + wl * 64 + lane);
+        const uint32_t cb = mb.cnt();
         uint32_t w3;
-        if (io::cx_record_kind(mb, mb.cnt(), &w3)) {
-          hi = (uint32_t)(mb.u64(0, MF_LOG_INDEX) >> 32);
+        uint64_t li;
+        bool anch;
+        if (mb_n(cb) && io::cx_classify(mb, cb, depth, &w3, &li, &anch) && anch) {
+          hi = (uint32_t)(li >> 32);
           have = true;
         }
       }
@@ -790,9 +794,12 @@ int gr_space_cx_pack_host(void* space_host, uint32_t n_chunks, uint32_t position
         const Mailbox mb = v.at(c * v.pc + pos);
         const uint32_t cb = mb.cnt();
         uint32_t w3 = 0;
-        const bool rec = io::cx_record_kind(mb, cb, &w3) && (uint32_t)(mb.u64(0, MF_LOG_INDEX) >> 32) == hi;
+        uint64_t li = 0;
+        bool anch = false;
+        const bool rec = mb_n(cb) && io::cx_classify(mb, cb, depth, &w3, &li, &anch) &&
+                         (!anch || (uint32_t)(li >> 32) == hi);
         if (rec && *nrec < capacity) {
-          io::cx_put_record(mb, w3, buf, L, (*nrec)++);
+          io::cx_put_record(io::cx_term_of(mb, cb), li, w3, buf, L, (*nrec)++);
           mask |= 1ull << lane;
           continue;
         }

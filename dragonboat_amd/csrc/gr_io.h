@@ -634,24 +634,187 @@ __host__ __device__ inline CxLayout cx_layout(uint32_t pc, uint32_t depth, uint3
   L.bytes = L.side + round256((uint64_t)scap * cx_side_entry_bytes(depth));
   return L;
 }
-// Mailbox mb (count byte cb) travels as a record: its hot fields are message 0's,
-// and a Replicate's Commit offset fits 24 bits (*w: the record's third word).
-__host__ __device__ inline bool cx_record_kind(const Mailbox& mb, uint32_t cb, uint32_t* w) {
+// Mailbox mb (count byte cb) travels as a uniform record: its hot fields are
+// message 0's, and a Replicate's Commit offset fits 24 bits (*w: the record's
+// third word).
+// From the count byte and message 0's Commit offset (cd0).
+__host__ __device__ inline bool cx_uniform_w3(uint32_t cb, uint32_t cd0, uint32_t* w) {
   const uint32_t n = mb_n(cb);
   if (!(n && (cb & MB_UNIFORM) && (n == 1 || mb_shared(cb)))) return false;
   if (cb & MB_RESP) {  // an accept has no Commit
     *w = cb;
     return true;
   }
-  const uint32_t d = mb.t32(0, MT_CDELTA) - 0x80000000u + 0x800000u;  // Commit - LogIndex + 2^23
+  const uint32_t d = cd0 - 0x80000000u + 0x800000u;  // Commit - LogIndex + 2^23
   *w = cb | (d << 8);
   return (d >> 24) == 0;
 }
-__host__ __device__ inline void cx_put_record(const Mailbox& mb, uint32_t w, uint8_t* buf, const CxLayout& L,
+__host__ __device__ inline bool cx_record_kind(const Mailbox& mb, uint32_t cb, uint32_t* w) {
+  const uint32_t n = mb_n(cb);
+  if (!(n && (cb & MB_UNIFORM) && (n == 1 || mb_shared(cb)))) return false;
+  return cx_uniform_w3(cb, (cb & MB_RESP) ? 0u : mb.t32(0, MT_CDELTA), w);
+}
+
+// Pattern records (round 6): any other mailbox of at most three messages whose
+// messages are a pass's steady or tick-pass traffic -- a leader's commit
+// broadcasts, heartbeat and proposal ([Replicate, Heartbeat, Replicate]:
+// broadcastHeartbeatMessage, raft.go:567-587, between the Replicates of
+// handleLeaderReplicateResp and ProposeEntries; after a tick pass the staggered
+// [Replicate, Replicate, Replicate] of two commit advances and a proposal), a
+// follower's acks with its HeartbeatResp between them ([accept, HeartbeatResp,
+// accept]: raft.go:923-931, 971-974), a uniform mailbox its writer did not
+// share -- also travels as one 12-byte record instead of a full entry (16 + 72
+// B per message), so a pass with ticks exchanges no more than a steady one.
+// Every message must be one of a few canonical forms that the receiver
+// rebuilds exactly:
+//   Replicate: tag CX_R0C/R1C (compact, as uniform_tag gives) or CX_R0/R1 (the
+//     general lane's full form: entry count 0 or 1, LogTerm = Term, one run at
+//     Term), at the mailbox's anchor LogIndex A;
+//   accept (ReplicateResp, flags 0): LogIndex A + its rank among the accepts;
+//   Heartbeat (flags 0): empty context (Hint = HintHigh = 0: no ReadIndex
+//     pending); its Commit in the chain below (sendHeartbeatMessage:
+//     min(match, committed), raft.go:548-563);
+//   HeartbeatResp (flags 0): empty context;
+// all at one term (the record's term word); Replicates and accepts do not mix.
+// The Commits of the Replicates and heartbeats form a chain: the first one's
+// is A + d0 - 2^16, each later one's the previous one's plus 0 or 1 (a commit
+// advance per ack). With no Replicate or accept the first Commit is A.
+// Third word: bits 0-1 the count (1..3), bits 2-3 clear (bit 3 = MB_UNIFORM
+// marks the uniform kind), bits 4-12 one 3-bit code per message, bits 13-14
+// the Commit steps of messages 1 and 2, bits 15-31 d0. The receiver rebuilds a
+// mailbox of Replicates only or accepts only as a uniform one (shared when its
+// messages repeat message 0's hot fields, as MB_SHARED says: the readers take
+// the same messages either way), any other as a full one. A mailbox that fits
+// neither kind travels as a full entry.
+enum CxCode : uint32_t { CX_R0C = 0, CX_R1C = 1, CX_R0 = 2, CX_R1 = 3, CX_ACC = 4, CX_HB = 5, CX_HBR = 6, CX_NONE = 7 };
+constexpr uint32_t kCxPatStepShift = 13, kCxPatCdShift = 15, kCxPatCdBias = 1u << 16;
+__host__ __device__ inline uint32_t cx_code_tag(uint32_t code) {  // the tag (type | flags << 8) a code stands for
+  switch (code) {
+    case CX_R0C: return GR_REPLICATE | ((uint32_t)MFL_COMPACT << 8);
+    case CX_R1C: return GR_REPLICATE | ((uint32_t)(MFL_COMPACT | MFL_N1 | (1u << MFL_RUNS_SHIFT)) << 8);
+    case CX_R0: return GR_REPLICATE;
+    case CX_R1: return GR_REPLICATE | ((1u << MFL_RUNS_SHIFT) << 8);
+    case CX_ACC: return GR_REPLICATE_RESP;
+    case CX_HB: return GR_HEARTBEAT;
+    case CX_HBR: return GR_HEARTBEAT_RESP;
+    default: return 0xFFFFu;
+  }
+}
+__host__ __device__ inline bool code_is_rep_full(uint32_t tag) {
+  return tag == cx_code_tag(CX_R0) || tag == cx_code_tag(CX_R1);
+}
+// Classify mailbox mb (count byte cb) for the compact exchange: true when it
+// travels as a record, with *w its third word, *li its anchor value and *anch
+// whether the anchor's high bits must match the wave's (false for a record of
+// HeartbeatResps alone, which has none).
+__host__ __device__ inline bool cx_classify(const Mailbox& mb, uint32_t cb, uint32_t depth, uint32_t* w, uint64_t* li,
+                                            bool* anch) {
+  *anch = true;
+  if (cx_record_kind(mb, cb, w)) {
+    *li = mb.u64(0, MF_LOG_INDEX);
+    return true;
+  }
+  const uint32_t n = mb_n(cb);
+  const bool uni = (cb & MB_UNIFORM) != 0;
+  if (!n || n > 3 || n > depth || (!uni && (cb & ~(uint32_t)MB_COUNT))) return false;
+  uint32_t codes = 0, term = uni ? mb.mterm() : 0u, nacc = 0, steps = 0, d0 = 0;
+  uint64_t a = 0, prevc = 0;
+  bool have_a = false, have_c = false, rep = false, acc = false, hbonly = true, ok = true;
+  for (uint32_t k = 0; k < n && ok; ++k) {
+    uint32_t tag, t;
+    uint64_t commit = 0, hint = 0, hint_hi = 0;
+    if (uni) {  // tag and term from the count byte and the term word (gr_layout.h)
+      tag = Mailbox::uniform_tag(cb, k);
+      t = term;
+    } else {
+      const uint32_t* r = reinterpret_cast<const uint32_t*>(mb.rec(k));
+      tag = r[0] & 0xFFFFu;
+      t = r[1];
+      commit = reinterpret_cast<const uint64_t*>(r)[4];
+      hint = reinterpret_cast<const uint64_t*>(r)[5];
+      hint_hi = reinterpret_cast<const uint64_t*>(r)[6];
+      if (k == 0) term = t;
+      if (code_is_rep_full(tag)) {  // the full form: the fields the general lane writes
+        const uint32_t ne = r[2], lt = r[4], rt0 = r[5];
+        const bool one = tag == cx_code_tag(CX_R1);
+        ok = ne == (one ? 1u : 0u) && lt == t && (!one || rt0 == t);
+      }
+    }
+    ok = ok && t == term;
+    uint32_t code = CX_NONE;
+    for (uint32_t c = 0; c < CX_NONE; ++c) code = (code == CX_NONE && cx_code_tag(c) == tag) ? c : code;
+    ok = ok && code != CX_NONE;
+    if (!ok) break;
+    bool carries = false;
+    if (code <= CX_R1) {
+      const uint64_t l = mb.log_index_at(k, cb);
+      commit = commit_of(mb.cdelta_at(k, cb), l);
+      ok = !acc && (!rep || l == a);
+      if (!rep && !have_a) a = l;
+      ok = ok && l == a;
+      rep = have_a = true;
+      hbonly = false;
+      carries = true;
+    } else if (code == CX_ACC) {
+      const uint64_t l = mb.log_index_at(k, cb);
+      ok = !rep && !have_c && (nacc ? l == a + nacc : true);
+      if (!nacc) a = l;
+      acc = have_a = true;
+      hbonly = false;
+      nacc++;
+    } else if (code == CX_HB) {
+      ok = !acc && hint == 0 && hint_hi == 0;
+      carries = true;
+    } else {  // CX_HBR
+      ok = hint == 0 && hint_hi == 0;
+    }
+    if (ok && carries) {
+      if (!have_c) {
+        prevc = commit;
+        have_c = true;
+      } else {
+        const uint64_t st = commit - prevc;
+        ok = st <= 1u;
+        steps |= (uint32_t)(st & 1u) << (k - 1);
+        prevc = commit;
+      }
+    }
+    codes |= code << (3 * k);
+  }
+  if (!ok) return false;
+  // the first Commit relative to the anchor
+  uint64_t first = 0;
+  {
+    uint64_t c0 = prevc;  // walk back the steps to the first Commit
+    for (uint32_t k = n; k-- > 1;) c0 -= (steps >> (k - 1)) & 1u;
+    first = c0;
+  }
+  if (have_c && !have_a) {  // heartbeats (and their acks) alone: the first Commit is the anchor
+    a = first;
+    have_a = true;
+  }
+  if (have_c) {
+    const uint64_t dd = first - a + kCxPatCdBias;  // mod 2^64
+    if (dd >= 2ull * kCxPatCdBias) return false;
+    d0 = (uint32_t)dd;
+  } else {
+    d0 = kCxPatCdBias;
+  }
+  (void)hbonly;
+  *anch = have_a;
+  *li = have_a ? a : 0ull;
+  *w = n | (codes << 4) | (steps << kCxPatStepShift) | (d0 << kCxPatCdShift);
+  return true;
+}
+__host__ __device__ inline void cx_put_record(uint32_t term, uint64_t li, uint32_t w, uint8_t* buf, const CxLayout& L,
                                               uint32_t r) {
-  reinterpret_cast<uint32_t*>(buf + L.term)[r] = mb.mterm();
-  reinterpret_cast<uint32_t*>(buf + L.lo)[r] = (uint32_t)mb.u64(0, MF_LOG_INDEX);
+  reinterpret_cast<uint32_t*>(buf + L.term)[r] = term;
+  reinterpret_cast<uint32_t*>(buf + L.lo)[r] = (uint32_t)li;
   reinterpret_cast<uint32_t*>(buf + L.cb)[r] = w;
+}
+// A record's term word: message 0's term (uniform mailboxes: the term word).
+__host__ __device__ inline uint32_t cx_term_of(const Mailbox& mb, uint32_t cb) {
+  return (cb & MB_UNIFORM) ? mb.mterm() : mb.t32(0, MT_TERM);
 }
 __host__ __device__ inline void cx_put_side(const Mailbox& mb, uint32_t cb, uint32_t pos, uint8_t* buf,
                                             const CxLayout& L, uint32_t depth, uint32_t x) {
@@ -686,12 +849,81 @@ __host__ __device__ inline void cx_get_side(const Mailbox& mb, const uint8_t* e,
     for (uint32_t q = 0; q < kColdUsed / 8; ++q) dst[q] = src[q];
   }
 }
+// A pattern record (third word w, term t, anchor a) rebuilt into mailbox mb.
+// Replicates only (all compact-equivalent) or accepts only: a uniform mailbox
+// (count byte, term word, per message its hot fields; shared when they repeat
+// message 0's). Otherwise a full one: the count byte, the term word, and per
+// message the fields its readers read (gr_lane.h read_msg / decode_record,
+// gr_tick.h): tag and term, LogIndex and Commit offset (Replicates; the full
+// form's entry count, LogTerm and run term too), LogIndex (accepts), Commit and
+// an empty context (heartbeats), an empty context (their acks).
+__host__ __device__ inline void cx_get_pattern(const Mailbox& mb, uint32_t w, uint32_t t, uint64_t a) {
+  const uint32_t n = w & 3u;
+  uint32_t nrep = 0, nacc = 0, n1 = 0, allsame = 1;
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t code = (w >> (4 + 3 * k)) & 7u;
+    nrep += code <= CX_R1;
+    nacc += code == CX_ACC;
+    n1 |= (uint32_t)(code == CX_R1 || code == CX_R1C) << k;
+    if (k) allsame &= ((w >> (kCxPatStepShift + k - 1)) & 1u) ^ 1u;
+  }
+  uint64_t commit = a + (uint64_t)(w >> kCxPatCdShift) - kCxPatCdBias;
+  mb.mterm() = t;
+  if (nrep == n || nacc == n) {  // uniform (gr_layout.h MB_UNIFORM)
+    const bool resp = nacc == n;
+    const bool shared = n > 1 && (resp || allsame);
+    mb.cnt() = (uint8_t)(n | MB_UNIFORM | (resp ? MB_RESP : 0u) | (shared ? MB_SHARED : 0u) |
+                         (resp ? 0u : n1 << MB_N1_SHIFT));
+    for (uint32_t k = 0; k < (shared ? 1u : n); ++k) {
+      if (k) commit += (w >> (kCxPatStepShift + k - 1)) & 1u;
+      mb.u64(k, MF_LOG_INDEX) = a + (resp ? (uint64_t)k : 0ull);
+      if (!resp) {
+        uint32_t cd = 0;
+        commit_delta(commit, a, &cd);
+        mb.t32(k, MT_CDELTA) = cd;
+      }
+    }
+    return;
+  }
+  mb.cnt() = (uint8_t)n;
+  uint32_t ai = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t code = (w >> (4 + 3 * k)) & 7u;
+    if (k) commit += (w >> (kCxPatStepShift + k - 1)) & 1u;
+    mb.tag(k) = (uint16_t)cx_code_tag(code);
+    mb.t32(k, MT_TERM) = t;
+    if (code <= CX_R1) {
+      uint32_t cd = 0;
+      commit_delta(commit, a, &cd);
+      mb.u64(k, MF_LOG_INDEX) = a;
+      mb.t32(k, MT_CDELTA) = cd;
+      const uint32_t ne = (code == CX_R1 || code == CX_R1C) ? 1u : 0u;
+      mb.n(k) = ne;
+      mb.t32(k, MT_LOG_TERM) = t;
+      mb.t32(k, MT_RT0) = ne ? t : 0u;
+    } else if (code == CX_ACC) {
+      mb.u64(k, MF_LOG_INDEX) = a + ai++;
+    } else if (code == CX_HB) {
+      mb.u64(k, MF_COMMIT) = commit;
+      mb.u64(k, MF_HINT) = 0;
+      mb.u64(k, MF_HINT_HIGH) = 0;
+    } else {
+      mb.u64(k, MF_HINT) = 0;
+      mb.u64(k, MF_HINT_HIGH) = 0;
+    }
+  }
+}
 // The wave header's effect on one position (lane): count byte and hot fields.
 __host__ __device__ inline void cx_get_lane(const Mailbox& mb, const uint8_t* buf, const CxLayout& L, uint64_t mask,
                                             uint64_t lost, uint32_t base, uint32_t hi, uint32_t lane) {
   if ((mask >> lane) & 1ull) {
     const uint32_t r = base + (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1));
     const uint32_t w = reinterpret_cast<const uint32_t*>(buf + L.cb)[r];
+    if (!(w & MB_UNIFORM)) {  // a pattern record
+      cx_get_pattern(mb, w, reinterpret_cast<const uint32_t*>(buf + L.term)[r],
+                     ((uint64_t)hi << 32) | reinterpret_cast<const uint32_t*>(buf + L.lo)[r]);
+      return;
+    }
     mb.cnt() = (uint8_t)w;
     mb.mterm() = reinterpret_cast<const uint32_t*>(buf + L.term)[r];
     if (!(w & MB_RESP)) mb.t32(0, MT_CDELTA) = (w >> 8) - 0x800000u + 0x80000000u;
@@ -722,51 +954,132 @@ __host__ __device__ inline CxCaps cx_caps(uint32_t pc, uint32_t depth, uint32_t 
   return C;
 }
 
-// Pack: one wave per 64 positions of the out space (their buffer headers zeroed
-// before). Record slots and side entries are taken with one returning atomic
-// per wave each; a wave's records are consecutive, in lane order.
-__global__ void cx_pack(SpaceView v, uint8_t* cx, CxCaps C) {
-  const uint32_t nwv = v.pc / 64;
-  const uint64_t nw = (uint64_t)v.n_chunks * nwv;
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t w = (uint64_t)blockIdx.x * (kIoBlock / 64) + (threadIdx.x >> 6); w < nw;
-       w += (uint64_t)gridDim.x * (kIoBlock / 64)) {
-    const uint32_t c = (uint32_t)(w / nwv), wl = (uint32_t)(w % nwv), pos = wl * 64 + lane;
-    const uint32_t cap = C.cap[c], scap = C.scap;
-    const CxLayout L = cx_layout(v.pc, v.depth, cap, scap);
-    uint8_t* buf = cx + C.off[c];
-    const Mailbox mb = v.at(c * v.pc + pos);
-    const uint32_t cb = mb.cnt();
-    uint32_t w3 = 0;
-    bool rec = cx_record_kind(mb, cb, &w3);
-    const uint64_t li = rec ? mb.u64(0, MF_LOG_INDEX) : 0ull;
-    const uint64_t any = __ballot(rec);
-    const uint32_t hi =
-        any ? (uint32_t)(__shfl((unsigned long long)li, __ffsll((unsigned long long)any) - 1) >> 32) : 0u;
-    rec = rec && (uint32_t)(li >> 32) == hi;
+// Pack: workgroup b of chunk c (blockIdx.y) takes kCxPackGroups consecutive
+// wave groups (64 positions each), each of its four waves kCxPackPer of them in
+// order (buffer headers zeroed before). A wave loads the hot fields of all its
+// groups at once (count byte, term word, message 0's Commit offset and LogIndex:
+// fixed addresses, no dependence on the count byte), classifies them (uniform
+// mailboxes from those words; the rare non-uniform ones with their cold
+// records, cx_classify) and counts records and side entries; the workgroup
+// takes its record slots, then its side entries (its own plus the records past
+// capacity), with one returning atomic each; then each wave writes its records,
+// side entries and wave headers from the same registers. A wave's records are
+// consecutive over its groups, in lane order. (Round 5 took the slots with a
+// returning atomic per wave on one word per chunk: 360 us per 500k-group pass
+// of one chunk, 47k waves queued on it; round 6's first cut, one group's loads
+// at a time, 44 us.)
+constexpr uint32_t kCxPackPer = 8, kCxPackGroups = kCxPackPer * (kIoBlock / 64);
+__global__ __launch_bounds__(kIoBlock) void cx_pack(SpaceView v, uint8_t* cx, CxCaps C) {
+  constexpr uint32_t nwave = kIoBlock / 64;
+  const uint32_t c = blockIdx.y, nwv = v.pc / 64;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t g0 = blockIdx.x * kCxPackGroups + wave * kCxPackPer;
+  const uint32_t cap = C.cap[c], scap = C.scap;
+  const CxLayout L = cx_layout(v.pc, v.depth, cap, scap);
+  uint8_t* buf = cx + C.off[c];
+  __shared__ uint32_t s_rec[nwave], s_side[nwave], s_base[2];
+  // ---- every group's hot words in one batch (groups past the chunk: position 0's)
+  uint32_t cb[kCxPackPer], cd[kCxPackPer], tw[kCxPackPer];
+  uint64_t li[kCxPackPer];
+#pragma unroll
+  for (uint32_t q = 0; q < kCxPackPer; ++q) {
+    const bool in = g0 + q < nwv;
+    const Mailbox mb = v.at(c * v.pc + (in ? (g0 + q) * 64 + lane : 0u));
+    cb[q] = mb.cnt();
+    tw[q] = mb.mterm();
+    cd[q] = mb.t32(0, MT_CDELTA);
+    li[q] = mb.u64(0, MF_LOG_INDEX);
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < kCxPackPer; ++q) {  // every load issued before any value is used
+    cb[q] = keep_value(cb[q]);
+    tw[q] = keep_value(tw[q]);
+    cd[q] = keep_value(cd[q]);
+    li[q] = keep_value(li[q]);
+  }
+  uint32_t w3[kCxPackPer], hi[kCxPackPer];
+  uint64_t recm = 0, msgm = 0;  // per group q: bit q
+  uint32_t nrec = 0, nside = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < kCxPackPer; ++q) {
+    const bool in = g0 + q < nwv;
+    const uint32_t b = in ? cb[q] : 0u;
+    const bool msgs = mb_n(b) != 0;
+    bool rec = false, anch = true;
+    w3[q] = 0;
+    if (msgs && (b & MB_UNIFORM)) {  // the uniform kind from the loaded words
+      rec = cx_uniform_w3(b, cd[q], &w3[q]);
+    }
+    if (__ballot(msgs && !rec)) {  // pattern records (tick passes, unshared pairs): cx_classify
+      if (msgs && !rec) {
+        const Mailbox mb = v.at(c * v.pc + (g0 + q) * 64 + lane);
+        uint64_t l = 0;
+        rec = cx_classify(mb, b, v.depth, &w3[q], &l, &anch);
+        if (rec) {
+          li[q] = l;
+          tw[q] = cx_term_of(mb, b);
+        }
+      }
+    }
+    const uint64_t any = __ballot(rec && anch);
+    hi[q] = any ? (uint32_t)(__shfl((unsigned long long)li[q], __ffsll((unsigned long long)any) - 1) >> 32) : 0u;
+    rec = rec && (!anch || (uint32_t)(li[q] >> 32) == hi[q]);
+    recm |= (uint64_t)rec << q;
+    msgm |= (uint64_t)msgs << q;
+    nrec += (uint32_t)__popcll(__ballot(rec));
+    nside += (uint32_t)__popcll(__ballot(msgs && !rec));
+  }
+  // ---- the workgroup's record slots and side entries
+  if (lane == 0) s_rec[wave] = nrec;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t q = 0; q < nwave; ++q) t += s_rec[q];
+    s_base[0] = t ? atomicAdd(reinterpret_cast<uint32_t*>(buf), t) : 0u;
+  }
+  __syncthreads();
+  uint32_t r = s_base[0];
+  for (uint32_t q = 0; q < wave; ++q) r += s_rec[q];
+  const uint32_t over = r >= cap ? nrec : (r + nrec > cap ? r + nrec - cap : 0u);  // records past capacity
+  if (lane == 0) s_side[wave] = nside + over;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t q = 0; q < nwave; ++q) t += s_side[q];
+    s_base[1] = t ? atomicAdd(reinterpret_cast<uint32_t*>(buf) + 1, t) : 0u;
+  }
+  __syncthreads();
+  uint32_t x0 = s_base[1];
+  for (uint32_t q = 0; q < wave; ++q) x0 += s_side[q];
+  // ---- records, side entries and wave headers
+  const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+  for (uint32_t q = 0; q < kCxPackPer; ++q) {
+    if (g0 + q >= nwv) break;  // wave-uniform
+    const uint32_t g = g0 + q, pos = g * 64 + lane;
+    const bool rec = (recm >> q) & 1u, msgs = (msgm >> q) & 1u;
     const uint64_t mask = __ballot(rec);
-    uint32_t base = 0;
-    if (lane == 0 && mask) base = atomicAdd(reinterpret_cast<uint32_t*>(buf), (uint32_t)__popcll(mask));
-    base = (uint32_t)__shfl((int)base, 0);
-    const uint32_t r = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1));
-    const bool fits = rec && r < cap;  // the lanes past cap are the wave's last ones
-    if (fits) cx_put_record(mb, w3, buf, L, r);
-    const bool side = mb_n(cb) && !fits;
+    const uint32_t ri = r + (uint32_t)__popcll(mask & below);
+    const bool fits = rec && ri < cap;  // past capacity: the group's last record lanes
+    if (fits) cx_put_record(tw[q], li[q], w3[q], buf, L, ri);
+    const bool side = msgs && !fits;
     const uint64_t smask = __ballot(side);
-    uint32_t sbase = 0;
-    if (lane == 0 && smask) sbase = atomicAdd(reinterpret_cast<uint32_t*>(buf) + 1, (uint32_t)__popcll(smask));
-    sbase = (uint32_t)__shfl((int)sbase, 0);
-    const uint32_t x = sbase + (uint32_t)__popcll(smask & ((1ull << lane) - 1));
-    const bool sfits = side && x < scap;
-    if (sfits) cx_put_side(mb, cb, pos, buf, L, v.depth, x);
+    const uint32_t xi = x0 + (uint32_t)__popcll(smask & below);
+    const bool sfits = side && xi < scap;
+    if (sfits) {
+      const Mailbox mb = v.at(c * v.pc + pos);
+      cx_put_side(mb, mb.cnt(), pos, buf, L, v.depth, xi);
+    }
     const uint64_t fmask = __ballot(fits), lost = __ballot(side && !sfits);
     if (lane == 0) {
-      uint8_t* h = buf + L.waves + (uint64_t)wl * kCxWave;
+      uint8_t* h = buf + L.waves + (uint64_t)g * kCxWave;
       reinterpret_cast<uint64_t*>(h)[0] = fmask;
       reinterpret_cast<uint64_t*>(h)[1] = lost;
-      reinterpret_cast<uint32_t*>(h)[4] = base;
-      reinterpret_cast<uint32_t*>(h)[5] = hi;
+      reinterpret_cast<uint32_t*>(h)[4] = r;
+      reinterpret_cast<uint32_t*>(h)[5] = hi[q];
     }
+    r += (uint32_t)__popcll(mask);
+    x0 += (uint32_t)__popcll(smask);
   }
 }
 // Unpack, part 1: every position's count byte and its record's hot fields.

@@ -59,13 +59,13 @@ def count_bytes(hot, n_chunks, hot_chunk, hot_tile, positions):
 TILE_W = 256  # gr_layout.h kTileW (GR_TILE_SHIFT = 8); Exchange checks it against the library
 SIDE_DIV, SIDE_MIN = 32, 1024  # side-buffer capacity per chunk: positions / SIDE_DIV, at least SIDE_MIN
 # compact exchange capacities per chunk: records for the share of a chunk's
-# positions that hold messages in the steady state plus CX_MARGIN, full entries
-# for 1/CX_SIDE_DIV of them (at least CX_SIDE_MIN). A chunk carries the replica
-# pairs (r -> j) of one rank offset; with the benchmark's leaders (replica 0 of
-# every group) only the pairs with the leader on one end hold messages (a
-# leader's Replicates, its followers' acks): half of an N = 8 chunk's positions,
-# two thirds at N = 3, all of the offset-2 chunk at N = 4.
-CX_MARGIN, CX_SIDE_DIV, CX_SIDE_MIN = 0.05, 256, 256
+# positions that hold messages in the steady state, whichever replica leads
+# (cx_fill_max), full entries for 1/CX_SIDE_DIV of them (at least CX_SIDE_MIN).
+# A chunk carries the replica pairs (r -> j) of one rank offset; only the pairs
+# with the leader on one end hold messages (a leader's Replicates, its
+# followers' acks).
+CX_MARGIN, CX_SIDE_DIV, CX_SIDE_MIN = 0.0, 256, 256
+CX_MAX_CHUNKS = 8  # gr_io.h kCxMaxChunks: a rank's destination chunks in one compact buffer set
 
 
 def cx_fill(R, N, offset, leader=0):
@@ -74,6 +74,16 @@ def cx_fill(R, N, offset, leader=0):
     pairs = offset_pairs(R, N)
     per = max(len(v) for v in pairs.values())
     return sum(1 for r, j in pairs[offset] if leader in (r, j)) / per
+
+
+def cx_fill_max(R, N, offset):
+    """The largest steady-state share over leader placements: leaders move
+    (config 5's churn, elections), and a chunk's fill depends on which replica
+    leads. With every group led by replica 1 at N = 8 the offset-1 and offset-7
+    chunks are full; with leaders spread evenly they are two thirds full. Sized
+    by this, the records of a steady state never overflow wherever leaders sit
+    (ADVICE r05): 3.0 vs 2.0 chunk-fills per rank at N = 8."""
+    return max(cx_fill(R, N, offset, leader) for leader in range(R))
 
 
 def cx_capacities(positions, fill, frac=None, side=None):
@@ -169,9 +179,13 @@ class Exchange:
     """Spaces + routes for one rank; `step` launches one pass and exchanges."""
 
     def __init__(self, G, R, S, world, rank, placement, seed=2, exchange=None, codec="cx", cx_frac=None,
-                 cx_side=None, depth=None):
-        """exchange=True keeps the one-rank spread exchange (copy + side buffers)
+                 cx_side=None, depth=None, collective=None):
+        """exchange=True keeps the one-rank spread exchange (pack, move, unpack)
         that a one-rank run otherwise skips (tests of the N > 1 code on one GPU).
+        collective: move the buffers with the process group's all_to_all_single
+        (RCCL: async on the pass's stream, waited on as a stream wait) even with
+        one rank, where a device copy would do (default: only with N > 1); the
+        one-GPU test of the N = 8 exchange path (tests/test_pipeline_rccl.py).
         codec: "cx" (compact exchange) or "dense" (hot region + side buffers).
         depth: messages per mailbox of a spread space (default 3; a fuller one
         escalates CAPACITY at its writer)."""
@@ -201,7 +215,14 @@ class Exchange:
         # one rank: every mailbox is the rank's own, at the same position on both
         # sides (the one chunk's sender and receiver positions coincide), so the
         # exchange is no copy at all: the two spaces ping-pong as in local placement
-        self.pingpong = placement == "local" or (world == 1 and not exchange)
+        self.pingpong = placement == "local" or (world == 1 and not exchange and not collective)
+        self.collective = placement == "spread" and (world > 1 or bool(collective))
+        if codec == "cx" and not self.pingpong and self.n_chunks > CX_MAX_CHUNKS:
+            import warnings
+            warnings.warn(f"spread placement with {self.n_chunks} peer chunks exceeds the compact exchange's "
+                          f"{CX_MAX_CHUNKS}: exchanging the dense form")
+            self.codec = codec = "dense"
+            self.last_cx = False
         if placement == "spread" and world == 1:
             assert self.n_chunks == 1 and np.array_equal(np.sort(self.in_pos[self.in_pos != NOPOS]),
                                                          np.sort(self.out_pos[self.out_pos != NOPOS]))
@@ -223,7 +244,7 @@ class Exchange:
             # sender (destination d: offset d - rank) and the receiver (source a:
             # offset rank - a)
             N = self.world
-            cap_of = lambda o: cx_capacities(self.positions, cx_fill(self.R, N, o), self.cx_frac, self.cx_side)
+            cap_of = lambda o: cx_capacities(self.positions, cx_fill_max(self.R, N, o), self.cx_frac, self.cx_side)
             self.cx_send_caps = [cap_of((d - self.rank) % N)[0] for d in self.dests]
             self.cx_recv_caps = [cap_of((self.rank - a) % N)[0] for a in self.srcs]
             self.cx_scap = cap_of(0)[1]
@@ -266,7 +287,7 @@ class Exchange:
             send, recv = self.cx
             eng.cx_pack(out.data_ptr(), self.n_chunks, self.positions, self.depth, send.data_ptr(),
                         self.cx_send_caps, self.cx_scap, h)
-            if self.world == 1:
+            if not self.collective:
                 recv.copy_(send)
                 return []
             return [_all_to_all(recv, send, self.cx_splits[1], self.cx_splits[0])]
@@ -274,7 +295,7 @@ class Exchange:
         eng.side_pack(out.data_ptr(), self.n_chunks, self.positions, self.depth, side_out.data_ptr(),
                       self.side_cap, h)
         hr = self.hot_region
-        if self.world == 1:
+        if not self.collective:
             inp[:hr].copy_(out[:hr])
             side_in.copy_(side_out)
             work = []
@@ -338,7 +359,12 @@ class Pipeline:
     """
 
     def __init__(self, G, R, S, world, rank, placement="spread", banks=None, seed=2, exchange=None, codec="cx",
-                 cx_frac=None, cx_side=None, depth=None):
+                 cx_frac=None, cx_side=None, depth=None, collective=None, verify_heavy=None):
+        """verify_heavy: check on every pass that all ranks passed the same
+        `heavy` (one 2-element all_reduce; a disagreement would pair buffers of
+        different sizes in the all-to-all). Default: on when GR_VERIFY_HEAVY=1."""
+        import os
+        self.verify_heavy = (os.environ.get("GR_VERIFY_HEAVY") == "1") if verify_heavy is None else verify_heavy
         if banks is None:  # banks overlap one another's exchange: only with one to overlap
             banks = 2 if placement == "spread" and world > 1 and G >= 128 else 1
         # bank sizes a multiple of 64 but the last: a wave's lanes then share a
@@ -347,7 +373,7 @@ class Pipeline:
         sizes = [base] * (banks - 1) + [G - base * (banks - 1)]
         self.R, self.S, self.world, self.rank, self.placement = R, S, world, rank, placement
         self.ex = [Exchange(Gb, R, S, world, rank, placement, seed=seed + 7919 * b, exchange=exchange, codec=codec,
-                            cx_frac=cx_frac, cx_side=cx_side, depth=depth)
+                            cx_frac=cx_frac, cx_side=cx_side, depth=depth, collective=collective)
                    for b, Gb in enumerate(sizes)]
         self.groups = G
         self.engines, self.spaces, self.streams = [], [], []
@@ -373,8 +399,10 @@ class Pipeline:
 
     def step(self, k, heavy=False):
         """Pass k of every bank (heavy: the pass's exchange in the dense form,
-        Exchange.exchange)."""
+        Exchange.exchange; it must be the same on every rank)."""
         import torch
+        if self.verify_heavy and any(ex.collective for ex in self.ex):
+            self._check_heavy(bool(heavy))
         for b, (ex, eng) in enumerate(zip(self.ex, self.engines)):
             s = self.streams[b]
             with torch.cuda.stream(s):
@@ -390,6 +418,18 @@ class Pipeline:
                                 ex.positions, ex.n_peers, s.cuda_stream, depth=ex.depth)
                 if not ex.pingpong:
                     self.work[b] = ex.exchange(eng, self.spaces[b], s.cuda_stream, heavy=heavy)
+
+    def _check_heavy(self, heavy):
+        """All ranks agree on `heavy` (max of (h, -h) over ranks: h and -h agree
+        iff every rank passed the same flag); raises before any buffer moves."""
+        import torch
+        import torch.distributed as dist
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([int(heavy), -int(heavy)], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        hi, lo = int(t[0]), -int(t[1])
+        if hi != lo:
+            raise RuntimeError(f"Pipeline.step: ranks disagree on heavy (rank {self.rank}: {heavy})")
 
     def graph_ready(self):
         """Graph mode applies: every bank's spaces ping-pong (no exchange step)."""

@@ -148,6 +148,41 @@ def test_gloo_all_to_all_delivery(world):
     assert all(e == 0 for _, e in res), res
 
 
+def _heavy_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pipe = X.Pipeline(128, 3, 3, world, rank, "spread", verify_heavy=True)
+    out = []
+    for heavy in (False, True, rank == 0):  # agree, agree, disagree
+        try:
+            pipe._check_heavy(heavy)
+            out.append("ok")
+        except RuntimeError:
+            out.append("refused")
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_heavy_flag_checked_across_ranks():
+    """ranks passing different `heavy` to Pipeline.step would pair
+    all-to-all buffers of different sizes; verify_heavy refuses the pass on
+    every rank before anything moves."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_heavy_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(o == ["ok", "ok", "refused"] for _, o in res), res
+
+
 @pytest.mark.parametrize("placement,N,rank", [("local", 1, 0), ("spread", 1, 0), ("spread", 2, 1),
                                               ("spread", 8, 5)])
 def test_routes_are_affine(built, placement, N, rank):
@@ -536,6 +571,123 @@ def test_cx_codec_round_trip(built):
     dests, _ = X.spread_peer_ranks(3, 8, 0)
     tot = 0
     for d in dests:
-        cap, scap = X.cx_capacities(pos, X.cx_fill(3, 8, d % 8))
+        cap, scap = X.cx_capacities(pos, X.cx_fill_max(3, 8, d % 8))
         tot += int(lib.gr_space_cx_bytes(1, pos, 3, cx_caps_array([cap], 1).ctypes.data, scap))
-    assert tot < 70e6, tot
+    # records for the worst leader placement: 3 chunk-fills of 2M
+    # positions x 12 B + wave headers + 1/256 full entries
+    assert tot < 90e6, tot
+
+
+def test_cx_capacity_covers_any_leader_placement():
+    """Sized by cx_fill_max, a chunk's record capacity holds the steady state
+    whichever replica leads every group (the worst case; mixed leaders fill
+    less), at N = 1..8 (leaders moved off replica 0 overflowed)."""
+    for N in range(1, 9):
+        pairs = X.offset_pairs(3, N)
+        per = max(len(v) for v in pairs.values())
+        positions = per * 1024
+        for o, lst in pairs.items():
+            if not lst:
+                continue
+            cap, _ = X.cx_capacities(positions, X.cx_fill_max(3, N, o))
+            for leader in range(3):
+                used = sum(1024 for r, j in lst if leader in (r, j))
+                assert used <= cap, (N, o, leader, used, cap)
+
+
+def _tick_space(n_chunks, positions, seed=5):
+    """Mailboxes of a tick pass (and near misses): [Replicate, Heartbeat,
+    Replicate] from a leader, [accept, HeartbeatResp, accept] from a follower,
+    a lone Heartbeat or HeartbeatResp, and variants the pattern records must
+    refuse (a context in the heartbeat, accepts out of sequence, a heartbeat
+    Commit that differs from the Replicates', a second entry). Returns the
+    messages, their positions, and per position whether it must travel as a
+    record."""
+    from dragonboat_amd import abi
+    rng = np.random.default_rng(seed)
+    pc = X.pad_positions(positions)
+    msgs, pos, want_rec = [], [], {}
+
+    def mk(**f):
+        m = np.zeros(1, abi.MESSAGE)[0]
+        for k, v in f.items():
+            m[k] = v
+        return m
+    for c in range(n_chunks):
+        for q in range(positions):
+            kind = int(rng.integers(0, 13))
+            T = 5 + (q % 3)
+            L = 2**32 + 1000 * q + 7
+            C = L - 2
+            rep = lambda n, c=C: mk(type=abi.REPLICATE, term=T, log_index=L, log_term=T, commit=c, n_entries=n,
+                                    n_runs=n, run_term=[T if n else 0, 0])
+            if kind == 0:
+                lst, rec = [rep(0), mk(type=abi.HEARTBEAT, term=T, commit=C), rep(1)], True
+            elif kind == 1:
+                lst, rec = [mk(type=abi.REPLICATE_RESP, term=T, log_index=L), mk(type=abi.HEARTBEAT_RESP, term=T),
+                            mk(type=abi.REPLICATE_RESP, term=T, log_index=L + 1)], True
+            elif kind == 2:
+                lst, rec = [mk(type=abi.HEARTBEAT, term=T, commit=L)], True
+            elif kind == 3:
+                lst, rec = [mk(type=abi.HEARTBEAT_RESP, term=T)], True
+            elif kind == 4:  # a ReadIndex context travels in full
+                lst, rec = [rep(0), mk(type=abi.HEARTBEAT, term=T, commit=C, hint=q + 1, hint_high=3)], False
+            elif kind == 5:  # accepts out of sequence
+                lst, rec = [mk(type=abi.REPLICATE_RESP, term=T, log_index=L), mk(type=abi.HEARTBEAT_RESP, term=T),
+                            mk(type=abi.REPLICATE_RESP, term=T, log_index=L + 5)], False
+            elif kind == 6:  # the heartbeat's Commit is not the Replicates'
+                lst, rec = [rep(0), mk(type=abi.HEARTBEAT, term=T, commit=C - 1)], False
+            elif kind == 7:  # two entries
+                lst, rec = [mk(type=abi.REPLICATE, term=T, log_index=L, log_term=T, commit=C, n_entries=2, n_runs=1,
+                               run_term=[T, 0]), mk(type=abi.HEARTBEAT, term=T, commit=C)], False
+            elif kind == 9:  # a commit broadcast and a proposal, unshared
+                lst, rec = [rep(0), rep(1)], True
+            elif kind == 10:  # two commit advances and a proposal (after a tick pass)
+                lst, rec = [rep(0, C - 1), rep(0), rep(1)], True
+            elif kind == 11:  # a Commit step of 2
+                lst, rec = [rep(0), rep(1, C + 2)], False
+            elif kind == 12:  # two accepts, unshared
+                lst, rec = [mk(type=abi.REPLICATE_RESP, term=T, log_index=L),
+                            mk(type=abi.REPLICATE_RESP, term=T, log_index=L + 1)], True
+            else:
+                continue
+            for m in lst:
+                msgs.append(m)
+                pos.append(c * pc + q)
+            want_rec[c * pc + q] = rec
+    return np.array(msgs, abi.MESSAGE), np.array(pos, np.uint32), want_rec
+
+
+def test_cx_pattern_records(built):
+    """Round 6: a tick pass's mailboxes (a leader's commit broadcast, heartbeat
+    and proposal; a follower's acks around its HeartbeatResp; lone heartbeats
+    and acks with an empty context), unshared uniform pairs and the staggered
+    commit advances after a tick travel as 12-byte records and unpack to the
+    very messages sent, every field; near misses go as full entries."""
+    from dragonboat_amd.engine import load_library, decode_space, cx_caps_array
+    lib = load_library()
+    n_chunks, positions, depth = 2, 900, 3
+    msgs, pos, want_rec = _tick_space(n_chunks, positions)
+    nb = int(lib.gr_space_bytes(n_chunks, positions, depth))
+    src = np.zeros(nb, np.uint8)
+    assert lib.gr_space_encode(src.ctypes.data, n_chunks, positions, depth, msgs.ctypes.data, len(msgs),
+                               pos.ctypes.data) == 0
+    want = decode_space(src.copy(), n_chunks, positions, depth)
+    pc = X.pad_positions(positions)
+    caps = cx_caps_array(pc, n_chunks)
+    cb = int(lib.gr_space_cx_bytes(n_chunks, positions, depth, caps.ctypes.data, pc))
+    cx = np.zeros(cb, np.uint8)
+    dst = np.full(nb, 0xA5, np.uint8)
+    assert lib.gr_space_cx_pack_host(src.ctypes.data, n_chunks, positions, depth, cx.ctypes.data,
+                                     caps.ctypes.data, pc) == 0
+    assert lib.gr_space_cx_unpack_host(dst.ctypes.data, n_chunks, positions, depth, cx.ctypes.data,
+                                       caps.ctypes.data, pc) == 0
+    got = decode_space(dst, n_chunks, positions, depth)
+    key = lambda a: np.sort(a, order=["peer", "slot"])
+    assert np.array_equal(key(got), key(want))  # every field of every message
+    chunk_bytes = cb // n_chunks
+    for c in range(n_chunks):
+        n_rec, n_side = np.frombuffer(cx[c * chunk_bytes:c * chunk_bytes + 8].tobytes(), np.uint32)
+        recs = sum(1 for p, r in want_rec.items() if r and p // pc == c)
+        sides = sum(1 for p, r in want_rec.items() if not r and p // pc == c)
+        assert (n_rec, n_side) == (recs, sides), (c, n_rec, n_side, recs, sides)

@@ -89,22 +89,24 @@ def test_spread_cold_fields_by_side_buffer(gpu, codec):
     """Spread exchange, no host read-back, parity every pass. dense: the hot region
     every pass, the cold fields of the mailboxes that need them (heartbeats and
     their acks, ticks every third pass) through the device-packed side buffers.
-    cx (the compact exchange), sized with a full entry for every position
-    (cx_side = 1: ticks every third pass at this scale leave few steady passes):
-    12-byte records for the steady mailboxes, full entries for the heartbeats,
-    acks and the catch-ups after them; every fourth pass exchanges the dense form
-    instead (a heavy pass), so the forms alternate between passes."""
+    cx (the compact exchange): 12-byte records for the steady mailboxes and,
+    round 6, for the tick passes' too (pattern records: a leader's commit
+    broadcast, heartbeat and proposal; a follower's acks around its
+    HeartbeatResp), so the compact passes carry no full entry at all; every
+    fourth pass exchanges the dense form instead (a heavy pass), so the forms
+    alternate between passes."""
     import devsim
     st = {}
     cx = codec == "cx"
     final = devsim.run_device(500, 3, 9, placement="spread", tick_every=3, stats=st, codec=codec,
-                              cx_side=1.0 if cx else None, heavy_every=4 if cx else 0)
+                              heavy_every=4 if cx else 0)
     assert np.all(final["committed"][:500] > 2**32)
     used = [n > 0 for n in st["side_entries"]]
     assert any(used) and not all(used), st
     if cx:
         assert st["records"][0] > 0 and st["records"][1] > 0, st  # steady passes: records only
-        assert any(st["side_entries"][k] > 0 for k in (2, 4, 5, 6, 8)), st  # full entries, compact form
+        compact = (0, 1, 2, 4, 5, 6, 8)  # ticks on 2, 5, 8; dense on 3, 7
+        assert all(st["records"][k] > 0 for k in compact) and not any(st["side_entries"][k] for k in compact), st
         assert any(st["side_entries"][k] > 0 for k in (3, 7)), st  # cold fields, dense form
 
 

@@ -12,8 +12,8 @@ churn: BASELINE config 5's leader changes (p = 0.1 of the settled groups on
 passes 1 and 4, applied to the oracle and to whichever rank holds each changed
 replica) and a Tick on every replica every third pass, so step-downs, rejects,
 multi-entry catch-ups, heartbeats and their acks -- full records -- cross ranks.
-With the compact exchange the tick passes are heavy (dense form) and the others
-compact, so both forms cross and alternate."""
+With the compact exchange every pass is compact, the tick passes' heartbeats
+and acks as pattern records (round 6; round 5 exchanged them in the dense form)."""
 import os
 import socket
 
@@ -23,7 +23,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, G, banks, passes, codec, churn, q):
+def _worker(rank, world, port, G, banks, passes, codec, churn, q, backend="gloo", collective=None, sizing="full",
+            heavy_after=(0,), ticks=None):
+    """One rank: Pipeline on cuda:0 beside the oracle, every pass. backend
+    "nccl" with collective=True runs RCCL's async all_to_all_single even with
+    one rank (tests/test_pipeline_rccl.py). sizing "full": room for a full entry
+    at every position and full-depth mailboxes (churn); "default": the shipped
+    capacities and depth, with `heavy` on the passes heavy_after says (offsets
+    from each leader-change pass), CAPACITY escalations reported. ticks: a Tick
+    on every replica every third pass (default: with churn)."""
     import torch
     import torch.distributed as dist
     from dragonboat_amd import abi, populations as P
@@ -35,13 +43,14 @@ def _worker(rank, world, port, G, banks, passes, codec, churn, q):
     R = 3
     try:
         torch.cuda.set_device(0)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group(backend, rank=rank, world_size=world)
         # with churn and ticks few passes are steady: room for a full entry (compact
         # form) or a side entry (dense form) at every position, and full-depth
         # mailboxes (a new leader's catch-ups, proposal and heartbeats to one
         # follower in one pass overflow depth 3: CAPACITY, the host's to resolve)
+        full = churn and sizing == "full"
         pipe = Pipeline(G, R, R, world, rank, "spread", banks=banks, seed=11, codec=codec,
-                        cx_side=1.0 if churn else None, depth=abi.GR_C if churn else None)
+                        cx_side=1.0 if full else None, depth=abi.GR_C if full else None, collective=collective)
         pipe.setup(Engine, torch.device("cuda", 0), 0)
         # the oracle: every bank's groups of every home, as one population each
         pops, msgs, topos = {}, {}, {}
@@ -53,8 +62,14 @@ def _worker(rank, world, port, G, banks, passes, codec, churn, q):
                 msgs[(b, h)] = np.zeros(0, abi.MESSAGE)
         rng = np.random.default_rng(100 + 0)  # the same draws on every rank
         bad, esc, first_esc = None, 0, None
+        # heavy (dense) passes with the default sizing: the leader-change passes and
+        # those heavy_after them; the tick passes travel compact (pattern records)
+        changes = {1, 4} if churn else set()
+        heavy_at = {k + d for k in changes for d in heavy_after} if sizing == "default" else set()
+        capacity = 0
+        ticks = churn if ticks is None else ticks
         for k in range(passes):
-            tk = 1 if churn and k % 3 == 2 else 0
+            tk = 1 if ticks and k % 3 == 2 else 0
             home_loc = {}
             for b, ex in enumerate(pipe.ex):
                 Gb = ex.G
@@ -80,9 +95,10 @@ def _worker(rank, world, port, G, banks, passes, codec, churn, q):
                     loc[sl] = home_loc[(b, h)][sl]
                 loc["peer"] = np.arange(R * Gb, dtype=np.uint32)
                 pipe.engines[b].set_locals(loc)
-            # the tick passes are heavy (the dense form crosses, exchange.py); the
-            # others, leader changes included, cross as compact records and full entries
-            pipe.step(k, heavy=bool(tk))
+            # "full" sizing: every pass compact, leader changes included (records and
+            # full entries; the tick passes as pattern records). "default": heavy
+            # where heavy_at says
+            pipe.step(k, heavy=k in heavy_at)
             pipe.synchronize()
             for b, ex in enumerate(pipe.ex):
                 Gb = ex.G
@@ -105,6 +121,7 @@ def _worker(rank, world, port, G, banks, passes, codec, churn, q):
                     # full mailboxes); a mailbox the exchange lost would escalate
                     # CAPACITY at its reader where the oracle does not
                     de, oe = res["escalation"][sl], outs[h]["results"]["escalation"][sl]
+                    capacity += int(((de == abi.ESC_NAMES.index("capacity")) & (oe != de)).sum())
                     mm = np.nonzero(de != oe)[0]
                     if len(mm) and esc == 0:
                         first_esc = (k, b, r, int(mm[0]), abi.ESC_NAMES[int(de[mm[0]])],
@@ -113,7 +130,7 @@ def _worker(rank, world, port, G, banks, passes, codec, churn, q):
         st = pipe.stats()
         pipe.close()
         dist.destroy_process_group()
-        q.put((rank, bad, (esc, first_esc), st["leader_commits"], None))
+        q.put((rank, bad, (esc, first_esc, capacity), st["leader_commits"], None))
     except Exception as e:  # reported to the test, never a hang
         import traceback
         q.put((rank, None, 0, 0, traceback.format_exc()))
