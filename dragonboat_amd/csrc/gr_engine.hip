@@ -748,8 +748,9 @@ int gr_space_cx_unpack(void* space, uint32_t n_chunks, uint32_t positions, uint3
   const hipStream_t s = (hipStream_t)stream;
   const SpaceView v = make_view(space, n_chunks, positions, depth);
   const io::CxCaps C = io::cx_caps(v.pc, depth, n_chunks, capacities, side_capacity);
-  hipLaunchKernelGGL(io::cx_unpack_waves, dim3(io_grid((size_t)n_chunks * v.pc)), dim3(io::kIoBlock), 0, s, v,
-                     (const uint8_t*)cx, C);
+  const uint32_t nwv = v.pc / 64;
+  hipLaunchKernelGGL(io::cx_unpack_waves, dim3((nwv + io::kCxUnpackGroups - 1) / io::kCxUnpackGroups, n_chunks),
+                     dim3(io::kIoBlock), 0, s, v, (const uint8_t*)cx, C);
   HIPCHK(hipGetLastError());
   if (side_capacity) {
     hipLaunchKernelGGL(io::cx_unpack_side, dim3(io_grid((size_t)n_chunks * side_capacity)), dim3(io::kIoBlock), 0, s,

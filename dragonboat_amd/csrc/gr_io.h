@@ -670,7 +670,9 @@ __host__ __device__ inline bool cx_record_kind(const Mailbox& mb, uint32_t cb, u
 //   Replicate: tag CX_R0C/R1C (compact, as uniform_tag gives) or CX_R0/R1 (the
 //     general lane's full form: entry count 0 or 1, LogTerm = Term, one run at
 //     Term), at the mailbox's anchor LogIndex A;
-//   accept (ReplicateResp, flags 0): LogIndex A + its rank among the accepts;
+//   accept (ReplicateResp, flags 0): LogIndex A for the first, each later one
+//     the previous one's plus 0 or 1 (one ack per Replicate received, the
+//     staggered commit advances' Replicates repeat a LogIndex);
 //   Heartbeat (flags 0): empty context (Hint = HintHigh = 0: no ReadIndex
 //     pending); its Commit in the chain below (sendHeartbeatMessage:
 //     min(match, committed), raft.go:548-563);
@@ -681,7 +683,8 @@ __host__ __device__ inline bool cx_record_kind(const Mailbox& mb, uint32_t cb, u
 // advance per ack). With no Replicate or accept the first Commit is A.
 // Third word: bits 0-1 the count (1..3), bits 2-3 clear (bit 3 = MB_UNIFORM
 // marks the uniform kind), bits 4-12 one 3-bit code per message, bits 13-14
-// the Commit steps of messages 1 and 2, bits 15-31 d0. The receiver rebuilds a
+// the steps of messages 1 and 2 (of the Commit chain, or of the accepts'
+// LogIndex chain), bits 15-31 d0. The receiver rebuilds a
 // mailbox of Replicates only or accepts only as a uniform one (shared when its
 // messages repeat message 0's hot fields, as MB_SHARED says: the readers take
 // the same messages either way), any other as a full one. A mailbox that fits
@@ -718,7 +721,7 @@ __host__ __device__ inline bool cx_classify(const Mailbox& mb, uint32_t cb, uint
   const bool uni = (cb & MB_UNIFORM) != 0;
   if (!n || n > 3 || n > depth || (!uni && (cb & ~(uint32_t)MB_COUNT))) return false;
   uint32_t codes = 0, term = uni ? mb.mterm() : 0u, nacc = 0, steps = 0, d0 = 0;
-  uint64_t a = 0, prevc = 0;
+  uint64_t a = 0, prevc = 0, prevl = 0;
   bool have_a = false, have_c = false, rep = false, acc = false, hbonly = true, ok = true;
   for (uint32_t k = 0; k < n && ok; ++k) {
     uint32_t tag, t;
@@ -755,10 +758,17 @@ __host__ __device__ inline bool cx_classify(const Mailbox& mb, uint32_t cb, uint
       rep = have_a = true;
       hbonly = false;
       carries = true;
-    } else if (code == CX_ACC) {
+    } else if (code == CX_ACC) {  // LogIndex steps of 0 or 1 (an ack per Replicate, raft.go:971-974)
       const uint64_t l = mb.log_index_at(k, cb);
-      ok = !rep && !have_c && (nacc ? l == a + nacc : true);
-      if (!nacc) a = l;
+      ok = !rep && !have_c;
+      if (nacc) {
+        const uint64_t st = l - prevl;
+        ok = ok && st <= 1u;
+        steps |= (uint32_t)(st & 1u) << (k - 1);
+      } else {
+        a = l;
+      }
+      prevl = l;
       acc = have_a = true;
       hbonly = false;
       nacc++;
@@ -782,9 +792,10 @@ __host__ __device__ inline bool cx_classify(const Mailbox& mb, uint32_t cb, uint
     codes |= code << (3 * k);
   }
   if (!ok) return false;
-  // the first Commit relative to the anchor
+  // the first Commit relative to the anchor (the steps are the Commit chain's
+  // when the mailbox carries Commits: accepts and Commits never mix)
   uint64_t first = 0;
-  {
+  if (have_c) {
     uint64_t c0 = prevc;  // walk back the steps to the first Commit
     for (uint32_t k = n; k-- > 1;) c0 -= (steps >> (k - 1)) & 1u;
     first = c0;
@@ -859,24 +870,31 @@ __host__ __device__ inline void cx_get_side(const Mailbox& mb, const uint8_t* e,
 // an empty context (heartbeats), an empty context (their acks).
 __host__ __device__ inline void cx_get_pattern(const Mailbox& mb, uint32_t w, uint32_t t, uint64_t a) {
   const uint32_t n = w & 3u;
-  uint32_t nrep = 0, nacc = 0, n1 = 0, allsame = 1;
+  uint32_t nrep = 0, nacc = 0, n1 = 0, allsame = 1, allone = 1;
   for (uint32_t k = 0; k < n; ++k) {
     const uint32_t code = (w >> (4 + 3 * k)) & 7u;
     nrep += code <= CX_R1;
     nacc += code == CX_ACC;
     n1 |= (uint32_t)(code == CX_R1 || code == CX_R1C) << k;
-    if (k) allsame &= ((w >> (kCxPatStepShift + k - 1)) & 1u) ^ 1u;
+    if (k) {
+      const uint32_t st = (w >> (kCxPatStepShift + k - 1)) & 1u;
+      allsame &= st ^ 1u;
+      allone &= st;
+    }
   }
   uint64_t commit = a + (uint64_t)(w >> kCxPatCdShift) - kCxPatCdBias;
   mb.mterm() = t;
   if (nrep == n || nacc == n) {  // uniform (gr_layout.h MB_UNIFORM)
     const bool resp = nacc == n;
-    const bool shared = n > 1 && (resp || allsame);
+    const bool shared = n > 1 && (resp ? allone : allsame);  // MB_SHARED: accepts at +1, Replicates repeated
     mb.cnt() = (uint8_t)(n | MB_UNIFORM | (resp ? MB_RESP : 0u) | (shared ? MB_SHARED : 0u) |
                          (resp ? 0u : n1 << MB_N1_SHIFT));
+    uint64_t li = a;
     for (uint32_t k = 0; k < (shared ? 1u : n); ++k) {
-      if (k) commit += (w >> (kCxPatStepShift + k - 1)) & 1u;
-      mb.u64(k, MF_LOG_INDEX) = a + (resp ? (uint64_t)k : 0ull);
+      const uint32_t st = k ? (w >> (kCxPatStepShift + k - 1)) & 1u : 0u;
+      if (resp) li += st;
+      else commit += st;
+      mb.u64(k, MF_LOG_INDEX) = li;
       if (!resp) {
         uint32_t cd = 0;
         commit_delta(commit, a, &cd);
@@ -886,10 +904,16 @@ __host__ __device__ inline void cx_get_pattern(const Mailbox& mb, uint32_t w, ui
     return;
   }
   mb.cnt() = (uint8_t)n;
-  uint32_t ai = 0;
+  uint64_t ali = a;  // the accepts' LogIndex chain
+  bool first_acc = true;
   for (uint32_t k = 0; k < n; ++k) {
     const uint32_t code = (w >> (4 + 3 * k)) & 7u;
-    if (k) commit += (w >> (kCxPatStepShift + k - 1)) & 1u;
+    const uint32_t st = k ? (w >> (kCxPatStepShift + k - 1)) & 1u : 0u;
+    if (nacc) {
+      if (code == CX_ACC && !first_acc) ali += st;
+    } else {
+      commit += st;
+    }
     mb.tag(k) = (uint16_t)cx_code_tag(code);
     mb.t32(k, MT_TERM) = t;
     if (code <= CX_R1) {
@@ -902,7 +926,8 @@ __host__ __device__ inline void cx_get_pattern(const Mailbox& mb, uint32_t w, ui
       mb.t32(k, MT_LOG_TERM) = t;
       mb.t32(k, MT_RT0) = ne ? t : 0u;
     } else if (code == CX_ACC) {
-      mb.u64(k, MF_LOG_INDEX) = a + ai++;
+      mb.u64(k, MF_LOG_INDEX) = ali;
+      first_acc = false;
     } else if (code == CX_HB) {
       mb.u64(k, MF_COMMIT) = commit;
       mb.u64(k, MF_HINT) = 0;
@@ -1083,19 +1108,61 @@ __global__ __launch_bounds__(kIoBlock) void cx_pack(SpaceView v, uint8_t* cx, Cx
   }
 }
 // Unpack, part 1: every position's count byte and its record's hot fields.
-__global__ void cx_unpack_waves(SpaceView v, const uint8_t* cx, CxCaps C) {
-  const uint32_t nwv = v.pc / 64;
-  const uint64_t nw = (uint64_t)v.n_chunks * nwv;
+// Each wave takes kCxUnpackPer consecutive wave groups of chunk blockIdx.y and
+// issues their header loads, then all their record loads, as one batch each
+// (round 5: one group per wave, two dependent round trips per group).
+constexpr uint32_t kCxUnpackPer = 8, kCxUnpackGroups = kCxUnpackPer * (kIoBlock / 64);
+__global__ __launch_bounds__(kIoBlock) void cx_unpack_waves(SpaceView v, const uint8_t* cx, CxCaps C) {
+  const uint32_t c = blockIdx.y, nwv = v.pc / 64;
   const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t w = (uint64_t)blockIdx.x * (kIoBlock / 64) + (threadIdx.x >> 6); w < nw;
-       w += (uint64_t)gridDim.x * (kIoBlock / 64)) {
-    const uint32_t c = (uint32_t)(w / nwv), wl = (uint32_t)(w % nwv);
-    const CxLayout L = cx_layout(v.pc, v.depth, C.cap[c], C.scap);
-    const uint8_t* buf = cx + C.off[c];
-    const uint8_t* h = buf + L.waves + (uint64_t)wl * kCxWave;
-    const uint64_t mask = reinterpret_cast<const uint64_t*>(h)[0], lost = reinterpret_cast<const uint64_t*>(h)[1];
-    const uint32_t base = reinterpret_cast<const uint32_t*>(h)[4], hi = reinterpret_cast<const uint32_t*>(h)[5];
-    cx_get_lane(v.at(c * v.pc + wl * 64 + lane), buf, L, mask, lost, base, hi, lane);
+  const uint32_t g0 = blockIdx.x * kCxUnpackGroups + (threadIdx.x >> 6) * kCxUnpackPer;
+  if (g0 >= nwv) return;  // wave-uniform; no barrier below
+  const uint32_t cap = C.cap[c];
+  const CxLayout L = cx_layout(v.pc, v.depth, cap, C.scap);
+  const uint8_t* buf = cx + C.off[c];
+  uint64_t mask[kCxUnpackPer], lost[kCxUnpackPer];
+  uint32_t base[kCxUnpackPer], hi[kCxUnpackPer];
+#pragma unroll
+  for (uint32_t q = 0; q < kCxUnpackPer; ++q) {
+    const uint8_t* h = buf + L.waves + (uint64_t)(g0 + q < nwv ? g0 + q : g0) * kCxWave;
+    mask[q] = g0 + q < nwv ? reinterpret_cast<const uint64_t*>(h)[0] : 0ull;
+    lost[q] = g0 + q < nwv ? reinterpret_cast<const uint64_t*>(h)[1] : 0ull;
+    base[q] = reinterpret_cast<const uint32_t*>(h)[4];
+    hi[q] = reinterpret_cast<const uint32_t*>(h)[5];
+  }
+  const uint64_t below = (1ull << lane) - 1;
+  uint32_t tw[kCxUnpackPer], lo[kCxUnpackPer], w[kCxUnpackPer];
+#pragma unroll
+  for (uint32_t q = 0; q < kCxUnpackPer; ++q) {  // the records (index 0's when the lane has none)
+    const bool has = cap && ((mask[q] >> lane) & 1ull);
+    const uint32_t r = has ? base[q] + (uint32_t)__builtin_popcountll(mask[q] & below) : 0u;
+    tw[q] = cap ? reinterpret_cast<const uint32_t*>(buf + L.term)[r] : 0u;
+    lo[q] = cap ? reinterpret_cast<const uint32_t*>(buf + L.lo)[r] : 0u;
+    w[q] = cap ? reinterpret_cast<const uint32_t*>(buf + L.cb)[r] : 0u;
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < kCxUnpackPer; ++q) {
+    tw[q] = keep_value(tw[q]);
+    lo[q] = keep_value(lo[q]);
+    w[q] = keep_value(w[q]);
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < kCxUnpackPer; ++q) {
+    if (g0 + q >= nwv) break;  // wave-uniform
+    const Mailbox mb = v.at(c * v.pc + (g0 + q) * 64 + lane);
+    if ((mask[q] >> lane) & 1ull) {
+      const uint64_t a = ((uint64_t)hi[q] << 32) | lo[q];
+      if (!(w[q] & MB_UNIFORM)) {
+        cx_get_pattern(mb, w[q], tw[q], a);
+      } else {
+        mb.cnt() = (uint8_t)w[q];
+        mb.mterm() = tw[q];
+        if (!(w[q] & MB_RESP)) mb.t32(0, MT_CDELTA) = (w[q] >> 8) - 0x800000u + 0x80000000u;
+        mb.u64(0, MF_LOG_INDEX) = a;
+      }
+    } else {
+      mb.cnt() = ((lost[q] >> lane) & 1ull) ? (uint8_t)(1u | MB_COLD_LOST) : (uint8_t)0;
+    }
   }
 }
 // Unpack, part 2 (after part 1): the side entries.

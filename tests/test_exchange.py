@@ -615,7 +615,7 @@ def _tick_space(n_chunks, positions, seed=5):
         return m
     for c in range(n_chunks):
         for q in range(positions):
-            kind = int(rng.integers(0, 13))
+            kind = int(rng.integers(0, 14))
             T = 5 + (q % 3)
             L = 2**32 + 1000 * q + 7
             C = L - 2
@@ -648,6 +648,10 @@ def _tick_space(n_chunks, positions, seed=5):
                 lst, rec = [rep(0), rep(1, C + 2)], False
             elif kind == 12:  # two accepts, unshared
                 lst, rec = [mk(type=abi.REPLICATE_RESP, term=T, log_index=L),
+                            mk(type=abi.REPLICATE_RESP, term=T, log_index=L + 1)], True
+            elif kind == 13:  # the acks of the staggered commit advances' Replicates
+                lst, rec = [mk(type=abi.REPLICATE_RESP, term=T, log_index=L),
+                            mk(type=abi.REPLICATE_RESP, term=T, log_index=L),
                             mk(type=abi.REPLICATE_RESP, term=T, log_index=L + 1)], True
             else:
                 continue
