@@ -631,8 +631,7 @@ def main():
                          "reference_width_note": "two Replicates + two acks per follower per round at "
                                                  "reference field widths (1,128 B/group): never used as frac",
                          "general_kernel_ms": gavg,
-                         "bailed_lanes_per_pass": tm["bailed_lanes"] / passes,
-                         "churn_lanes_per_pass": tm.get("churn_lanes", 0) / passes},
+                         "bailed_lanes_per_pass": tm["bailed_lanes"] / passes},
         }
         if args.host_path == "on" and world == 1:
             try:

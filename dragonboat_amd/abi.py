@@ -150,7 +150,7 @@ class Stats(ctypes.Structure):
 
 class Timing(ctypes.Structure):
     _fields_ = [("passes", ctypes.c_uint64), ("fast_ms", ctypes.c_double), ("general_ms", ctypes.c_double),
-                ("bailed_lanes", ctypes.c_uint64), ("churn_lanes", ctypes.c_uint64)]
+                ("bailed_lanes", ctypes.c_uint64)]
 
 
 # settings.Soft.MaxEntrySize (internal/settings/soft.go:236)

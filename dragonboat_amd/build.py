@@ -18,7 +18,7 @@ CSRC = os.path.join(ROOT, "dragonboat_amd", "csrc")
 ENGINE_SRC = [os.path.join(CSRC, "gr_engine.hip")] + [os.path.join(CSRC, f"gr_kernels_s{s}.hip") for s in (1, 3, 5, 8)]
 ENGINE_DEPS = ENGINE_SRC + [os.path.join(CSRC, f)
                             for f in ("gr_lane.h", "gr_layout.h", "gr_host.h", "gr_fast.h", "gr_steady.h", "gr_tick.h", "gr_io.h",
-                                      "gr_cover.h", "gr_kernels.h", "gr_scan.h", "gr_churn.h")] + \
+                                      "gr_cover.h", "gr_kernels.h", "gr_scan.h")] + \
     [os.path.join(ROOT, "include", "gpuraft.h")]
 JOBS = max(1, min(8, os.cpu_count() or 1))
 ENGINE_LIB = os.path.join(ROOT, "dragonboat_amd", "_build", "libgpuraft.so")

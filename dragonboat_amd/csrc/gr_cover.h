@@ -37,7 +37,7 @@ namespace gr {
   X(PROP_APPEND) X(PROP_DROP_SELF_REMOVED) X(PROP_DROP_TRANSFER) X(PROP_FORWARD)                \
   X(PROP_DROP_NO_LEADER) X(PROP_CANDIDATE)                                                      \
   X(FAST_LEADER) X(FAST_FOLLOWER) X(FAST_QUIESCED) X(TICKLANE_LEADER) X(TICKLANE_FOLLOWER)     \
-  X(STEADY_LEADER) X(STEADY_FOLLOWER) X(QUIET_STEP) X(CHURN_ADOPT) X(CHURN_FOLLOWER)                                             \
+  X(STEADY_LEADER) X(STEADY_FOLLOWER) X(QUIET_STEP)                                              \
   X(GENERAL_LANE)                                                                               \
   X(ESC_TERM_WINDOW) X(ESC_RANDOM) X(ESC_UNSUPPORTED) X(ESC_ELECTION) X(ESC_PANIC)              \
   X(ESC_CAPACITY) X(ESC_SNAPSHOT) X(ESC_ENTRY_SIZE) X(ESC_MSG_RUNS) X(ESC_NONMEMBER)            \

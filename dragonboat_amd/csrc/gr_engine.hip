@@ -86,7 +86,6 @@ struct gr_engine {
   uint64_t hint_flip = 0;
   uint64_t launches = 0;         // never reset: selects the live counter set
   uint64_t timing_bailed0 = 0;   // ST_BAILED when timing began
-  uint64_t timing_churn0 = 0;      // ST_CHURN when timing began
   bool timing = false;
   std::vector<PassTiming> timings;  // one per pass while timing
   bool routes_bound = false;
@@ -1546,8 +1545,6 @@ int gr_timing_begin(gr_engine* e) {
   e->timings.reserve(1 << 16);  // records are referenced by pointer until the pass is enqueued
   int r = stat_total(e, ST_BAILED, &e->timing_bailed0);
   if (r) return r;
-  r = stat_total(e, ST_CHURN, &e->timing_churn0);
-  if (r) return r;
   e->timing = true;
   return GR_OK;
 }
@@ -1568,10 +1565,6 @@ int gr_timing_end(gr_engine* e, gr_timing* out) {
   const int r = stat_total(e, ST_BAILED, &bailed);
   if (r) return r;
   out->bailed_lanes = bailed - e->timing_bailed0;  // lanes that left the lean kernels while timing
-  uint64_t churn = 0;
-  const int r2 = stat_total(e, ST_CHURN, &churn);
-  if (r2) return r2;
-  out->churn_lanes = churn - e->timing_churn0;  // ... of which the churn lane finished
   free_timings(e);
   e->timing = false;
   return GR_OK;

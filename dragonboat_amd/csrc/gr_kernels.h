@@ -16,7 +16,6 @@
 #include "gr_fast.h"
 #include "gr_steady.h"
 #include "gr_lane.h"
-#include "gr_churn.h"
 #include "gr_tick.h"
 
 namespace gr {
@@ -36,18 +35,18 @@ __device__ inline __attribute__((always_inline)) uint32_t wave_sum(uint32_t v) {
 // barrier, so a wave never waits for the rest of its workgroup to finish.
 __device__ inline __attribute__((always_inline)) void block_stats(const StepParams& kp, const LaneStats& ls,
                                                                   uint32_t bid = blockIdx.x) {
-  constexpr int N = 10;
+  constexpr int N = 9;
   // one named field at a time: a register array indexed in a loop was put in scratch
   const uint32_t f0 = wave_sum(ls.leader_commit), f1 = wave_sum(ls.follower_commit),
                  f2 = wave_sum(ls.escalated), f3 = wave_sum(ls.msgs_in), f4 = wave_sum(ls.msgs_out),
                  f5 = wave_sum(ls.leader_in), f6 = wave_sum(ls.leader_out), f7 = wave_sum(ls.entries),
-                 f8 = wave_sum(ls.bailed), f9 = wave_sum(ls.churn);
+                 f8 = wave_sum(ls.bailed);
   const uint32_t k = threadIdx.x & 63;
   if (k < (uint32_t)N) {
     constexpr uint32_t field[N] = {ST_LEADER_COMMITS, ST_FOLLOWER_COMMITS, ST_ESCALATIONS, ST_MSGS_IN, ST_MSGS_OUT,
-                                   ST_LEADER_MSGS_IN, ST_LEADER_MSGS_OUT, ST_REPLICATE_ENTRIES, ST_BAILED, ST_CHURN};
+                                   ST_LEADER_MSGS_IN, ST_LEADER_MSGS_OUT, ST_REPLICATE_ENTRIES, ST_BAILED};
     const uint32_t v = k == 0 ? f0 : k == 1 ? f1 : k == 2 ? f2 : k == 3 ? f3 : k == 4 ? f4 : k == 5 ? f5
-                     : k == 6 ? f6 : k == 7 ? f7 : k == 8 ? f8 : f9;
+                     : k == 6 ? f6 : k == 7 ? f7 : f8;
     uint32_t f = 0;
 #pragma unroll
     for (uint32_t x = 0; x < (uint32_t)N; ++x) f = k == x ? field[x] : f;
@@ -88,13 +87,8 @@ constexpr uint32_t kTickLists = 64;
 // GR_WAVE_CLOCK records per region (the general grid's waves at most; the tick
 // kernel's one-wave workgroups in the second region)
 constexpr uint32_t kGeneralWaveSlots = 4096;
-// The churn kernel's leftovers (round 5): lanes of general list l the churn lane
-// (gr_churn.h) hands back go to churn list l / 2 (their handler class), after
-// the tick lists.
-constexpr uint32_t kChurnLists = 16;
 constexpr uint32_t kBailLists = 40, kGeneralLists = 32, kRetryList0 = 32,
-                   kTickCounter0 = kBailLists, kChurnCounter0 = kBailLists + kTickLists,
-                   kCounters = kBailLists + kTickLists + kChurnLists,
+                   kTickCounter0 = kBailLists, kCounters = kBailLists + kTickLists,
                    kCounterStride = 64;  // counters 256 B apart
 constexpr uint32_t WF_LISTED = 0x80;     // wave flag: the role instances step this wave's masked lanes
 // Word 1 of counter 0's 256-B slot: nonzero when a split pass's steady kernel
@@ -108,13 +102,10 @@ constexpr uint32_t kListedWord = 1;
 // holds puts the extra chunks on the waves that finish first). Cleared with the
 // next pass's counters.
 constexpr uint32_t kGeneralNext = 2;
-// Word 3: the churn kernel's next 64-lane chunk (as kGeneralNext).
-constexpr uint32_t kChurnNext = 3;
-// Tail kernel modes (TailPlan): the general kernel walks the churn leftover lists
-// instead of the general lists (the churn kernel ran); GM_RETRY: the retry lists
-// (32..39) hold lanes no role instance stepped (the steady kernel's no_roles
-// mode), so the churn and general kernels walk lists 0..39, not 0..31.
-constexpr uint32_t GM_CHURN_LISTS = 1, GM_RETRY = 2;
+// Tail kernel mode (TailPlan): GM_RETRY: the retry lists (32..39) hold lanes no
+// role instance stepped (the steady kernel's no_roles mode), so the general
+// kernel walks lists 0..39, not 0..31.
+constexpr uint32_t GM_RETRY = 2;
 __host__ __device__ inline uint64_t wave_flag_words(uint32_t cap) { return ((uint64_t)cap / 64 + 64) / 4 * 2; }
 // Lanes one tick list can receive: the lanes of every kTickLists-th block, from
 // the steady kernel and the listed role waves (keyed by lane), plus as many
@@ -127,11 +118,9 @@ __host__ __device__ inline uint64_t tick_cap(uint32_t cap) {
 __host__ __device__ inline uint64_t tick_off(uint32_t cap) {
   return (uint64_t)kBailLists * cap + wave_flag_words(cap) + 2 * ((uint64_t)cap / 64 + 1);
 }
-__host__ __device__ inline uint64_t churn_off(uint32_t cap) { return tick_off(cap) + kTickLists * tick_cap(cap); }
 // u32 words of the list storage: kBailLists lane lists of cap, the wave flags,
-// the wave masks (u64), the kTickLists tick lists of tick_cap, the kChurnLists
-// churn leftover lists of cap
-__host__ __device__ inline uint64_t bail_words(uint32_t cap) { return churn_off(cap) + (uint64_t)kChurnLists * cap; }
+// the wave masks (u64), the kTickLists tick lists of tick_cap
+__host__ __device__ inline uint64_t bail_words(uint32_t cap) { return tick_off(cap) + kTickLists * tick_cap(cap); }
 __host__ __device__ inline uint8_t* wave_flags(uint32_t* bail_list, uint32_t cap) {
   return (uint8_t*)(bail_list + (uint64_t)kBailLists * cap);
 }
@@ -519,7 +508,7 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
     }
     if (kp.no_roles) {
       // no role instances follow (TailPlan): the rest go straight to the retry
-      // lists, which the churn and general kernels then walk with their own lists
+      // lists, which the general kernel then walks with its own
       bail_append(q == QS_OTHER, kRetryList0 + blockIdx.x % 8, bail_list, counters, list_cap, i);
       if ((threadIdx.x & 63) == 0) {
         wave_flags(bail_list, list_cap)[wave] = 0;
@@ -723,67 +712,6 @@ __device__ inline __attribute__((always_inline)) void stats_add(LaneStats& acc, 
   acc.entries += ls.entries;
 }
 
-// One wave's appends to the churn leftover list of each lane's class `key`
-// (< kChurnLists): one returning atomic per class present, as general_append.
-__device__ inline __attribute__((always_inline)) void churn_append(bool mine, uint32_t key, uint32_t i, uint32_t* bail_list,
-                                                                 uint32_t* counters, uint32_t list_cap) {
-  const uint64_t bm = __ballot(mine);
-  if (!bm) return;
-  uint64_t same = 0;
-  for (uint64_t rest = bm; rest;) {  // wave-uniform
-    const uint32_t k = (uint32_t)__shfl((int)key, __ffsll((unsigned long long)rest) - 1);
-    const uint64_t m = __ballot(mine && key == k);
-    if (mine && key == k) same = m;
-    rest &= ~m;
-  }
-  const uint32_t lane = threadIdx.x & 63;
-  const int first = mine ? __ffsll((unsigned long long)same) - 1 : (int)lane;
-  uint32_t base = 0;
-  if (mine && (uint32_t)first == lane)
-    base = atomicAdd(counters + (kChurnCounter0 + key) * kCounterStride, (uint32_t)__popcll(same));
-  base = (uint32_t)__shfl((int)base, first);
-  if (mine)
-    bail_list[churn_off(list_cap) + (uint64_t)key * list_cap + base + (uint32_t)__popcll(same & ((1ull << lane) - 1))] = i;
-}
-
-// Pass 2a': the churn lane (gr_churn.h: the general lane's follower path, term
-// adoption and step-down included) over the general lists, in a kernel of its
-// own so its register file is its own (216 VGPRs, two waves per SIMD; the full
-// lane holds 256 VGPRs + 256 AGPRs and spills: one wave per SIMD). A lane it
-// finishes is done; one it hands back (nothing stored) goes to churn list l / 2.
-// Launched when the tail hint says the general kernel had work lately
-// (TailPlan): the general kernel then walks the churn lists instead.
-#ifndef GR_CHURN_MIN_WAVES
-#define GR_CHURN_MIN_WAVES 1
-#endif
-template <int S>
-__global__ __launch_bounds__(kBlock, GR_CHURN_MIN_WAVES) void gr_churn_kernel(StepParams kp, uint32_t* bail_list,
-                                                                           uint32_t* counters, uint32_t list_cap,
-                                                                           uint32_t mode) {
-  ListRange<kBailLists> r;
-  r.init(counters, 0, bail_list, list_cap, (mode & GM_RETRY) ? kBailLists : kGeneralLists);
-  if (blockIdx.x * kBlock >= r.total()) return;  // no stats row touched
-  LaneStats acc;
-  walk_chunks(r, counters, kChurnNext, [&](uint32_t i, uint32_t l, bool valid) {
-    bool back = false;
-    if (valid) {
-      const uint32_t p = kp.has_lane_peer ? kp.ln.u32(LR_LANE_PEER)[i] : i;
-      LaneStats ls;
-      if (churn_step<S>(kp, i, p, &ls)) {
-        GR_CHECK_STATE(kp.st, p);
-        stats_add(acc, ls);
-        acc.bailed += 1;
-        acc.churn += 1;
-      } else {
-        back = true;
-      }
-    }
-    // a retry lane (no role instance ran) joins the last class
-    churn_append(back, l < kGeneralLists ? l >> 1 : kChurnLists - 1, i, bail_list, counters, list_cap);
-  });
-  if (kp.stats) block_stats(kp, acc);
-}
-
 // Pass 2b: the general lane (every handler, escalation with prefix re-run)
 // over the handed-over lanes, in 64-lane chunks of the concatenated lists; also
 // clears the counters the next pass's kernels will use.
@@ -795,12 +723,10 @@ __global__ __launch_bounds__(kBlock, GR_GENERAL_MIN_WAVES) void gr_step_kernel(S
                                                          uint32_t* counters, uint32_t* next_counters,
                                                          uint32_t list_cap, uint32_t mode) {
   ListRange<kBailLists> rl;
-  if (mode & GM_CHURN_LISTS) rl.init(counters, kChurnCounter0, bail_list + churn_off(list_cap), list_cap, kChurnLists);
-  else rl.init(counters, 0, bail_list, list_cap, (mode & GM_RETRY) ? kBailLists : kGeneralLists);
+  rl.init(counters, 0, bail_list, list_cap, (mode & GM_RETRY) ? kBailLists : kGeneralLists);
   if (blockIdx.x == 0 && threadIdx.x < kCounters) next_counters[threadIdx.x * kCounterStride] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters) next_counters[kListedWord] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters + 1) next_counters[kGeneralNext] = 0;
-  if (blockIdx.x == 0 && threadIdx.x == kCounters + 2) next_counters[kChurnNext] = 0;
   LaneStats acc;
   // the general lane's message prefetch (gr_lane.h Lane::prefetch): one region
   // per wave (S <= 3: 30 KB; 120 KB for the workgroup's four waves)
@@ -890,7 +816,6 @@ __global__ __launch_bounds__(kBlock, 1) void gr_small_kernel(StepParams kp, uint
   if (blockIdx.x == 0 && threadIdx.x < kCounters) next_counters[threadIdx.x * kCounterStride] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters) next_counters[kListedWord] = 0;
   if (blockIdx.x == 0 && threadIdx.x == kCounters + 1) next_counters[kGeneralNext] = 0;
-  if (blockIdx.x == 0 && threadIdx.x == kCounters + 2) next_counters[kChurnNext] = 0;
   const uint32_t hw = kp.hints ? sload_u32(kp.hints + (uint64_t)blockIdx.x * (kBlock / 64)) : 0u;
   const uint32_t hint = (hw >> (8 * (wave & 3))) & 0xFFu;
   const int wk = wave_kernel(hint, S);
@@ -935,8 +860,7 @@ struct PassTiming {
 // The tail plan: which optional launches a pass makes after its lean kernels.
 // Every tail launch but the general kernel's is optional for correctness: the
 // general lane handles any lane (the lanes no role instance steps reach it
-// through the retry lists, GM_RETRY; every hand-over when the churn kernel does
-// not run). So the host decides from the last pass the device has reported
+// through the retry lists, GM_RETRY). So the host decides from the last pass the device has reported
 // (StepParams::tail_hint, written by the steady kernel of each split pass from
 // the previous pass's counts into host-visible memory, read here without
 // synchronising: one or more passes back). In the steady state nothing is
@@ -944,41 +868,31 @@ struct PassTiming {
 // with nothing to do costs its workgroups' dispatch (round-5 A/B, 1M x 3: steady
 // kernel alone 0.0622 ms per pass, with the round-4 tail of role instances +
 // general kernel 0.0671).
-// The churn kernel (gr_churn.h) runs only when forced (GR_TAIL_MODE=1): as a
-// launch of its own it measured slower on config 5 (296 vs 246 us per pass, one
-// A/B call, round 5): it took 25.7k of the 53.5k hand-overs, but the general
-// kernel's span is its slowest wave's chain of dependent scattered loads, which
-// half the lanes did not shorten. Inlined into the role instances instead (the
-// lanes FastLane hands over, in the same wave) it raised their kernel to 255
-// VGPRs, one wave per SIMD: config 5 400 us per pass (role instances 109 -> 281).
+// An empty general launch costs 4.6-5.2 us whatever its grid (1, 16 or 256
+// workgroups: GR_GENERAL_BLOCKS, round-6 traces, profiles/r06_tail): the cost is
+// the launch, not its waves.
+// Round 5 also built a churn lane (the general lane's follower path: term
+// adoption and step-down without the remote rows) as a kernel of its own before
+// the general kernel: it took half the hand-overs of config 5 but the pass got
+// slower (296 vs 246 us, the general kernel's span is its slowest waves'), and
+// inlined into the role instances it cost them their occupancy (400 us). Round
+// 6 removed it.
 constexpr uint32_t kTailAll = 0xFFFFFFFFu;  // no report yet: every launch
 inline uint32_t tail_word(const StepParams& kp) {
   return kp.tail_hint ? __atomic_load_n(kp.tail_hint, __ATOMIC_RELAXED) : kTailAll;
 }
 struct TailPlan {
-  bool roles, churn;
+  bool roles;
 };
 inline TailPlan tail_plan(const StepParams& kp) {
   const uint32_t th = tail_word(kp);
   switch (kp.tail_mode) {
-    case 1: return {true, true};
-    case 2: return {false, false};
-    case 3: return {true, false};
-    default: return {(th & 1u) != 0, false};
+    case 1:
+    case 3: return {true};
+    case 2: return {false};
+    default: return {(th & 1u) != 0};
   }
 }
-// The churn kernel's grid: resident capacity at two waves per SIMD (GR_CHURN_BLOCKS
-// overrides it, A/B runs).
-constexpr uint32_t kChurnBlocks = 512;
-inline uint32_t churn_blocks() {
-  static const uint32_t v = [] {
-    const char* e = getenv("GR_CHURN_BLOCKS");
-    const long x = e ? strtol(e, nullptr, 10) : 0;
-    return x > 0 ? (uint32_t)x : kChurnBlocks;
-  }();
-  return v;
-}
-
 // The tick kernel's grid: its lanes are at most the active share of a pass
 // (kTickBlocks x 256 lanes in flight, in workgroups of tick_wg() lanes).
 constexpr uint32_t kTickBlocks = 1024;
@@ -1120,7 +1034,7 @@ hipError_t launch(const StepParams& kp_in, uint32_t* bail_list, uint32_t* counte
     err = launch_fast<S, RT_AFFINE>(kq, blocks, bail_list, cur, nxt, list_cap, s, skip, plan.roles, &retry_left);
   else
     err = launch_fast<S, RM_ANY>(kq, blocks, bail_list, cur, nxt, list_cap, s, skip, plan.roles, &retry_left);
-  const uint32_t mode = (plan.churn ? GM_CHURN_LISTS : 0u) | (retry_left ? GM_RETRY : 0u);
+  const uint32_t mode = retry_left ? GM_RETRY : 0u;
   if (err != hipSuccess) return err;
   if (t && (err = hipEventRecord(t->ev[1], s)) != hipSuccess) return err;
   if (skip) return t ? hipEventRecord(t->ev[2], s) : hipSuccess;
@@ -1135,11 +1049,6 @@ hipError_t launch(const StepParams& kp_in, uint32_t* bail_list, uint32_t* counte
       hipLaunchKernelGGL((gr_tick_kernel<S, RT_AFFINE>), dim3(tblocks), dim3(tw), 0, s, kp, bail_list, cur, list_cap);
     else
       hipLaunchKernelGGL((gr_tick_kernel<S, RM_ANY>), dim3(tblocks), dim3(tw), 0, s, kp, bail_list, cur, list_cap);
-    if ((err = hipGetLastError()) != hipSuccess) return err;
-  }
-  if (plan.churn) {  // the churn lane first; the general kernel then walks its leftovers
-    const uint32_t cblocks = blocks < churn_blocks() ? blocks : churn_blocks();
-    hipLaunchKernelGGL(gr_churn_kernel<S>, dim3(cblocks), dim3(kBlock), 0, s, kp, bail_list, cur, list_cap, mode);
     if ((err = hipGetLastError()) != hipSuccess) return err;
   }
   uint32_t gblocks = blocks < general_blocks() ? blocks : general_blocks();

@@ -507,7 +507,7 @@ struct SpaceView {
 enum StatField : uint32_t {
   ST_PASSES = 0, ST_LEADER_COMMITS = 1, ST_FOLLOWER_COMMITS = 2, ST_ESCALATIONS = 3,
   ST_MSGS_IN = 4, ST_MSGS_OUT = 5, ST_LEADER_MSGS_IN = 6, ST_LEADER_MSGS_OUT = 7,
-  ST_REPLICATE_ENTRIES = 8, ST_BAILED = 9, ST_CHURN = 10, NSTAT = 16
+  ST_REPLICATE_ENTRIES = 8, ST_BAILED = 9, NSTAT = 16
 };
 // Per-lane counters of one pass (reduced per workgroup into the stats rows).
 // "leader" = the lane ended the pass as leader; entries = sum of n over the
@@ -515,8 +515,7 @@ enum StatField : uint32_t {
 struct LaneStats {
   uint32_t leader_commit = 0, follower_commit = 0, escalated = 0;
   uint32_t msgs_in = 0, msgs_out = 0, leader_in = 0, leader_out = 0, entries = 0;
-  uint32_t bailed = 0;  // left the lean kernels (stepped by the tick, churn or general lane)
-  uint32_t churn = 0;   // ... and finished by the churn lane (gr_churn.h)
+  uint32_t bailed = 0;  // left the lean kernels (stepped by the tick or general lane)
 };
 
 // Route modes: where lane i reads (dir 0) / writes (dir 1) the mailbox of
@@ -585,9 +584,9 @@ struct StepParams {
   // host reads, unsynchronised, to size the next launches' grids; nullptr: off
   uint32_t* tail_hint;
   // which tail launches a pass makes (gr_kernels.h TailPlan): 0 = from the
-  // tail hint; 1 = role instances and the churn kernel always; 2 = neither (the
-  // general kernel steps the listed waves and every hand-over); 3 = role
-  // instances always, no churn kernel (round 4's schedule). GR_TAIL_MODE at gr_create.
+  // tail hint; 1 or 3 = the role instances always (round 4's schedule); 2 =
+  // never (the general kernel steps the listed waves and every hand-over).
+  // GR_TAIL_MODE at gr_create.
   uint8_t tail_mode;
   // set by the launcher for the steady kernel of a pass whose role instances do
   // not run: its non-steady lanes go to the retry lists (gr_kernels.h GM_RETRY)

@@ -490,7 +490,7 @@ class Pipeline:
             eng.timing_begin()
 
     def timing_end(self):
-        tot = {"passes": 0, "fast_ms": 0.0, "general_ms": 0.0, "bailed_lanes": 0, "churn_lanes": 0}
+        tot = {"passes": 0, "fast_ms": 0.0, "general_ms": 0.0, "bailed_lanes": 0}
         for eng in self.engines:
             for f, v in eng.timing_end().items():
                 tot[f] += v

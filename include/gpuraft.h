@@ -444,17 +444,14 @@ int gr_stats_reset(gr_engine* e);
  * Per-kernel timing (benchmarks/profiling; not in the reference). Between
  * gr_timing_begin and gr_timing_end every pass records HIP events around its
  * kernels on the pass's stream: fast_ms brackets the lean kernels over all
- * lanes (steady kernel, role instances), general_ms the tail (tick, churn and
- * general kernels) over the lanes the lean kernels handed over ("bailed");
- * churn_lanes of those were finished by the churn lane (round 5: a leader
- * change's follower side), the rest by the tick lane or the general lane.
+ * lanes (steady kernel, role instances), general_ms the tail (tick and general
+ * kernels) over the lanes the lean kernels handed over ("bailed").
  */
 typedef struct gr_timing {
   uint64_t passes;
   double fast_ms;         /* summed over passes */
   double general_ms;
   uint64_t bailed_lanes;  /* summed over passes */
-  uint64_t churn_lanes;   /* summed over passes */
 } gr_timing;
 int gr_timing_begin(gr_engine* e);
 int gr_timing_end(gr_engine* e, gr_timing* out);

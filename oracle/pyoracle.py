@@ -64,7 +64,6 @@ def hostlane_lib():
         lib.hl_tick_lanes.restype = c.c_uint64
         lib.hl_steady_lanes.restype = c.c_uint64
         lib.hl_steady_leaders.restype = c.c_uint64
-        lib.hl_churn_lanes.restype = c.c_uint64
         lib.hl_detect_affine.argtypes = [c.c_void_p, c.c_void_p, c.c_uint32, c.c_uint32, c.c_void_p,
                                          c.POINTER(c.c_uint32)]
         lib.hl_detect_affine.restype = c.c_int
@@ -212,10 +211,6 @@ def hostlane_tick_lanes():
     """Lanes the heartbeat/ReadIndex/tick lane (gr_tick.h) finished since load."""
     return int(hostlane_lib().hl_tick_lanes())
 
-
-def hostlane_churn_lanes():
-    """lanes the churn lane (gr_churn.h) finished (of the handed-over ones)"""
-    return int(hostlane_lib().hl_churn_lanes())
 
 
 def hostlane_steady_lanes():

@@ -194,7 +194,7 @@ def quiesced(backend, G=256, passes=6, seed=13):
 def device_battery(lib_path):
     """The device-resident split schedule (devsim.DeviceLockstep, split forced on
     a small population): the steady kernel's closed-form leader and follower
-    lanes and quiet_step, the role instances, staggered acks, churn; oracle
+    lanes and quiet_step, the role instances, staggered acks, leader changes; oracle
     every pass. Returns the stats of each run."""
     import os
     import devsim
@@ -202,7 +202,7 @@ def device_battery(lib_path):
     saved = {k: os.environ.get(k) for k in ("GR_SPLIT_MIN_LANES", "GR_SMALL_BLOCKS", "GR_TAIL_MODE")}
     os.environ["GR_SPLIT_MIN_LANES"] = "1"  # all three read at gr_create
     os.environ["GR_SMALL_BLOCKS"] = "0"     # not the fused small-pass kernel
-    os.environ["GR_TAIL_MODE"] = "1"        # the role instances and the churn kernel (gr_churn.h) every pass
+    os.environ["GR_TAIL_MODE"] = "1"        # the role instances every pass
     try:
         G, R = 1024, 3
         topo = P.Topology(G, R)

@@ -14,7 +14,6 @@
 #include "gr_steady.h"
 #include "gr_host.h"
 #include "gr_lane.h"
-#include "gr_churn.h"
 #include "gr_tick.h"
 
 #ifdef GR_BAIL_TRACE
@@ -40,8 +39,7 @@ using namespace gr::host;
 
 namespace {
 
-static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0, g_tick_lanes = 0, g_steady_lanes = 0, g_steady_leaders = 0,
-                g_churn_lanes = 0;
+static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0, g_tick_lanes = 0, g_steady_lanes = 0, g_steady_leaders = 0;
 static uint32_t g_hint_salt = 0;  // varies the drawn wave hints from call to call
 static bool g_true_hints = false;  // hl_true_hints: every wave gets the device's hint (diagnostics)
 
@@ -167,17 +165,6 @@ void run_lanes(const StepParams& kp) {
       GR_CHECK_STATE(kp.st, p);
       g_tick_lanes++;
       continue;
-    }
-    // the churn lane (gr_kernels.h gr_churn_kernel) first on three passes in
-    // four, as the device does when the tail hint says the general lists had
-    // work; a lane it hands back stored nothing and the general lane steps it
-    if ((g_hint_salt >> 5) & 3u) {
-      ls = LaneStats{};
-      if (churn_step<S>(kp, i, p, &ls)) {
-        GR_CHECK_STATE(kp.st, p);
-        g_churn_lanes++;
-        continue;
-      }
     }
     ls = LaneStats{};
     Lane<S> L(kp, i, p);
@@ -321,8 +308,6 @@ extern "C" void hl_counters(uint64_t* fast, uint64_t* bailed) {
 // lanes the heartbeat/ReadIndex/tick lane finished (of the bailed ones)
 extern "C" uint64_t hl_tick_lanes() { return g_tick_lanes; }
 
-// lanes the churn lane finished (of the bailed ones)
-extern "C" uint64_t hl_churn_lanes() { return g_churn_lanes; }
 
 // lanes the split pass's steady kernel emulation finished (gr_steady.h)
 extern "C" uint64_t hl_steady_lanes() { return g_steady_lanes; }

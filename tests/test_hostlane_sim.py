@@ -36,18 +36,16 @@ def test_steady_state_commit(built):
 
 
 def test_leader_change_churn(built):
-    """BASELINE config 5 shape: rejects, decreaseTo, conflict truncation. The
-    churn lane (gr_churn.h) finishes the follower side of the hand-overs --
-    step-downs, term adoptions, truncating merges, lookups below the newest run
-    -- checked against the oracle like every other lane."""
-    from oracle.pyoracle import hostlane_counters, hostlane_churn_lanes
-    f0, b0 = hostlane_counters()
-    c0 = hostlane_churn_lanes()
+    """BASELINE config 5 shape: rejects, decreaseTo, conflict truncation; the
+    general lane steps the follower side of the hand-overs -- step-downs, term
+    adoptions, truncating merges, lookups below the newest run -- checked
+    against the oracle like every other lane."""
+    from oracle.pyoracle import hostlane_counters
+    _, b0 = hostlane_counters()
     st = _run(200, 20, seed=5, inject_p=0.1)
     assert st["commits"] > 0
     _, b1 = hostlane_counters()
-    churn = hostlane_churn_lanes() - c0
-    assert churn > (b1 - b0) // 4, (churn, b1 - b0)
+    assert b1 > b0
 
 
 def test_forwarded_proposals(built):

@@ -51,7 +51,7 @@ def run(name, peers, G, R, passes, warmup, prepare, graph_reps=0, stream_reps=0)
     spaces = ex.allocate(eng, torch.device("cuda", 0))
     stream = torch.cuda.current_stream()
     fast = gen = 0.0
-    bailed = churn = 0
+    bailed = 0
     t_host = 0.0
     # a device fill queued ahead of each timed pass keeps the GPU busy while the
     # CPU launches the pass, so the HIP events time the kernels, not the launch
@@ -72,7 +72,6 @@ def run(name, peers, G, R, passes, warmup, prepare, graph_reps=0, stream_reps=0)
             fast += tm["fast_ms"]
             gen += tm["general_ms"]
             bailed += tm["bailed_lanes"]
-            churn += tm.get("churn_lanes", 0)
     st = eng.stats()
     graph = None
     if graph_reps:
@@ -129,8 +128,8 @@ def run(name, peers, G, R, passes, warmup, prepare, graph_reps=0, stream_reps=0)
     ms = (fast + gen) / passes
     out = {"config": name, "groups": G, "replicas": R, "passes": passes,
            "device_ms_per_pass": ms, "fast_ms": fast / passes, "general_ms": gen / passes,
-           "bailed_lanes_per_pass": bailed / passes, "churn_lanes_per_pass": churn / passes,
-           "general_lanes_per_pass": (bailed - churn) / passes, "lanes": ex.n_peers,
+           "bailed_lanes_per_pass": bailed / passes,
+           "general_lanes_per_pass": bailed / passes, "lanes": ex.n_peers,
            "lanes_per_s": ex.n_peers / (ms * 1e-3),
            "leader_commits_per_s": st["leader_commits"] / (passes * ms * 1e-3),
            "escalations_per_pass": st["escalations"] / passes,

@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 BENCH="$R/bench.py --steps ${STEPS:-10} --warmup 3 --cpu-baseline off ${BENCH_ARGS:-}"
 # counter passes: the device-resident passes only (the host-path leg runs other kernels)
 BENCH_PMC="$BENCH --host-path off"
-KRE="gr_fast|gr_roles|gr_step|gr_steady|gr_tick|gr_churn"
+KRE="gr_fast|gr_roles|gr_step|gr_steady|gr_tick"
 echo "[0] available counters (non-fatal)"
 timeout -s KILL 60 rocprofv3 -L > $O/counters_avail.txt 2>&1 || echo "counter list failed"
 echo "[1] kernel trace"
