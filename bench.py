@@ -572,6 +572,20 @@ def main():
                 traffic = None
         copy_gbs = copy_peak_gbs()
         traffic_gbs = traffic / (kavg * 1e-3) / 1e9 if traffic else None
+        configs_ev = None  # BASELINE configs 2, 3, 5 on this build (tools/configs_summary.py), never `value`
+        cfg_path = os.path.join(ROOT, "profiles", "configs_latest.json")
+        if os.path.exists(cfg_path):
+            try:
+                from dragonboat_amd.build import source_digest
+                rec = json.load(open(cfg_path))
+                if rec.get("source_digest") == source_digest():
+                    configs_ev = {k: {f: v.get(f) for f in ("config", "device_ms_per_pass", "stream_ms_per_pass",
+                                                              "pmc_bytes_per_pass", "canonical_bytes_per_pass",
+                                                              "pmc_over_canonical", "canonical_frac")}
+                                  for k, v in rec.get("configs", {}).items()}
+                    configs_ev["source"] = "profiles/configs_latest.json (same source digest as this build)"
+            except (OSError, ValueError):
+                configs_ev = None
         try:  # provenance: the loaded library's build record against this tree's sources
             from dragonboat_amd.build import build_record, source_digest
             brec = build_record(os.environ.get("GPURAFT_LIB") or None) or {}
@@ -609,6 +623,7 @@ def main():
                 " (one-rank rehearsal: GR_BENCH_COLLECTIVE=1)" if world == 1 else "")
             if placement == "spread" and (world > 1 or collective) else None,
             "build": build_info,
+            "configs_evidence": configs_ev,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"lean kernels of one pass (gr_steady_kernel<{S}> + gr_roles_kernel<{S}>, the role instances in one launch)",

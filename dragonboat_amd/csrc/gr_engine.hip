@@ -759,8 +759,11 @@ int gr_space_cx_unpack(void* space, uint32_t n_chunks, uint32_t positions, uint3
   return GR_OK;
 }
 
-// The same codec over host memory (tests): records and side entries in position
-// order (the device packer's order may differ; what unpacks does not).
+// The same codec over host memory (tests): records in the device's regions
+// (wave group wl belongs to pack workgroup wl / kCxPackGroups, whose region is
+// that workgroup's index modulo cx_regions), each region and the side entries
+// filled in position order (the device packer's order within a region may
+// differ; what unpacks does not).
 int gr_space_cx_pack_host(void* space_host, uint32_t n_chunks, uint32_t positions, uint32_t depth, void* cx_host,
                           const uint32_t* capacities, uint32_t side_capacity) {
   if (!GR_CX_ARGS_OK(space_host, cx_host, depth, n_chunks, capacities)) return GR_EINVAL;
@@ -771,9 +774,14 @@ int gr_space_cx_pack_host(void* space_host, uint32_t n_chunks, uint32_t position
     const io::CxLayout L = io::cx_layout(v.pc, depth, capacity, side_capacity);
     uint8_t* buf = (uint8_t*)cx_host + C.off[c];
     memset(buf, 0, io::kCxHdr);
-    uint32_t* nrec = (uint32_t*)buf;
-    uint32_t* nside = nrec + 1;
+    uint32_t* ctr = (uint32_t*)buf;
+    uint32_t* nside = ctr + io::kCxSub * io::kCxCtr;
+    const uint32_t nreg = io::cx_regions(L.nwv);
     for (uint32_t wl = 0; wl < L.nwv; ++wl) {
+      const uint32_t reg = (wl / io::kCxPackGroups) % nreg;
+      uint32_t roff, rcap;
+      io::cx_region(L.nwv, capacity, reg, &roff, &rcap);
+      uint32_t* nrec = ctr + reg * io::kCxCtr;
       uint32_t hi = 0;
       bool have = false;
       for (uint32_t lane = 0; lane < 64 && !have; ++lane) {
@@ -788,7 +796,7 @@ int gr_space_cx_pack_host(void* space_host, uint32_t n_chunks, uint32_t position
         }
       }
       uint64_t mask = 0, lost = 0;
-      const uint32_t base = *nrec;
+      const uint32_t base = roff + *nrec;
       for (uint32_t lane = 0; lane < 64; ++lane) {
         const uint32_t pos = wl * 64 + lane;
         const Mailbox mb = v.at(c * v.pc + pos);
@@ -798,8 +806,8 @@ int gr_space_cx_pack_host(void* space_host, uint32_t n_chunks, uint32_t position
         bool anch = false;
         const bool rec = mb_n(cb) && io::cx_classify(mb, cb, depth, &w3, &li, &anch) &&
                          (!anch || (uint32_t)(li >> 32) == hi);
-        if (rec && *nrec < capacity) {
-          io::cx_put_record(io::cx_term_of(mb, cb), li, w3, buf, L, (*nrec)++);
+        if (rec && *nrec < rcap) {
+          io::cx_put_record(io::cx_term_of(mb, cb), li, w3, buf, L, roff + (*nrec)++);
           mask |= 1ull << lane;
           continue;
         }
@@ -833,7 +841,7 @@ int gr_space_cx_unpack_host(void* space_host, uint32_t n_chunks, uint32_t positi
         io::cx_get_lane(v.at(c * v.pc + wl * 64 + lane), buf, L, ((const uint64_t*)h)[0], ((const uint64_t*)h)[1],
                         ((const uint32_t*)h)[4], ((const uint32_t*)h)[5], lane);
     }
-    const uint32_t ns = ((const uint32_t*)buf)[1];
+    const uint32_t ns = ((const uint32_t*)buf)[io::kCxSub * io::kCxCtr];
     for (uint32_t x = 0; x < ns && x < side_capacity; ++x) {
       const uint8_t* e = buf + L.side + (uint64_t)x * io::cx_side_entry_bytes(depth);
       io::cx_get_side(v.at(c * v.pc + ((const uint32_t*)e)[0]), e, depth);

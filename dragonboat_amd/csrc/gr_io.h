@@ -597,11 +597,19 @@ __global__ void side_unpack(SpaceView v, const uint8_t* side, uint32_t cap) {
 // path. Every other mailbox with messages travels
 // as a full side entry (hot fields of every message and their cold records). An
 // empty mailbox costs one bit. Layout of a chunk's buffer (cx_layout):
-//   header 64 B: u32 records, u32 side entries (the packers' counters)
+//   header (kCxSub + 1) x 64 B: per record region one u32 counter of the
+//     records taken (the packers' counters, records past the region's capacity
+//     included), then the side entries taken, each counter on a 64-B line of
+//     its own (kCxCtr words apart: atomics on one line serialise)
 //   per 64 positions (a wave): u64 record mask, u64 lost mask, u32 first record,
 //     u32 LogIndex high bits
 //   records, structure of arrays over `cap`: u32 term word, u32 LogIndex low
-//     bits, u32 count byte | Commit offset << 8
+//     bits, u32 count byte | Commit offset << 8. The capacity is split into
+//     cx_regions() equal regions, and the pack's workgroup b takes its records
+//     in region b % regions: one returning atomic per workgroup on its region's
+//     counter (round 6: 1,465 workgroups queued on one counter word cost ~25 us
+//     per 500k-group pass; regions balance, since every region gets every
+//     regions-th workgroup of the chunk).
 //   side entries (`scap`): u32 position, u32 count byte, u32 term word, u32 pad,
 //     per message (u32 Commit offset, u32 pad, u64 LogIndex), then per message
 //     the kColdUsed bytes of its cold record
@@ -614,7 +622,7 @@ __global__ void side_unpack(SpaceView v, const uint8_t* side, uint32_t cap) {
 // 4 x (cap x 12 B + 31k wave headers x 24 B + side entries) = 58 MB per pass at
 // cap = 0.55 x positions, 70 MB at 0.7, against 328 MB for the hot regions
 // (41 B per position). exchange.py sizes cap.
-constexpr uint32_t kCxHdr = 64, kCxWave = 24;
+constexpr uint32_t kCxSub = 16, kCxCtr = 16, kCxHdr = (kCxSub + 1) * kCxCtr * 4, kCxWave = 24;
 __host__ __device__ inline uint32_t cx_side_entry_bytes(uint32_t depth) { return 16 + depth * (16 + kColdUsed); }
 struct CxLayout {
   uint64_t waves, cb, term, lo, cd, side, bytes;
@@ -633,6 +641,30 @@ __host__ __device__ inline CxLayout cx_layout(uint32_t pc, uint32_t depth, uint3
   L.side = L.cb + round256(4ull * cap);
   L.bytes = L.side + round256((uint64_t)scap * cx_side_entry_bytes(depth));
   return L;
+}
+// Record regions of a chunk of nwv wave groups: one per kCxRegionWgs pack
+// workgroups (the pack's workgroups take kCxPackGroups wave groups each), at
+// most kCxSub, at least one. A chunk's fill follows its replica pairs' position
+// ranges (pair-major), and a region serves every regions-th workgroup, so its
+// demand is its share of the chunk's within one workgroup per pair range: with
+// kCxRegionWgs = 256 that is under 2.5 % of a region (exchange.py CX_MARGIN
+// covers it), and a chunk of fewer than 512 workgroups has one region (exact).
+constexpr uint32_t kCxPackPer = 8, kCxPackGroups = kCxPackPer * 4, kCxRegionWgs = 256;
+__host__ __device__ inline uint32_t cx_regions(uint32_t nwv) {
+  const uint32_t n = ((nwv + kCxPackGroups - 1) / kCxPackGroups) / kCxRegionWgs;
+  return n < 1u ? 1u : (n > kCxSub ? kCxSub : n);
+}
+// Region r's first record and capacity: its share of the chunk's capacity in
+// proportion to the pack workgroups it serves (workgroups b with b % regions
+// == r), so that a capacity sized for every position's worst case holds it in
+// every region.
+__host__ __device__ inline void cx_region(uint32_t nwv, uint32_t cap, uint32_t r, uint32_t* off, uint32_t* rcap) {
+  const uint32_t wgs = (nwv + kCxPackGroups - 1) / kCxPackGroups, n = cx_regions(nwv);
+  const uint32_t per = wgs / n, extra = wgs % n;  // regions below `extra` serve one workgroup more
+  const uint32_t before = r * per + (r < extra ? r : extra), mine = per + (r < extra ? 1u : 0u);
+  const uint32_t w = wgs ? wgs : 1u;
+  *off = (uint32_t)((uint64_t)cap * before / w);
+  *rcap = (uint32_t)((uint64_t)cap * (before + mine) / w) - *off;
 }
 // Mailbox mb (count byte cb) travels as a uniform record: its hot fields are
 // message 0's, and a Replicate's Commit offset fits 24 bits (*w: the record's
@@ -993,7 +1025,7 @@ __host__ __device__ inline CxCaps cx_caps(uint32_t pc, uint32_t depth, uint32_t 
 // returning atomic per wave on one word per chunk: 360 us per 500k-group pass
 // of one chunk, 47k waves queued on it; round 6's first cut, one group's loads
 // at a time, 44 us.)
-constexpr uint32_t kCxPackPer = 8, kCxPackGroups = kCxPackPer * (kIoBlock / 64);
+static_assert(kCxPackGroups == kCxPackPer * (kIoBlock / 64), "a pack workgroup is four waves");
 __global__ __launch_bounds__(kIoBlock) void cx_pack(SpaceView v, uint8_t* cx, CxCaps C) {
   constexpr uint32_t nwave = kIoBlock / 64;
   const uint32_t c = blockIdx.y, nwv = v.pc / 64;
@@ -1003,6 +1035,9 @@ __global__ __launch_bounds__(kIoBlock) void cx_pack(SpaceView v, uint8_t* cx, Cx
   const CxLayout L = cx_layout(v.pc, v.depth, cap, scap);
   uint8_t* buf = cx + C.off[c];
   __shared__ uint32_t s_rec[nwave], s_side[nwave], s_base[2];
+  const uint32_t reg = blockIdx.x % cx_regions(nwv);
+  uint32_t roff, rcap;
+  cx_region(nwv, cap, reg, &roff, &rcap);
   // ---- every group's hot words in one batch (groups past the chunk: position 0's)
   uint32_t cb[kCxPackPer], cd[kCxPackPer], tw[kCxPackPer];
   uint64_t li[kCxPackPer];
@@ -1060,18 +1095,18 @@ __global__ __launch_bounds__(kIoBlock) void cx_pack(SpaceView v, uint8_t* cx, Cx
   if (threadIdx.x == 0) {
     uint32_t t = 0;
     for (uint32_t q = 0; q < nwave; ++q) t += s_rec[q];
-    s_base[0] = t ? atomicAdd(reinterpret_cast<uint32_t*>(buf), t) : 0u;
+    s_base[0] = t ? atomicAdd(reinterpret_cast<uint32_t*>(buf) + reg * kCxCtr, t) : 0u;
   }
   __syncthreads();
-  uint32_t r = s_base[0];
+  uint32_t r = s_base[0];  // within the workgroup's region
   for (uint32_t q = 0; q < wave; ++q) r += s_rec[q];
-  const uint32_t over = r >= cap ? nrec : (r + nrec > cap ? r + nrec - cap : 0u);  // records past capacity
+  const uint32_t over = r >= rcap ? nrec : (r + nrec > rcap ? r + nrec - rcap : 0u);  // records past capacity
   if (lane == 0) s_side[wave] = nside + over;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t t = 0;
     for (uint32_t q = 0; q < nwave; ++q) t += s_side[q];
-    s_base[1] = t ? atomicAdd(reinterpret_cast<uint32_t*>(buf) + 1, t) : 0u;
+    s_base[1] = t ? atomicAdd(reinterpret_cast<uint32_t*>(buf) + kCxSub * kCxCtr, t) : 0u;
   }
   __syncthreads();
   uint32_t x0 = s_base[1];
@@ -1085,8 +1120,8 @@ __global__ __launch_bounds__(kIoBlock) void cx_pack(SpaceView v, uint8_t* cx, Cx
     const bool rec = (recm >> q) & 1u, msgs = (msgm >> q) & 1u;
     const uint64_t mask = __ballot(rec);
     const uint32_t ri = r + (uint32_t)__popcll(mask & below);
-    const bool fits = rec && ri < cap;  // past capacity: the group's last record lanes
-    if (fits) cx_put_record(tw[q], li[q], w3[q], buf, L, ri);
+    const bool fits = rec && ri < rcap;  // past capacity: the group's last record lanes
+    if (fits) cx_put_record(tw[q], li[q], w3[q], buf, L, roff + ri);
     const bool side = msgs && !fits;
     const uint64_t smask = __ballot(side);
     const uint32_t xi = x0 + (uint32_t)__popcll(smask & below);
@@ -1100,7 +1135,7 @@ __global__ __launch_bounds__(kIoBlock) void cx_pack(SpaceView v, uint8_t* cx, Cx
       uint8_t* h = buf + L.waves + (uint64_t)g * kCxWave;
       reinterpret_cast<uint64_t*>(h)[0] = fmask;
       reinterpret_cast<uint64_t*>(h)[1] = lost;
-      reinterpret_cast<uint32_t*>(h)[4] = r;
+      reinterpret_cast<uint32_t*>(h)[4] = roff + r;
       reinterpret_cast<uint32_t*>(h)[5] = hi[q];
     }
     r += (uint32_t)__popcll(mask);
@@ -1173,7 +1208,7 @@ __global__ void cx_unpack_side(SpaceView v, const uint8_t* cx, CxCaps C) {
     const uint32_t c = (uint32_t)(t / scap), x = (uint32_t)(t % scap);
     const CxLayout L = cx_layout(v.pc, v.depth, C.cap[c], scap);
     const uint8_t* buf = cx + C.off[c];
-    if (x >= reinterpret_cast<const uint32_t*>(buf)[1]) continue;
+    if (x >= reinterpret_cast<const uint32_t*>(buf)[kCxSub * kCxCtr]) continue;
     const uint8_t* e = buf + L.side + (uint64_t)x * cx_side_entry_bytes(v.depth);
     cx_get_side(v.at(c * v.pc + reinterpret_cast<const uint32_t*>(e)[0]), e, v.depth);
   }

@@ -60,12 +60,28 @@ TILE_W = 256  # gr_layout.h kTileW (GR_TILE_SHIFT = 8); Exchange checks it again
 SIDE_DIV, SIDE_MIN = 32, 1024  # side-buffer capacity per chunk: positions / SIDE_DIV, at least SIDE_MIN
 # compact exchange capacities per chunk: records for the share of a chunk's
 # positions that hold messages in the steady state, whichever replica leads
-# (cx_fill_max), full entries for 1/CX_SIDE_DIV of them (at least CX_SIDE_MIN).
+# (cx_fill_max), plus CX_MARGIN for the pack's record regions (gr_io.h
+# cx_region: each region holds its workgroups' share of the capacity, and the
+# workgroups' fills differ by a few workgroups' worth between regions: at a
+# chunk filled to its capacity, 0 % margin sent 3 % of the records to full
+# entries), full entries for 1/CX_SIDE_DIV of them (at least CX_SIDE_MIN).
 # A chunk carries the replica pairs (r -> j) of one rank offset; only the pairs
 # with the leader on one end hold messages (a leader's Replicates, its
 # followers' acks).
-CX_MARGIN, CX_SIDE_DIV, CX_SIDE_MIN = 0.0, 256, 256
+CX_MARGIN, CX_SIDE_DIV, CX_SIDE_MIN = 0.04, 256, 256
 CX_MAX_CHUNKS = 8  # gr_io.h kCxMaxChunks: a rank's destination chunks in one compact buffer set
+CX_SUB, CX_CTR = 16, 16  # gr_io.h kCxSub record regions, their counters kCxCtr words apart; then the side counter
+CX_HDR = (CX_SUB + 1) * CX_CTR * 4
+
+
+def cx_counts(hdr):
+    """(records, full entries) a compact-exchange chunk's packer took, from its
+    header (bytes or a uint8 array of at least CX_HDR bytes): the region
+    counters' sum (records past a region's capacity included) and the side
+    counter."""
+    import numpy as _np
+    w = _np.frombuffer(bytes(hdr[:CX_HDR]), _np.uint32)
+    return int(w[0:CX_SUB * CX_CTR:CX_CTR].sum()), int(w[CX_SUB * CX_CTR])
 
 
 def cx_fill(R, N, offset, leader=0):

@@ -511,8 +511,13 @@ int gr_space_side_unpack_host(void* space_host, uint32_t n_chunks, uint32_t posi
  * its whole hot region plus side buffers. Per chunk one fixed-size buffer
  * (gr_space_cx_bytes) carries only the mailboxes with messages: a 12-byte record
  * for a uniform mailbox whose messages repeat message 0's hot fields (one
- * message, or the steady state's shared pairs), a full entry (hot fields and cold
- * records) for any other, one bit for an empty one. capacities[c] records for
+ * message, or the steady state's shared pairs) and, round 6, for any mailbox of
+ * up to three messages in a tick pass's or a commit advance's canonical forms
+ * (a pattern record: Replicates at one LogIndex with Commits 0 or 1 apart,
+ * accepts 0 or 1 apart, heartbeats and their acks with an empty context), a
+ * full entry (hot fields and cold records) for any other, one bit for an empty
+ * one. The buffer's header holds the packer's counters: records taken per
+ * record region (16 regions, counters 64 B apart) and the full entries taken. capacities[c] records for
  * chunk c (at most 8 chunks) and `side_capacity` full entries per chunk; the
  * receiver passes the sender's capacities for its chunks. A mailbox that fits neither arrives as
  * lost (count 1 with bit 4, not uniform) and its reader escalates

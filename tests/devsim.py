@@ -92,9 +92,10 @@ def run_device(G, R, passes, placement="local", seed=2, tick_every=0, stats=None
         torch.cuda.synchronize()
         if placement == "spread" and stats is not None:  # what the exchange carried
             if ex.last_cx:  # records, full entries (one chunk: headers at offset 0)
-                hdr = ex.cx[1][:8].cpu().numpy().view(np.uint32)
-                stats.setdefault("records", []).append(int(hdr[0]))
-                stats.setdefault("side_entries", []).append(int(hdr[1]))
+                from dragonboat_amd.exchange import cx_counts, CX_HDR
+                nrec, nside = cx_counts(ex.cx[1][:CX_HDR].cpu().numpy())
+                stats.setdefault("records", []).append(nrec)
+                stats.setdefault("side_entries", []).append(nside)
             else:
                 sb = len(ex.side[1]) // ex.n_chunks
                 hdr = ex.side[1].cpu().numpy().reshape(ex.n_chunks, sb)[:, :4].copy().view(np.uint32)[:, 0]

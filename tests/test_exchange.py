@@ -691,7 +691,7 @@ def test_cx_pattern_records(built):
     assert np.array_equal(key(got), key(want))  # every field of every message
     chunk_bytes = cb // n_chunks
     for c in range(n_chunks):
-        n_rec, n_side = np.frombuffer(cx[c * chunk_bytes:c * chunk_bytes + 8].tobytes(), np.uint32)
+        n_rec, n_side = X.cx_counts(cx[c * chunk_bytes:(c + 1) * chunk_bytes])
         recs = sum(1 for p, r in want_rec.items() if r and p // pc == c)
         sides = sum(1 for p, r in want_rec.items() if not r and p // pc == c)
         assert (n_rec, n_side) == (recs, sides), (c, n_rec, n_side, recs, sides)

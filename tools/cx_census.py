@@ -53,14 +53,14 @@ def main():
         hcx = np.zeros(cb, np.uint8)
         assert lib.gr_space_cx_pack_host(out.ctypes.data, ex.n_chunks, ex.positions, ex.depth, hcx.ctypes.data,
                                          caps.ctypes.data, ex.cx_scap) == 0
-        nrec, nside = np.frombuffer(hcx[:8].tobytes(), np.uint32)
+        nrec, nside = X.cx_counts(hcx)
         # full entries: positions whose messages did not pack as records (host codec, position order)
         msgs = decode_space(out.copy(), ex.n_chunks, ex.positions, ex.depth, lost_ok=True)
         by = collections.defaultdict(list)
         for m in msgs:
             by[int(m["peer"])].append(m)
         # records: read the wave masks of the host-packed buffer
-        L_waves = 64
+        L_waves = X.CX_HDR
         pc = X.pad_positions(ex.positions)
         nwv = pc // 64
         hdr = hcx[L_waves:L_waves + nwv * 24].reshape(nwv, 24)
