@@ -40,7 +40,7 @@ def main(o):
         if n.startswith("gr_") and "kernel" in n:
             tr[n].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
     out["trace"] = {k: {"launches": len(v), "avg_us": sum(v) / len(v), "min_us": min(v)} for k, v in tr.items()}
-    for d in sorted(glob.glob(os.path.join(o, "fetch*"))):
+    for d in sorted(x for x in glob.glob(os.path.join(o, "fetch*")) if os.path.isdir(x)):
         c = os.path.basename(d)[len("fetch"):]
         per = {}
         for sub, cnt, unit in (("fetch", "FETCH_SIZE", cal["read"]), ("write", "WRITE_SIZE", cal["write"])):

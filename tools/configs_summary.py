@@ -6,7 +6,11 @@ summary per BASELINE config: pass time, HBM bytes per pass by PMC, SURVEY.md
 8 TB/s spec. bench.py reports it beside the headline (never as `value`) when
 its source digest is the build's.
 
-    python tools/configs_summary.py gpurun_out/cfgprof_r06 > profiles/r06_configs/summary.json
+    python tools/configs_summary.py gpurun_out/cfgprof_r06 [untraced_configs.json] > profiles/r06_configs/summary.json
+
+The pass times come from the untraced run when one is given (tools/bench_configs.py
+without the profiler: the kernel trace slows every launch), the bytes from the
+counter passes.
 """
 import glob
 import json
@@ -32,18 +36,24 @@ def canonical(cfg):
     return G * b_round(R)
 
 
-def main(d):
-    from dragonboat_amd.build import source_digest
-    cfgs = []
-    with open(os.path.join(d, "configs.json")) as fh:
+def load_lines(path):
+    out = []
+    with open(path) as fh:
         for ln in fh:
             ln = ln.strip()
             if ln.startswith("{"):
-                cfgs.append(json.loads(ln))
+                out.append(json.loads(ln))
+    return out
+
+
+def main(d, untraced=None):
+    from dragonboat_amd.build import source_digest
+    cfgs = load_lines(untraced) if untraced else load_lines(os.path.join(d, "configs.json"))
     summ = {}
     pmc_path = os.path.join(d, "summary.json")
     pmc = json.load(open(pmc_path)) if os.path.exists(pmc_path) else {}
-    out = {"source_digest": source_digest(), "hbm_peak_GBs": HBM_PEAK, "configs": {}}
+    out = {"source_digest": source_digest(), "hbm_peak_GBs": HBM_PEAK, "configs": {},
+           "times_from": "untraced tools/bench_configs.py" if untraced else "the traced run"}
     for c in cfgs:
         key = c["config"].split(":")[0]
         ms = c["device_ms_per_pass"]
@@ -74,4 +84,4 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)

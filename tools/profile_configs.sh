@@ -12,7 +12,7 @@ mkdir -p $O
 cd /tmp
 export TMPDIR=/tmp
 CFG="$R/tools/bench_configs.py --passes ${PASSES:-10} --warmup 3"
-KRE="gr_fast|gr_roles|gr_step|gr_steady|gr_tick"
+KRE="gr_fast|gr_roles|gr_step|gr_steady|gr_tick|gr_small"
 echo "[1] configs + kernel trace"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o cfg -- python3 $CFG --only ${ONLY:-2,3,5} > $O/configs.json 2> $O/trace.log
 for c in $(echo ${PMC_ONLY:-3,5} | tr , ' '); do
