@@ -100,6 +100,7 @@ def _worker(rank, world, port, G, banks, passes, codec, churn, q, backend="gloo"
             # where heavy_at says
             pipe.step(k, heavy=k in heavy_at)
             pipe.synchronize()
+            print(f"rank {rank}/{world} pass {k}", flush=True)  # progress (pytest -s)
             for b, ex in enumerate(pipe.ex):
                 Gb = ex.G
                 dev = pipe.engines[b].sync(ex.n_peers)
@@ -164,3 +165,41 @@ def test_pipeline_world2_gloo_matches_oracle(gpu, banks, codec, churn):
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
+
+
+def _run_world(world, G, banks, passes, codec, churn):
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, G, banks, passes, codec, churn, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = []
+        for _ in procs:
+            out.append(q.get(timeout=300))
+        return out
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+
+
+# Three to five ranks: every replica of a group on its own rank, as at N = 8
+# (at world 2 replica 2 shares its home's rank); from N = 5 on a rank's chunks
+# go to 4 of the N ranks (offsets 1, 2, N - 2, N - 1), as at N = 8, and the
+# all-to-all's splits to the others are 0.
+@pytest.mark.parametrize("world,G,churn", [(3, 4096, False), (3, 2048, True), (4, 2048, True),
+                                           (4, 32768, True), (5, 4096, True)])
+def test_pipeline_world_n_gloo_matches_oracle(gpu, world, G, churn):
+    for rank, bad, esc, commits, err in _run_world(world, G, 1, 7 if churn else 5, "cx", churn):
+        assert err is None, (rank, err)
+        assert bad is None, (rank, bad, esc)
+        assert esc[0] == 0, (rank, esc)
+        assert commits > 0
