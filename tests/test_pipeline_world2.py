@@ -167,7 +167,7 @@ def test_pipeline_world2_gloo_matches_oracle(gpu, banks, codec, churn):
                 p.kill()
 
 
-def _run_world(world, G, banks, passes, codec, churn):
+def _run_world(world, G, banks, passes, codec, churn, **kw):
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -175,7 +175,7 @@ def _run_world(world, G, banks, passes, codec, churn):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, G, banks, passes, codec, churn, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, G, banks, passes, codec, churn, q), kwargs=kw)
              for r in range(world)]
     for p in procs:
         p.start()
@@ -202,4 +202,17 @@ def test_pipeline_world_n_gloo_matches_oracle(gpu, world, G, churn):
         assert err is None, (rank, err)
         assert bad is None, (rank, bad, esc)
         assert esc[0] == 0, (rank, esc)
+        assert commits > 0
+
+
+# The shipped sizing (record capacities for the worst leader placement, full
+# entries for 1/256 of the positions, depth 3) with a Tick on every replica every
+# third pass and no heavy pass: heartbeats and acks cross 4 and 5 ranks as
+# pattern records, and nothing escalates CAPACITY that the oracle does not.
+@pytest.mark.parametrize("world", [4, 5])
+def test_pipeline_world_n_default_sizing_ticks(gpu, world):
+    for rank, bad, esc, commits, err in _run_world(world, 8192, 2, 7, "cx", False, sizing="default", ticks=True):
+        assert err is None, (rank, err)
+        assert bad is None, (rank, bad, esc)
+        assert esc[0] == 0 and esc[2] == 0, (rank, esc)
         assert commits > 0
