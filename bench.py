@@ -626,7 +626,8 @@ def main():
             "configs_evidence": configs_ev,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": f"lean kernels of one pass (gr_steady_kernel<{S}> + gr_roles_kernel<{S}>, the role instances in one launch)",
+                         "kernel": f"lean kernels of one pass (gr_steady_kernel<{S},{R}>; gr_roles_kernel<{S},{R}> too on a pass "
+                                   "whose tail plan launches the role instances, none in the steady state)",
                          "kernel_ms": kavg,
                          "algorithmic_bytes_per_launch": alg,
                          "algorithmic_unit": (f"group-round at this engine's encoding, {ENCODED_ROUND_BYTES[R]} B "
