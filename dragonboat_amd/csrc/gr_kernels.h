@@ -382,6 +382,12 @@ __device__ inline __attribute__((always_inline)) void roles_listed(const StepPar
   // the lanes the steady kernel left (lists 24..31, final: it ran before this
   // launch on the stream), grid-stride; each role instance takes the lanes of
   // its role. No hint is written for them (their waves were the steady kernel's).
+  // A wave of list entries may hold lanes of several replica blocks (a wave that
+  // appends some of its lanes leaves the next wave's entries unaligned), so the
+  // routes' replica block is each lane's own, not the wave's first lane's
+  // (StepParams::route_wu).
+  StepParams kr = kp;
+  kr.route_wu = 0;
   LaneStats acc;
   for (uint32_t base = bid * kBlock; base < n; base += nblk * kBlock) {
     const uint32_t x = base + threadIdx.x;
@@ -394,7 +400,7 @@ __device__ inline __attribute__((always_inline)) void roles_listed(const StepPar
       LaneStats ls;
       bool skip = false;
       uint32_t h = 0;
-      bail = !lean_step<S, R, RM>(kp, li, li, &ls, &role, 0u, &h, R, &skip);
+      bail = !lean_step<S, R, RM>(kr, li, li, &ls, &role, 0u, &h, R, &skip);
       bail = bail && !skip;
       if (!bail && !skip) {
         GR_CHECK_STATE(kp.st, li);
@@ -466,7 +472,12 @@ __global__ __launch_bounds__(kBlock, GR_LISTED_MIN_WAVES) void gr_roles_kernel(S
 // with FastLane in the same kernel the allocation rose to FastLane's and
 // beyond): the waves whose hint says they were steady. A lane whose
 // preconditions fail stores nothing and is queued for FastLane (lists 24..31).
-template <int S, int RM>
+// LC: unhinted waves' lanes try their own role's closed form (lane_closed_form),
+// the instance a pass runs when role instances follow it (TailPlan: the last
+// pass left lanes to them); a pass without them runs LC = false, whose code is
+// the steady state's alone (the headline measured 2-4 % slower with the branch
+// compiled in, though its waves never take it).
+template <int S, int RM, bool LC>
 __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(StepParams kp, uint32_t* bail_list,
                                                                                uint32_t* counters, uint32_t list_cap,
                                                                                const uint32_t* prev_counters) {
@@ -505,6 +516,26 @@ __global__ __launch_bounds__(kBlock, GR_FAST_MIN_WAVES) void gr_steady_kernel(St
       uint64_t* r = kp.tick_stage + te * kTickStageWords;
 #pragma unroll
       for (uint32_t w = 0; w < kTickStageWords; ++w) r[w] = stage[w];
+    }
+    if constexpr (LC) {
+      // the rest try the closed form of their own role (lane_closed_form); what
+      // it leaves goes to the retry lists, which the role instances walk as
+      // dense waves (or, with no role instances after this kernel, the general
+      // kernel), instead of listing the whole wave
+      LaneStats ls;
+      uint32_t role = 0, myhint = 0;
+      const bool fin = q == QS_OTHER && lane_closed_form<S, RM>(kp, i, i, &ls, &role, &myhint);
+      if (fin) GR_CHECK_STATE(kp.st, i);
+      if ((threadIdx.x & 63) == 0) wave_flags(bail_list, list_cap)[wave] = 0;
+      // the next pass's hint, as a hinted wave's: the lanes finished here agree
+      // on it, the quiesced ones and those the closed form left are wildcards
+      // (the latter go on to FastLane either way); a lane with ticks or a
+      // ReadIndex blocks it (its wave stays on quiet_step's path)
+      const bool tk = q == QS_TICK;
+      wave_finish<S>(kp, i, wave, true, active, tk, false, role, myhint, ls, bail_list, counters, list_cap);
+      if (!__ballot(active && !tk) && (threadIdx.x & 63) == 0) kp.hints_out[wave] = 0;
+      bail_append(q == QS_OTHER && !fin, kRetryList0 + blockIdx.x % 8, bail_list, counters, list_cap, i);
+      return;
     }
     if (kp.no_roles) {
       // no role instances follow (TailPlan): the rest go straight to the retry
@@ -574,6 +605,9 @@ __global__ __launch_bounds__(kBlock, GR_TICK_MIN_WAVES) void gr_tick_kernel(Step
   }
   __syncthreads();
   const uint32_t n = tstart[kTickLists];
+  // list entries: a wave may hold lanes of several replica blocks, so no
+  // wave-uniform replica block for the routes (roles_listed)
+  kp.route_wu = 0;
   // one-wave workgroups by default (tick_wg): a config-3 pass hands ~50k lanes to
   // this kernel, 196 workgroups of 256 lanes would leave 60 of the 256 CUs idle
   const uint32_t bw = blockDim.x;
@@ -966,8 +1000,12 @@ hipError_t launch_fast(const StepParams& kp0, uint32_t blocks, uint32_t* bail_li
       // the steady lanes, then the role instances over the waves it listed and
       // the lanes it left
       kp.no_roles = roles ? 0 : 1;
-      hipLaunchKernelGGL((gr_steady_kernel<S, RM>), dim3(blocks), dim3(kBlock), steady_lds(), s, kp, bail_list, cur,
-                         list_cap, (const uint32_t*)prev);
+      if (roles && GR_LANE_CLOSED)
+        hipLaunchKernelGGL((gr_steady_kernel<S, RM, true>), dim3(blocks), dim3(kBlock), steady_lds(), s, kp, bail_list,
+                           cur, list_cap, (const uint32_t*)prev);
+      else
+        hipLaunchKernelGGL((gr_steady_kernel<S, RM, false>), dim3(blocks), dim3(kBlock), steady_lds(), s, kp, bail_list,
+                           cur, list_cap, (const uint32_t*)prev);
       const hipError_t e0 = hipGetLastError();
       if (e0 != hipSuccess || skip_tail) return e0;
       if (!roles) {

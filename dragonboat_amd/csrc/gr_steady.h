@@ -395,6 +395,34 @@ GF_HD int quiet_step(const StepParams& kp, uint32_t i, uint32_t p, uint64_t* sta
   return QS_DONE;
 }
 
+// A lane of an unhinted wave with messages or a proposal (quiet_step's
+// QS_OTHER): the closed form of the role its own header names, with the slot a
+// wave hint would carry read from the header (a leader's own slot; a follower's
+// leader slot, F_LSLOT). A wave whose groups' leaders sit on different replicas
+// (elections, config 5's leader changes) has no common hint, and without this
+// every lane of it ran FastLane. The closed forms check every precondition, the
+// slot included, against the lane's state, so a lane that fails them has stored
+// nothing (false) and goes on to FastLane.
+#ifndef GR_LANE_CLOSED
+#define GR_LANE_CLOSED 1  // the steady kernel tries it on unhinted waves (A/B builds: 0)
+#endif
+template <int S, int RM>
+GF_HD bool lane_closed_form(const StepParams& kp, uint32_t i, uint32_t p, LaneStats* ls, uint32_t* role,
+                            uint32_t* hint_out) {
+  const uint64_t hdr = kp.st.u64(SR_HDR)[p];
+  const uint32_t st = h_state(hdr);
+  if constexpr (S == 3) {
+    if (st == GR_LEADER) {
+      *role = GR_LEADER;
+      return SteadyLeader<S, RM>(kp, i, p).step(ls, WH_STEADY_LEADER | (h_self(hdr) << WH_SLOT_SHIFT), hint_out);
+    }
+  }
+  const uint32_t sl = (h_flags(hdr) & F_LSLOT) >> F_LSLOT_SHIFT;  // the leader's slot + 1, 0: none known
+  if (st != GR_FOLLOWER || sl == 0 || sl > (uint32_t)S) return false;
+  *role = GR_FOLLOWER;
+  return SteadyFollower<S, RM>(kp, i, p).step(ls, WH_FOLLOWER | WH_RUNS | ((sl - 1) << WH_SLOT_SHIFT), hint_out);
+}
+
 // Kernel-side entry (gr_kernels.h, and the host build of the lane): a wave
 // hinted steady runs the closed-form lane of its role first; any lane it does
 // not finish (nothing stored) runs FastLane; false = hand the lane to the

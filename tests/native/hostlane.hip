@@ -95,7 +95,7 @@ void run_lanes(const StepParams& kp) {
     const int fk = wave_kernel(hint, S);
     const bool split = g_true_hints || ((g_hint_salt >> 3) & 1u);
     bool done = false;
-    uint32_t sh = 0;
+    uint32_t sh = 0, role_cf = 0;
     int q0 = QS_OTHER;
     if (split && steady_hint<S>(hint)) {
       // a split pass's steady kernel (gr_kernels.h gr_steady_kernel): the closed
@@ -124,6 +124,22 @@ void run_lanes(const StepParams& kp) {
       done = q0 == QS_DONE;
       staged[i] = q0 == QS_TICK;
       g_steady_lanes += done;
+    } else if (split && q0 == QS_OTHER && !steady_hint<S>(hint) && GR_LANE_CLOSED &&
+               (((i >> 6) + (g_hint_salt >> 4)) & 7u) != 3u && lane_closed_form<S, RM_ANY>(kp, i, p, &ls, &role_cf, &sh)) {
+      // a pass with role instances runs the steady kernel's LC instance: the
+      // closed form of an unhinted wave's lane's own role (gr_steady.h
+      // lane_closed_form)
+      done = true;
+      g_steady_lanes++;
+    } else if (split && GR_LANE_CLOSED && (((i >> 6) + (g_hint_salt >> 4)) & 7u) != 3u) {
+      // what it leaves: the role instances' retry pass (FastLane without a hint, by role)
+      bool skip = false;
+      done = lean_step<S, FL_FOLLOWER>(kp, i, p, &ls, nullptr, 0u, nullptr, FL_FOLLOWER, &skip);
+      if (skip) {
+        ls = LaneStats{};
+        done = lean_step<S, FL_LEADER>(kp, i, p, &ls, nullptr, 0u, nullptr, FL_LEADER, &skip);
+        if (skip) abort();
+      }
     } else if (split && (((i >> 6) + (g_hint_salt >> 4)) & 7u) == 3u) {
       // a lane of a pass whose role instances did not run (gr_kernels.h TailPlan,
       // GM_RETRY): the steady kernel lists it for the general kernel

@@ -32,8 +32,8 @@ def counters(d, kernel_sub):
 # wave lists, in one launch (gr_roles_kernel, round 4) or as <S, 2> (followers)
 # and <S, 1> (leaders) with GR_ROLES_MERGED=0. A device pass's lean-kernel bytes
 # are the sum over the kernels it ran.
-ROLE_INSTANCES_MERGED = ("gr_steady_kernel<3, 3>", "gr_roles_kernel<3, 3>")
-ROLE_INSTANCES_SPLIT = ("gr_steady_kernel<3, 3>", "gr_fast_kernel<3, 2, 3, true>", "gr_fast_kernel<3, 1, 3, true>")
+ROLE_INSTANCES_MERGED = ("gr_steady_kernel<3, 3", "gr_roles_kernel<3, 3>")  # steady: <3, 3, LC>
+ROLE_INSTANCES_SPLIT = ("gr_steady_kernel<3, 3", "gr_fast_kernel<3, 2, 3, true>", "gr_fast_kernel<3, 1, 3, true>")
 
 
 def main(o):
