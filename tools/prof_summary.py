@@ -94,7 +94,7 @@ def main(o):
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         from dragonboat_amd.build import source_digest
         with open(os.path.join(o, "pmc_latest.json"), "w") as fh:
-            json.dump({"kernel": " + ".join(ROLE_INSTANCES) + " (the lean kernels of one pass)", "groups": groups, "replicas": 3,
+            json.dump({"kernel": " + ".join(k + (", LC>" if k.endswith(", 3") else "") for k in ROLE_INSTANCES) + " (the lean kernels of one pass)", "groups": groups, "replicas": 3,
                        "source_digest": source_digest(),
                        "hbm_bytes_per_launch": fk["hbm_bytes_per_launch"],
                        "read_bytes": fk["read_bytes"], "write_bytes": fk["write_bytes"],
