@@ -50,6 +50,8 @@ def main(o):
                     agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * unit)
             for k, v in agg.items():
                 per.setdefault(k, {})[sub + "_bytes_avg"] = sum(v) / len(v)
+                per[k][sub + "_bytes_sum"] = sum(v)  # over the run's dispatches
+                per[k][sub + "_dispatches"] = len(v)
         sq = defaultdict(lambda: defaultdict(list))
         for r in rows(os.path.join(o, "sq" + c, "**", "*counter_collection.csv")):
             sq[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))

@@ -71,10 +71,20 @@ def main(d, untraced=None):
         row["canonical_frac"] = row["canonical_GBs"] / HBM_PEAK
         per = pmc.get("pmc", {}).get("config" + key)
         if per:
-            hb = sum(v.get("fetch_bytes_avg", 0) + v.get("write_bytes_avg", 0) for v in per.values())
+            # per pass: every dispatch's bytes over the run's passes (the kernel
+            # launched every pass sets the count), so kernels a pass may skip (the
+            # role instances) or alternatives (the steady kernel's LC and plain
+            # instances) count by how often they ran, not once each
+            npass = max((v.get("fetch_dispatches", 0) for v in per.values()), default=0)
+            if npass and all("fetch_bytes_sum" in v for v in per.values()):
+                hb = sum(v.get("fetch_bytes_sum", 0) + v.get("write_bytes_sum", 0) for v in per.values()) / npass
+            else:  # summaries without sums (before round 6's LC instance): one launch of each per pass
+                hb = sum(v.get("fetch_bytes_avg", 0) + v.get("write_bytes_avg", 0) for v in per.values())
             row["pmc_bytes_per_pass"] = hb
-            row["pmc_by_kernel"] = {k: {"fetch": v.get("fetch_bytes_avg"), "write": v.get("write_bytes_avg")}
+            row["pmc_by_kernel"] = {k: {"fetch": v.get("fetch_bytes_avg"), "write": v.get("write_bytes_avg"),
+                                        "dispatches": v.get("fetch_dispatches")}
                                     for k, v in per.items()}
+            row["pmc_passes"] = npass
             row["pmc_over_canonical"] = hb / canon
             row["pmc_GBs"] = hb / (ms * 1e-3) / 1e9
         row["fast_ms"], row["general_ms"] = c.get("fast_ms"), c.get("general_ms")
