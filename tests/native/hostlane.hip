@@ -42,6 +42,7 @@ namespace {
 static uint64_t g_fast_lanes = 0, g_bailed_lanes = 0, g_tick_lanes = 0, g_steady_lanes = 0, g_steady_leaders = 0;
 static uint32_t g_hint_salt = 0;  // varies the drawn wave hints from call to call
 static bool g_true_hints = false;  // hl_true_hints: every wave gets the device's hint (diagnostics)
+static bool g_force_unhinted = false;  // hl_force_unhinted: every wave unhinted, split passes (lane_closed_form)
 
 template <int S>
 void run_lanes(const StepParams& kp) {
@@ -92,8 +93,9 @@ void run_lanes(const StepParams& kp) {
     // a split pass (drawn half the time here) runs the two role instances, an
     // unhinted wave through both (each takes the lanes of its role); a small
     // pass runs the FL_ANY instance
+    if (g_force_unhinted) hint = 0;
     const int fk = wave_kernel(hint, S);
-    const bool split = g_true_hints || ((g_hint_salt >> 3) & 1u);
+    const bool split = g_force_unhinted || g_true_hints || ((g_hint_salt >> 3) & 1u);
     bool done = false;
     uint32_t sh = 0, role_cf = 0;
     int q0 = QS_OTHER;
@@ -314,6 +316,7 @@ extern "C" int hl_commit_update(uint32_t slots, gr_peer* peers, uint32_t n_peers
 // draw only the hints the device would give, and run split passes (the large-pass
 // schedule), as tools/bail_trace.py wants; 0 restores the test default
 extern "C" void hl_true_hints(int on) { g_true_hints = on != 0; }
+extern "C" void hl_force_unhinted(int on) { g_force_unhinted = on != 0; }
 
 // lanes finished by the fast subset / by the general lane since load
 extern "C" void hl_counters(uint64_t* fast, uint64_t* bailed) {

@@ -48,6 +48,26 @@ def test_leader_change_churn(built):
     assert b1 > b0
 
 
+@pytest.mark.parametrize("inject_p", [0.0, 0.1])
+def test_unhinted_waves_lane_closed_form(built, inject_p):
+    """Every wave unhinted in a split pass (as in a pass's first passes, or waves
+    whose groups' leaders sit on different replicas): the steady kernel's LC
+    instance runs each lane's own role's closed form (gr_steady.h
+    lane_closed_form, the slot from the header), the rest FastLane by role and
+    the general lane; steady state and config-5 churn, bit-exact with the
+    oracle after every pass, and the closed forms did finish lanes."""
+    from oracle.pyoracle import hostlane_lib, hostlane_steady_lanes
+    hl = hostlane_lib()
+    hl.hl_force_unhinted(1)
+    try:
+        s0 = hostlane_steady_lanes()
+        st = _run(128, 10, seed=7, inject_p=inject_p)
+        assert st["commits"] > 0
+        assert hostlane_steady_lanes() - s0 > 0
+    finally:
+        hl.hl_force_unhinted(0)
+
+
 def test_forwarded_proposals(built):
     """ProposeEntries on every replica: followers forward (handleFollowerPropose,
     raft.go:1346-1357) and the leader appends the forwarded batches on the device
